@@ -1,0 +1,197 @@
+"""ctypes front-end of the CPU oracle (oracle/uam_oracle.c).  TEST INFRASTRUCTURE, NOT PRODUCT.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, as the
+checker / the timed CPU baseline.  The product path never does.  See uam_oracle.c's header for
+the reference file:line each routine restates, and tests/test_oracle_golden.py for the golden
+vectors (recorded from the reference itself) that pin it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from .geometry import MAX_REGIONS, FlatGeometry, compile_spec  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_f32p = ctypes.POINTER(ctypes.c_float)
+
+
+class _Geom(ctypes.Structure):
+    _fields_ = [("n_ineq", ctypes.c_int32), ("ineq_kind", _i32p), ("ineq_par", _f64p),
+                ("n_shapes", ctypes.c_int32), ("shape_first", _i32p), ("shape_count", _i32p),
+                ("shape_center", _f64p), ("n_obstacles", ctypes.c_int32),
+                ("n_regions", ctypes.c_int32), ("region_first", _i32p)]
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int32), ("length_smooth", ctypes.c_int32),
+                ("penalty_smooth", ctypes.c_int32), ("obstacle_smooth", ctypes.c_int32),
+                ("maxratio_smooth", ctypes.c_int32), ("quirk_length", ctypes.c_int32),
+                ("anchor_mode", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("anchor_x", ctypes.c_double), ("anchor_y", ctypes.c_double),
+                ("maxratio", ctypes.c_double), ("maxalpha", ctypes.c_double),
+                ("enlargement", ctypes.c_double), ("altitude", ctypes.c_double),
+                ("weights", ctypes.c_double * MAX_REGIONS)]
+
+
+class _Raster(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("x0", ctypes.c_double),
+                ("y_top", ctypes.c_double), ("dx", ctypes.c_double), ("dy", ctypes.c_double),
+                ("nodata", ctypes.c_float), ("dem_threshold", ctypes.c_float)]
+
+
+def build():
+    """Compile liboracle.so (gcc) if it is missing or older than its source."""
+    src = os.path.join(HERE, "uam_oracle.c")
+    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        for name in ("orc_eval_points", "orc_gen_paths", "orc_raster_build", "orc_eval_paths",
+                     "orc_argmin"):
+            getattr(_lib, name).restype = ctypes.c_int
+    return _lib
+
+
+def _ptr(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+class Oracle:
+    """Bundle of flat geometry + params in the oracle's own C structs."""
+
+    def __init__(self, geom, N, options=None, maxratio=1.0, maxalpha=0.0, enlargement=0.0,
+                 weights=(), quirk_length=True, anchor=None, altitude=0.0):
+        opts = {"length_smooth": False, "penalty_smooth": True, "obstacle_smooth": False,
+                "maxratio_smooth": False}
+        if options:
+            opts.update(options)
+        self.geom = geom
+        self.N = int(N)
+        self._keep = [geom.ineq_kind, geom.ineq_par, geom.shape_first, geom.shape_count,
+                      geom.shape_center, geom.region_first]
+        self.g = _Geom(len(geom.ineq_kind), _ptr(geom.ineq_kind, _i32p),
+                       _ptr(geom.ineq_par, _f64p), len(geom.shape_first),
+                       _ptr(geom.shape_first, _i32p), _ptr(geom.shape_count, _i32p),
+                       _ptr(geom.shape_center, _f64p), geom.n_obstacles, geom.n_regions,
+                       _ptr(geom.region_first, _i32p))
+        w = (ctypes.c_double * MAX_REGIONS)(*([float(x) for x in weights] +
+                                              [1.0] * (MAX_REGIONS - len(weights))))
+        self.p = _Params(self.N, int(bool(opts["length_smooth"])),
+                         int(bool(opts["penalty_smooth"])), int(bool(opts["obstacle_smooth"])),
+                         int(bool(opts["maxratio_smooth"])), int(bool(quirk_length)),
+                         0 if anchor is None else 1, 0,
+                         0.0 if anchor is None else float(anchor[0]),
+                         0.0 if anchor is None else float(anchor[1]),
+                         float(maxratio), float(maxalpha), float(enlargement), float(altitude), w)
+
+    # -- points ----------------------------------------------------------------------------
+    def eval_points(self, pts):
+        pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 2)
+        n = pts.shape[0]
+        R = self.geom.n_regions
+        out = {"phi": np.zeros(n), "phi_regions": np.zeros((n, R)), "obs_norm": np.zeros(n),
+               "psi_raw": np.zeros(n), "collide": np.zeros(n, np.int32)}
+        lib().orc_eval_points(ctypes.byref(self.g), ctypes.byref(self.p), _ptr(pts, _f64p),
+                              ctypes.c_int64(n), _ptr(out["phi"], _f64p),
+                              _ptr(out["phi_regions"], _f64p), _ptr(out["obs_norm"], _f64p),
+                              _ptr(out["psi_raw"], _f64p), _ptr(out["collide"], _i32p))
+        return out
+
+    # -- raster ----------------------------------------------------------------------------
+    @staticmethod
+    def raster_desc(nx, ny, x0, y_top, dx, dy, nodata=-9999.0, dem_threshold=0.0):
+        return _Raster(int(nx), int(ny), float(x0), float(y_top), float(dx), float(dy),
+                       float(nodata), float(dem_threshold))
+
+    def raster_build(self, rdesc, dem=None):
+        rec = np.zeros((rdesc.ny, rdesc.nx, 4), dtype=np.float32)
+        dem_a = None if dem is None else np.ascontiguousarray(dem, dtype=np.float32)
+        lib().orc_raster_build(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.byref(rdesc),
+                               _ptr(dem_a, _f32p), _ptr(rec, _f32p))
+        return rec
+
+    # -- paths -----------------------------------------------------------------------------
+    def eval_paths(self, wp, mode="analytic", rdesc=None, rec=None, want_cells=False,
+                   want_g=False):
+        W = self.N + 2
+        wp = np.ascontiguousarray(wp, dtype=np.float64).reshape(-1, W, 2)
+        P = wp.shape[0]
+        out = {k: np.zeros(P) for k in ("cost", "lq", "length", "kin", "nfz", "min_clearance")}
+        out["nfz_hits"] = np.zeros(P, np.int32)
+        out["offmap"] = np.zeros(P, np.int32)
+        cells = np.zeros((P, W), np.int32) if want_cells else None
+        n_rows = 3 * self.N + self.geom.n_obstacles * W
+        g = np.zeros((P, n_rows)) if want_g else None
+        m = 0 if mode == "analytic" else 1
+        if m == 1:
+            rec = np.ascontiguousarray(rec, dtype=np.float32)
+        lib().orc_eval_paths(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.c_int32(m),
+                             None if rdesc is None else ctypes.byref(rdesc),
+                             _ptr(rec if m == 1 else None, _f32p), _ptr(wp, _f64p),
+                             ctypes.c_int64(P), _ptr(out["cost"], _f64p),
+                             _ptr(out["lq"], _f64p), _ptr(out["length"], _f64p),
+                             _ptr(out["kin"], _f64p), _ptr(out["nfz"], _f64p),
+                             _ptr(out["nfz_hits"], _i32p), _ptr(out["min_clearance"], _f64p),
+                             _ptr(out["offmap"], _i32p), _ptr(cells, _i32p), _ptr(g, _f64p))
+        if want_cells:
+            out["cells"] = cells
+        if want_g:
+            out["g"] = g
+        return out
+
+
+def gen_paths(pairs, utab):
+    pairs = np.ascontiguousarray(pairs, dtype=np.float64).reshape(-1, 4)
+    utab = np.ascontiguousarray(utab, dtype=np.float64)
+    D, N = utab.shape[0], utab.shape[1]
+    out = np.zeros((pairs.shape[0] * D, N + 2, 2))
+    lib().orc_gen_paths(_ptr(pairs, _f64p), ctypes.c_int64(pairs.shape[0]), _ptr(utab, _f64p),
+                        ctypes.c_int32(D), ctypes.c_int32(N), _ptr(out, _f64p))
+    return out
+
+
+def argmin(values, G, take_sqrt):
+    v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
+    groups = v.shape[0] // G
+    best = np.zeros(groups, np.int32)
+    lib().orc_argmin(_ptr(v, _f64p), ctypes.c_int64(groups), ctypes.c_int32(G),
+                     ctypes.c_int32(1 if take_sqrt else 0), _ptr(best, _i32p))
+    return best
+
+
+def arc_table(N, displacements):
+    """Oracle copy of the unit-arc table (solver.py:103-136 normalised by a = |x0-xf|/2):
+    u_k(d) such that p_k = C + 0.5*[[vx,-vy],[vy,vx]] u_k, k = 1..N."""
+    ds = np.asarray(displacements, dtype=np.float64).reshape(-1)
+    out = np.zeros((ds.shape[0], N, 2))
+    for i, d in enumerate(ds):
+        if abs(d) > 1:
+            raise ValueError(f"abs(displacement) = {abs(d)} must be smaller than 1")
+        if d == 0:
+            s = np.arange(1, N + 1, dtype=np.float64) / (N + 1)
+            out[i, :, 0] = 1.0 - 2.0 * s
+            continue
+        with np.errstate(divide="ignore"):
+            beta = 2 * np.arctan(2 * d / (1 - d * d))
+        rho = (1 + d * d) / (2 * d)
+        off = (d * d - 1) / (2 * d)
+        t = np.linspace((np.pi - beta) / 2, (np.pi + beta) / 2, N + 2)[1:-1]
+        out[i, :, 0] = rho * np.cos(t)
+        out[i, :, 1] = off + rho * np.sin(t)
+    return out

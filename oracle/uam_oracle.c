@@ -1,0 +1,396 @@
+/*
+ * uam_oracle.c -- CPU restatement of the uam_path_planning hot path.
+ *
+ * TEST INFRASTRUCTURE, NOT PRODUCT.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load this library, and only as the checker / the timed CPU baseline.
+ * The product (uam_path_planning_amd, libuampath.so) never links or calls it.
+ *
+ * Parity pinning: tests/test_oracle_golden.py checks this file against golden vectors that
+ * tests/golden/make_golden.py recorded by running the reference's own cost model
+ * (geo_simulation_project/path_generation/ *.py) under a numeric casadi stand-in.
+ *
+ * Every routine restates, in plain float64 C with the reference's operation order, one
+ * reference function (file:line relative to /root/reference/geo_simulation_project/):
+ *   ineq_h          polygon.py:69-71,98  ball.py:209-213(func)  square.py:266-288
+ *   psi             path_generation/quadratic_obstacle.py:27-39  (penalty_function)
+ *   contains        path_generation/quadratic_obstacle.py:89-94, map.py:41-43 (collides)
+ *   region_penalty  path_generation/problem.py:59-82 (get_penalty_function)
+ *   total_penalty   path_generation/problem.py:49-56 (get_total_penalty_function)
+ *   path loop       path_generation/problem.py:38-44 (get_cost), 84-114 (get_nonlincon),
+ *                   130-146 (length_of)
+ *   orc_gen_paths   path_generation/solver.py:103-136 (create_x_init, restated through a
+ *                   host-computed unit-arc table)
+ *   orc_raster_build  map_generation/data_manager.py:14-17 (DEM mask) + the penalty above at
+ *                   cell centres (the build's raster mode)
+ *   orc_argmin      path_generation/main.py:175-180 (strict <, first index wins)
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define ORC_HALFPLANE 0
+#define ORC_ELLIPSE 1
+#define ORC_AXIS 2
+
+#define ORC_MAX_REGIONS 16
+
+#define ORC_FLAG_NFZ 1u
+#define ORC_FLAG_MASK 2u
+#define ORC_FLAG_NODATA 4u
+
+typedef struct {
+    int32_t n_ineq;
+    const int32_t* ineq_kind;    /* [n_ineq] */
+    const double* ineq_par;      /* [n_ineq][6] */
+    int32_t n_shapes;            /* obstacles first, then regions region-major */
+    const int32_t* shape_first;  /* [n_shapes] index into ineq */
+    const int32_t* shape_count;  /* [n_shapes] */
+    const double* shape_center;  /* [n_shapes][2]; NaN => no normalisation */
+    int32_t n_obstacles;         /* shapes [0, n_obstacles) are no-fly obstacles */
+    int32_t n_regions;
+    const int32_t* region_first; /* [n_regions+1] shape offsets */
+} orc_geom;
+
+typedef struct {
+    int32_t N;
+    int32_t length_smooth, penalty_smooth, obstacle_smooth, maxratio_smooth;
+    int32_t quirk_length;        /* 1: get_cost length term as the reference computes it */
+    int32_t anchor_mode;         /* 0: anchor = path's own p_0; 1: (anchor_x, anchor_y) */
+    int32_t pad_;
+    double anchor_x, anchor_y;
+    double maxratio, maxalpha, enlargement;
+    double altitude;
+    double weights[ORC_MAX_REGIONS];
+} orc_params;
+
+typedef struct {
+    int32_t nx, ny;
+    double x0, y_top, dx, dy;
+    float nodata, dem_threshold;
+} orc_raster;
+
+/* ---- geometry ------------------------------------------------------------------------ */
+
+static double ineq_h(const orc_geom* g, int i, double x0, double x1) {
+    const double* p = g->ineq_par + 6 * (int64_t)i;
+    switch (g->ineq_kind[i]) {
+        case ORC_HALFPLANE: {
+            /* polygon.py:69-71: (Pb_y-Pa_y)*(x0-Pa_x) - (Pb_x-Pa_x)*(x1-Pa_y); h = -sgn*line */
+            double line = p[3] * (x0 - p[0]) - p[2] * (x1 - p[1]);
+            return p[4] * line;
+        }
+        case ORC_ELLIPSE: {
+            /* ball.py: diff=x-c; sumsqr(vertcat(diff0/r1, diff1/r2)) - 1 ; sumsqr from 0 */
+            double a = (x0 - p[0]) / p[2];
+            double b = (x1 - p[1]) / p[3];
+            double s = 0.0;
+            s = s + a * a;
+            s = s + b * b;
+            return s - 1.0;
+        }
+        default: { /* ORC_AXIS: square.py sides: s*(x_k - c) - r */
+            double xk = (p[0] == 0.0) ? x0 : x1;
+            return p[3] * (xk - p[1]) - p[2];
+        }
+    }
+}
+
+/* quadratic_obstacle.py:27-39 */
+static double psi(const orc_geom* g, int s, double x0, double x1, int smooth, double e) {
+    double r = 1.0;
+    int f = g->shape_first[s], c = g->shape_count[s];
+    for (int i = f; i < f + c; ++i) {
+        double h = ineq_h(g, i, x0, x1);
+        if (smooth) {
+            double m = fmin(h - e, 0.0);
+            r = r * (m * m);
+        } else {
+            r = r * fmin(e - h, 0.0);
+        }
+    }
+    return r;
+}
+
+/* quadratic_obstacle.py:89-94 */
+static int contains(const orc_geom* g, int s, double x0, double x1) {
+    int f = g->shape_first[s], c = g->shape_count[s];
+    for (int i = f; i < f + c; ++i)
+        if (ineq_h(g, i, x0, x1) > 1e-14) return 0;
+    return 1;
+}
+
+/* problem.py:72-80: Σ_o ψ(x)/ψ(c) (raw ψ when the centre is NaN), times w */
+static double shape_sum(const orc_geom* g, int s0, int s1, double x0, double x1, int smooth,
+                        double e) {
+    double total = 0.0;
+    for (int s = s0; s < s1; ++s) {
+        double cx = g->shape_center[2 * s], cy = g->shape_center[2 * s + 1];
+        double v = psi(g, s, x0, x1, smooth, e);
+        if (isnan(cx) || isnan(cy))
+            total = total + v;
+        else
+            total = total + v / psi(g, s, cx, cy, smooth, e);
+    }
+    return total;
+}
+
+static double region_penalty(const orc_geom* g, const orc_params* p, int r, double x0,
+                             double x1) {
+    double t = shape_sum(g, g->region_first[r], g->region_first[r + 1], x0, x1,
+                         p->penalty_smooth, p->enlargement);
+    return p->weights[r] * t;
+}
+
+/* problem.py:49-56 */
+static double total_penalty(const orc_geom* g, const orc_params* p, double x0, double x1) {
+    double pen = 0.0;
+    for (int r = 0; r < g->n_regions; ++r) pen = pen + region_penalty(g, p, r, x0, x1);
+    return pen;
+}
+
+/* Σ_o raw ψ_o(x; obstacle_smooth, e=0): the per-waypoint sum of the no-fly g rows
+ * (problem.py:109-112 -- penalty_function(smooth) leaves enlargement at its default 0). */
+static double obstacle_psi_sum(const orc_geom* g, const orc_params* p, double x0, double x1) {
+    double acc = 0.0;
+    for (int s = 0; s < g->n_obstacles; ++s)
+        acc = acc + psi(g, s, x0, x1, p->obstacle_smooth, 0.0);
+    return acc;
+}
+
+static int collides(const orc_geom* g, double x0, double x1) {
+    for (int s = 0; s < g->n_obstacles; ++s)
+        if (contains(g, s, x0, x1)) return 1;
+    return 0;
+}
+
+/* ---- point evaluation (Problem.get_*_penalty_function) ------------------------------- */
+
+int orc_eval_points(const orc_geom* g, const orc_params* p, const double* pts, int64_t n,
+                    double* phi, double* phi_regions, double* obs_norm, double* psi_raw,
+                    int32_t* collide) {
+    for (int64_t i = 0; i < n; ++i) {
+        double x0 = pts[2 * i], x1 = pts[2 * i + 1];
+        if (phi) phi[i] = total_penalty(g, p, x0, x1);
+        if (phi_regions)
+            for (int r = 0; r < g->n_regions; ++r)
+                phi_regions[i * g->n_regions + r] = region_penalty(g, p, r, x0, x1);
+        if (obs_norm) /* get_penalty_function(None): obstacles, obstacle_smooth, enlargement */
+            obs_norm[i] = 1.0 * shape_sum(g, 0, g->n_obstacles, x0, x1, p->obstacle_smooth,
+                                          p->enlargement);
+        if (psi_raw) psi_raw[i] = obstacle_psi_sum(g, p, x0, x1);
+        if (collide) collide[i] = collides(g, x0, x1);
+    }
+    return 0;
+}
+
+/* ---- candidate generator (solver.py:103-136) ------------------------------------------ */
+/* pairs [Q][4] = (x0, y0, xf, yf); utab [D][N][2] unit-arc table; out [Q*D][N+2][2].
+ * p_k = C + 0.5*[[vx,-vy],[vy,vx]] u_k with v = x0 - xf, C = (xf + x0)/2. */
+static void gen_point(const double* pr, const double* u, double* px, double* py) {
+    double vx = pr[0] - pr[2], vy = pr[1] - pr[3];
+    double cx = (pr[2] + pr[0]) * 0.5, cy = (pr[3] + pr[1]) * 0.5;
+    *px = cx + 0.5 * (vx * u[0] - vy * u[1]);
+    *py = cy + 0.5 * (vy * u[0] + vx * u[1]);
+}
+
+int orc_gen_paths(const double* pairs, int64_t Q, const double* utab, int32_t D, int32_t N,
+                  double* out) {
+    int W = N + 2;
+    for (int64_t q = 0; q < Q; ++q) {
+        const double* pr = pairs + 4 * q;
+        for (int d = 0; d < D; ++d) {
+            double* o = out + ((q * D + d) * (int64_t)W) * 2;
+            o[0] = pr[0];
+            o[1] = pr[1];
+            for (int k = 0; k < N; ++k)
+                gen_point(pr, utab + ((int64_t)d * N + k) * 2, &o[2 * (k + 1)],
+                          &o[2 * (k + 1) + 1]);
+            o[2 * (N + 1)] = pr[2];
+            o[2 * (N + 1) + 1] = pr[3];
+        }
+    }
+    return 0;
+}
+
+/* ---- raster build ------------------------------------------------------------------------
+ * record (16 B) per cell, row-major, row 0 = north: {phi f32, psi f32, dem f32, flags u32} */
+int orc_raster_build(const orc_geom* g, const orc_params* p, const orc_raster* rs,
+                     const float* dem, float* rec) {
+    for (int64_t iy = 0; iy < rs->ny; ++iy) {
+        for (int64_t ix = 0; ix < rs->nx; ++ix) {
+            int64_t c = iy * rs->nx + ix;
+            double xc = rs->x0 + ((double)ix + 0.5) * rs->dx;
+            double yc = rs->y_top - ((double)iy + 0.5) * rs->dy;
+            float z = dem ? dem[c] : 0.0f;
+            uint32_t fl = 0;
+            if (collides(g, xc, yc)) fl |= ORC_FLAG_NFZ;
+            /* data_manager.py:14-17 */
+            if (rs->dem_threshold == -9999.0f ? (z == -9999.0f) : (z > rs->dem_threshold))
+                fl |= ORC_FLAG_MASK;
+            if (z == rs->nodata) fl |= ORC_FLAG_NODATA;
+            rec[4 * c + 0] = (float)total_penalty(g, p, xc, yc);
+            rec[4 * c + 1] = (float)obstacle_psi_sum(g, p, xc, yc);
+            rec[4 * c + 2] = z;
+            memcpy(&rec[4 * c + 3], &fl, 4);
+        }
+    }
+    return 0;
+}
+
+/* ---- path evaluation ------------------------------------------------------------------
+ * mode 0 = analytic (reference formulas at the waypoint), 1 = raster (gather the record of
+ * the waypoint's cell).  wp [P][W][2], W = N+2 (p_0 = start ... p_{N+1} = goal). */
+static double nrm_of(double d2, int smooth) {
+    double n = sqrt(d2);
+    return smooth ? n * n : n; /* problem.py:94,132: norm_2(.)**2 when smooth */
+}
+
+int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const orc_raster* rs,
+                   const float* rec, const double* wp, int64_t P, double* cost, double* lq,
+                   double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
+                   int32_t* offmap, int32_t* cells, double* g_rows) {
+    const int N = p->N, W = N + 2;
+    const double mincos = cos(p->maxalpha);
+    const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
+    const int n_rows = 3 * N + g->n_obstacles * W;
+    double inv_dx = 0, inv_dy = 0;
+    if (mode == 1) {
+        inv_dx = 1.0 / rs->dx;
+        inv_dy = 1.0 / rs->dy;
+    }
+    for (int64_t pi = 0; pi < P; ++pi) {
+        const double* z = wp + pi * (int64_t)W * 2;
+        /* length_of (problem.py:130-146): y = [anchor, p_0..p_{N+1}, goal]; N+1 segments */
+        double ax = p->anchor_mode ? p->anchor_x : z[0];
+        double ay = p->anchor_mode ? p->anchor_y : z[1];
+        double L = 0.0;
+        if (p->quirk_length) {
+            double dx = z[0] - ax, dy = z[1] - ay;
+            double s = 0.0;
+            s = s + dx * dx;
+            s = s + dy * dy;
+            L = L + nrm_of(s, p->length_smooth);
+            for (int k = 1; k <= N; ++k) {
+                dx = z[2 * k] - z[2 * k - 2];
+                dy = z[2 * k + 1] - z[2 * k - 1];
+                s = 0.0;
+                s = s + dx * dx;
+                s = s + dy * dy;
+                L = L + nrm_of(s, p->length_smooth);
+            }
+        } else {
+            for (int k = 1; k <= N + 1; ++k) {
+                double dx = z[2 * k] - z[2 * k - 2], dy = z[2 * k + 1] - z[2 * k - 1];
+                double s = 0.0;
+                s = s + dx * dx;
+                s = s + dy * dy;
+                L = L + nrm_of(s, p->length_smooth);
+            }
+        }
+        /* true polyline length (solver.py:49 length_of(x_sol), non-smooth, all segments) */
+        double len = 0.0;
+        for (int k = 1; k <= N + 1; ++k) {
+            double dx = z[2 * k] - z[2 * k - 2], dy = z[2 * k + 1] - z[2 * k - 1];
+            double s = 0.0;
+            s = s + dx * dx;
+            s = s + dy * dy;
+            len = len + sqrt(s);
+        }
+        /* kinematic rows (problem.py:100-107) */
+        double ksum = 0.0;
+        double* grow = g_rows ? g_rows + pi * (int64_t)n_rows : 0;
+        for (int k = 0; k < N; ++k) {
+            double ax0 = z[2 * (k + 1)] - z[2 * k], ay0 = z[2 * (k + 1) + 1] - z[2 * k + 1];
+            double bx = z[2 * (k + 2)] - z[2 * (k + 1)];
+            double by = z[2 * (k + 2) + 1] - z[2 * (k + 1) + 1];
+            double sa = 0.0, sb = 0.0, dt = 0.0;
+            sa = sa + ax0 * ax0;
+            sa = sa + ay0 * ay0;
+            sb = sb + bx * bx;
+            sb = sb + by * by;
+            dt = dt + ax0 * bx;
+            dt = dt + ay0 * by;
+            double na = nrm_of(sa, p->maxratio_smooth), nb = nrm_of(sb, p->maxratio_smooth);
+            double c1 = fmax(0.0, nb - r * na);
+            double c2 = fmax(0.0, na / r - nb);
+            double c3 = fmax(0.0, mincos - dt / (na * nb));
+            ksum = ksum + c1;
+            ksum = ksum + c2;
+            ksum = ksum + c3;
+            if (grow) {
+                grow[3 * k] = c1;
+                grow[3 * k + 1] = c2;
+                grow[3 * k + 2] = c3;
+            }
+        }
+        /* per-waypoint penalty, no-fly rows, clearance */
+        double c = (double)(N + 1) * L;
+        double nsum = 0.0, hmax = -INFINITY;
+        int32_t nh = 0, off = 0;
+        for (int j = 0; j < W; ++j) {
+            double x0 = z[2 * j], x1 = z[2 * j + 1];
+            if (mode == 0) {
+                c = c + total_penalty(g, p, x0, x1) / (double)N;
+                for (int s = 0; s < g->n_obstacles; ++s) {
+                    double v = psi(g, s, x0, x1, p->obstacle_smooth, 0.0);
+                    nsum = nsum + v;
+                    if (grow) grow[3 * N + s * W + j] = v;
+                }
+                nh += collides(g, x0, x1);
+            } else {
+                double fx = floor((x0 - rs->x0) * inv_dx);
+                double fy = floor((rs->y_top - x1) * inv_dy);
+                int inside = (fx >= 0.0) && (fx < (double)rs->nx) && (fy >= 0.0) &&
+                             (fy < (double)rs->ny);
+                if (!inside) {
+                    ++off;
+                    if (cells) cells[pi * W + j] = -1;
+                    if (0.0 > hmax) hmax = 0.0; /* off-raster counts as sea level */
+                    continue;
+                }
+                int64_t cell = (int64_t)fy * rs->nx + (int64_t)fx;
+                if (cells) cells[pi * W + j] = (int32_t)cell;
+                const float* rc = rec + 4 * cell;
+                uint32_t fl;
+                memcpy(&fl, &rc[3], 4);
+                c = c + (double)rc[0] / (double)N;
+                nsum = nsum + (double)rc[1];
+                nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
+                double terrain = (fl & ORC_FLAG_NODATA) ? 0.0 : (double)rc[2];
+                if (terrain > hmax) hmax = terrain;
+            }
+        }
+        if (cost) cost[pi] = c;
+        if (lq) lq[pi] = L;
+        if (length) length[pi] = len;
+        if (kin) kin[pi] = ksum;
+        if (nfz) nfz[pi] = nsum;
+        if (hits) hits[pi] = nh;
+        if (offmap) offmap[pi] = off;
+        if (minclr) minclr[pi] = (mode == 1) ? p->altitude - hmax : NAN;
+    }
+    return 0;
+}
+
+/* main.py:175-180 over groups of G consecutive paths.  The reference keeps index i when
+ * `min_v == 0 or v_i < min_v` with min_v initialised to the sentinel 0, so: the first entry
+ * always wins first, later entries replace it on strict '<' (ties keep the first), a NaN never
+ * wins, and a best value of exactly 0 is replaced by the next entry (sentinel quirk).  For
+ * fval the compared value is sqrt(cost) (solver.py:48), for length the length itself. */
+int orc_argmin(const double* v, int64_t groups, int32_t G, int32_t take_sqrt, int32_t* best) {
+    for (int64_t q = 0; q < groups; ++q) {
+        int32_t bi = 0;
+        double bv = 0.0;
+        for (int32_t d = 0; d < G; ++d) {
+            double x = take_sqrt ? sqrt(v[q * G + d]) : v[q * G + d];
+            if (bv == 0.0 || x < bv) {
+                bv = x;
+                bi = d;
+            }
+        }
+        best[q] = bi;
+    }
+    return 0;
+}

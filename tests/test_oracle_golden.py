@@ -1,0 +1,142 @@
+"""Pin the CPU oracle (oracle/uam_oracle.c + oracle/geometry.py) against golden vectors that
+tests/golden/make_golden.py recorded from the reference's own cost model
+(problem.py get_cost/get_nonlincon/length_of/get_penalty_function, solver.py create_x_init)."""
+import numpy as np
+import pytest
+
+import golden_io as G
+
+
+def _oracle(O, meta):
+    geom = O.compile_spec(meta["map"])
+    return O.Oracle(geom, meta["N"], meta["options"], meta["maxratio"], meta["maxalpha"],
+                    meta["enlargement"], meta["weights"])
+
+
+def test_canonical_bit_exact(oracle_mod):
+    meta, arr = G.canonical()
+    orc = _oracle(oracle_mod, meta)
+    wp = G.canonical_paths(meta, arr)
+    out = orc.eval_paths(wp, want_g=True)
+    np.testing.assert_array_equal(out["cost"], arr["cost"])
+    np.testing.assert_array_equal(out["length"], arr["length"])
+    np.testing.assert_array_equal(out["lq"], arr["lq"])
+    np.testing.assert_array_equal(out["g"], arr["g"])
+    np.testing.assert_array_equal(out["nfz_hits"], arr["collide"].sum(1))
+    # the survey's quoted numbers
+    np.testing.assert_allclose(out["cost"], [2497.86843688, 3226.73830892, 2565.28161896,
+                                             2288.09556814, 3428.58186125], rtol=1e-11)
+    assert int(np.argmin(np.sqrt(out["cost"]))) == 3
+    # g sum split (kinematic + no-fly rows) equals the golden row sum
+    np.testing.assert_allclose(out["kin"] + out["nfz"], arr["g"].sum(1), rtol=1e-13, atol=1e-13)
+
+
+def test_canonical_points(oracle_mod):
+    meta, arr = G.canonical()
+    orc = _oracle(oracle_mod, meta)
+    pts = G.canonical_paths(meta, arr).reshape(-1, 2)
+    pe = orc.eval_points(pts)
+    np.testing.assert_array_equal(pe["phi"], arr["phi"].reshape(-1))
+    np.testing.assert_array_equal(pe["phi_regions"],
+                                  arr["phi_r"].transpose(0, 2, 1).reshape(-1, 3))
+    np.testing.assert_array_equal(pe["obs_norm"], arr["obs_norm"].reshape(-1))
+    np.testing.assert_array_equal(pe["collide"], arr["collide"].reshape(-1))
+
+
+def test_variants(oracle_mod):
+    meta, arr = G.canonical()
+    v = G.variants()
+    m = dict(meta)
+    m["enlargement"] = 0.5
+    orc = _oracle(oracle_mod, m)
+    out = orc.eval_paths(G.canonical_paths(meta, arr), want_g=True)
+    np.testing.assert_array_equal(out["cost"], v["enl05_cost"])
+    np.testing.assert_array_equal(out["g"], v["enl05_g"])
+    # problem.py demo: N=10, default options, weights 4/13/45
+    m2 = dict(meta)
+    m2.update(N=10, options=None, maxratio=1.25, maxalpha=np.pi / 10, enlargement=0.0,
+              weights=[4, 13, 45])
+    orc2 = _oracle(oracle_mod, m2)
+    xs, xg = np.asarray(meta["map"]["x_start"]), np.asarray(meta["map"]["x_goal"])
+    wp = np.stack([np.concatenate([xs, x, xg]).reshape(-1, 2) for x in v["n10_x_init"]])
+    out2 = orc2.eval_paths(wp, want_g=True)
+    np.testing.assert_array_equal(out2["cost"], v["n10_cost"])
+    np.testing.assert_array_equal(out2["g"], v["n10_g"])
+
+
+@pytest.mark.parametrize("ci", range(24))
+def test_random_cases(oracle_mod, ci):
+    case = G.random_cases()[ci]
+    orc = _oracle(oracle_mod, case)
+    wp = np.asarray(case["paths"]).reshape(len(case["paths"]), -1, 2)
+    out = orc.eval_paths(wp, want_g=True)
+    for i, o in enumerate(case["outputs"]):
+        np.testing.assert_allclose(out["cost"][i], o["cost"], rtol=1e-13, equal_nan=True)
+        np.testing.assert_allclose(out["g"][i], np.asarray(o["g"], float), rtol=1e-13,
+                                   atol=1e-300, equal_nan=True)
+        np.testing.assert_allclose(out["length"][i], o["length"], rtol=1e-14)
+        np.testing.assert_allclose(out["lq"][i], o["lq"], rtol=1e-14)
+        pe = orc.eval_points(wp[i])
+        np.testing.assert_allclose(pe["phi"], np.asarray(o["phi"], float), rtol=1e-13,
+                                   equal_nan=True)
+        np.testing.assert_allclose(pe["phi_regions"], np.asarray(o["phi_r"], float).T,
+                                   rtol=1e-13, equal_nan=True)
+        np.testing.assert_allclose(pe["obs_norm"], np.asarray(o["obs_norm"], float),
+                                   rtol=1e-13, equal_nan=True)
+        np.testing.assert_array_equal(pe["collide"], np.asarray(o["collide"]))
+
+
+def test_arcs(oracle_mod):
+    a = G.arcs()
+    for pi, pr in enumerate(a["pairs"]):
+        for N in a["Ns"]:
+            ref = a[f"p{pi}_N{N}"]
+            ut = oracle_mod.arc_table(int(N), a["ds"])
+            got = oracle_mod.gen_paths(pr[None, :], ut)[:, 1:-1, :].reshape(len(a["ds"]), -1)
+            scale = max(1.0, float(np.abs(pr).max()))
+            for i, d in enumerate(a["ds"]):
+                # the arc's radius (1+d^2)/(2|d|) sets the cancellation both formulas suffer
+                rho = 1.0 if d == 0 else (1 + d * d) / (2 * abs(d))
+                np.testing.assert_allclose(got[i], ref[i], rtol=0,
+                                           atol=1e-14 * scale * max(1.0, rho) * 8)
+
+
+def test_raster_cell_centres(oracle_mod):
+    """Raster mode pin: a record computed at a cell centre equals the reference's Φ / ψ /
+    collides evaluated at that centre (rounded to f32)."""
+    meta, _ = G.canonical()
+    gr = G.grid()
+    nx, ny, X0, Ytop, dx, dy = gr["geo"]
+    geom = oracle_mod.compile_spec(meta["map"])
+    rd = oracle_mod.Oracle.raster_desc(nx, ny, X0, Ytop, dx, dy)
+    for tag, opts, enl in (("a", {"penalty_smooth": True, "obstacle_smooth": True}, 0.0),
+                           ("b", {"penalty_smooth": False, "obstacle_smooth": False}, 0.25)):
+        orc = oracle_mod.Oracle(geom, 4, opts, 1.1, 0.3, enl, [200, 15000, 27000])
+        rec = orc.raster_build(rd)
+        np.testing.assert_array_equal(rec[..., 0], gr[f"phi_{tag}"].astype(np.float32))
+        np.testing.assert_array_equal(rec[..., 1], gr[f"psi_{tag}"].astype(np.float32))
+        flags = rec[..., 3].view(np.uint32)
+        np.testing.assert_array_equal(flags & 1, gr[f"collide_{tag}"])
+
+
+def test_argmin_semantics(oracle_mod):
+    # strict '<', first index wins on ties, NaN never wins, sentinel-0 quirk (main.py:175-180)
+    v = np.array([3.0, 1.0, 1.0, 2.0,
+                  np.nan, 5.0, 4.0, 4.0,
+                  2.0, 0.0, 7.0, 9.0])
+    best = oracle_mod.argmin(v, 4, False)
+    assert best.tolist() == [1, 0, 2]
+
+
+def test_geometry_errors(oracle_mod):
+    errs = G.errors()
+    from oracle import geometry as og
+    for case, pts in (("polygon_two_points", [[0.0, 0.0], [1.0, 0.0]]),
+                      ("polygon_collinear", [[0.0, 0.0], [1.0, 0.0], [2.0, 0.0], [1.0, 1.0]]),
+                      ("polygon_nonconvex", [[0.0, 0.0], [4.0, 0.0], [1.0, 1.0], [0.0, 4.0]])):
+        with pytest.raises(ValueError) as ei:
+            og.shape_from_spec({"kind": "polygon", "vertices": pts})
+        assert str(ei.value) == errs[case]["message"]
+    with pytest.raises(ValueError) as ei:
+        oracle_mod.arc_table(4, [1.5])
+    assert str(ei.value) == errs["arc_displacement_gt1"]["message"]
