@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Headline benchmark: candidate-paths/s (+ waypoint-evals/s) of the batched candidate-path
+cost evaluation on an R x R DEM cost raster (BASELINE.json metric), MI355X.
+
+One "step" = one pass of the hot path over the batch resident in HBM: the fused kernel
+(arc generator K4 + raster gather / cost reduction K2) over every pair x displacement, then
+the reference's candidate selection (argmin on fval and on length, K5).  Default workload:
+BASELINE config 3 (4096^2 DEM + 69 no-fly shapes, 100k start/goal pairs x 5 displacements =
+500k paths x 82 waypoints per GPU; weak scaling: every rank gets its own 100k pairs).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU, RCCL; rank 0 builds the cost raster (K1) and broadcasts it once over xGMI (timed
+separately, outside the step); pairs are sharded with no collective in the hot loop.
+
+Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline (algorithmic bytes
+/ HIP-event kernel time vs 8 TB/s HBM) and a CPU baseline: the C oracle (oracle/, a "port")
+timed on this host on a bounded sample of the same workload, which doubles as a bit-exact
+parity check of the GPU outputs on that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "candidate-paths/sec + waypoint-evals/sec on N×N DEM at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--mode", default="raster", choices=["raster", "analytic"])
+    ap.add_argument("--pairs", type=int, default=None, help="override pairs per GPU")
+    ap.add_argument("--R", type=int, default=None, help="override raster size")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from uam_path_planning_amd import build
+    build.build_library()
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import CostRaster, Engine
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import (CONFIGS, build_region_map, canonical_params,
+                                                canonical_spec, displacements, raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    cfg = dict(CONFIGS[args.workload])
+    if args.pairs:
+        cfg["pairs"] = args.pairs
+    if args.R:
+        cfg["R"] = args.R
+    R, Q, D, N = cfg["R"], cfg["pairs"], cfg["D"], cfg["N"]
+    W = N + 2
+    raster_mode = args.mode == "raster"
+
+    spec = canonical_spec(nfz_polygons=cfg["nfz_polygons"])
+    geom = compile_map(build_region_map(spec))
+    params = canonical_params(spec, N=N, altitude=320.0)
+    eng = Engine(local)
+    eng.set_geometry(geom)
+    eng.set_params(params)
+    ut_host = arc_table(N, displacements(D))
+
+    # ---- cost raster: rank 0 builds (K1), one RCCL broadcast -------------------------------
+    setup = {}
+    geo = raster_geo(R)
+    raster = None
+    dem = None
+    if raster_mode:
+        t0 = time.perf_counter()
+        if rank == 0:
+            dem = synthetic_dem(R)
+            setup["dem_gen_s"] = round(time.perf_counter() - t0, 3)
+            dem_dev = eng.tensor(dem, torch.float32)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            raster = eng.raster_build(geo, dem_dev)
+            torch.cuda.synchronize()
+            setup["raster_build_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+            del dem_dev
+        else:
+            raster = CostRaster(geo, eng.empty((R, R, 4), torch.int32))
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            dist.broadcast(raster.rec, src=0)
+            torch.cuda.synchronize()
+            setup["raster_bcast_ms"] = round((time.perf_counter() - t2) * 1e3, 3)
+            setup["raster_bytes"] = raster.nbytes
+
+    # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
+    all_pairs = random_pairs(Q * world, seed=0)
+    pairs_host = all_pairs[rank * Q:(rank + 1) * Q]
+    pairs = eng.tensor(pairs_host, torch.float64)
+    ut = eng.tensor(ut_host, torch.float64)
+    P = Q * D
+    outs = eng.outputs(P, W)
+    best_f = eng.empty((Q,), torch.int32)
+    best_l = eng.empty((Q,), torch.int32)
+    o = outs[0]
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
+        if ev is not None:
+            ev[1].record()
+        eng.argmin(o["cost"], D, True, out=best_f)
+        eng.argmin(o["length"], D, False, out=best_l)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.torch_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_paths = P * world * args.steps
+    value = total_paths / elapsed
+    # algorithmic bytes per launch of the dominant kernel
+    gather_b = 16 * W if raster_mode else 0
+    pair_b = 32.0 / D
+    out_b = 6 * 8 + 2 * 4
+    bytes_per_path = gather_b + pair_b + out_b
+    launch_bytes = bytes_per_path * P
+    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            key = f"{args.workload}:{args.mode}:R{R}:Q{Q}"
+            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "candidate-paths/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (DEM seed 1 with the Nagasaki DEM's statistics, pairs seed 0, "
+                "NFZ polygons seed 2; canonical map geometry from the reference data files)",
+        "config": {"workload": f"{args.workload}: {cfg['name']}",
+                   "dem": f"{R}x{R}", "pairs_per_gpu": Q, "displacements": D,
+                   "waypoints_per_path": W, "paths_per_gpu": P, "mode": args.mode,
+                   "no_fly_shapes": geom.n_obstacles, "region_shapes":
+                   int(geom.region_first[-1] - geom.region_first[0]),
+                   "parallelism": f"pair-sharded dp{world}, raster broadcast once"},
+        "waypoint_evals_per_s": round(value * W, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "k_eval_generated<raster>" if raster_mode
+                     else "k_eval_generated<analytic>",
+                     "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_path": bytes_per_path,
+                     "algorithmic_bytes_per_launch": launch_bytes},
+        "setup": setup,
+    }
+
+    # ---- CPU baseline + parity sample (rank 0, N=1 only) ----------------------------------
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        O.build()
+        orc = O.Oracle(O.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                       spec["maxalpha"], spec["enlargement"], spec["weights"],
+                       altitude=params.altitude)
+        rd = rec = None
+        if raster_mode:
+            rd = O.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                      geo.nodata, geo.dem_threshold)
+            rec = raster.rec.cpu().numpy().view(np.float32)
+        gpu_cost = o["cost"].cpu().numpy()
+        chunk = 2000 if raster_mode else 50
+        done, t_cpu, mism = 0, 0.0, 0
+        while done < Q and t_cpu < args.cpu_seconds:
+            sl = pairs_host[done:done + chunk]
+            ts = time.perf_counter()
+            wp = O.gen_paths(sl, ut_host)
+            r = orc.eval_paths(wp, mode="raster" if raster_mode else "analytic", rdesc=rd,
+                               rec=rec)
+            t_cpu += time.perf_counter() - ts
+            mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
+            done += len(sl)
+        result["cpu_baseline"] = {
+            "value": round(done * D / t_cpu, 1), "unit": "candidate-paths/s", "cores": 1,
+            "kind": "port",
+            "sample": f"first {done} of {Q} pairs x {D} displacements ({done * D} paths, "
+                      f"{t_cpu:.1f} s) through oracle/uam_oracle.c (gcc -O2, 1 thread): "
+                      "arc generation + raster gather + cost reduction"}
+        result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
+                            "rule": "bit-exact float64 vs CPU oracle"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

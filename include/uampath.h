@@ -1,0 +1,196 @@
+/*
+ * uampath.h -- C ABI of libuampath.so, the MI355X (gfx950) batched candidate-path cost
+ * evaluator for the uam_path_planning hot path.
+ *
+ * The reference (nomaporon/uam_path_planning) has no FFI: its boundary is the Python class
+ * surface of geo_simulation_project/path_generation.  Each entry point below replaces one
+ * reference call (file:line relative to /root/reference/geo_simulation_project/); the Python
+ * package uam_path_planning_amd keeps those class names and binds these symbols with ctypes
+ * (INTEGRATION.md shows the binding a maintainer would add).
+ *
+ *   uam_set_geometry     RegionMap.add_obstacles / new_region / add_shape(s)_to_region
+ *                        (path_generation/region_map.py:14-56) + polygon()/ball()/square()
+ *                        inequalities (polygon.py:7-143, ball.py:7-52, square.py:6-65)
+ *   uam_set_params       Problem.params / set_weight / options (problem.py:12-34) and the
+ *                        OpEn parameter vector p = [xs, xg, maxratio, maxalpha, e, w...]
+ *                        (solver.py:60-78)
+ *   uam_eval_points      Problem.get_total_penalty_function / get_penalty_function(region|None)
+ *                        (problem.py:49-82), QuadraticObstacle.contains / Map.collides
+ *                        (quadratic_obstacle.py:89-94, map.py:41-43)
+ *   uam_eval_waypoints   Problem.get_cost (problem.py:38-44) + get_nonlincon (84-114) +
+ *                        length_of (130-146), batched over paths
+ *   uam_eval_generated   Main.run candidate loop (main.py:158-193) with Solver.create_x_init
+ *                        (solver.py:103-136) fused on device
+ *   uam_gen_paths        Solver.create_x_init (solver.py:103-136), batched
+ *   uam_argmin           main.py:175-180 best-candidate selection
+ *   uam_path_length      Problem.length_of (problem.py:130-146) for arbitrary point counts
+ *   uam_raster_build     map_generation DataManager.load_dem_polygons_from_geotiff mask
+ *                        (map_generation/data_manager.py:11-17) + the region / no-fly
+ *                        penalty at every cell centre: the per-cell cost record the raster
+ *                        mode gathers
+ *   uam_dem_mosaic       the VRT tile mosaic (data/raw/nagasaki_geotiff/mergeLL.vrt:1-10)
+ *
+ * Conventions: all array pointers marked _dev are device pointers (hipMalloc'd or torch
+ * CUDA tensors); the caller owns every buffer; the library never frees caller memory.
+ * Streams are hipStream_t passed as void* (NULL = default stream).  Calls are asynchronous
+ * on that stream except uam_set_geometry.  Every function returns UAM_OK (0) or a negative
+ * status; uam_last_error() returns a thread-local message for the last failure.
+ */
+#ifndef UAMPATH_H
+#define UAMPATH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UAM_ABI_VERSION 1
+#define UAM_MAX_REGIONS 16
+#define UAM_RECORD_BYTES 16
+
+enum {
+    UAM_OK = 0,
+    UAM_E_INVALID = -1, /* bad argument: the reference raises ValueError/AssertionError */
+    UAM_E_HIP = -2,     /* HIP runtime failure */
+    UAM_E_NOMEM = -3,
+    UAM_E_STATE = -4,   /* call order: e.g. eval before set_geometry / set_params */
+    UAM_E_VERSION = -5  /* abi_version field does not match UAM_ABI_VERSION */
+};
+
+/* inequality kinds h(x) <= 0 (parameters p[0..5]) */
+enum {
+    UAM_INEQ_HALFPLANE = 0, /* polygon edge a->b: h = s*((by-ay)*(x0-ax) - (bx-ax)*(x1-ay));
+                               p = {ax, ay, bx-ax, by-ay, s = -sgn, 0} (polygon.py:69-71,98) */
+    UAM_INEQ_ELLIPSE = 1,   /* h = ((x0-c0)/r1)^2 + ((x1-c1)/r2)^2 - 1; p = {c0,c1,r1,r2,0,0} */
+    UAM_INEQ_AXIS = 2       /* square side h = s*(x_k - c) - r; p = {k, c, r, s, 0, 0} */
+};
+
+enum { UAM_MODE_ANALYTIC = 0, UAM_MODE_RASTER = 1 };
+
+/* record flag bits (record = {float phi, float psi_nfz, float dem, uint32 flags}) */
+enum { UAM_FLAG_NFZ = 1u, UAM_FLAG_MASK = 2u, UAM_FLAG_NODATA = 4u };
+
+typedef struct uam_ctx uam_ctx;
+typedef void* uam_stream; /* hipStream_t */
+
+/* Host-side flat geometry.  Shapes: no-fly obstacles [0, n_obstacles) in add order, then
+ * region shapes region-major; region r owns shapes [region_first[r], region_first[r+1]). */
+typedef struct {
+    uint32_t abi_version;
+    int32_t n_ineq;
+    const int32_t* ineq_kind;    /* [n_ineq] */
+    const double* ineq_par;      /* [n_ineq][6] */
+    int32_t n_shapes;
+    const int32_t* shape_first;  /* [n_shapes] first inequality */
+    const int32_t* shape_count;  /* [n_shapes] number of inequalities (>= 1) */
+    const double* shape_center;  /* [n_shapes][2]; NaN => penalty not normalised */
+    int32_t n_obstacles;
+    int32_t n_regions;           /* <= UAM_MAX_REGIONS */
+    const int32_t* region_first; /* [n_regions + 1] */
+} uam_geometry;
+
+/* Problem options + OpEn parameter vector. */
+typedef struct {
+    uint32_t abi_version;
+    int32_t N;               /* interior waypoints; a path has W = N + 2 points */
+    int32_t length_smooth;   /* problem.py:13-16 */
+    int32_t penalty_smooth;
+    int32_t obstacle_smooth;
+    int32_t maxratio_smooth;
+    int32_t quirk_length;    /* 1 = reference get_cost length term: y = [anchor, p_0..p_{N+1}],
+                                first N+1 segments (drops p_N->p_{N+1}); 0 = all segments */
+    int32_t anchor_mode;     /* 0: anchor = each path's p_0 (segment is 0); 1: anchor_x/y
+                                (the map.x_start baked into a reference solver build) */
+    double anchor_x, anchor_y;
+    double maxratio, maxalpha, enlargement;
+    double altitude;         /* cruise altitude for min-clearance (raster mode), metres */
+    double weights[UAM_MAX_REGIONS];
+} uam_params;
+
+/* Raster geotransform (GeoTIFF convention: row 0 is the northern edge).
+ * cell (ix, iy) covers x in [x0 + ix*dx, x0 + (ix+1)*dx), y in (y_top - (iy+1)*dy, y_top - iy*dy];
+ * a point maps to ix = floor((x - x0) * (1/dx)), iy = floor((y_top - y) * (1/dy)) in float64. */
+typedef struct {
+    int32_t nx, ny;
+    double x0, y_top, dx, dy;
+    float nodata;          /* DEM nodata value (-9999 in the reference DEM) */
+    float dem_threshold;   /* data_manager.py:11-17 mask: (dem == -9999) if thr == -9999 else
+                              (dem > thr) */
+} uam_raster_desc;
+
+/* Per-path outputs (device pointers, any may be NULL).  Index p of a path. */
+typedef struct {
+    double* cost;          /* get_cost (problem.py:38-44) */
+    double* length_q;      /* the length term inside get_cost (quirk per params) */
+    double* length;        /* true polyline length, non-smooth (solver.py:49) */
+    double* kin_sum;       /* sum of the 3N kinematic g rows (problem.py:100-107) */
+    double* nfz_sum;       /* sum of the no-fly g rows (problem.py:109-112) */
+    int32_t* nfz_hits;     /* waypoints inside a no-fly zone (Map.collides) */
+    double* min_clearance; /* raster: altitude - max terrain over the waypoints; analytic NaN */
+    int32_t* offmap;       /* raster: waypoints outside the raster */
+    int32_t* cells;        /* [P][W] raster cell index iy*nx+ix, -1 off-raster (raster only) */
+    double* g_rows;        /* [P][3N + n_obstacles*W] full get_nonlincon vector (analytic) */
+} uam_path_outputs;
+
+int uam_abi_version(void);
+const char* uam_last_error(void);
+int uam_device_count(int* n);
+
+int uam_ctx_create(int device, uam_ctx** out);
+void uam_ctx_destroy(uam_ctx* ctx);
+
+/* Copies the geometry to the device (synchronous). */
+int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom);
+/* Stores params and computes per-shape normalisers psi(centre) on the device. */
+int uam_set_params(uam_ctx* ctx, const uam_params* params, uam_stream stream);
+
+/* Per point (pts_dev [n][2] f64): phi = total penalty, phi_regions [n][n_regions] weighted
+ * region penalties, obs_norm = get_penalty_function(None), psi_raw = sum of raw obstacle psi
+ * (constraint semantics), collide = Map.collides. */
+int uam_eval_points(uam_ctx* ctx, const double* pts_dev, int64_t n, double* phi_dev,
+                    double* phi_regions_dev, double* obs_norm_dev, double* psi_raw_dev,
+                    int32_t* collide_dev, uam_stream stream);
+
+/* K1: one 16-byte record per cell, row-major.  dem_dev [ny][nx] f32 (NULL = all zero). */
+int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem_dev,
+                     void* rec_dev, uam_stream stream);
+
+/* VRT mosaic: n_tiles tiles of th x tw f32 (tiles_dev [n_tiles][th][tw]) placed at
+ * (xoff[t], yoff[t]) (DstRect) into dem_dev [ny][nx]; cells no tile covers keep their value. */
+int uam_dem_mosaic(uam_ctx* ctx, const float* tiles_dev, int32_t n_tiles, int32_t th,
+                   int32_t tw, const int32_t* xoff_dev, const int32_t* yoff_dev, float* dem_dev,
+                   int32_t nx, int32_t ny, uam_stream stream);
+
+/* K4: pairs_dev [Q][4] (x0,y0,xf,yf), utab_dev [D][N][2] unit-arc table -> wp [Q*D][N+2][2]. */
+int uam_gen_paths(uam_ctx* ctx, const double* pairs_dev, int64_t n_pairs,
+                  const double* utab_dev, int32_t D, double* wp_dev, uam_stream stream);
+
+/* K2 (raster) / K3 (analytic) over explicit waypoints wp_dev [P][N+2][2]. */
+int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                       const void* rec_dev, const double* wp_dev, int64_t n_paths,
+                       const uam_path_outputs* out, uam_stream stream);
+
+/* K2/K3 with the candidate generator fused: path p = q*D + d. */
+int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                       const void* rec_dev, const double* pairs_dev, int64_t n_pairs,
+                       const double* utab_dev, int32_t D, const uam_path_outputs* out,
+                       uam_stream stream);
+
+/* K5: per group of G consecutive values, the reference's selection rule (main.py:175-180):
+ * compare sqrt(v) when take_sqrt (fval = sqrt(cost), solver.py:48), else v. */
+int uam_argmin(uam_ctx* ctx, const double* values_dev, int64_t groups, int32_t G,
+               int32_t take_sqrt, int32_t* best_dev, uam_stream stream);
+
+/* length_of: pts_dev [n_paths][n_points][2]; sum of the first n_segments segment norms
+ * (squared-after-sqrt when smooth). */
+int uam_path_length(uam_ctx* ctx, const double* pts_dev, int64_t n_paths, int32_t n_points,
+                    int32_t n_segments, int32_t smooth, double* out_dev, uam_stream stream);
+
+int uam_synchronize(uam_ctx* ctx, uam_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UAMPATH_H */

@@ -1,0 +1,316 @@
+"""GPU parity: every kernel of libuampath against the CPU oracle (bit-exact: the kernels and
+the oracle both compute in float64 with the reference's operation order and no FMA
+contraction), and -- through the oracle -- against the reference's golden vectors.
+Tolerances written here: exact equality for indices, counts, argmin and for every float64
+output (the north_star bar is 1e-5 relative; we hold 0).  Raster-mode float32 record values
+are compared exactly too (identical f64 -> f32 rounding)."""
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from uam_path_planning_amd import build
+    from uam_path_planning_amd.engine import Engine
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    build.build_library()
+    return Engine(0)
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+def _setup(eng, oracle_mod, spec, N, options, maxratio, maxalpha, enl, weights, anchor=None,
+           altitude=150.0):
+    from uam_path_planning_amd.engine import PathParams
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import build_region_map
+
+    opts = {"length_smooth": False, "penalty_smooth": True, "obstacle_smooth": False,
+            "maxratio_smooth": False}
+    if options:
+        opts.update(options)
+    eng.set_geometry(compile_map(build_region_map(spec)))
+    eng.set_params(PathParams(N=N, **opts, maxratio=maxratio, maxalpha=maxalpha,
+                              enlargement=enl, weights=tuple(weights), anchor=anchor,
+                              altitude=altitude))
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, opts, maxratio, maxalpha, enl,
+                            weights, anchor=anchor, altitude=altitude)
+    return orc
+
+
+PATH_KEYS = (("cost", "cost"), ("length_q", "lq"), ("length", "length"), ("kin_sum", "kin"),
+             ("nfz_sum", "nfz"), ("nfz_hits", "nfz_hits"), ("offmap", "offmap"))
+
+
+def _assert_paths_equal(gpu, ref, raster=False):
+    for gk, ok in PATH_KEYS:
+        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+    if raster:
+        np.testing.assert_array_equal(_np(gpu["min_clearance"]), ref["min_clearance"])
+    else:
+        assert np.isnan(_np(gpu["min_clearance"])).all()
+
+
+# ---- analytic mode (K3) vs oracle vs reference goldens ------------------------------------
+def test_canonical_analytic(eng, oracle_mod):
+    meta, arr = G.canonical()
+    xs = tuple(meta["map"]["x_start"])
+    orc = _setup(eng, oracle_mod, meta["map"], meta["N"], meta["options"], meta["maxratio"],
+                 meta["maxalpha"], meta["enlargement"], meta["weights"], anchor=xs)
+    wp = G.canonical_paths(meta, arr)
+    gpu = eng.eval_waypoints(wp, want_g=True)
+    ref = orc.eval_paths(wp, want_g=True)
+    _assert_paths_equal(gpu, ref)
+    np.testing.assert_array_equal(_np(gpu["g_rows"]), ref["g"])
+    # and therefore the reference itself, bit for bit
+    np.testing.assert_array_equal(_np(gpu["cost"]), arr["cost"])
+    np.testing.assert_array_equal(_np(gpu["g_rows"]), arr["g"])
+    np.testing.assert_array_equal(_np(gpu["length"]), arr["length"])
+    pe = eng.eval_points(wp.reshape(-1, 2))
+    np.testing.assert_array_equal(_np(pe["phi"]), arr["phi"].reshape(-1))
+    np.testing.assert_array_equal(_np(pe["phi_regions"]),
+                                  arr["phi_r"].transpose(0, 2, 1).reshape(-1, 3))
+    np.testing.assert_array_equal(_np(pe["obs_norm"]), arr["obs_norm"].reshape(-1))
+    np.testing.assert_array_equal(_np(pe["collide"]), arr["collide"].reshape(-1))
+
+
+@pytest.mark.parametrize("ci", range(24))
+def test_random_cases_analytic(eng, oracle_mod, ci):
+    c = G.random_cases()[ci]
+    orc = _setup(eng, oracle_mod, c["map"], c["N"], c["options"], c["maxratio"],
+                 c["maxalpha"], c["enlargement"], c["weights"], anchor=tuple(c["map"]["x_start"]))
+    wp = np.asarray(c["paths"]).reshape(len(c["paths"]), -1, 2)
+    gpu = eng.eval_waypoints(wp, want_g=True)
+    ref = orc.eval_paths(wp, want_g=True)
+    for gk, ok in PATH_KEYS:
+        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+    np.testing.assert_array_equal(_np(gpu["g_rows"]), ref["g"])
+    for i, o in enumerate(c["outputs"]):   # reference goldens (NaN where the reference is)
+        np.testing.assert_allclose(_np(gpu["cost"])[i], o["cost"], rtol=1e-13, equal_nan=True)
+    pts = wp.reshape(-1, 2)
+    pe = eng.eval_points(pts)
+    pr = orc.eval_points(pts)
+    for k in ("phi", "phi_regions", "obs_norm", "psi_raw", "collide"):
+        np.testing.assert_array_equal(_np(pe[k]), pr[k], err_msg=k)
+
+
+def test_generated_analytic_and_argmin(eng, oracle_mod):
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    meta, arr = G.canonical()
+    orc = _setup(eng, oracle_mod, meta["map"], meta["N"], meta["options"], meta["maxratio"],
+                 meta["maxalpha"], meta["enlargement"], meta["weights"])
+    ds = meta["displacements"]
+    ut = arc_table(meta["N"], ds)
+    pairs = np.concatenate([np.array([[*meta["map"]["x_start"], *meta["map"]["x_goal"]]]),
+                            random_pairs(130, seed=5)])
+    gpu = eng.eval_generated(pairs, ut)
+    wp = oracle_mod.gen_paths(pairs, ut)
+    np.testing.assert_array_equal(_np(eng.gen_paths(pairs, ut)), wp)
+    ref = orc.eval_paths(wp)
+    _assert_paths_equal(gpu, ref)
+    # reference candidate costs (create_x_init arcs differ from the table by <= 1e-14)
+    np.testing.assert_allclose(_np(gpu["cost"])[:5], arr["cost"], rtol=1e-12)
+    bf = _np(eng.argmin(gpu["cost"], len(ds), True))
+    bl = _np(eng.argmin(gpu["length"], len(ds), False))
+    np.testing.assert_array_equal(bf, oracle_mod.argmin(ref["cost"], len(ds), True))
+    np.testing.assert_array_equal(bl, oracle_mod.argmin(ref["length"], len(ds), False))
+    assert bf[0] == 3
+
+
+def test_argmin_semantics_gpu(eng):
+    v = np.array([3.0, 1.0, 1.0, 2.0, np.nan, 5.0, 4.0, 4.0, 2.0, 0.0, 7.0, 9.0])
+    assert _np(eng.argmin(v, 4, False)).tolist() == [1, 0, 2]
+
+
+# ---- raster build (K1) --------------------------------------------------------------------
+def test_raster_build_cell_centres_golden(eng, oracle_mod):
+    from uam_path_planning_amd.engine import RasterGeo
+
+    meta, _ = G.canonical()
+    gr = G.grid()
+    nx, ny, X0, Ytop, dx, dy = gr["geo"]
+    geo = RasterGeo(int(nx), int(ny), X0, Ytop, dx, dy)
+    for tag, opts, enl in (("a", {"penalty_smooth": True, "obstacle_smooth": True}, 0.0),
+                           ("b", {"penalty_smooth": False, "obstacle_smooth": False}, 0.25)):
+        _setup(eng, oracle_mod, meta["map"], 4, opts, 1.1, 0.3, enl, [200, 15000, 27000])
+        rec = _np(eng.raster_build(geo).rec)
+        np.testing.assert_array_equal(rec[..., 0].view(np.float32),
+                                      gr[f"phi_{tag}"].astype(np.float32))
+        np.testing.assert_array_equal(rec[..., 1].view(np.float32),
+                                      gr[f"psi_{tag}"].astype(np.float32))
+        np.testing.assert_array_equal(rec[..., 3] & 1, gr[f"collide_{tag}"])
+
+
+@pytest.mark.parametrize("thr", [0.0, 100.0, -9999.0])
+def test_raster_build_vs_oracle(eng, oracle_mod, thr):
+    from uam_path_planning_amd.scenario import canonical_spec, raster_geo
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=8)
+    orc = _setup(eng, oracle_mod, spec, 80, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"])
+    geo = raster_geo(256, dem_threshold=thr)
+    dem = synthetic_dem(256)
+    rec = _np(eng.raster_build(geo, dem).rec)
+    ref = orc.raster_build(oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top,
+                                                         geo.dx, geo.dy, geo.nodata, thr), dem)
+    np.testing.assert_array_equal(rec, ref.view(np.int32))
+
+
+# ---- raster eval (K2) ---------------------------------------------------------------------
+def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5):
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=nfz)
+    orc = _setup(eng, oracle_mod, spec, N, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"], altitude=320.0)
+    geo = raster_geo(R)
+    dem = synthetic_dem(R)
+    raster = eng.raster_build(geo, dem)
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                       geo.nodata, geo.dem_threshold)
+    rec = _np(raster.rec).view(np.float32)
+    pairs = random_pairs(Q, seed=seed)
+    ut = arc_table(N, displacements(D))
+    return orc, raster, rd, rec, pairs, ut
+
+
+@pytest.mark.parametrize("R,Q,N", [(256, 300, 80), (2048, 200, 254), (512, 64, 1)])
+def test_raster_eval_generated_vs_oracle(eng, oracle_mod, R, Q, N):
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, R, Q, N, nfz=4)
+    gpu = eng.eval_generated(pairs, ut, raster=raster, want_cells=True)
+    wp = oracle_mod.gen_paths(pairs, ut)
+    ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, want_cells=True)
+    _assert_paths_equal(gpu, ref, raster=True)
+    np.testing.assert_array_equal(_np(gpu["cells"]), ref["cells"])
+    # explicit-waypoint kernel on the same paths gives the same bits
+    gpu2 = eng.eval_waypoints(wp, raster=raster, want_cells=True)
+    _assert_paths_equal(gpu2, ref, raster=True)
+    np.testing.assert_array_equal(_np(gpu2["cells"]), ref["cells"])
+
+
+def test_raster_matches_reference_at_snapped_centres(eng, oracle_mod):
+    """Raster-mode cost == analytic cost of the path snapped to its cells' centres, up to the
+    f32 rounding of the stored record (|rel| <= 1e-6 <= the 1e-5 bar)."""
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 40, 80, nfz=0)
+    gpu = eng.eval_generated(pairs, ut, raster=raster, want_cells=True)
+    cells = _np(gpu["cells"])
+    geo = raster.geo
+    ix, iy = cells % geo.nx, cells // geo.nx
+    snapped = np.stack([geo.x0 + (ix + 0.5) * geo.dx, geo.y_top - (iy + 0.5) * geo.dy], -1)
+    ok = (cells >= 0).all(1)
+    # the length terms use the true waypoints; only the penalty is read at the cell centre
+    pen_gpu = _np(gpu["cost"]) - (orc.N + 1) * _np(gpu["length_q"])
+    pts = snapped.reshape(-1, 2)
+    phi = orc.eval_points(pts)["phi"].reshape(cells.shape)
+    pen_ref = (phi / orc.N).sum(1)
+    np.testing.assert_allclose(pen_gpu[ok], pen_ref[ok], rtol=1e-5, atol=1e-9)
+    assert ok.sum() > 50
+
+
+def test_offmap_and_empty(eng, oracle_mod):
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 128, 8, 20, nfz=0)
+    far = pairs.copy()
+    far[:, 0] += 100.0           # starts far off the raster
+    gpu = eng.eval_generated(far, ut, raster=raster, want_cells=True)
+    ref = orc.eval_paths(oracle_mod.gen_paths(far, ut), mode="raster", rdesc=rd, rec=rec,
+                         want_cells=True)
+    _assert_paths_equal(gpu, ref, raster=True)
+    assert (_np(gpu["offmap"]) > 0).all()
+    empty = eng.eval_generated(np.zeros((0, 4)), ut, raster=raster)
+    assert empty["cost"].numel() == 0
+    e2 = eng.eval_waypoints(np.zeros((0, 22, 2)), raster=raster)
+    assert e2["cost"].numel() == 0
+
+
+def test_dem_mosaic(eng):
+    rng = np.random.default_rng(3)
+    tiles = rng.standard_normal((6, 9, 15)).astype(np.float32)
+    xoff = np.array([0, 15, 30, 0, 15, 30], np.int32)
+    yoff = np.array([0, 0, 0, 9, 9, 9], np.int32)
+    dem = _np(eng.dem_mosaic(tiles, xoff, yoff, 40, 20))
+    ref = np.full((20, 40), -9999.0, np.float32)
+    for t in range(6):
+        ys, xs = yoff[t], xoff[t]
+        h, w = min(9, 20 - ys), min(15, 40 - xs)
+        ref[ys:ys + h, xs:xs + w] = tiles[t, :h, :w]
+    np.testing.assert_array_equal(dem, ref)
+
+
+def test_full_size_cfg3_properties(eng, oracle_mod):
+    """BASELINE config 3 at full size (4096^2 DEM + 69 no-fly shapes, 100k pairs x 5):
+    oracle on a 2k-pair subsample (bit-exact), size-independent properties on the rest."""
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 4096, 100_000, 80, nfz=64)
+    gpu = eng.eval_generated(pairs, ut, raster=raster)
+    sub = np.random.default_rng(7).choice(len(pairs), 2000, replace=False)
+    sub.sort()
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs[sub], ut), mode="raster", rdesc=rd, rec=rec)
+    idx = (sub[:, None] * 5 + np.arange(5)).reshape(-1)
+    for gk, ok in PATH_KEYS:
+        np.testing.assert_array_equal(_np(gpu[gk])[idx], ref[ok], err_msg=gk)
+    cost, lq = _np(gpu["cost"]), _np(gpu["length_q"])
+    assert np.isfinite(cost).all()
+    assert (cost >= 81 * lq - 1e-9).all()                 # penalties are non-negative
+    # permutation: shuffling pairs permutes outputs bit-for-bit (no cross-path coupling)
+    perm = np.random.default_rng(9).permutation(len(pairs))
+    gp = eng.eval_generated(pairs[perm], ut, raster=raster)
+    pidx = (perm[:, None] * 5 + np.arange(5)).reshape(-1)
+    np.testing.assert_array_equal(_np(gp["cost"]), cost[pidx])
+    # determinism: a second launch is bit-identical
+    g2 = eng.eval_generated(pairs, ut, raster=raster)
+    np.testing.assert_array_equal(_np(g2["cost"]), cost)
+    # argmin over the full batch vs the oracle's rule on the GPU costs
+    bf = _np(eng.argmin(gpu["cost"], 5, True))
+    np.testing.assert_array_equal(bf, oracle_mod.argmin(cost, 5, True))
+
+
+# ---- drop-in API --------------------------------------------------------------------------
+def test_dropin_problem_and_solver(eng):
+    from uam_path_planning_amd.path_generation import Solver
+    from uam_path_planning_amd.scenario import canonical_problem
+
+    meta, arr = G.canonical()
+    prob = canonical_problem()
+    wp = G.canonical_paths(meta, arr)
+    for i in range(5):
+        z = wp[i].reshape(-1)
+        assert prob.get_cost(z) == arr["cost"][i]
+        np.testing.assert_array_equal(prob.get_nonlincon(z), arr["g"][i])
+        assert prob.length_of(arr["x_init"][i]) == arr["length"][i]
+        assert prob.length_of(z, prob.options["length_smooth"]) == arr["lq"][i]
+    tp = prob.get_total_penalty_function()
+    assert tp(wp[2, 10]) == arr["phi"][2, 10]
+    pl = prob.get_penalty_function("Population")
+    assert pl(wp[2, 10]) == arr["phi_r"][2, 1, 10]
+    solver = Solver(prob, {})
+    for i, d in enumerate(meta["displacements"]):
+        np.testing.assert_allclose(solver.create_x_init(d), arr["x_init"][i], rtol=0,
+                                   atol=1e-12)
+    res = solver.evaluate_candidates(meta["displacements"])
+    np.testing.assert_allclose(res["cost"], arr["cost"], rtol=1e-12)
+    assert res["min_fval_index"] == 3
+    with pytest.raises(ValueError):
+        solver.create_x_init(1.5)
+    with pytest.raises(NotImplementedError):
+        solver.solve(None, None)
+    # shape primitives on the device
+    m = prob.map
+    assert m.collides(np.array([38.66652661075855, -9.203164091309498]))
+    assert not m[(0.0, 0.0)]
+    obs = m.obstacles[0]
+    assert obs.contains([38.7, -9.2])
+    assert obs.penalty_function(True, 0)([38.66652661075855, -9.203164091309498]) == 1.0

@@ -1,0 +1,123 @@
+"""ctypes binding of libuampath.so (include/uampath.h).
+
+The library is built in-tree (uam_path_planning_amd/lib/libuampath.so) by
+``uam_path_planning_amd.build.build_library()`` / ``__graft_entry__.build()``.  There is no
+CPU fallback: if the library is missing or no GPU is visible, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libuampath.so")
+
+ABI_VERSION = 1
+MAX_REGIONS = 16
+RECORD_BYTES = 16
+
+UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
+INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
+MODE_ANALYTIC, MODE_RASTER = 0, 1
+FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+
+
+class Geometry(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("n_ineq", ctypes.c_int32),
+                ("ineq_kind", _i32p), ("ineq_par", _f64p), ("n_shapes", ctypes.c_int32),
+                ("shape_first", _i32p), ("shape_count", _i32p), ("shape_center", _f64p),
+                ("n_obstacles", ctypes.c_int32), ("n_regions", ctypes.c_int32),
+                ("region_first", _i32p)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("N", ctypes.c_int32),
+                ("length_smooth", ctypes.c_int32), ("penalty_smooth", ctypes.c_int32),
+                ("obstacle_smooth", ctypes.c_int32), ("maxratio_smooth", ctypes.c_int32),
+                ("quirk_length", ctypes.c_int32), ("anchor_mode", ctypes.c_int32),
+                ("anchor_x", ctypes.c_double), ("anchor_y", ctypes.c_double),
+                ("maxratio", ctypes.c_double), ("maxalpha", ctypes.c_double),
+                ("enlargement", ctypes.c_double), ("altitude", ctypes.c_double),
+                ("weights", ctypes.c_double * MAX_REGIONS)]
+
+
+class RasterDesc(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("x0", ctypes.c_double),
+                ("y_top", ctypes.c_double), ("dx", ctypes.c_double), ("dy", ctypes.c_double),
+                ("nodata", ctypes.c_float), ("dem_threshold", ctypes.c_float)]
+
+
+class PathOutputs(ctypes.Structure):
+    _fields_ = [(name, _vp) for name in ("cost", "length_q", "length", "kin_sum", "nfz_sum",
+                                         "nfz_hits", "min_clearance", "offmap", "cells",
+                                         "g_rows")]
+
+
+# name -> (restype, argtypes); the full exported surface of include/uampath.h
+SIGNATURES = {
+    "uam_abi_version": (ctypes.c_int, []),
+    "uam_last_error": (ctypes.c_char_p, []),
+    "uam_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "uam_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "uam_ctx_destroy": (None, [_vp]),
+    "uam_set_geometry": (ctypes.c_int, [_vp, ctypes.POINTER(Geometry)]),
+    "uam_set_params": (ctypes.c_int, [_vp, ctypes.POINTER(Params), _vp]),
+    "uam_eval_points": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "uam_raster_build": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp, _vp]),
+    "uam_dem_mosaic": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      _vp, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _vp]),
+    "uam_gen_paths": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int32, _vp, _vp]),
+    "uam_eval_waypoints": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(RasterDesc), _vp,
+                                          _vp, ctypes.c_int64, ctypes.POINTER(PathOutputs), _vp]),
+    "uam_eval_generated": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(RasterDesc), _vp,
+                                          _vp, ctypes.c_int64, _vp, ctypes.c_int32,
+                                          ctypes.POINTER(PathOutputs), _vp]),
+    "uam_argmin": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp,
+                                  _vp]),
+    "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, _vp, _vp]),
+    "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
+}
+
+_lib = None
+
+
+class UamError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libuampath.so (no fallback: raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.uam_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libuampath ABI {lib.uam_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def last_error():
+    msg = load().uam_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(status, what=""):
+    if status == UAM_OK:
+        return
+    msg = last_error()
+    text = f"{what}: {msg}" if what else msg
+    if status == UAM_E_INVALID:
+        raise ValueError(text)
+    raise UamError(f"[status {status}] {text}")

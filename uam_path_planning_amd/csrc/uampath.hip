@@ -1,0 +1,928 @@
+// uampath.hip -- MI355X (gfx950) kernels + C ABI for batched candidate-path cost evaluation.
+//
+// Kernels (SURVEY.md §2 native inventory):
+//   k_prepare        per-shape normaliser psi(centre) (problem.py:79 recomputes it per call)
+//   k_eval_points    Φ / per-region / obstacle penalties + collides at arbitrary points
+//   k_raster_build   K1: one 16-B record per DEM cell {Φ, Σψ_nfz, dem, flags}
+//   k_dem_mosaic     VRT tile mosaic into the DEM plane
+//   k_eval_paths     K2 (raster gather) / K3 (analytic) with K4 (arc generator) fused
+//   k_argmin         K5: reference selection rule per candidate group
+//   k_gen_paths, k_path_length  batched create_x_init / length_of
+//
+// Numerics: float64 throughout, compiled with -ffp-contract=off so every product and sum is a
+// separately rounded IEEE operation in the reference's order (problem.py, quadratic_obstacle.py,
+// polygon.py, ball.py, square.py); f64 sqrt and divide lower to gfx950's correctly rounded
+// sequences.  Results are therefore bit-identical to the CPU oracle (oracle/uam_oracle.c).
+//
+// Thread mapping of the path kernels: one lane per path, waypoints walked in order, so the
+// per-path sums keep the reference's sequential order with no cross-lane reduction.  In the
+// fused-generator kernel each wave owns ONE displacement d (wave-uniform) and 64 start/goal
+// pairs, so the unit-arc table row u[d][*] is read with scalar (SMEM) loads and the geometry
+// tables are read with wave-uniform addresses (scalar cache) in the analytic mode.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/uampath.h"
+
+namespace {
+
+// ----------------------------------------------------------------------------------------
+// device-side tables
+
+struct alignas(16) DevIneq {  // 64 B: one s_load_dwordx16
+    double p[6];
+    int32_t kind;
+    int32_t pad0;
+    double pad1;
+};
+
+struct alignas(16) DevShape {  // 48 B
+    int32_t first, count, has_center, pad;
+    double norm_pen;  // psi(centre; penalty_smooth, e)
+    double norm_obs;  // psi(centre; obstacle_smooth, e)
+    double cx, cy;
+};
+
+struct KGeom {
+    const DevIneq* __restrict__ ineq;
+    const DevShape* __restrict__ shape;
+    int32_t n_obstacles;
+    int32_t n_regions;
+    int32_t region_first[UAM_MAX_REGIONS + 1];
+};
+
+struct KParams {
+    int32_t N;
+    int32_t length_smooth, penalty_smooth, obstacle_smooth, maxratio_smooth;
+    int32_t quirk_length, anchor_mode, pad;
+    double anchor_x, anchor_y;
+    double r_eff;      // maxratio, or maxratio**2 when maxratio_smooth (problem.py:95-96)
+    double mincos;     // cos(maxalpha), computed on the host with libm (problem.py:98)
+    double enlargement;
+    double altitude;
+    double weights[UAM_MAX_REGIONS];
+};
+
+struct KRaster {
+    int32_t nx, ny;
+    double x0, y_top, dx, dy, inv_dx, inv_dy;
+};
+
+struct KOut {
+    double* cost;
+    double* length_q;
+    double* length;
+    double* kin_sum;
+    double* nfz_sum;
+    int32_t* nfz_hits;
+    double* min_clearance;
+    int32_t* offmap;
+    int32_t* cells;
+    double* g_rows;
+};
+
+// ----------------------------------------------------------------------------------------
+// reference formulas (device)
+
+__device__ __forceinline__ double ineq_h(const DevIneq* __restrict__ q, double x0, double x1) {
+    const int kind = q->kind;
+    if (kind == UAM_INEQ_HALFPLANE) {
+        // polygon.py:69-71 line_F, h = -sgn * line (polygon.py:98)
+        double line = q->p[3] * (x0 - q->p[0]) - q->p[2] * (x1 - q->p[1]);
+        return q->p[4] * line;
+    } else if (kind == UAM_INEQ_ELLIPSE) {
+        // ball.py func: sumsqr(vertcat((x0-c0)/r1, (x1-c1)/r2)) - 1, sumsqr accumulates from 0
+        double a = (x0 - q->p[0]) / q->p[2];
+        double b = (x1 - q->p[1]) / q->p[3];
+        double s = 0.0;
+        s = s + a * a;
+        s = s + b * b;
+        return s - 1.0;
+    } else {
+        // square.py right/left/top/bottom: s*(x_k - c) - r
+        double xk = (q->p[0] == 0.0) ? x0 : x1;
+        return q->p[3] * (xk - q->p[1]) - q->p[2];
+    }
+}
+
+// quadratic_obstacle.py:27-39
+__device__ __forceinline__ double psi(const KGeom& g, const DevShape& sh, double x0, double x1,
+                                      bool smooth, double e) {
+    double r = 1.0;
+    const int end = sh.first + sh.count;
+    for (int i = sh.first; i < end; ++i) {
+        double h = ineq_h(g.ineq + i, x0, x1);
+        if (smooth) {
+            double m = fmin(h - e, 0.0);
+            r = r * (m * m);
+        } else {
+            r = r * fmin(e - h, 0.0);
+        }
+    }
+    return r;
+}
+
+// quadratic_obstacle.py:89-94
+__device__ __forceinline__ bool contains(const KGeom& g, const DevShape& sh, double x0,
+                                         double x1) {
+    const int end = sh.first + sh.count;
+    bool in = true;
+    for (int i = sh.first; i < end; ++i) in = in && !(ineq_h(g.ineq + i, x0, x1) > 1e-14);
+    return in;
+}
+
+// problem.py:72-80 for region r (penalty_smooth, enlargement), weighted (problem.py:80)
+__device__ __forceinline__ double region_penalty(const KGeom& g, const KParams& p, int r,
+                                                 double x0, double x1) {
+    double t = 0.0;
+    const int s1 = g.region_first[r + 1];
+    for (int s = g.region_first[r]; s < s1; ++s) {
+        const DevShape sh = g.shape[s];
+        double v = psi(g, sh, x0, x1, p.penalty_smooth != 0, p.enlargement);
+        t = sh.has_center ? t + v / sh.norm_pen : t + v;
+    }
+    return p.weights[r] * t;
+}
+
+// problem.py:49-56
+__device__ __forceinline__ double total_penalty(const KGeom& g, const KParams& p, double x0,
+                                                double x1) {
+    double pen = 0.0;
+    for (int r = 0; r < g.n_regions; ++r) pen = pen + region_penalty(g, p, r, x0, x1);
+    return pen;
+}
+
+__device__ __forceinline__ bool collides(const KGeom& g, double x0, double x1) {
+    bool hit = false;
+    for (int s = 0; s < g.n_obstacles; ++s) {
+        const DevShape sh = g.shape[s];
+        hit = hit || contains(g, sh, x0, x1);
+    }
+    return hit;
+}
+
+// Σ_o raw psi_o(x; obstacle_smooth, e = 0) -- the per-waypoint sum of the no-fly g rows
+__device__ __forceinline__ double obstacle_psi_sum(const KGeom& g, const KParams& p, double x0,
+                                                   double x1) {
+    double acc = 0.0;
+    for (int s = 0; s < g.n_obstacles; ++s) {
+        const DevShape sh = g.shape[s];
+        acc = acc + psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+    }
+    return acc;
+}
+
+// ----------------------------------------------------------------------------------------
+// kernels
+
+__global__ void k_prepare(KGeom g, KParams p, DevShape* __restrict__ shapes, int n_shapes) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_shapes) return;
+    DevShape sh = shapes[s];
+    sh.has_center = !(isnan(sh.cx) || isnan(sh.cy));
+    sh.norm_pen = psi(g, sh, sh.cx, sh.cy, p.penalty_smooth != 0, p.enlargement);
+    sh.norm_obs = psi(g, sh, sh.cx, sh.cy, p.obstacle_smooth != 0, p.enlargement);
+    shapes[s] = sh;
+}
+
+__global__ __launch_bounds__(256) void k_eval_points(KGeom g, KParams p,
+                                                     const double* __restrict__ pts, int64_t n,
+                                                     double* phi, double* phi_regions,
+                                                     double* obs_norm, double* psi_raw,
+                                                     int32_t* collide) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x0 = pts[2 * i], x1 = pts[2 * i + 1];
+    if (phi) phi[i] = total_penalty(g, p, x0, x1);
+    if (phi_regions)
+        for (int r = 0; r < g.n_regions; ++r)
+            phi_regions[i * g.n_regions + r] = region_penalty(g, p, r, x0, x1);
+    if (obs_norm) {  // get_penalty_function(None): w = 1, obstacle_smooth, enlargement
+        double t = 0.0;
+        for (int s = 0; s < g.n_obstacles; ++s) {
+            const DevShape sh = g.shape[s];
+            double v = psi(g, sh, x0, x1, p.obstacle_smooth != 0, p.enlargement);
+            t = sh.has_center ? t + v / sh.norm_obs : t + v;
+        }
+        obs_norm[i] = 1.0 * t;
+    }
+    if (psi_raw) psi_raw[i] = obstacle_psi_sum(g, p, x0, x1);
+    if (collide) collide[i] = collides(g, x0, x1) ? 1 : 0;
+}
+
+// K1: record per cell.  One lane per cell, rows contiguous -> coalesced DEM reads and
+// 16-B record stores (one global_store_dwordx4 per lane).
+__global__ __launch_bounds__(256) void k_raster_build(KGeom g, KParams p, KRaster rs,
+                                                      const float* __restrict__ dem,
+                                                      float nodata, float thr,
+                                                      uint4* __restrict__ rec) {
+    const int64_t total = (int64_t)rs.nx * rs.ny;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t iy = c / rs.nx, ix = c - iy * rs.nx;
+        const double xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
+        const double yc = rs.y_top - ((double)iy + 0.5) * rs.dy;
+        const float z = dem ? dem[c] : 0.0f;
+        uint32_t fl = 0;
+        if (collides(g, xc, yc)) fl |= UAM_FLAG_NFZ;
+        if (thr == -9999.0f ? (z == -9999.0f) : (z > thr)) fl |= UAM_FLAG_MASK;
+        if (z == nodata) fl |= UAM_FLAG_NODATA;
+        const float phi = (float)total_penalty(g, p, xc, yc);
+        const float ps = (float)obstacle_psi_sum(g, p, xc, yc);
+        rec[c] = make_uint4(__float_as_uint(phi), __float_as_uint(ps), __float_as_uint(z), fl);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dem_mosaic(const float* __restrict__ tiles, int n_tiles,
+                                                    int th, int tw,
+                                                    const int32_t* __restrict__ xoff,
+                                                    const int32_t* __restrict__ yoff,
+                                                    float* __restrict__ dem, int nx, int ny) {
+    const int64_t per = (int64_t)th * tw;
+    const int64_t total = per * n_tiles;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(i / per);
+        const int64_t r = i - t * per;
+        const int y = (int)(r / tw), x = (int)(r - (int64_t)y * tw);
+        const int gx = xoff[t] + x, gy = yoff[t] + y;
+        if (gx >= 0 && gx < nx && gy >= 0 && gy < ny) dem[(int64_t)gy * nx + gx] = tiles[i];
+    }
+}
+
+// candidate point k (1..N) of pair pr: solver.py:121-136 restated as
+// p = C + 0.5*[[vx,-vy],[vy,vx]] u, v = x0 - xf, C = (xf + x0)/2
+__device__ __forceinline__ void arc_point(double x0, double y0, double xf, double yf, double ux,
+                                          double uy, double& px, double& py) {
+    const double vx = x0 - xf, vy = y0 - yf;
+    const double cx = (xf + x0) * 0.5, cy = (yf + y0) * 0.5;
+    px = cx + 0.5 * (vx * ux - vy * uy);
+    py = cy + 0.5 * (vy * ux + vx * uy);
+}
+
+// Source of a path's waypoints: explicit [P][W][2] or generated from (pair, u[d]).
+template <bool GEN>
+struct PathSrc {
+    const double* __restrict__ wp;  // explicit: this path's W points
+    double x0, y0, xf, yf;          // generated: the pair
+    const double* __restrict__ u;   // generated: u[d][0..N-1][2] (wave-uniform address)
+    int W;
+    __device__ __forceinline__ void at(int j, double& px, double& py) const {
+        if (GEN) {
+            if (j == 0) {
+                px = x0;
+                py = y0;
+            } else if (j == W - 1) {
+                px = xf;
+                py = yf;
+            } else {
+                arc_point(x0, y0, xf, yf, u[2 * (j - 1)], u[2 * (j - 1) + 1], px, py);
+            }
+        } else {
+            const double2 v = reinterpret_cast<const double2*>(wp)[j];
+            px = v.x;
+            py = v.y;
+        }
+    }
+};
+
+constexpr int kChunk = 8;  // raster gathers in flight per lane
+
+template <int MODE, bool GEN>
+__device__ __forceinline__ void eval_one_path(const KGeom& g, const KParams& p, const KRaster& rs,
+                                              const uint4* __restrict__ rec,
+                                              const PathSrc<GEN>& src, int64_t path,
+                                              const KOut& out) {
+    const int N = p.N, W = N + 2;
+    const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
+    const int n_rows = 3 * N + g.n_obstacles * W;
+    double* grow = (MODE == UAM_MODE_ANALYTIC && out.g_rows) ? out.g_rows + path * n_rows : nullptr;
+
+    // ---- pass 1: geometry-only terms (length_of, true length, kinematic rows) ----------
+    double px, py;
+    src.at(0, px, py);
+    double L = 0.0;
+    if (p.quirk_length) {
+        const double ax = p.anchor_mode ? p.anchor_x : px;
+        const double ay = p.anchor_mode ? p.anchor_y : py;
+        const double dx = px - ax, dy = py - ay;
+        double s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        const double n = sqrt(s);
+        L = L + (ls ? n * n : n);
+    }
+    double len = 0.0, ksum = 0.0;
+    double pdx = 0.0, pdy = 0.0, pn = 0.0;
+    for (int j = 1; j < W; ++j) {
+        double qx, qy;
+        src.at(j, qx, qy);
+        const double dx = qx - px, dy = qy - py;
+        double s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        const double n = sqrt(s);
+        len = len + n;
+        if (!p.quirk_length || j <= N) L = L + (ls ? n * n : n);
+        const double nk = ms ? n * n : n;
+        if (j >= 2) {  // kinematic row k = j-2 (problem.py:100-107)
+            double dt = 0.0;
+            dt = dt + pdx * dx;
+            dt = dt + pdy * dy;
+            const double c1 = fmax(0.0, nk - p.r_eff * pn);
+            const double c2 = fmax(0.0, pn / p.r_eff - nk);
+            const double c3 = fmax(0.0, p.mincos - dt / (pn * nk));
+            ksum = ksum + c1;
+            ksum = ksum + c2;
+            ksum = ksum + c3;
+            if (grow) {
+                grow[3 * (j - 2)] = c1;
+                grow[3 * (j - 2) + 1] = c2;
+                grow[3 * (j - 2) + 2] = c3;
+            }
+        }
+        pdx = dx;
+        pdy = dy;
+        pn = nk;
+        px = qx;
+        py = qy;
+    }
+
+    // ---- pass 2: per-waypoint penalty (get_cost loop problem.py:42-43) ------------------
+    double c = (double)(N + 1) * L;
+    const double dN = (double)N;
+    double nsum = 0.0;
+    int32_t nh = 0, off = 0;
+    double hmax = -INFINITY;
+    if (MODE == UAM_MODE_ANALYTIC) {
+        for (int j = 0; j < W; ++j) {
+            double x0, x1;
+            src.at(j, x0, x1);
+            c = c + total_penalty(g, p, x0, x1) / dN;
+            for (int s = 0; s < g.n_obstacles; ++s) {
+                const DevShape sh = g.shape[s];
+                const double v = psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+                nsum = nsum + v;
+                if (grow) grow[3 * N + s * W + j] = v;
+            }
+            nh += collides(g, x0, x1) ? 1 : 0;
+        }
+    } else {
+        int32_t* cells = out.cells ? out.cells + path * W : nullptr;
+        for (int j0 = 0; j0 < W; j0 += kChunk) {
+            uint4 r[kChunk];
+            bool in[kChunk];
+#pragma unroll
+            for (int t = 0; t < kChunk; ++t) {
+                const int j = j0 + t;
+                in[t] = false;
+                r[t] = make_uint4(0, 0, 0, 0);
+                if (j < W) {
+                    double x0, x1;
+                    src.at(j, x0, x1);
+                    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+                    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+                    in[t] = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) &&
+                            (fy < (double)rs.ny);
+                    const int64_t cell =
+                        in[t] ? (int64_t)fy * rs.nx + (int64_t)fx : (int64_t)0;
+                    r[t] = rec[cell];
+                    if (cells) cells[j] = in[t] ? (int32_t)cell : -1;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < kChunk; ++t) {
+                const int j = j0 + t;
+                if (j >= W) break;
+                if (!in[t]) {
+                    ++off;
+                    hmax = fmax(hmax, 0.0);  // off-raster counts as sea level
+                    continue;
+                }
+                c = c + (double)__uint_as_float(r[t].x) / dN;
+                nsum = nsum + (double)__uint_as_float(r[t].y);
+                nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+                const double terrain =
+                    (r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r[t].z);
+                hmax = fmax(hmax, terrain);
+            }
+        }
+    }
+    if (out.cost) out.cost[path] = c;
+    if (out.length_q) out.length_q[path] = L;
+    if (out.length) out.length[path] = len;
+    if (out.kin_sum) out.kin_sum[path] = ksum;
+    if (out.nfz_sum) out.nfz_sum[path] = nsum;
+    if (out.nfz_hits) out.nfz_hits[path] = nh;
+    if (out.offmap) out.offmap[path] = off;
+    if (out.min_clearance)
+        out.min_clearance[path] = (MODE == UAM_MODE_RASTER) ? p.altitude - hmax : NAN;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_eval_waypoints(KGeom g, KParams p, KRaster rs,
+                                                        const uint4* __restrict__ rec,
+                                                        const double* __restrict__ wp,
+                                                        int64_t n_paths, KOut out) {
+    const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (path >= n_paths) return;
+    PathSrc<false> src;
+    src.W = p.N + 2;
+    src.wp = wp + path * (int64_t)src.W * 2;
+    src.u = nullptr;
+    src.x0 = src.y0 = src.xf = src.yf = 0.0;
+    eval_one_path<MODE, false>(g, p, rs, rec, src, path, out);
+}
+
+// wave w (global) -> displacement d = w % D (wave-uniform), pairs [(w / D)*64, +64)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRaster rs,
+                                                        const uint4* __restrict__ rec,
+                                                        const double* __restrict__ pairs,
+                                                        int64_t n_pairs,
+                                                        const double* __restrict__ utab, int D,
+                                                        int64_t n_waves, KOut out) {
+    const int64_t wave = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    if (wave >= n_waves) return;
+    const int lane = threadIdx.x & 63;
+    const int d = (int)(wave % D);
+    const int64_t q = (wave / D) * 64 + lane;
+    if (q >= n_pairs) return;
+    const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+    PathSrc<true> src;
+    src.W = p.N + 2;
+    src.wp = nullptr;
+    src.x0 = pr.x;
+    src.y0 = pr.y;
+    src.xf = pr.z;
+    src.yf = pr.w;
+    src.u = utab + (int64_t)d * p.N * 2;
+    eval_one_path<MODE, true>(g, p, rs, rec, src, q * D + d, out);
+}
+
+__global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
+                                                   int64_t n_pairs,
+                                                   const double* __restrict__ utab, int D,
+                                                   int N, double* __restrict__ wp) {
+    const int W = N + 2;
+    const int64_t total = n_pairs * D * W;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t path = i / W;
+        const int j = (int)(i - path * W);
+        const int64_t q = path / D;
+        const int d = (int)(path - q * D);
+        const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+        double px, py;
+        if (j == 0) {
+            px = pr.x;
+            py = pr.y;
+        } else if (j == W - 1) {
+            px = pr.z;
+            py = pr.w;
+        } else {
+            const double* u = utab + ((int64_t)d * N + (j - 1)) * 2;
+            arc_point(pr.x, pr.y, pr.z, pr.w, u[0], u[1], px, py);
+        }
+        wp[2 * i] = px;
+        wp[2 * i + 1] = py;
+    }
+}
+
+// main.py:175-180 (see uam_argmin)
+__global__ __launch_bounds__(256) void k_argmin(const double* __restrict__ v, int64_t groups,
+                                                int G, int take_sqrt, int32_t* __restrict__ best) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= groups) return;
+    int bi = 0;
+    double bv = 0.0;
+    for (int d = 0; d < G; ++d) {
+        const double x = take_sqrt ? sqrt(v[q * G + d]) : v[q * G + d];
+        if (bv == 0.0 || x < bv) {
+            bv = x;
+            bi = d;
+        }
+    }
+    best[q] = bi;
+}
+
+__global__ __launch_bounds__(256) void k_path_length(const double* __restrict__ pts,
+                                                     int64_t n_paths, int n_points, int n_seg,
+                                                     int smooth, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_paths) return;
+    const double* z = pts + i * (int64_t)n_points * 2;
+    double acc = 0.0;
+    for (int k = 0; k < n_seg; ++k) {
+        const double dx = z[2 * k + 2] - z[2 * k], dy = z[2 * k + 3] - z[2 * k + 1];
+        double s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        const double n = sqrt(s);
+        acc = acc + (smooth ? n * n : n);
+    }
+    out[i] = acc;
+}
+
+// ----------------------------------------------------------------------------------------
+// host side
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(UAM_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int grid_for(int64_t n, int block, int64_t cap = 1 << 20) {
+    int64_t b = (n + block - 1) / block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (int)b;
+}
+
+}  // namespace
+
+struct uam_ctx {
+    int device = 0;
+    DevIneq* d_ineq = nullptr;
+    DevShape* d_shape = nullptr;
+    int n_ineq = 0, n_shapes = 0;
+    KGeom kg{};
+    KParams kp{};
+    bool have_geom = false, have_params = false;
+};
+
+namespace {
+
+int check_ctx(uam_ctx* ctx, bool need_params) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (!ctx->have_geom) return fail(UAM_E_STATE, "uam_set_geometry has not been called");
+    if (need_params && !ctx->have_params)
+        return fail(UAM_E_STATE, "uam_set_params has not been called");
+    return UAM_OK;
+}
+
+int make_kraster(const uam_raster_desc* d, KRaster* k) {
+    if (!d) return fail(UAM_E_INVALID, "raster mode needs a raster descriptor");
+    if (d->nx <= 0 || d->ny <= 0) return fail(UAM_E_INVALID, "raster size %dx%d", d->nx, d->ny);
+    if ((int64_t)d->nx * d->ny >= ((int64_t)1 << 31))
+        return fail(UAM_E_INVALID, "raster has more than 2^31 cells");
+    if (!(d->dx > 0.0) || !(d->dy > 0.0)) return fail(UAM_E_INVALID, "dx, dy must be > 0");
+    k->nx = d->nx;
+    k->ny = d->ny;
+    k->x0 = d->x0;
+    k->y_top = d->y_top;
+    k->dx = d->dx;
+    k->dy = d->dy;
+    k->inv_dx = 1.0 / d->dx;
+    k->inv_dy = 1.0 / d->dy;
+    return UAM_OK;
+}
+
+KOut make_kout(const uam_path_outputs* o) {
+    KOut k{};
+    if (!o) return k;
+    k.cost = o->cost;
+    k.length_q = o->length_q;
+    k.length = o->length;
+    k.kin_sum = o->kin_sum;
+    k.nfz_sum = o->nfz_sum;
+    k.nfz_hits = o->nfz_hits;
+    k.min_clearance = o->min_clearance;
+    k.offmap = o->offmap;
+    k.cells = o->cells;
+    k.g_rows = o->g_rows;
+    return k;
+}
+
+}  // namespace
+
+extern "C" {
+
+int uam_abi_version(void) { return UAM_ABI_VERSION; }
+
+const char* uam_last_error(void) { return g_last_error.c_str(); }
+
+int uam_device_count(int* n) {
+    if (!n) return fail(UAM_E_INVALID, "n is NULL");
+    HIP_TRY(hipGetDeviceCount(n));
+    return UAM_OK;
+}
+
+int uam_ctx_create(int device, uam_ctx** out) {
+    if (!out) return fail(UAM_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n)
+        return fail(UAM_E_INVALID, "device %d out of range (%d devices)", device, n);
+    uam_ctx* c = new (std::nothrow) uam_ctx();
+    if (!c) return fail(UAM_E_NOMEM, "ctx allocation failed");
+    c->device = device;
+    *out = c;
+    return UAM_OK;
+}
+
+void uam_ctx_destroy(uam_ctx* ctx) {
+    if (!ctx) return;
+    DeviceGuard dg(ctx->device);
+    if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
+    if (ctx->d_shape) (void)hipFree(ctx->d_shape);
+    delete ctx;
+}
+
+int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
+    if (!ctx || !geom) return fail(UAM_E_INVALID, "ctx/geom is NULL");
+    if (geom->abi_version != UAM_ABI_VERSION)
+        return fail(UAM_E_VERSION, "geometry abi_version %u != %d", geom->abi_version,
+                    UAM_ABI_VERSION);
+    const int ni = geom->n_ineq, ns = geom->n_shapes, nr = geom->n_regions;
+    if (ni < 0 || ns < 0 || geom->n_obstacles < 0 || geom->n_obstacles > ns)
+        return fail(UAM_E_INVALID, "bad counts n_ineq=%d n_shapes=%d n_obstacles=%d", ni, ns,
+                    geom->n_obstacles);
+    if (nr < 0 || nr > UAM_MAX_REGIONS)
+        return fail(UAM_E_INVALID, "n_regions %d exceeds %d", nr, UAM_MAX_REGIONS);
+    if (ns > 0 && (!geom->shape_first || !geom->shape_count || !geom->shape_center))
+        return fail(UAM_E_INVALID, "shape arrays are NULL");
+    if (ni > 0 && (!geom->ineq_kind || !geom->ineq_par))
+        return fail(UAM_E_INVALID, "inequality arrays are NULL");
+    if (!geom->region_first) return fail(UAM_E_INVALID, "region_first is NULL");
+    if (geom->region_first[0] != geom->n_obstacles || geom->region_first[nr] != ns)
+        return fail(UAM_E_INVALID, "region_first must run from n_obstacles to n_shapes");
+    for (int r = 0; r < nr; ++r)
+        if (geom->region_first[r + 1] < geom->region_first[r])
+            return fail(UAM_E_INVALID, "region_first not monotonic at %d", r);
+    for (int s = 0; s < ns; ++s)
+        if (geom->shape_count[s] < 1 || geom->shape_first[s] < 0 ||
+            geom->shape_first[s] + geom->shape_count[s] > ni)
+            return fail(UAM_E_INVALID, "shape %d inequality range out of bounds", s);
+    for (int i = 0; i < ni; ++i)
+        if (geom->ineq_kind[i] < UAM_INEQ_HALFPLANE || geom->ineq_kind[i] > UAM_INEQ_AXIS)
+            return fail(UAM_E_INVALID, "inequality %d has unknown kind %d", i,
+                        geom->ineq_kind[i]);
+
+    DeviceGuard dg(ctx->device);
+    if (!dg.ok) return fail(UAM_E_HIP, "hipSetDevice(%d) failed", ctx->device);
+    std::string hi(sizeof(DevIneq) * (ni > 0 ? ni : 1), '\0');
+    std::string hs(sizeof(DevShape) * (ns > 0 ? ns : 1), '\0');
+    DevIneq* ti = reinterpret_cast<DevIneq*>(&hi[0]);
+    DevShape* ts = reinterpret_cast<DevShape*>(&hs[0]);
+    for (int i = 0; i < ni; ++i) {
+        for (int k = 0; k < 6; ++k) ti[i].p[k] = geom->ineq_par[6 * i + k];
+        ti[i].kind = geom->ineq_kind[i];
+    }
+    for (int s = 0; s < ns; ++s) {
+        ts[s].first = geom->shape_first[s];
+        ts[s].count = geom->shape_count[s];
+        ts[s].cx = geom->shape_center[2 * s];
+        ts[s].cy = geom->shape_center[2 * s + 1];
+    }
+    if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
+    if (ctx->d_shape) (void)hipFree(ctx->d_shape);
+    ctx->d_ineq = nullptr;
+    ctx->d_shape = nullptr;
+    ctx->have_geom = ctx->have_params = false;
+    HIP_TRY(hipMalloc(&ctx->d_ineq, hi.size()));
+    HIP_TRY(hipMalloc(&ctx->d_shape, hs.size()));
+    HIP_TRY(hipMemcpy(ctx->d_ineq, hi.data(), hi.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->d_shape, hs.data(), hs.size(), hipMemcpyHostToDevice));
+    ctx->n_ineq = ni;
+    ctx->n_shapes = ns;
+    KGeom& kg = ctx->kg;
+    kg.ineq = ctx->d_ineq;
+    kg.shape = ctx->d_shape;
+    kg.n_obstacles = geom->n_obstacles;
+    kg.n_regions = nr;
+    for (int r = 0; r <= UAM_MAX_REGIONS; ++r)
+        kg.region_first[r] = r <= nr ? geom->region_first[r] : ns;
+    ctx->have_geom = true;
+    return UAM_OK;
+}
+
+int uam_set_params(uam_ctx* ctx, const uam_params* prm, uam_stream stream) {
+    int st = check_ctx(ctx, false);
+    if (st) return st;
+    if (!prm) return fail(UAM_E_INVALID, "params is NULL");
+    if (prm->abi_version != UAM_ABI_VERSION)
+        return fail(UAM_E_VERSION, "params abi_version %u != %d", prm->abi_version,
+                    UAM_ABI_VERSION);
+    if (prm->N < 1) return fail(UAM_E_INVALID, "N must be >= 1 (got %d)", prm->N);
+    KParams& k = ctx->kp;
+    k.N = prm->N;
+    k.length_smooth = prm->length_smooth != 0;
+    k.penalty_smooth = prm->penalty_smooth != 0;
+    k.obstacle_smooth = prm->obstacle_smooth != 0;
+    k.maxratio_smooth = prm->maxratio_smooth != 0;
+    k.quirk_length = prm->quirk_length != 0;
+    k.anchor_mode = prm->anchor_mode != 0;
+    k.anchor_x = prm->anchor_x;
+    k.anchor_y = prm->anchor_y;
+    k.r_eff = prm->maxratio_smooth ? prm->maxratio * prm->maxratio : prm->maxratio;
+    k.mincos = std::cos(prm->maxalpha);
+    k.enlargement = prm->enlargement;
+    k.altitude = prm->altitude;
+    for (int r = 0; r < UAM_MAX_REGIONS; ++r) k.weights[r] = prm->weights[r];
+    DeviceGuard dg(ctx->device);
+    if (ctx->n_shapes > 0) {
+        hipLaunchKernelGGL(k_prepare, dim3(grid_for(ctx->n_shapes, 64)), dim3(64), 0,
+                           (hipStream_t)stream, ctx->kg, k, ctx->d_shape, ctx->n_shapes);
+        HIP_TRY(hipGetLastError());
+    }
+    ctx->have_params = true;
+    return UAM_OK;
+}
+
+int uam_eval_points(uam_ctx* ctx, const double* pts, int64_t n, double* phi,
+                    double* phi_regions, double* obs_norm, double* psi_raw, int32_t* collide,
+                    uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (n < 0) return fail(UAM_E_INVALID, "n < 0");
+    if (n == 0) return UAM_OK;
+    if (!pts) return fail(UAM_E_INVALID, "pts is NULL");
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_eval_points, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       ctx->kg, ctx->kp, pts, n, phi, phi_regions, obs_norm, psi_raw, collide);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem, void* rec,
+                     uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    KRaster kr;
+    st = make_kraster(desc, &kr);
+    if (st) return st;
+    if (!rec) return fail(UAM_E_INVALID, "rec is NULL");
+    DeviceGuard dg(ctx->device);
+    const int64_t cells = (int64_t)kr.nx * kr.ny;
+    hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0,
+                       (hipStream_t)stream, ctx->kg, ctx->kp, kr, dem, desc->nodata,
+                       desc->dem_threshold, (uint4*)rec);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_dem_mosaic(uam_ctx* ctx, const float* tiles, int32_t n_tiles, int32_t th, int32_t tw,
+                   const int32_t* xoff, const int32_t* yoff, float* dem, int32_t nx, int32_t ny,
+                   uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (n_tiles < 0 || th <= 0 || tw <= 0 || nx <= 0 || ny <= 0)
+        return fail(UAM_E_INVALID, "bad mosaic sizes");
+    if (n_tiles == 0) return UAM_OK;
+    if (!tiles || !xoff || !yoff || !dem) return fail(UAM_E_INVALID, "mosaic pointer is NULL");
+    DeviceGuard dg(ctx->device);
+    const int64_t total = (int64_t)n_tiles * th * tw;
+    hipLaunchKernelGGL(k_dem_mosaic, dim3(grid_for(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, tiles, n_tiles, th, tw, xoff, yoff, dem, nx, ny);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_gen_paths(uam_ctx* ctx, const double* pairs, int64_t n_pairs, const double* utab,
+                  int32_t D, double* wp, uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (n_pairs < 0 || D < 1) return fail(UAM_E_INVALID, "n_pairs < 0 or D < 1");
+    if (n_pairs == 0) return UAM_OK;
+    if (!pairs || !utab || !wp) return fail(UAM_E_INVALID, "pointer is NULL");
+    DeviceGuard dg(ctx->device);
+    const int64_t total = n_pairs * D * (ctx->kp.N + 2);
+    hipLaunchKernelGGL(k_gen_paths, dim3(grid_for(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, pairs, n_pairs, utab, D, ctx->kp.N, wp);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                       const void* rec, const double* wp, int64_t n_paths,
+                       const uam_path_outputs* out, uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (n_paths < 0) return fail(UAM_E_INVALID, "n_paths < 0");
+    if (n_paths == 0) return UAM_OK;
+    if (!wp) return fail(UAM_E_INVALID, "wp is NULL");
+    KRaster kr{};
+    if (mode == UAM_MODE_RASTER) {
+        st = make_kraster(desc, &kr);
+        if (st) return st;
+        if (!rec) return fail(UAM_E_INVALID, "raster mode needs rec");
+    } else if (mode != UAM_MODE_ANALYTIC) {
+        return fail(UAM_E_INVALID, "unknown mode %d", mode);
+    }
+    const KOut ko = make_kout(out);
+    DeviceGuard dg(ctx->device);
+    const dim3 grid(grid_for(n_paths, 256, INT32_MAX)), block(256);
+    if (mode == UAM_MODE_RASTER)
+        hipLaunchKernelGGL(k_eval_waypoints<UAM_MODE_RASTER>, grid, block, 0, (hipStream_t)stream,
+                           ctx->kg, ctx->kp, kr, (const uint4*)rec, wp, n_paths, ko);
+    else
+        hipLaunchKernelGGL(k_eval_waypoints<UAM_MODE_ANALYTIC>, grid, block, 0,
+                           (hipStream_t)stream, ctx->kg, ctx->kp, kr, (const uint4*)rec, wp,
+                           n_paths, ko);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                       const void* rec, const double* pairs, int64_t n_pairs,
+                       const double* utab, int32_t D, const uam_path_outputs* out,
+                       uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (n_pairs < 0 || D < 1) return fail(UAM_E_INVALID, "n_pairs < 0 or D < 1");
+    if (n_pairs == 0) return UAM_OK;
+    if (!pairs || !utab) return fail(UAM_E_INVALID, "pairs/utab is NULL");
+    KRaster kr{};
+    if (mode == UAM_MODE_RASTER) {
+        st = make_kraster(desc, &kr);
+        if (st) return st;
+        if (!rec) return fail(UAM_E_INVALID, "raster mode needs rec");
+    } else if (mode != UAM_MODE_ANALYTIC) {
+        return fail(UAM_E_INVALID, "unknown mode %d", mode);
+    }
+    const KOut ko = make_kout(out);
+    DeviceGuard dg(ctx->device);
+    const int64_t n_waves = ((n_pairs + 63) / 64) * D;
+    const int64_t blocks = (n_waves + 3) / 4;
+    if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
+    const dim3 grid((unsigned)blocks), block(256);
+    if (mode == UAM_MODE_RASTER)
+        hipLaunchKernelGGL(k_eval_generated<UAM_MODE_RASTER>, grid, block, 0, (hipStream_t)stream,
+                           ctx->kg, ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D,
+                           n_waves, ko);
+    else
+        hipLaunchKernelGGL(k_eval_generated<UAM_MODE_ANALYTIC>, grid, block, 0,
+                           (hipStream_t)stream, ctx->kg, ctx->kp, kr, (const uint4*)rec, pairs,
+                           n_pairs, utab, D, n_waves, ko);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_argmin(uam_ctx* ctx, const double* values, int64_t groups, int32_t G, int32_t take_sqrt,
+               int32_t* best, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (groups < 0 || G < 1) return fail(UAM_E_INVALID, "groups < 0 or G < 1");
+    if (groups == 0) return UAM_OK;
+    if (!values || !best) return fail(UAM_E_INVALID, "pointer is NULL");
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_argmin, dim3(grid_for(groups, 256, INT32_MAX)), dim3(256), 0,
+                       (hipStream_t)stream, values, groups, G, take_sqrt, best);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_path_length(uam_ctx* ctx, const double* pts, int64_t n_paths, int32_t n_points,
+                    int32_t n_segments, int32_t smooth, double* out, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (n_paths < 0 || n_points < 1 || n_segments < 0 || n_segments > n_points - 1)
+        return fail(UAM_E_INVALID, "bad sizes n_points=%d n_segments=%d", n_points, n_segments);
+    if (n_paths == 0) return UAM_OK;
+    if (!pts || !out) return fail(UAM_E_INVALID, "pointer is NULL");
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_path_length, dim3(grid_for(n_paths, 256, INT32_MAX)), dim3(256), 0,
+                       (hipStream_t)stream, pts, n_paths, n_points, n_segments, smooth, out);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_synchronize(uam_ctx* ctx, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    DeviceGuard dg(ctx->device);
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return UAM_OK;
+}
+
+}  // extern "C"

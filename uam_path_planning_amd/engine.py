@@ -1,0 +1,342 @@
+"""Device engine: one libuampath context per GPU, torch tensors as device buffers.
+
+PyTorch is plumbing here (allocation, streams, H2D/D2H); every arithmetic step of the hot path
+runs in the hand-written HIP kernels of csrc/uampath.hip.  There is no CPU fallback: without a
+visible GPU or without libuampath.so, constructing an Engine raises.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .geometry import FlatGeometry, compile_map, compile_shapes
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+@dataclass
+class PathParams:
+    """Problem options + the OpEn parameter vector p (solver.py:60-78, problem.py:12-22)."""
+    N: int
+    length_smooth: bool = False
+    penalty_smooth: bool = True
+    obstacle_smooth: bool = False
+    maxratio_smooth: bool = False
+    maxratio: float = 1.0
+    maxalpha: float = 0.0
+    enlargement: float = 0.0
+    weights: tuple = ()
+    quirk_length: bool = True
+    anchor: tuple = None          # map.x_start baked into a reference build; None = p_0
+    altitude: float = 150.0       # cruise altitude (m) for min-clearance in raster mode
+
+    def as_struct(self):
+        w = [float(x) for x in self.weights]
+        if len(w) > _lib.MAX_REGIONS:
+            raise ValueError(f"at most {_lib.MAX_REGIONS} region weights")
+        arr = (ctypes.c_double * _lib.MAX_REGIONS)(*(w + [1.0] * (_lib.MAX_REGIONS - len(w))))
+        a = self.anchor
+        return _lib.Params(_lib.ABI_VERSION, int(self.N), int(bool(self.length_smooth)),
+                           int(bool(self.penalty_smooth)), int(bool(self.obstacle_smooth)),
+                           int(bool(self.maxratio_smooth)), int(bool(self.quirk_length)),
+                           0 if a is None else 1, 0.0 if a is None else float(a[0]),
+                           0.0 if a is None else float(a[1]), float(self.maxratio),
+                           float(self.maxalpha), float(self.enlargement), float(self.altitude),
+                           arr)
+
+
+@dataclass
+class RasterGeo:
+    """GeoTIFF-convention geotransform of the cost raster (row 0 = north edge)."""
+    nx: int
+    ny: int
+    x0: float
+    y_top: float
+    dx: float
+    dy: float
+    nodata: float = -9999.0
+    dem_threshold: float = 0.0
+
+    def as_struct(self):
+        return _lib.RasterDesc(int(self.nx), int(self.ny), float(self.x0), float(self.y_top),
+                               float(self.dx), float(self.dy), float(self.nodata),
+                               float(self.dem_threshold))
+
+    def cell_centres(self):
+        ix = np.arange(self.nx, dtype=np.float64)
+        iy = np.arange(self.ny, dtype=np.float64)
+        return self.x0 + (ix + 0.5) * self.dx, self.y_top - (iy + 0.5) * self.dy
+
+
+@dataclass
+class CostRaster:
+    """Device record raster: rec [ny, nx, 4] int32 view of {phi f32, psi f32, dem f32, flags}."""
+    geo: RasterGeo
+    rec: object = field(repr=False)
+
+    @property
+    def nbytes(self):
+        return self.geo.nx * self.geo.ny * _lib.RECORD_BYTES
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+class Engine:
+    """libuampath context bound to one GPU."""
+
+    def __init__(self, device=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible: uam_path_planning_amd runs only on the HIP "
+                               "kernels of libuampath.so (there is no CPU path)")
+        self.lib = _lib.load()
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.uam_ctx_create(self.device, ctypes.byref(h)), "uam_ctx_create")
+        self._ctx = h
+        self._geom_sig = None
+        self.geometry = None
+        self.params = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_ctx", None):
+                self.lib.uam_ctx_destroy(self._ctx)
+                self._ctx = None
+        except Exception:
+            pass
+
+    # -- helpers --------------------------------------------------------------------------
+    @property
+    def stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def tensor(self, x, dtype):
+        torch = _torch()
+        if isinstance(x, torch.Tensor):
+            t = x.to(device=self.torch_device, dtype=dtype)
+        else:
+            t = torch.as_tensor(np.asarray(x), dtype=dtype, device=self.torch_device)
+        return t.contiguous()
+
+    def empty(self, shape, dtype):
+        return _torch().empty(shape, dtype=dtype, device=self.torch_device)
+
+    # -- state ----------------------------------------------------------------------------
+    def set_geometry(self, geom):
+        if not isinstance(geom, FlatGeometry):
+            geom = compile_map(geom)
+        sig = geom.signature()
+        if sig != self._geom_sig:
+            _lib.check(self.lib.uam_set_geometry(self._ctx, ctypes.byref(geom.as_struct())),
+                       "uam_set_geometry")
+            self._geom_sig = sig
+            self.params = None
+        self.geometry = geom
+        return geom
+
+    def set_params(self, params):
+        if params != self.params:
+            _lib.check(self.lib.uam_set_params(self._ctx, ctypes.byref(params.as_struct()),
+                                               self.stream), "uam_set_params")
+            self.params = params
+        return params
+
+    # -- points ---------------------------------------------------------------------------
+    def eval_points(self, pts, want=("phi", "phi_regions", "obs_norm", "psi_raw", "collide")):
+        torch = _torch()
+        p = self.tensor(pts, torch.float64).reshape(-1, 2)
+        n = p.shape[0]
+        R = self.geometry.n_regions
+        out = {}
+        if "phi" in want:
+            out["phi"] = self.empty((n,), torch.float64)
+        if "phi_regions" in want:
+            out["phi_regions"] = self.empty((n, R), torch.float64)
+        if "obs_norm" in want:
+            out["obs_norm"] = self.empty((n,), torch.float64)
+        if "psi_raw" in want:
+            out["psi_raw"] = self.empty((n,), torch.float64)
+        if "collide" in want:
+            out["collide"] = self.empty((n,), torch.int32)
+        _lib.check(self.lib.uam_eval_points(
+            self._ctx, _ptr(p), n, _ptr(out.get("phi")), _ptr(out.get("phi_regions")),
+            _ptr(out.get("obs_norm")), _ptr(out.get("psi_raw")), _ptr(out.get("collide")),
+            self.stream), "uam_eval_points")
+        return out
+
+    # -- raster ---------------------------------------------------------------------------
+    def raster_build(self, geo, dem=None, out=None):
+        torch = _torch()
+        d = None if dem is None else self.tensor(dem, torch.float32).reshape(geo.ny, geo.nx)
+        rec = out if out is not None else self.empty((geo.ny, geo.nx, 4), torch.int32)
+        _lib.check(self.lib.uam_raster_build(self._ctx, ctypes.byref(geo.as_struct()), _ptr(d),
+                                             _ptr(rec), self.stream), "uam_raster_build")
+        return CostRaster(geo, rec)
+
+    def dem_mosaic(self, tiles, xoff, yoff, nx, ny, fill=-9999.0, dem=None):
+        torch = _torch()
+        t = self.tensor(tiles, torch.float32)
+        nt, th, tw = t.shape
+        xo = self.tensor(xoff, torch.int32)
+        yo = self.tensor(yoff, torch.int32)
+        if dem is None:
+            dem = torch.full((ny, nx), float(fill), dtype=torch.float32, device=self.torch_device)
+        _lib.check(self.lib.uam_dem_mosaic(self._ctx, _ptr(t), nt, th, tw, _ptr(xo), _ptr(yo),
+                                           _ptr(dem), nx, ny, self.stream), "uam_dem_mosaic")
+        return dem
+
+    # -- paths ----------------------------------------------------------------------------
+    def outputs(self, P, W, want_cells=False, want_g=False):
+        """Preallocated per-path output tensors (reuse them across launches)."""
+        return self._outputs(P, W, None, want_cells, want_g)
+
+    def _outputs(self, P, W, mode, want_cells, want_g):
+        torch = _torch()
+        o = {k: self.empty((P,), torch.float64) for k in ("cost", "length_q", "length",
+                                                           "kin_sum", "nfz_sum",
+                                                           "min_clearance")}
+        o["nfz_hits"] = self.empty((P,), torch.int32)
+        o["offmap"] = self.empty((P,), torch.int32)
+        if want_cells:
+            o["cells"] = self.empty((P, W), torch.int32)
+        if want_g:
+            n_rows = 3 * (W - 2) + self.geometry.n_obstacles * W
+            o["g_rows"] = self.empty((P, n_rows), torch.float64)
+        s = _lib.PathOutputs(*[ctypes.c_void_p(o[k].data_ptr()) if k in o else None
+                               for k, _ in _lib.PathOutputs._fields_])
+        return o, s
+
+    def _mode(self, raster):
+        return _lib.MODE_ANALYTIC if raster is None else _lib.MODE_RASTER
+
+    def eval_waypoints(self, wp, raster=None, want_cells=False, want_g=False):
+        """wp [P, N+2, 2] float64 (p_0 = start .. p_{N+1} = goal).  raster=None: analytic."""
+        torch = _torch()
+        N = self.params.N
+        w = self.tensor(wp, torch.float64).reshape(-1, N + 2, 2)
+        P = w.shape[0]
+        o, s = self._outputs(P, N + 2, self._mode(raster), want_cells and raster is not None,
+                             want_g and raster is None)
+        geo = None if raster is None else ctypes.byref(raster.geo.as_struct())
+        _lib.check(self.lib.uam_eval_waypoints(
+            self._ctx, self._mode(raster), geo, _ptr(None if raster is None else raster.rec),
+            _ptr(w), P, ctypes.byref(s), self.stream), "uam_eval_waypoints")
+        return o
+
+    def eval_generated(self, pairs, utab, raster=None, want_cells=False, outputs=None):
+        """pairs [Q, 4] (x0, y0, xf, yf); utab [D, N, 2]; path p = q*D + d."""
+        torch = _torch()
+        pr = self.tensor(pairs, torch.float64).reshape(-1, 4)
+        ut = self.tensor(utab, torch.float64)
+        D = ut.shape[0]
+        if ut.shape[1] != self.params.N:
+            raise ValueError(f"arc table has N={ut.shape[1]}, params N={self.params.N}")
+        Q = pr.shape[0]
+        if outputs is None:
+            o, s = self._outputs(Q * D, self.params.N + 2, self._mode(raster),
+                                 want_cells and raster is not None, False)
+        else:
+            o, s = outputs
+        geo = None if raster is None else ctypes.byref(raster.geo.as_struct())
+        _lib.check(self.lib.uam_eval_generated(
+            self._ctx, self._mode(raster), geo, _ptr(None if raster is None else raster.rec),
+            _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated")
+        return o
+
+    def gen_paths(self, pairs, utab):
+        torch = _torch()
+        pr = self.tensor(pairs, torch.float64).reshape(-1, 4)
+        ut = self.tensor(utab, torch.float64)
+        D, N = ut.shape[0], ut.shape[1]
+        if N != self.params.N:
+            raise ValueError(f"arc table has N={N}, params N={self.params.N}")
+        wp = self.empty((pr.shape[0] * D, N + 2, 2), torch.float64)
+        _lib.check(self.lib.uam_gen_paths(self._ctx, _ptr(pr), pr.shape[0], _ptr(ut), D,
+                                          _ptr(wp), self.stream), "uam_gen_paths")
+        return wp
+
+    def argmin(self, values, G, take_sqrt, out=None):
+        torch = _torch()
+        v = self.tensor(values, torch.float64).reshape(-1)
+        groups = v.shape[0] // G
+        best = out if out is not None else self.empty((groups,), torch.int32)
+        _lib.check(self.lib.uam_argmin(self._ctx, _ptr(v), groups, int(G), int(bool(take_sqrt)),
+                                       _ptr(best), self.stream), "uam_argmin")
+        return best
+
+    def path_length(self, pts, n_segments, smooth):
+        torch = _torch()
+        p = self.tensor(pts, torch.float64)
+        if p.dim() == 2:
+            p = p.unsqueeze(0)
+        P, n_points = p.shape[0], p.shape[1]
+        out = self.empty((P,), torch.float64)
+        _lib.check(self.lib.uam_path_length(self._ctx, _ptr(p), P, n_points, int(n_segments),
+                                            int(bool(smooth)), _ptr(out), self.stream),
+                   "uam_path_length")
+        return out
+
+    def synchronize(self):
+        _lib.check(self.lib.uam_synchronize(self._ctx, self.stream), "uam_synchronize")
+
+
+_default = {}
+
+
+def default_engine(device=None):
+    torch = _torch()
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    if device not in _default:
+        _default[device] = Engine(device)
+    return _default[device]
+
+
+# ---- single-shape helpers used by the drop-in classes (scratch contexts) ------------------
+def _scratch(geom, params):
+    eng = Engine(default_engine().device)
+    eng.set_geometry(geom)
+    eng.set_params(params)
+    return eng
+
+
+def _as_points(x):
+    a = np.asarray(x, dtype=np.float64)
+    single = a.size == 2
+    return a.reshape(-1, 2), single
+
+
+def shape_psi(obs, x, smooth, enlargement):
+    """psi(x) of one shape: a one-region geometry with no centre and weight 1 -> phi = psi."""
+    pts, single = _as_points(x)
+    shape = type(obs).__new__(type(obs))
+    shape.__dict__.update(obs.__dict__)
+    shape.center = float("nan")
+    geom = compile_shapes((), [[shape]])
+    eng = _scratch(geom, PathParams(N=1, penalty_smooth=smooth, enlargement=enlargement,
+                                    weights=(1.0,)))
+    v = eng.eval_points(pts, want=("phi",))["phi"].cpu().numpy()
+    return float(v[0]) if single else v
+
+
+def shape_contains(obs, x):
+    pts, single = _as_points(x)
+    eng = _scratch(compile_shapes([obs], []), PathParams(N=1))
+    v = eng.eval_points(pts, want=("collide",))["collide"].cpu().numpy().astype(bool)
+    return bool(v[0]) if single else v
+
+
+def map_collides(m, x):
+    pts, single = _as_points(x)
+    eng = _scratch(compile_shapes(list(m.obstacles), []), PathParams(N=1))
+    v = eng.eval_points(pts, want=("collide",))["collide"].cpu().numpy().astype(bool)
+    return bool(v[0]) if single else v
