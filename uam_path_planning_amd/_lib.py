@@ -89,10 +89,17 @@ class UamError(RuntimeError):
 
 
 def load():
-    """Load libuampath.so (no fallback: raises if it was not built)."""
+    """Load libuampath.so (no fallback: raises if it was not built).
+
+    torch is imported first on purpose: torch ships its own libamdhip64 (soname
+    libamdhip64.so.7) and libtorch_hip links it unversioned.  Loaded after torch, libuampath's
+    libamdhip64.so.7 dependency resolves to torch's already-loaded runtime, so device buffers
+    and streams are shared by ONE HIP runtime.  Loaded before torch, the system runtime would
+    come in first and torch would then load a second one that sees no device."""
     global _lib
     if _lib is not None:
         return _lib
+    import torch  # noqa: F401  (see docstring: one HIP runtime per process)
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(
             f"{LIB_PATH} is missing: build the HIP library first "
