@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--R", type=int, default=None, help="override raster size")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -126,19 +127,18 @@ def main():
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
-    outs = eng.outputs(P, W)
-    best_f = eng.empty((Q,), torch.int32)
-    best_l = eng.empty((Q,), torch.int32)
+    outs = eng.outputs(P, W, n_pairs=Q)
     o = outs[0]
+    if args.variant:
+        eng.set_tuning(args.variant)
 
     def step(ev=None):
+        # one launch: arc generation + gather + cost reduction + candidate selection
         if ev is not None:
             ev[0].record()
         eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
         if ev is not None:
             ev[1].record()
-        eng.argmin(o["cost"], D, True, out=best_f)
-        eng.argmin(o["length"], D, False, out=best_l)
 
     for _ in range(args.warmup):
         step()
@@ -166,7 +166,7 @@ def main():
     # algorithmic bytes per launch of the dominant kernel
     gather_b = 16 * W if raster_mode else 0
     pair_b = 32.0 / D
-    out_b = 6 * 8 + 2 * 4
+    out_b = 6 * 8 + 2 * 4 + 8.0 / D   # 6 f64 + 2 i32 per path, 2 i32 best indices per pair
     bytes_per_path = gather_b + pair_b + out_b
     launch_bytes = bytes_per_path * P
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
@@ -224,8 +224,9 @@ def main():
                                       geo.nodata, geo.dem_threshold)
             rec = raster.rec.cpu().numpy().view(np.float32)
         gpu_cost = o["cost"].cpu().numpy()
+        gpu_best = o["best_fval_idx"].cpu().numpy()
         chunk = 2000 if raster_mode else 50
-        done, t_cpu, mism = 0, 0.0, 0
+        done, t_cpu, mism, bmis = 0, 0.0, 0, 0
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
@@ -234,6 +235,7 @@ def main():
                                rec=rec)
             t_cpu += time.perf_counter() - ts
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
+            bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
             done += len(sl)
         result["cpu_baseline"] = {
             "value": round(done * D / t_cpu, 1), "unit": "candidate-paths/s", "cores": 1,
@@ -242,6 +244,7 @@ def main():
                       f"{t_cpu:.1f} s) through oracle/uam_oracle.c (gcc -O2, 1 thread): "
                       "arc generation + raster gather + cost reduction"}
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
+                            "best_index_mismatches": bmis,
                             "rule": "bit-exact float64 vs CPU oracle"}
     if rank == 0:
         print(json.dumps(result), flush=True)

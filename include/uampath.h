@@ -131,6 +131,9 @@ typedef struct {
     int32_t* offmap;       /* raster: waypoints outside the raster */
     int32_t* cells;        /* [P][W] raster cell index iy*nx+ix, -1 off-raster (raster only) */
     double* g_rows;        /* [P][3N + n_obstacles*W] full get_nonlincon vector (analytic) */
+    int32_t* best_fval_idx;   /* uam_eval_generated only: [Q] per pair, the displacement index
+                                 the reference keeps as "Min fval result" (main.py:175-177) */
+    int32_t* best_length_idx; /* [Q] "Min path length result" (main.py:178-180) */
 } uam_path_outputs;
 
 int uam_abi_version(void);
@@ -188,6 +191,12 @@ int uam_path_length(uam_ctx* ctx, const double* pts_dev, int64_t n_paths, int32_
                     int32_t n_segments, int32_t smooth, double* out_dev, uam_stream stream);
 
 int uam_synchronize(uam_ctx* ctx, uam_stream stream);
+
+/* Kernel variant for uam_eval_generated (0 = default).  1 = one wave per (displacement,
+ * 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup per 64 pairs x D
+ * (D <= 16) with LDS-staged coalesced stores and the selection fused, differing in gathers per
+ * chunk / software pipelining / occupancy.  All variants return bit-identical results. */
+int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 #ifdef __cplusplus
 }

@@ -314,3 +314,27 @@ def test_dropin_problem_and_solver(eng):
     obs = m.obstacles[0]
     assert obs.contains([38.7, -9.2])
     assert obs.penalty_function(True, 0)([38.66652661075855, -9.203164091309498]) == 1.0
+
+
+@pytest.mark.parametrize("D", [5, 3, 17])
+def test_kernel_variants_bit_identical(eng, oracle_mod, D):
+    """Every uam_set_tuning variant returns the same bits (and the fused selection matches the
+    oracle's rule); D=17 exercises the fallback to the per-wave kernel + separate selection."""
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 333, 80, nfz=4, D=D)
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
+    try:
+        for v in range(0, 9):
+            eng.set_tuning(v)
+            gpu = eng.eval_generated(pairs, ut, raster=raster)
+            _assert_paths_equal(gpu, ref, raster=True)
+            np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                          oracle_mod.argmin(ref["cost"], D, True))
+            np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
+                                          oracle_mod.argmin(ref["length"], D, False))
+            ga = eng.eval_generated(pairs[:50], ut)      # analytic path of the same variant
+            ra = orc.eval_paths(oracle_mod.gen_paths(pairs[:50], ut))
+            _assert_paths_equal(ga, ra)
+    finally:
+        eng.set_tuning(0)
+    with pytest.raises(ValueError):
+        eng.set_tuning(99)

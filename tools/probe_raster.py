@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=100_000)
     ap.add_argument("--sizes", default="64,512,1024,2048,4096,8192")
     ap.add_argument("--analytic-pairs", type=int, default=20_000)
+    ap.add_argument("--variants", default="", help="comma list: interleaved A/B at R=4096")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import Engine
@@ -49,7 +51,33 @@ def main():
     ut = eng.tensor(arc_table(80, displacements(5)), torch.float64)
     pairs = eng.tensor(random_pairs(args.pairs, seed=0), torch.float64)
     P = args.pairs * 5
-    outs = eng.outputs(P, 82)
+    outs = eng.outputs(P, 82, n_pairs=args.pairs)
+    if args.variants:
+        geo = raster_geo(4096)
+        raster = eng.raster_build(geo, eng.tensor(synthetic_dem(4096), torch.float32))
+        vs = [int(x) for x in args.variants.split(",")]
+        res = {v: [] for v in vs}
+        ref = None
+        for _ in range(args.rounds):
+            for v in vs:
+                eng.set_tuning(v)
+                med, best = timed(lambda: eng.eval_generated(pairs, ut, raster=raster,
+                                                             outputs=outs), reps=10)
+                res[v].append(med)
+                cur = (outs[0]["cost"].clone(), outs[0]["best_fval_idx"].clone())
+                if ref is None:
+                    ref = cur
+                assert torch.equal(cur[0], ref[0]) and torch.equal(cur[1], ref[1]), v
+        for v in vs:
+            ts = sorted(res[v])
+            print(json.dumps({"probe": "variant", "variant": v, "R": 4096, "paths": P,
+                              "kernel_ms_median": round(ts[len(ts) // 2], 4),
+                              "kernel_ms_min": round(ts[0], 4),
+                              "paths_per_s": round(P / (ts[len(ts) // 2] * 1e-3), 1)}),
+                  flush=True)
+        eng.set_tuning(0)
+        del raster
+        torch.cuda.empty_cache()
     for R in [int(x) for x in args.sizes.split(",")]:
         geo = raster_geo(R)
         dem = eng.tensor(synthetic_dem(R), torch.float32)

@@ -52,7 +52,7 @@ class RasterDesc(ctypes.Structure):
 class PathOutputs(ctypes.Structure):
     _fields_ = [(name, _vp) for name in ("cost", "length_q", "length", "kin_sum", "nfz_sum",
                                          "nfz_hits", "min_clearance", "offmap", "cells",
-                                         "g_rows")]
+                                         "g_rows", "best_fval_idx", "best_length_idx")]
 
 
 # name -> (restype, argtypes); the full exported surface of include/uampath.h
@@ -79,6 +79,7 @@ SIGNATURES = {
     "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _vp, _vp]),
     "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
+    "uam_set_tuning": (ctypes.c_int, [_vp, ctypes.c_int32]),
 }
 
 _lib = None

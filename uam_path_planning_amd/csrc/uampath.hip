@@ -29,6 +29,9 @@
 
 #include "../../include/uampath.h"
 
+#define UAM_TUNING_MAX 8
+#define UAM_TUNING_DEFAULT 2
+
 namespace {
 
 // ----------------------------------------------------------------------------------------
@@ -291,23 +294,84 @@ struct PathSrc {
     }
 };
 
-constexpr int kChunk = 8;  // raster gathers in flight per lane
+// Per-path results, in the reference's summation order (see eval_path).
+struct PathAcc {
+    double cost, L, len, ksum, nsum, hmax;
+    int32_t nh, off;
+};
 
-template <int MODE, bool GEN>
-__device__ __forceinline__ void eval_one_path(const KGeom& g, const KParams& p, const KRaster& rs,
-                                              const uint4* __restrict__ rec,
-                                              const PathSrc<GEN>& src, int64_t path,
-                                              const KOut& out) {
+// Gathers of one chunk of C consecutive waypoints (issued together, consumed together).
+template <int C>
+struct Chunk {
+    uint4 r[C];
+    bool in[C];
+};
+
+template <bool GEN, int C>
+__device__ __forceinline__ void issue_chunk(const KRaster& rs, const uint4* __restrict__ rec,
+                                            const PathSrc<GEN>& src, int j0, int W,
+                                            int32_t* cells, Chunk<C>& ch) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        const int j = j0 + t;
+        ch.in[t] = false;
+        ch.r[t] = make_uint4(0, 0, 0, 0);
+        if (j < W) {
+            double x0, x1;
+            src.at(j, x0, x1);
+            // uampath.h raster convention: float64 floor of the scaled offset
+            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+            const bool in = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) &&
+                            (fy < (double)rs.ny);
+            const int64_t cell = in ? (int64_t)fy * rs.nx + (int64_t)fx : (int64_t)0;
+            ch.in[t] = in;
+            ch.r[t] = rec[cell];  // unconditional: off-raster lanes read cell 0 (cached)
+            if (cells) cells[j] = in ? (int32_t)cell : -1;
+        }
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void consume_chunk(const Chunk<C>& ch, int j0, int W, double dN,
+                                              PathAcc& a) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        if (j0 + t >= W) break;
+        if (!ch.in[t]) {
+            ++a.off;
+            a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
+            continue;
+        }
+        a.cost = a.cost + (double)__uint_as_float(ch.r[t].x) / dN;
+        a.nsum = a.nsum + (double)__uint_as_float(ch.r[t].y);
+        a.nh += (ch.r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+        const double terrain =
+            (ch.r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(ch.r[t].z);
+        a.hmax = fmax(a.hmax, terrain);
+    }
+}
+
+// One path: pass 1 = geometry-only terms (length_of, true length, kinematic rows), pass 2 =
+// per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk,
+// PIPE = issue chunk k+1's gathers before consuming chunk k (two chunks in flight).
+template <int MODE, bool GEN, int C, bool PIPE>
+__device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
+                                             const uint4* __restrict__ rec,
+                                             const PathSrc<GEN>& src, int64_t path,
+                                             const KOut& out) {
     const int N = p.N, W = N + 2;
     const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     const int n_rows = 3 * N + g.n_obstacles * W;
-    double* grow = (MODE == UAM_MODE_ANALYTIC && out.g_rows) ? out.g_rows + path * n_rows : nullptr;
+    double* grow =
+        (MODE == UAM_MODE_ANALYTIC && out.g_rows) ? out.g_rows + path * n_rows : nullptr;
+    PathAcc a;
 
-    // ---- pass 1: geometry-only terms (length_of, true length, kinematic rows) ----------
+    // ---- pass 1 ---------------------------------------------------------------------------
     double px, py;
     src.at(0, px, py);
     double L = 0.0;
-    if (p.quirk_length) {
+    if (p.quirk_length) {  // y_0 = anchor (map.x_start), y_1 = p_0 (problem.py:137-140)
         const double ax = p.anchor_mode ? p.anchor_x : px;
         const double ay = p.anchor_mode ? p.anchor_y : py;
         const double dx = px - ax, dy = py - ay;
@@ -326,7 +390,7 @@ __device__ __forceinline__ void eval_one_path(const KGeom& g, const KParams& p, 
         double s = 0.0;
         s = s + dx * dx;
         s = s + dy * dy;
-        const double n = sqrt(s);
+        const double n = sqrt(s);  // norm_2 = sqrt(dot) (casadi_norm_2)
         len = len + n;
         if (!p.quirk_length || j <= N) L = L + (ls ? n * n : n);
         const double nk = ms ? n * n : n;
@@ -352,76 +416,80 @@ __device__ __forceinline__ void eval_one_path(const KGeom& g, const KParams& p, 
         px = qx;
         py = qy;
     }
+    a.L = L;
+    a.len = len;
+    a.ksum = ksum;
 
-    // ---- pass 2: per-waypoint penalty (get_cost loop problem.py:42-43) ------------------
-    double c = (double)(N + 1) * L;
+    // ---- pass 2: cost = (N+1) L + sum_j phi(p_j)/N  (problem.py:41-43) ------------------
+    a.cost = (double)(N + 1) * L;
+    a.nsum = 0.0;
+    a.nh = 0;
+    a.off = 0;
+    a.hmax = -INFINITY;
     const double dN = (double)N;
-    double nsum = 0.0;
-    int32_t nh = 0, off = 0;
-    double hmax = -INFINITY;
     if (MODE == UAM_MODE_ANALYTIC) {
         for (int j = 0; j < W; ++j) {
             double x0, x1;
             src.at(j, x0, x1);
-            c = c + total_penalty(g, p, x0, x1) / dN;
+            a.cost = a.cost + total_penalty(g, p, x0, x1) / dN;
             for (int s = 0; s < g.n_obstacles; ++s) {
                 const DevShape sh = g.shape[s];
                 const double v = psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
-                nsum = nsum + v;
+                a.nsum = a.nsum + v;
                 if (grow) grow[3 * N + s * W + j] = v;
             }
-            nh += collides(g, x0, x1) ? 1 : 0;
+            a.nh += collides(g, x0, x1) ? 1 : 0;
         }
     } else {
         int32_t* cells = out.cells ? out.cells + path * W : nullptr;
-        for (int j0 = 0; j0 < W; j0 += kChunk) {
-            uint4 r[kChunk];
-            bool in[kChunk];
-#pragma unroll
-            for (int t = 0; t < kChunk; ++t) {
-                const int j = j0 + t;
-                in[t] = false;
-                r[t] = make_uint4(0, 0, 0, 0);
-                if (j < W) {
-                    double x0, x1;
-                    src.at(j, x0, x1);
-                    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
-                    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
-                    in[t] = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) &&
-                            (fy < (double)rs.ny);
-                    const int64_t cell =
-                        in[t] ? (int64_t)fy * rs.nx + (int64_t)fx : (int64_t)0;
-                    r[t] = rec[cell];
-                    if (cells) cells[j] = in[t] ? (int32_t)cell : -1;
-                }
+        if (!PIPE) {
+            for (int j0 = 0; j0 < W; j0 += C) {
+                Chunk<C> ch;
+                issue_chunk<GEN, C>(rs, rec, src, j0, W, cells, ch);
+                consume_chunk<C>(ch, j0, W, dN, a);
             }
-#pragma unroll
-            for (int t = 0; t < kChunk; ++t) {
-                const int j = j0 + t;
-                if (j >= W) break;
-                if (!in[t]) {
-                    ++off;
-                    hmax = fmax(hmax, 0.0);  // off-raster counts as sea level
-                    continue;
+        } else {
+            Chunk<C> ca, cb;
+            issue_chunk<GEN, C>(rs, rec, src, 0, W, cells, ca);
+            for (int j0 = 0; j0 < W; j0 += 2 * C) {
+                if (j0 + C < W) issue_chunk<GEN, C>(rs, rec, src, j0 + C, W, cells, cb);
+                consume_chunk<C>(ca, j0, W, dN, a);
+                if (j0 + C < W) {
+                    if (j0 + 2 * C < W)
+                        issue_chunk<GEN, C>(rs, rec, src, j0 + 2 * C, W, cells, ca);
+                    consume_chunk<C>(cb, j0 + C, W, dN, a);
                 }
-                c = c + (double)__uint_as_float(r[t].x) / dN;
-                nsum = nsum + (double)__uint_as_float(r[t].y);
-                nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
-                const double terrain =
-                    (r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r[t].z);
-                hmax = fmax(hmax, terrain);
             }
         }
     }
-    if (out.cost) out.cost[path] = c;
-    if (out.length_q) out.length_q[path] = L;
-    if (out.length) out.length[path] = len;
-    if (out.kin_sum) out.kin_sum[path] = ksum;
-    if (out.nfz_sum) out.nfz_sum[path] = nsum;
-    if (out.nfz_hits) out.nfz_hits[path] = nh;
-    if (out.offmap) out.offmap[path] = off;
+    return a;
+}
+
+__device__ __forceinline__ void write_path(const KOut& out, const KParams& p, int mode,
+                                           int64_t path, const PathAcc& a) {
+    if (out.cost) out.cost[path] = a.cost;
+    if (out.length_q) out.length_q[path] = a.L;
+    if (out.length) out.length[path] = a.len;
+    if (out.kin_sum) out.kin_sum[path] = a.ksum;
+    if (out.nfz_sum) out.nfz_sum[path] = a.nsum;
+    if (out.nfz_hits) out.nfz_hits[path] = a.nh;
+    if (out.offmap) out.offmap[path] = a.off;
     if (out.min_clearance)
-        out.min_clearance[path] = (MODE == UAM_MODE_RASTER) ? p.altitude - hmax : NAN;
+        out.min_clearance[path] = (mode == UAM_MODE_RASTER) ? p.altitude - a.hmax : NAN;
+}
+
+// main.py:175-180 selection over D values (see uam_argmin)
+__device__ __forceinline__ int select_best(const double* v, int stride, int D, bool take_sqrt) {
+    int bi = 0;
+    double bv = 0.0;
+    for (int d = 0; d < D; ++d) {
+        const double x = take_sqrt ? sqrt(v[d * stride]) : v[d * stride];
+        if (bv == 0.0 || x < bv) {
+            bv = x;
+            bi = d;
+        }
+    }
+    return bi;
 }
 
 template <int MODE>
@@ -436,10 +504,12 @@ __global__ __launch_bounds__(256) void k_eval_waypoints(KGeom g, KParams p, KRas
     src.wp = wp + path * (int64_t)src.W * 2;
     src.u = nullptr;
     src.x0 = src.y0 = src.xf = src.yf = 0.0;
-    eval_one_path<MODE, false>(g, p, rs, rec, src, path, out);
+    const PathAcc a = eval_path<MODE, false, 8, false>(g, p, rs, rec, src, path, out);
+    write_path(out, p, MODE, path, a);
 }
 
-// wave w (global) -> displacement d = w % D (wave-uniform), pairs [(w / D)*64, +64)
+// Variant 1 (first version): global wave w -> displacement d = w % D (wave-uniform),
+// pairs [(w / D)*64, +64); outputs stored straight from registers (stride-D stores).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRaster rs,
                                                         const uint4* __restrict__ rec,
@@ -463,7 +533,79 @@ __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRas
     src.xf = pr.z;
     src.yf = pr.w;
     src.u = utab + (int64_t)d * p.N * 2;
-    eval_one_path<MODE, true>(g, p, rs, rec, src, q * D + d, out);
+    const PathAcc a = eval_path<MODE, true, 8, false>(g, p, rs, rec, src, q * D + d, out);
+    write_path(out, p, MODE, q * D + d, a);
+}
+
+// Variant 2+: one workgroup = one block of 64 pairs x all D displacements (wave = d,
+// lane = pair).  Results are staged in LDS and written with unit-stride (coalesced) stores
+// over the block's contiguous path range [b*64*D, (b+1)*64*D); the candidate selection
+// (main.py:175-180) runs in the same launch on the staged costs / lengths.
+template <int MODE, int C, bool PIPE, int MINW>
+__global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, KRaster rs,
+                                                           const uint4* __restrict__ rec,
+                                                           const double* __restrict__ pairs,
+                                                           int64_t n_pairs,
+                                                           const double* __restrict__ utab,
+                                                           int D, KOut out,
+                                                           int32_t* __restrict__ best_f,
+                                                           int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int BP = 64 * D;                     // paths per block
+    double* s_cost = smem;
+    double* s_L = s_cost + BP;
+    double* s_len = s_L + BP;
+    double* s_k = s_len + BP;
+    double* s_n = s_k + BP;
+    double* s_clr = s_n + BP;
+    int32_t* s_nh = reinterpret_cast<int32_t*>(s_clr + BP);
+    int32_t* s_off = s_nh + BP;
+
+    const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int64_t q = q0 + lane;
+    const int slot = d * 64 + lane;
+    if (q < n_pairs) {
+        const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+        PathSrc<true> src;
+        src.W = p.N + 2;
+        src.wp = nullptr;
+        src.x0 = pr.x;
+        src.y0 = pr.y;
+        src.xf = pr.z;
+        src.yf = pr.w;
+        src.u = utab + (int64_t)d * p.N * 2;
+        const PathAcc a = eval_path<MODE, true, C, PIPE>(g, p, rs, rec, src, q * D + d, out);
+        s_cost[slot] = a.cost;
+        s_L[slot] = a.L;
+        s_len[slot] = a.len;
+        s_k[slot] = a.ksum;
+        s_n[slot] = a.nsum;
+        s_clr[slot] = (MODE == UAM_MODE_RASTER) ? p.altitude - a.hmax : NAN;
+        s_nh[slot] = a.nh;
+        s_off[slot] = a.off;
+    }
+    __syncthreads();
+    // coalesced stores: thread t -> block-local path t = (pair t / D, displacement t % D)
+    const int t = threadIdx.x;
+    const int qi = t / D, di = t - qi * D;
+    const int64_t gp = q0 * D + t;
+    if (q0 + qi < n_pairs) {
+        const int s = di * 64 + qi;
+        if (out.cost) out.cost[gp] = s_cost[s];
+        if (out.length_q) out.length_q[gp] = s_L[s];
+        if (out.length) out.length[gp] = s_len[s];
+        if (out.kin_sum) out.kin_sum[gp] = s_k[s];
+        if (out.nfz_sum) out.nfz_sum[gp] = s_n[s];
+        if (out.min_clearance) out.min_clearance[gp] = s_clr[s];
+        if (out.nfz_hits) out.nfz_hits[gp] = s_nh[s];
+        if (out.offmap) out.offmap[gp] = s_off[s];
+    }
+    if (d == 0 && q < n_pairs) {
+        if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
+        if (best_l) best_l[q] = select_best(s_len + lane, 64, D, false);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
@@ -581,6 +723,7 @@ struct uam_ctx {
     KGeom kg{};
     KParams kp{};
     bool have_geom = false, have_params = false;
+    int variant = 0;  // uam_set_tuning; 0 = default
 };
 
 namespace {
@@ -856,6 +999,15 @@ int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     return UAM_OK;
 }
 
+int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (variant < 0 || variant > UAM_TUNING_MAX)
+        return fail(UAM_E_INVALID, "tuning variant %d out of range [0, %d]", variant,
+                    UAM_TUNING_MAX);
+    ctx->variant = variant;
+    return UAM_OK;
+}
+
 int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec, const double* pairs, int64_t n_pairs,
                        const double* utab, int32_t D, const uam_path_outputs* out,
@@ -874,19 +1026,58 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
         return fail(UAM_E_INVALID, "unknown mode %d", mode);
     }
     const KOut ko = make_kout(out);
+    int32_t* best_f = out ? out->best_fval_idx : nullptr;
+    int32_t* best_l = out ? out->best_length_idx : nullptr;
     DeviceGuard dg(ctx->device);
-    const int64_t n_waves = ((n_pairs + 63) / 64) * D;
-    const int64_t blocks = (n_waves + 3) / 4;
+    hipStream_t s = (hipStream_t)stream;
+    int v = ctx->variant == 0 ? UAM_TUNING_DEFAULT : ctx->variant;
+    if (D > 16) v = 1;  // the block-of-pairs kernels hold all D waves in one workgroup
+    if (v == 1) {
+        const int64_t n_waves = ((n_pairs + 63) / 64) * D;
+        const int64_t blocks = (n_waves + 3) / 4;
+        if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
+        const dim3 grid((unsigned)blocks), block(256);
+        if (mode == UAM_MODE_RASTER)
+            hipLaunchKernelGGL(k_eval_generated<UAM_MODE_RASTER>, grid, block, 0, s, ctx->kg,
+                               ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D, n_waves,
+                               ko);
+        else
+            hipLaunchKernelGGL(k_eval_generated<UAM_MODE_ANALYTIC>, grid, block, 0, s, ctx->kg,
+                               ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D, n_waves,
+                               ko);
+        HIP_TRY(hipGetLastError());
+        if (best_f || best_l) {  // selection needs the costs/lengths even if not requested
+            if ((best_f && !ko.cost) || (best_l && !ko.length))
+                return fail(UAM_E_INVALID, "best_*_idx needs cost/length outputs (variant 1)");
+            const dim3 g2(grid_for(n_pairs, 256, INT32_MAX));
+            if (best_f) hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.cost, n_pairs, D, 1, best_f);
+            if (best_l) hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.length, n_pairs, D, 0, best_l);
+            HIP_TRY(hipGetLastError());
+        }
+        return UAM_OK;
+    }
+    const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
-    const dim3 grid((unsigned)blocks), block(256);
-    if (mode == UAM_MODE_RASTER)
-        hipLaunchKernelGGL(k_eval_generated<UAM_MODE_RASTER>, grid, block, 0, (hipStream_t)stream,
-                           ctx->kg, ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D,
-                           n_waves, ko);
-    else
-        hipLaunchKernelGGL(k_eval_generated<UAM_MODE_ANALYTIC>, grid, block, 0,
-                           (hipStream_t)stream, ctx->kg, ctx->kp, kr, (const uint4*)rec, pairs,
-                           n_pairs, utab, D, n_waves, ko);
+    const dim3 grid((unsigned)blocks), block(64 * D);
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 2 * sizeof(int32_t));
+#define UAM_LAUNCH_PAIRS(MODE_, C_, PIPE_, MINW_)                                          \
+    hipLaunchKernelGGL((k_eval_pairs<MODE_, C_, PIPE_, MINW_>), grid, block, lds, s, ctx->kg, \
+                       ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D, ko, best_f,  \
+                       best_l)
+    if (mode == UAM_MODE_ANALYTIC) {
+        UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
+    } else {
+        switch (v) {
+            case 2: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 1); break;
+            case 3: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 1); break;
+            case 4: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, true, 1); break;
+            case 5: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 6); break;
+            case 6: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 6); break;
+            case 7: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 2, true, 8); break;
+            default: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, false, 8); break;  // 8
+        }
+    }
+#undef UAM_LAUNCH_PAIRS
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }

@@ -195,11 +195,14 @@ class Engine:
         return dem
 
     # -- paths ----------------------------------------------------------------------------
-    def outputs(self, P, W, want_cells=False, want_g=False):
-        """Preallocated per-path output tensors (reuse them across launches)."""
-        return self._outputs(P, W, None, want_cells, want_g)
+    def outputs(self, P, W, n_pairs=None, want_cells=False, want_g=False):
+        """Preallocated per-path (and per-pair best-index) outputs, reusable across launches."""
+        return self._outputs(P, W, None, want_cells, want_g, n_pairs)
 
-    def _outputs(self, P, W, mode, want_cells, want_g):
+    def set_tuning(self, variant):
+        _lib.check(self.lib.uam_set_tuning(self._ctx, int(variant)), "uam_set_tuning")
+
+    def _outputs(self, P, W, mode, want_cells, want_g, n_pairs=None):
         torch = _torch()
         o = {k: self.empty((P,), torch.float64) for k in ("cost", "length_q", "length",
                                                            "kin_sum", "nfz_sum",
@@ -211,6 +214,9 @@ class Engine:
         if want_g:
             n_rows = 3 * (W - 2) + self.geometry.n_obstacles * W
             o["g_rows"] = self.empty((P, n_rows), torch.float64)
+        if n_pairs is not None:
+            o["best_fval_idx"] = self.empty((n_pairs,), torch.int32)
+            o["best_length_idx"] = self.empty((n_pairs,), torch.int32)
         s = _lib.PathOutputs(*[ctypes.c_void_p(o[k].data_ptr()) if k in o else None
                                for k, _ in _lib.PathOutputs._fields_])
         return o, s
@@ -243,7 +249,7 @@ class Engine:
         Q = pr.shape[0]
         if outputs is None:
             o, s = self._outputs(Q * D, self.params.N + 2, self._mode(raster),
-                                 want_cells and raster is not None, False)
+                                 want_cells and raster is not None, False, n_pairs=Q)
         else:
             o, s = outputs
         geo = None if raster is None else ctypes.byref(raster.geo.as_struct())

@@ -53,10 +53,8 @@ class Solver:
         out = eng.eval_generated(self._pair(), arc_table(self.problem.N, ds), raster=raster)
         res = {k: v.cpu().numpy() for k, v in out.items()}
         res["fval"] = np.sqrt(res["cost"])
-        best_f = eng.argmin(out["cost"], len(ds), True).cpu().numpy()
-        best_l = eng.argmin(out["length"], len(ds), False).cpu().numpy()
-        res["min_fval_index"] = int(best_f[0])
-        res["min_length_index"] = int(best_l[0])
+        res["min_fval_index"] = int(res.pop("best_fval_idx")[0])
+        res["min_length_index"] = int(res.pop("best_length_idx")[0])
         res["displacements"] = np.asarray(ds)
         return res
 
