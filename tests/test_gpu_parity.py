@@ -338,3 +338,40 @@ def test_kernel_variants_bit_identical(eng, oracle_mod, D):
         eng.set_tuning(0)
     with pytest.raises(ValueError):
         eng.set_tuning(99)
+
+
+@pytest.mark.parametrize("enl", [-0.5, -1e-3, 0.0, 1e-3, 0.3, 2.0])
+def test_culling_is_exact_near_boundaries(eng, oracle_mod, enl):
+    """The kernels skip a shape outside a padded box of {h_i < e}; the oracle never skips.
+    Points on vertices, on edges, just inside/outside and on the box margins must agree
+    bit for bit for every output."""
+    rng = np.random.default_rng(int(abs(enl) * 1000) + 11)
+    shapes = [{"kind": "polygon", "vertices": [[0.0, 0.0], [3.0, 0.2], [2.5, 2.0], [0.4, 1.7]]},
+              {"kind": "polygon", "vertices": [[5.0, 5.0], [5.001, 5.0], [5.0005, 5.002]]},
+              {"kind": "ball", "center": [-3.0, 1.0], "r1": 1.5, "r2": 0.4},
+              {"kind": "square", "center": [2.0, -3.0], "r1": 0.7, "r2": 1.9}]
+    spec = {"obstacles": shapes, "regions": [{"name": "A", "color": "Red", "shapes": shapes}],
+            "x_start": [0.0, 0.0], "x_goal": [1.0, 1.0]}
+    pts = []
+    for s in shapes:
+        if s["kind"] == "polygon":
+            v = np.asarray(s["vertices"])
+            pts += list(v)
+            for i in range(len(v)):
+                a, b = v[i], v[(i + 1) % len(v)]
+                for t in np.linspace(0, 1, 7):
+                    m = a + t * (b - a)
+                    pts += [m, m + rng.normal(scale=1e-9, size=2), m + rng.normal(scale=1e-3, size=2)]
+        else:
+            c = np.asarray(s["center"], float)
+            pts += [c + rng.normal(scale=2.0, size=2) for _ in range(60)]
+    lo, hi = np.min(pts, 0) - 3, np.max(pts, 0) + 3
+    pts += list(rng.uniform(lo, hi, size=(2000, 2)))
+    pts = np.asarray(pts, dtype=np.float64)
+    for opts in ({"penalty_smooth": True, "obstacle_smooth": True},
+                 {"penalty_smooth": False, "obstacle_smooth": False}):
+        orc = _setup(eng, oracle_mod, spec, 4, opts, 1.1, 0.3, enl, [7.0])
+        ge = eng.eval_points(pts)
+        oe = orc.eval_points(pts)
+        for k in ("phi", "phi_regions", "obs_norm", "psi_raw", "collide"):
+            np.testing.assert_array_equal(_np(ge[k]), oe[k], err_msg=f"{k} opts={opts}")

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/uampath.h"
 
@@ -44,12 +45,29 @@ struct alignas(16) DevIneq {  // 64 B: one s_load_dwordx16
     double pad1;
 };
 
-struct alignas(16) DevShape {  // 48 B
-    int32_t first, count, has_center, pad;
+// Shape culling (see shape_box): outside box_pen / box_obs the smooth penalty of the shape is
+// exactly +0 (some factor min(h_i - e, 0) is 0), so skipping it leaves every sum bit-identical.
+enum : int32_t {
+    SHAPE_BOX_PEN_OK = 1,   // host: box_pen bounds {h_i < enlargement for all i}
+    SHAPE_BOX_OBS_OK = 2,   // host: box_obs bounds {h_i < 1e-14 for all i}
+    SHAPE_CULL_PEN = 4,     // device: region penalty term may be skipped outside box_pen
+    SHAPE_CULL_PSI = 8,     // device: raw obstacle psi may be skipped outside box_obs
+    SHAPE_CULL_HIT = 16     // device: contains() may be skipped outside box_obs
+};
+
+struct alignas(16) DevShape {  // 128 B
+    int32_t first, count, has_center, flags;
     double norm_pen;  // psi(centre; penalty_smooth, e)
     double norm_obs;  // psi(centre; obstacle_smooth, e)
     double cx, cy;
+    double box_pen[4];  // xmin, xmax, ymin, ymax
+    double box_obs[4];
+    double pad[2];
 };
+
+__host__ __device__ __forceinline__ bool outside(const double* b, double x0, double x1) {
+    return x0 < b[0] || x0 > b[1] || x1 < b[2] || x1 > b[3];  // NaN -> false (evaluate)
+}
 
 struct KGeom {
     const DevIneq* __restrict__ ineq;
@@ -145,7 +163,8 @@ __device__ __forceinline__ double region_penalty(const KGeom& g, const KParams& 
     double t = 0.0;
     const int s1 = g.region_first[r + 1];
     for (int s = g.region_first[r]; s < s1; ++s) {
-        const DevShape sh = g.shape[s];
+        const DevShape& sh = g.shape[s];
+        if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;  // adds +0
         double v = psi(g, sh, x0, x1, p.penalty_smooth != 0, p.enlargement);
         t = sh.has_center ? t + v / sh.norm_pen : t + v;
     }
@@ -163,7 +182,8 @@ __device__ __forceinline__ double total_penalty(const KGeom& g, const KParams& p
 __device__ __forceinline__ bool collides(const KGeom& g, double x0, double x1) {
     bool hit = false;
     for (int s = 0; s < g.n_obstacles; ++s) {
-        const DevShape sh = g.shape[s];
+        const DevShape& sh = g.shape[s];
+        if ((sh.flags & SHAPE_CULL_HIT) && outside(sh.box_obs, x0, x1)) continue;
         hit = hit || contains(g, sh, x0, x1);
     }
     return hit;
@@ -174,10 +194,19 @@ __device__ __forceinline__ double obstacle_psi_sum(const KGeom& g, const KParams
                                                    double x1) {
     double acc = 0.0;
     for (int s = 0; s < g.n_obstacles; ++s) {
-        const DevShape sh = g.shape[s];
+        const DevShape& sh = g.shape[s];
+        if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) continue;
         acc = acc + psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
     }
     return acc;
+}
+
+// raw psi of obstacle s (a no-fly g row): exactly +0 when culled
+__device__ __forceinline__ double obstacle_psi(const KGeom& g, const KParams& p, int s, double x0,
+                                               double x1) {
+    const DevShape& sh = g.shape[s];
+    if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) return 0.0;
+    return psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -190,6 +219,13 @@ __global__ void k_prepare(KGeom g, KParams p, DevShape* __restrict__ shapes, int
     sh.has_center = !(isnan(sh.cx) || isnan(sh.cy));
     sh.norm_pen = psi(g, sh, sh.cx, sh.cy, p.penalty_smooth != 0, p.enlargement);
     sh.norm_obs = psi(g, sh, sh.cx, sh.cy, p.obstacle_smooth != 0, p.enlargement);
+    int32_t f = sh.flags & (SHAPE_BOX_PEN_OK | SHAPE_BOX_OBS_OK);
+    // v / norm with v = +0 stays +0 only for a finite positive normaliser (0/0 = NaN must stay)
+    const bool norm_ok = !sh.has_center || (isfinite(sh.norm_pen) && sh.norm_pen > 0.0);
+    if ((f & SHAPE_BOX_PEN_OK) && p.penalty_smooth && norm_ok) f |= SHAPE_CULL_PEN;
+    if ((f & SHAPE_BOX_OBS_OK) && p.obstacle_smooth) f |= SHAPE_CULL_PSI;
+    if (f & SHAPE_BOX_OBS_OK) f |= SHAPE_CULL_HIT;
+    sh.flags = f;
     shapes[s] = sh;
 }
 
@@ -433,8 +469,7 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
             src.at(j, x0, x1);
             a.cost = a.cost + total_penalty(g, p, x0, x1) / dN;
             for (int s = 0; s < g.n_obstacles; ++s) {
-                const DevShape sh = g.shape[s];
-                const double v = psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+                const double v = obstacle_psi(g, p, s, x0, x1);
                 a.nsum = a.nsum + v;
                 if (grow) grow[3 * N + s * W + j] = v;
             }
@@ -713,6 +748,76 @@ int grid_for(int64_t n, int block, int64_t cap = 1 << 20) {
     return (int)b;
 }
 
+// Conservative axis-aligned box of {x : h_i(x) < e for all inequalities i of a shape},
+// padded by 1e-6 km (>> float64 error of h) so that x outside the box has some h_i(x) >= e
+// exactly as the kernels compute it.  Returns false when no safe box is known (no culling).
+bool shape_box(const DevIneq* q, int n, double e, double box[4]) {
+    if (n < 1) return false;
+    const int kind = q[0].kind;
+    for (int i = 1; i < n; ++i)
+        if (q[i].kind != kind) return false;
+    double b[4] = {INFINITY, -INFINITY, INFINITY, -INFINITY};
+    if (kind == UAM_INEQ_ELLIPSE) {
+        if (n != 1) return false;
+        const double s = 1.0 + e;
+        if (!(s > 0.0)) {  // empty region: every point is outside
+            box[0] = INFINITY, box[1] = -INFINITY, box[2] = INFINITY, box[3] = -INFINITY;
+            return s <= 0.0;
+        }
+        const double k = std::sqrt(s), r1 = std::fabs(q[0].p[2]), r2 = std::fabs(q[0].p[3]);
+        b[0] = q[0].p[0] - r1 * k, b[1] = q[0].p[0] + r1 * k;
+        b[2] = q[0].p[1] - r2 * k, b[3] = q[0].p[1] + r2 * k;
+    } else if (kind == UAM_INEQ_AXIS) {
+        for (int i = 0; i < n; ++i) {
+            const int k = q[i].p[0] == 0.0 ? 0 : 1;
+            const double c = q[i].p[1], r = q[i].p[2], sg = q[i].p[3];
+            if (sg > 0) b[2 * k + 1] = std::fmin(b[2 * k + 1], c + r + e);  // x_k < c + r + e
+            else if (sg < 0) b[2 * k] = std::fmax(b[2 * k], c - r - e);     // x_k > c - r - e
+            else return false;
+        }
+    } else {  // half-planes a x + b y < c, vertices among pairwise intersections
+        if (n < 3) return false;
+        std::vector<double> A(n), B(n), C(n);
+        for (int i = 0; i < n; ++i) {
+            const double* p = q[i].p;  // {ax, ay, dx, dy, s}
+            A[i] = p[4] * p[3];
+            B[i] = -p[4] * p[2];
+            C[i] = e + p[4] * (p[3] * p[0] - p[2] * p[1]);
+        }
+        int found = 0;
+        for (int i = 0; i < n; ++i)
+            for (int j = i + 1; j < n; ++j) {
+                const double det = A[i] * B[j] - A[j] * B[i];
+                if (!(std::fabs(det) > 1e-300)) continue;
+                const double x = (C[i] * B[j] - C[j] * B[i]) / det;
+                const double y = (A[i] * C[j] - A[j] * C[i]) / det;
+                bool feas = std::isfinite(x) && std::isfinite(y);
+                for (int k = 0; k < n && feas; ++k) {
+                    const double tol =
+                        1e-9 * (std::fabs(A[k] * x) + std::fabs(B[k] * y) + std::fabs(C[k])) + 1e-12;
+                    feas = A[k] * x + B[k] * y <= C[k] + tol;
+                }
+                if (!feas) continue;
+                ++found;
+                b[0] = std::fmin(b[0], x), b[1] = std::fmax(b[1], x);
+                b[2] = std::fmin(b[2], y), b[3] = std::fmax(b[3], y);
+            }
+        if (found < 3) return false;
+        // sanity for e >= 0: the polygon's own vertices (edge start points) lie inside
+        if (e >= 0)
+            for (int i = 0; i < n; ++i)
+                if (q[i].p[0] < b[0] - 1e-9 || q[i].p[0] > b[1] + 1e-9 ||
+                    q[i].p[1] < b[2] - 1e-9 || q[i].p[1] > b[3] + 1e-9)
+                    return false;
+    }
+    for (int k = 0; k < 4; ++k)
+        if (!std::isfinite(b[k])) return false;
+    const double m = 1e-6 * (1.0 + std::fmax(std::fmax(std::fabs(b[0]), std::fabs(b[1])),
+                                             std::fmax(std::fabs(b[2]), std::fabs(b[3]))));
+    box[0] = b[0] - m, box[1] = b[1] + m, box[2] = b[2] - m, box[3] = b[3] + m;
+    return true;
+}
+
 }  // namespace
 
 struct uam_ctx {
@@ -724,6 +829,8 @@ struct uam_ctx {
     KParams kp{};
     bool have_geom = false, have_params = false;
     int variant = 0;  // uam_set_tuning; 0 = default
+    std::vector<DevIneq> h_ineq;
+    std::vector<DevShape> h_shape;
 };
 
 namespace {
@@ -862,6 +969,8 @@ int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
     HIP_TRY(hipMemcpy(ctx->d_shape, hs.data(), hs.size(), hipMemcpyHostToDevice));
     ctx->n_ineq = ni;
     ctx->n_shapes = ns;
+    ctx->h_ineq.assign(ti, ti + ni);
+    ctx->h_shape.assign(ts, ts + ns);
     KGeom& kg = ctx->kg;
     kg.ineq = ctx->d_ineq;
     kg.shape = ctx->d_shape;
@@ -897,7 +1006,16 @@ int uam_set_params(uam_ctx* ctx, const uam_params* prm, uam_stream stream) {
     k.altitude = prm->altitude;
     for (int r = 0; r < UAM_MAX_REGIONS; ++r) k.weights[r] = prm->weights[r];
     DeviceGuard dg(ctx->device);
+    for (int sh = 0; sh < ctx->n_shapes; ++sh) {
+        DevShape& d = ctx->h_shape[sh];
+        const DevIneq* q = ctx->h_ineq.data() + d.first;
+        d.flags = 0;
+        if (shape_box(q, d.count, prm->enlargement, d.box_pen)) d.flags |= SHAPE_BOX_PEN_OK;
+        if (shape_box(q, d.count, 1e-14, d.box_obs)) d.flags |= SHAPE_BOX_OBS_OK;
+    }
     if (ctx->n_shapes > 0) {
+        HIP_TRY(hipMemcpy(ctx->d_shape, ctx->h_shape.data(), sizeof(DevShape) * ctx->n_shapes,
+                          hipMemcpyHostToDevice));
         hipLaunchKernelGGL(k_prepare, dim3(grid_for(ctx->n_shapes, 64)), dim3(64), 0,
                            (hipStream_t)stream, ctx->kg, k, ctx->d_shape, ctx->n_shapes);
         HIP_TRY(hipGetLastError());
