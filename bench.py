@@ -68,6 +68,7 @@ def main():
         torch.cuda.set_device(local)
 
     from uam_path_planning_amd import build
+    from uam_path_planning_amd import distributed as D
     build.build_library()
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import CostRaster, Engine
@@ -114,16 +115,12 @@ def main():
             raster = CostRaster(geo, eng.empty((R, R, 4), torch.int32))
         if world > 1:
             dist.barrier()
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            dist.broadcast(raster.rec, src=0)
-            torch.cuda.synchronize()
-            setup["raster_bcast_ms"] = round((time.perf_counter() - t2) * 1e3, 3)
+            secs = D.broadcast_raster(raster.rec, src=0)
+            setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = raster.nbytes
 
     # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
-    all_pairs = random_pairs(Q * world, seed=0)
-    pairs_host = all_pairs[rank * Q:(rank + 1) * Q]
+    pairs_host = D.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
@@ -157,9 +154,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.torch_device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
 
     total_paths = P * world * args.steps
     value = total_paths / elapsed

@@ -1,0 +1,91 @@
+"""world_size-2 gloo tests (CPU) of the multi-GPU plumbing used by bench.py: weak pair
+sharding, the one-time raster broadcast, max-over-ranks timing and the cross-rank best
+candidate (bit-identical to the single-rank answer)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from uam_path_planning_amd import distributed as D
+        from uam_path_planning_amd.synthetic import random_pairs
+
+        res = {}
+        per = 1000
+        allp = random_pairs(per * world, seed=0)
+        mine = D.weak_shard(allp, per, rank, world)
+        res["shard_sum"] = float(mine.sum())
+        res["shard_first"] = mine[0].tolist()
+        # rank 0 owns the raster; others receive it
+        rec = torch.zeros((32, 48, 4), dtype=torch.int32)
+        if rank == 0:
+            g = torch.Generator().manual_seed(123)
+            rec = torch.randint(-2**31, 2**31 - 1, (32, 48, 4), dtype=torch.int32, generator=g)
+        secs = D.broadcast_raster(rec, src=0)
+        res["rec_checksum"] = int(rec.to(torch.int64).sum())
+        res["bcast_s"] = secs
+        res["max"] = D.max_over_ranks([float(rank), 10.0 - rank])
+        # a cost vector per rank: global best must equal the single-process answer
+        costs = torch.tensor(np.random.default_rng(rank + 5).uniform(1, 2, size=50))
+        if rank == 1:
+            costs[7] = 0.25          # global best lives on rank 1
+            costs[9] = 0.25          # tie: lower global index (50 + 7) wins
+        best = D.global_best(costs, local_offset=rank * 50)
+        res["best"] = best
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    allp = random_pairs(2000, seed=0)
+    assert out[0]["shard_first"] == allp[0].tolist()
+    assert out[1]["shard_first"] == allp[1000].tolist()
+    assert out[0]["shard_sum"] + out[1]["shard_sum"] == pytest.approx(float(allp.sum()))
+    assert out[0]["rec_checksum"] == out[1]["rec_checksum"] != 0
+    assert out[0]["max"] == out[1]["max"] == [1.0, 10.0]
+    assert out[0]["best"] == out[1]["best"] == (0.5, 57)
+
+
+def test_shard_ranges_cover():
+    from uam_path_planning_amd.distributed import shard_range
+
+    for n in (0, 1, 7, 100, 12345):
+        for world in (1, 2, 3, 8):
+            got = [shard_range(n, r, world) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+            assert max(h - lo for lo, h in got) - min(h - lo for lo, h in got) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)

@@ -1,0 +1,92 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed (RCCL over xGMI on the GPU box,
+gloo for CPU tests).
+
+The path shards with no data-path collective: pairs are independent and every displacement of a
+pair stays on one rank, so the reference's per-pair selection (main.py:175-180) is local.  The
+only exchange is the one-time broadcast of the cost raster from the rank that built it, plus
+scalar max/all-gather reductions outside the timed region.
+"""
+import os
+import time
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist
+
+
+def env_rank():
+    """(rank, world_size, local_rank) from the torchrun environment (defaults: single rank)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_range(n, rank, world):
+    """Contiguous shard [lo, hi) of n items for rank r of world (sizes differ by <= 1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank {rank} of world {world}")
+    return n * rank // world, n * (rank + 1) // world
+
+
+def weak_shard(global_pairs, per_rank, rank, world):
+    """Weak scaling: every rank owns per_rank consecutive pairs of one seeded global set."""
+    if len(global_pairs) < per_rank * world:
+        raise ValueError("global pair set smaller than per_rank * world")
+    return global_pairs[rank * per_rank:(rank + 1) * per_rank]
+
+
+def broadcast_raster(rec, src=0, group=None):
+    """Broadcast the record raster tensor (in place) from src; returns seconds taken
+    (synchronised on the tensor's device before and after)."""
+    import torch
+
+    dist = _dist()
+    dev = rec.device
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dist.broadcast(rec, src=src, group=group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(values, device=None):
+    """Element-wise max of a list of floats over all ranks."""
+    import torch
+
+    dist = _dist()
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64,
+                     device=device if device is not None else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
+
+
+def global_best(local_values, local_offset, take_sqrt=True):
+    """Best candidate over all ranks with the reference's rule (strict '<' on fval =
+    sqrt(cost), ties to the lowest global index, NaN never wins) -- identical to the single
+    GPU answer.  local_values: 1-D CPU float64 tensor of this rank's per-path costs."""
+    import torch
+
+    dist = _dist()
+    v = local_values.to(torch.float64)
+    f = torch.sqrt(v) if take_sqrt else v
+    ok = ~torch.isnan(f)
+    if ok.any():
+        fv = torch.where(ok, f, torch.full_like(f, float("inf")))
+        i = int(torch.argmin(fv))           # torch.argmin returns the first minimum
+        cand = torch.tensor([float(f[i]), float(local_offset + i)], dtype=torch.float64)
+    else:
+        cand = torch.tensor([float("nan"), float("inf")], dtype=torch.float64)
+    world = dist.get_world_size()
+    allc = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(allc, cand)
+    best_v, best_i = float("nan"), -1
+    for c in allc:
+        cv, ci = float(c[0]), c[1]
+        if cv != cv:
+            continue
+        if best_i < 0 or cv < best_v or (cv == best_v and ci < best_i):
+            best_v, best_i = cv, int(ci)
+    return best_v, best_i
