@@ -1,0 +1,94 @@
+"""DEM ingest and cost-raster build -- the hot-path part of the reference's
+map_generation/data_manager.py (DataManager, 8-86).
+
+* ``load_dem(path)``: a single GeoTIFF or a VRT tile mosaic (mergeLL.vrt layout); VRT tiles are
+  placed by the device mosaic kernel.
+* ``load_dem_mask(path, threshold_dem)``: the mask of load_dem_polygons_from_geotiff
+  (data_manager.py:14-17): ``dem == -9999`` when threshold_dem == -9999, else ``dem > thr``,
+  computed on the GPU as the MASK flag bit of the cost-raster build (K1).
+* ``build_cost_raster(...)``: DEM -> device record raster {Φ, Σψ_nfz, dem, flags} (K1).
+* ``save_polygons(vertex_lists, path)``: the D1 text format of data_manager.py:56-81
+  (coordinates / 1000, m -> km), readable by path_generation.utils.get_var_from_file.
+Polygonisation (rasterio.features.shapes + shapely, data_manager.py:18-19) and shapefile IO
+(geopandas) are out of scope.
+"""
+from ..engine import RasterGeo, default_engine
+from .geotiff import read_geotiff
+from .vrt import load_tiles, read_vrt
+
+
+def geo_from_geotransform(width, height, gt, nodata=-9999.0, dem_threshold=0.0):
+    x0, dx, rx, ytop, ry, ndy = gt
+    if rx != 0 or ry != 0:
+        raise ValueError("rotated geotransforms are not supported")
+    if not (dx > 0 and ndy < 0):
+        raise ValueError("expected north-up rasters (dx > 0, dy < 0)")
+    return RasterGeo(nx=int(width), ny=int(height), x0=float(x0), y_top=float(ytop),
+                     dx=float(dx), dy=float(-ndy), nodata=float(nodata),
+                     dem_threshold=float(dem_threshold))
+
+
+class DataManager:
+    def __init__(self, engine=None):
+        self._engine = engine
+
+    @property
+    def engine(self):
+        return self._engine if self._engine is not None else default_engine()
+
+    def load_dem(self, input_file, dem_threshold=0.0):
+        """-> (dem device tensor [ny][nx] float32, RasterGeo)."""
+        eng = self.engine
+        if input_file.lower().endswith(".vrt"):
+            v = read_vrt(input_file)
+            nod = -9999.0 if v.nodata is None else v.nodata
+            tiles, xo, yo = load_tiles(v)
+            dem = eng.dem_mosaic(tiles, xo, yo, v.width, v.height, fill=nod)
+            return dem, geo_from_geotransform(v.width, v.height, v.geotransform, nod,
+                                              dem_threshold)
+        data, gt, nod = read_geotiff(input_file)
+        nod = -9999.0 if nod is None else nod
+        import torch
+
+        dem = eng.tensor(data, torch.float32)
+        gt = gt or (0.0, 1.0, 0.0, float(data.shape[0]), 0.0, -1.0)
+        return dem, geo_from_geotransform(data.shape[1], data.shape[0], gt, nod, dem_threshold)
+
+    def build_cost_raster(self, input_file, geometry, params, dem_threshold=0.0):
+        eng = self.engine
+        dem, geo = self.load_dem(input_file, dem_threshold)
+        eng.set_geometry(geometry)
+        eng.set_params(params)
+        return eng.raster_build(geo, dem)
+
+    def load_dem_mask(self, input_file, threshold_dem=0):
+        """Boolean mask [rows][cols] of data_manager.py:14-17, evaluated on the GPU (K1)."""
+        from ..engine import Engine, PathParams
+        from ..geometry import compile_shapes
+
+        eng = Engine(self.engine.device)
+        dem, geo = DataManager(eng).load_dem(input_file, float(threshold_dem))
+        eng.set_geometry(compile_shapes((), []))
+        eng.set_params(PathParams(N=1))
+        rec = eng.raster_build(geo, dem).rec
+        return ((rec[..., 3] & 2) != 0).cpu().numpy()
+
+    def load_dem_polygons_from_geotiff(self, input_file, threshold_dem=0):
+        raise NotImplementedError("polygonising the DEM mask (rasterio.features.shapes + "
+                                  "shapely) is outside the device hot path; use "
+                                  "load_dem_mask() for the mask itself")
+
+    @staticmethod
+    def save_polygons(polygons, output_file):
+        """polygons: list of vertex lists [[x, y], ...] in metres (closing vertex optional)."""
+        with open(output_file, "w") as f:
+            f.write("vertices = [")
+            for i, pts in enumerate(polygons):
+                pts = [tuple(p) for p in pts]
+                if len(pts) > 1 and pts[0] == pts[-1]:
+                    pts = pts[:-1]
+                body = ", ".join("[" + str(x / 1000) + ", " + str(y / 1000) + "]"
+                                 for x, y in pts)
+                f.write("polygon(" + body + (")\n" if i == len(polygons) - 1 else "),\n"))
+            f.write("]")
+
