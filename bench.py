@@ -68,7 +68,7 @@ def main():
         torch.cuda.set_device(local)
 
     from uam_path_planning_amd import build
-    from uam_path_planning_amd import distributed as D
+    from uam_path_planning_amd import distributed as udist
     build.build_library()
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import CostRaster, Engine
@@ -115,12 +115,12 @@ def main():
             raster = CostRaster(geo, eng.empty((R, R, 4), torch.int32))
         if world > 1:
             dist.barrier()
-            secs = D.broadcast_raster(raster.rec, src=0)
+            secs = udist.broadcast_raster(raster.rec, src=0)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = raster.nbytes
 
     # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
-    pairs_host = D.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
+    pairs_host = udist.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
@@ -154,7 +154,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     if world > 1:
-        elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
+        elapsed, kern_ms = udist.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
 
     total_paths = P * world * args.steps
     value = total_paths / elapsed
