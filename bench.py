@@ -31,6 +31,8 @@ import torch  # noqa: E402
 
 METRIC = "candidate-paths/sec + waypoint-evals/sec on N×N DEM at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# independent random 16-B gathers from a 256 MiB table, one MI355X (profiles/r01/gather_ceiling.log)
+RANDOM_GATHER_CEILING = 55.5e9
 
 
 def parse():
@@ -198,11 +200,20 @@ def main():
         "waypoint_evals_per_s": round(value * W, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "k_eval_generated<raster>" if raster_mode
-                     else "k_eval_generated<analytic>",
+                     "traffic": traffic,
+                     "kernel": ("k_eval_pairs<raster>" if raster_mode
+                                else "k_eval_pairs<analytic>") + f" (variant {args.variant or 2})",
                      "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_path": bytes_per_path,
-                     "algorithmic_bytes_per_launch": launch_bytes},
+                     "algorithmic_bytes_per_launch": launch_bytes,
+                     "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if traffic else None),
+                     "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1) if raster_mode else None,
+                     "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING if raster_mode
+                     else None,
+                     "note": "each 16-B record gather moves one 128-B line (PMC); the measured "
+                             "random-gather ceiling (tools/gather_ceiling.hip) bounds the "
+                             "kernel, see DESIGN.md §5"},
         "setup": setup,
     }
 
