@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg3")
-    ap.add_argument("--mode", default="raster", choices=["raster", "analytic"])
+    ap.add_argument("--mode", default=None, choices=["raster", "analytic", "volume"],
+                    help="default: the workload's mode (raster; volume for cfg5)")
     ap.add_argument("--pairs", type=int, default=None, help="override pairs per GPU")
     ap.add_argument("--R", type=int, default=None, help="override raster size")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -73,11 +74,12 @@ def main():
     from uam_path_planning_amd import distributed as udist
     build.build_library()
     from uam_path_planning_amd.arcs import arc_table
-    from uam_path_planning_amd.engine import CostRaster, Engine
+    from uam_path_planning_amd.engine import CostRaster, Engine, RiskVolume, VolumeGeo
     from uam_path_planning_amd.geometry import compile_map
     from uam_path_planning_amd.scenario import (CONFIGS, build_region_map, canonical_params,
-                                                canonical_spec, displacements, raster_geo)
-    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+                                                canonical_spec, displacements, layer_weights,
+                                                raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs, random_pairs3d, synthetic_dem
 
     cfg = dict(CONFIGS[args.workload])
     if args.pairs:
@@ -86,7 +88,10 @@ def main():
         cfg["R"] = args.R
     R, Q, D, N = cfg["R"], cfg["pairs"], cfg["D"], cfg["N"]
     W = N + 2
-    raster_mode = args.mode == "raster"
+    mode = args.mode or cfg["mode"]
+    args.mode = mode
+    raster_mode = mode == "raster"
+    volume_mode = mode == "volume"
 
     spec = canonical_spec(nfz_polygons=cfg["nfz_polygons"])
     geom = compile_map(build_region_map(spec))
@@ -96,12 +101,11 @@ def main():
     eng.set_params(params)
     ut_host = arc_table(N, displacements(D))
 
-    # ---- cost raster: rank 0 builds (K1), one RCCL broadcast -------------------------------
+    # ---- cost raster / volume: rank 0 builds (K1), one RCCL broadcast --------------------
     setup = {}
     geo = raster_geo(R)
-    raster = None
-    dem = None
-    if raster_mode:
+    raster = volume = None
+    if raster_mode or volume_mode:
         t0 = time.perf_counter()
         if rank == 0:
             dem = synthetic_dem(R)
@@ -112,17 +116,31 @@ def main():
             raster = eng.raster_build(geo, dem_dev)
             torch.cuda.synchronize()
             setup["raster_build_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+            if volume_mode:
+                t2 = time.perf_counter()
+                volume = eng.volume_build(raster, cfg["nz"], cfg["z0"], cfg["dz"],
+                                          layer_weights(cfg["nz"]))
+                torch.cuda.synchronize()
+                setup["volume_build_ms"] = round((time.perf_counter() - t2) * 1e3, 3)
             del dem_dev
         else:
             raster = CostRaster(geo, eng.empty((R, R, 4), torch.int32))
+            if volume_mode:
+                vg = VolumeGeo(R, R, cfg["nz"], geo.x0, geo.y_top, geo.dx, geo.dy, cfg["z0"],
+                               cfg["dz"])
+                volume = RiskVolume(vg, eng.empty((R, R, cfg["nz"], 4), torch.int32))
         if world > 1:
             dist.barrier()
-            secs = udist.broadcast_raster(raster.rec, src=0)
+            table = volume.vox if volume_mode else raster.rec
+            secs = udist.broadcast_raster(table, src=0)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
-            setup["raster_bytes"] = raster.nbytes
+            setup["raster_bytes"] = table.numel() * 4
 
     # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
-    pairs_host = udist.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
+    if volume_mode:
+        pairs_host = udist.weak_shard(random_pairs3d(Q * world, seed=0), Q, rank, world)
+    else:
+        pairs_host = udist.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
@@ -135,7 +153,10 @@ def main():
         # one launch: arc generation + gather + cost reduction + candidate selection
         if ev is not None:
             ev[0].record()
-        eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
+        if volume_mode:
+            eng.eval_generated3d(pairs, ut, volume, outputs=outs)
+        else:
+            eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
         if ev is not None:
             ev[1].record()
 
@@ -161,9 +182,10 @@ def main():
     total_paths = P * world * args.steps
     value = total_paths / elapsed
     # algorithmic bytes per launch of the dominant kernel
-    gather_b = 16 * W if raster_mode else 0
-    pair_b = 32.0 / D
-    out_b = 6 * 8 + 2 * 4 + 8.0 / D   # 6 f64 + 2 i32 per path, 2 i32 best indices per pair
+    gather_b = 16 * W if (raster_mode or volume_mode) else 0
+    pair_b = (48.0 if volume_mode else 32.0) / D
+    # 6 f64 + 3 i32 per path (nfz_hits, offmap, below_terrain), 2 i32 best indices per pair
+    out_b = 6 * 8 + 3 * 4 + 8.0 / D
     bytes_per_path = gather_b + pair_b + out_b
     launch_bytes = bytes_per_path * P
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
@@ -201,16 +223,15 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": ("k_eval_pairs<raster>" if raster_mode
-                                else "k_eval_pairs<analytic>") + f" (variant {args.variant or 2})",
+                     "kernel": f"k_eval_pairs<{mode}>" + (
+                         f" (variant {args.variant or 2})" if raster_mode else ""),
                      "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_path": bytes_per_path,
                      "algorithmic_bytes_per_launch": launch_bytes,
                      "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                       if traffic else None),
-                     "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1) if raster_mode else None,
-                     "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING if raster_mode
-                     else None,
+                     "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1) if gather_b else None,
+                     "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING if gather_b else None,
                      "note": "each 16-B record gather moves one 128-B line (PMC); the measured "
                              "random-gather ceiling (tools/gather_ceiling.hip) bounds the "
                              "kernel, see DESIGN.md §5"},
@@ -224,21 +245,26 @@ def main():
         orc = O.Oracle(O.compile_spec(spec), N, spec["options"], spec["maxratio"],
                        spec["maxalpha"], spec["enlargement"], spec["weights"],
                        altitude=params.altitude)
-        rd = rec = None
+        rd = rec = vd = vox = None
         if raster_mode:
             rd = O.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
                                       geo.nodata, geo.dem_threshold)
             rec = raster.rec.cpu().numpy().view(np.float32)
+        if volume_mode:
+            g3 = volume.geo
+            vd = O.volume_desc(g3.nx, g3.ny, g3.nz, g3.x0, g3.y_top, g3.dx, g3.dy, g3.z0, g3.dz)
+            vox = volume.vox.cpu().numpy().view(np.float32)
         gpu_cost = o["cost"].cpu().numpy()
         gpu_best = o["best_fval_idx"].cpu().numpy()
-        chunk = 2000 if raster_mode else 50
+        chunk = 50 if mode == "analytic" else 2000
         done, t_cpu, mism, bmis = 0, 0.0, 0, 0
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
-            wp = O.gen_paths(sl, ut_host)
-            r = orc.eval_paths(wp, mode="raster" if raster_mode else "analytic", rdesc=rd,
-                               rec=rec)
+            if volume_mode:
+                r = orc.eval_paths3d(O.gen_paths3d(sl, ut_host), vd, vox)
+            else:
+                r = orc.eval_paths(O.gen_paths(sl, ut_host), mode=mode, rdesc=rd, rec=rec)
             t_cpu += time.perf_counter() - ts
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
@@ -248,7 +274,7 @@ def main():
             "kind": "port",
             "sample": f"first {done} of {Q} pairs x {D} displacements ({done * D} paths, "
                       f"{t_cpu:.1f} s) through oracle/uam_oracle.c (gcc -O2, 1 thread): "
-                      "arc generation + raster gather + cost reduction"}
+                      f"arc generation + {mode} evaluation + cost reduction"}
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
                             "best_index_mismatches": bmis,
                             "rule": "bit-exact float64 vs CPU oracle"}

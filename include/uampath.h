@@ -66,10 +66,11 @@ enum {
     UAM_INEQ_AXIS = 2       /* square side h = s*(x_k - c) - r; p = {k, c, r, s, 0, 0} */
 };
 
-enum { UAM_MODE_ANALYTIC = 0, UAM_MODE_RASTER = 1 };
+enum { UAM_MODE_ANALYTIC = 0, UAM_MODE_RASTER = 1, UAM_MODE_VOLUME = 2 };
 
-/* record flag bits (record = {float phi, float psi_nfz, float dem, uint32 flags}) */
-enum { UAM_FLAG_NFZ = 1u, UAM_FLAG_MASK = 2u, UAM_FLAG_NODATA = 4u };
+/* record flag bits (record = {float phi, float psi_nfz, float dem, uint32 flags}; a volume
+ * voxel = {float risk, float psi_nfz, float terrain, uint32 flags}) */
+enum { UAM_FLAG_NFZ = 1u, UAM_FLAG_MASK = 2u, UAM_FLAG_NODATA = 4u, UAM_FLAG_BELOW_TERRAIN = 8u };
 
 typedef struct uam_ctx uam_ctx;
 typedef void* uam_stream; /* hipStream_t */
@@ -119,6 +120,15 @@ typedef struct {
                               (dem > thr) */
 } uam_raster_desc;
 
+/* 3-D risk volume (BASELINE config 5; no reference counterpart): the raster's x/y grid
+ * times nz altitude layers [z0 + iz*dz, z0 + (iz+1)*dz) in metres; voxels [ny][nx][nz]
+ * (layer fastest), 16 bytes each; iz = floor((z - z0) * (1/dz)). */
+typedef struct {
+    int32_t nx, ny, nz;
+    double x0, y_top, dx, dy;
+    double z0, dz;
+} uam_volume_desc;
+
 /* Per-path outputs (device pointers, any may be NULL).  Index p of a path. */
 typedef struct {
     double* cost;          /* get_cost (problem.py:38-44) */
@@ -127,13 +137,16 @@ typedef struct {
     double* kin_sum;       /* sum of the 3N kinematic g rows (problem.py:100-107) */
     double* nfz_sum;       /* sum of the no-fly g rows (problem.py:109-112) */
     int32_t* nfz_hits;     /* waypoints inside a no-fly zone (Map.collides) */
-    double* min_clearance; /* raster: altitude - max terrain over the waypoints; analytic NaN */
+    double* min_clearance; /* raster: altitude - max terrain over the waypoints; volume: min
+                              over waypoints of (waypoint altitude - terrain); analytic NaN */
     int32_t* offmap;       /* raster: waypoints outside the raster */
     int32_t* cells;        /* [P][W] raster cell index iy*nx+ix, -1 off-raster (raster only) */
     double* g_rows;        /* [P][3N + n_obstacles*W] full get_nonlincon vector (analytic) */
     int32_t* best_fval_idx;   /* uam_eval_generated only: [Q] per pair, the displacement index
                                  the reference keeps as "Min fval result" (main.py:175-177) */
     int32_t* best_length_idx; /* [Q] "Min path length result" (main.py:178-180) */
+    int32_t* below_terrain;   /* volume mode: waypoints whose altitude layer lies below the
+                                 column's terrain */
 } uam_path_outputs;
 
 int uam_abi_version(void);
@@ -191,6 +204,17 @@ int uam_path_length(uam_ctx* ctx, const double* pts_dev, int64_t n_paths, int32_
                     int32_t n_segments, int32_t smooth, double* out_dev, uam_stream stream);
 
 int uam_synchronize(uam_ctx* ctx, uam_stream stream);
+
+/* Config 5: build the volume from a 2-D record raster with the same x/y grid (rec2d_dev),
+ * risk = phi * layer_w[iz] (layer_w_dev [nz] f64). */
+int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* desc, const void* rec2d_dev,
+                     const double* layer_w_dev, void* vol_dev, uam_stream stream);
+/* Config 5 path evaluation: pairs6_dev [Q][6] = (x0, y0, z0, xf, yf, zf) (km, km, m); x/y
+ * candidates as uam_eval_generated, altitude z_j = z0 + (zf - z0) * (j / (N+1)); cost =
+ * (N+1) L + sum_j risk(voxel_j) / N.  D <= 16. */
+int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
+                         const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
+                         int32_t D, const uam_path_outputs* out, uam_stream stream);
 
 /* Kernel variant for uam_eval_generated (0 = default).  1 = one wave per (displacement,
  * 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup per 64 pairs x D

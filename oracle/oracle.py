@@ -45,6 +45,12 @@ class _Raster(ctypes.Structure):
                 ("nodata", ctypes.c_float), ("dem_threshold", ctypes.c_float)]
 
 
+class _Volume(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32),
+                ("x0", ctypes.c_double), ("y_top", ctypes.c_double), ("dx", ctypes.c_double),
+                ("dy", ctypes.c_double), ("z0", ctypes.c_double), ("dz", ctypes.c_double)]
+
+
 def build():
     """Compile liboracle.so (gcc) if it is missing or older than its source."""
     src = os.path.join(HERE, "uam_oracle.c")
@@ -63,7 +69,7 @@ def lib():
             build()
         _lib = ctypes.CDLL(LIB_PATH)
         for name in ("orc_eval_points", "orc_gen_paths", "orc_raster_build", "orc_eval_paths",
-                     "orc_argmin"):
+                     "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d"):
             getattr(_lib, name).restype = ctypes.c_int
     return _lib
 
@@ -99,6 +105,27 @@ class Oracle:
                          0.0 if anchor is None else float(anchor[0]),
                          0.0 if anchor is None else float(anchor[1]),
                          float(maxratio), float(maxalpha), float(enlargement), float(altitude), w)
+
+    # -- volume (config 5) -----------------------------------------------------------------
+    def eval_paths3d(self, wp3, vdesc, vol, want_cells=False):
+        W = self.N + 2
+        wp3 = np.ascontiguousarray(wp3, dtype=np.float64).reshape(-1, W, 3)
+        P = wp3.shape[0]
+        vol = np.ascontiguousarray(vol, dtype=np.float32)
+        out = {k: np.zeros(P) for k in ("cost", "lq", "length", "kin", "nfz", "min_clearance")}
+        for k in ("nfz_hits", "offmap", "below"):
+            out[k] = np.zeros(P, np.int32)
+        cells = np.zeros((P, W), np.int32) if want_cells else None
+        lib().orc_eval_paths3d(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.byref(vdesc),
+                               _ptr(vol, _f32p), _ptr(wp3, _f64p), ctypes.c_int64(P),
+                               _ptr(out["cost"], _f64p), _ptr(out["lq"], _f64p),
+                               _ptr(out["length"], _f64p), _ptr(out["kin"], _f64p),
+                               _ptr(out["nfz"], _f64p), _ptr(out["nfz_hits"], _i32p),
+                               _ptr(out["min_clearance"], _f64p), _ptr(out["offmap"], _i32p),
+                               _ptr(out["below"], _i32p), _ptr(cells, _i32p))
+        if want_cells:
+            out["cells"] = cells
+        return out
 
     # -- points ----------------------------------------------------------------------------
     def eval_points(self, pts):
@@ -154,6 +181,31 @@ class Oracle:
         if want_g:
             out["g"] = g
         return out
+
+
+def volume_desc(nx, ny, nz, x0, y_top, dx, dy, z0, dz):
+    return _Volume(int(nx), int(ny), int(nz), float(x0), float(y_top), float(dx), float(dy),
+                   float(z0), float(dz))
+
+
+def volume_build(vdesc, rec2, layer_w):
+    rec2 = np.ascontiguousarray(rec2, dtype=np.float32)
+    lw = np.ascontiguousarray(layer_w, dtype=np.float64)
+    vol = np.zeros((vdesc.ny, vdesc.nx, vdesc.nz, 4), dtype=np.float32)
+    lib().orc_volume_build(ctypes.byref(vdesc), _ptr(rec2, _f32p), _ptr(lw, _f64p),
+                           _ptr(vol, _f32p))
+    return vol
+
+
+def gen_paths3d(pairs6, utab):
+    pairs6 = np.ascontiguousarray(pairs6, dtype=np.float64).reshape(-1, 6)
+    utab = np.ascontiguousarray(utab, dtype=np.float64)
+    D, N = utab.shape[0], utab.shape[1]
+    out = np.zeros((pairs6.shape[0] * D, N + 2, 3))
+    lib().orc_gen_paths3d(_ptr(pairs6, _f64p), ctypes.c_int64(pairs6.shape[0]),
+                          _ptr(utab, _f64p), ctypes.c_int32(D), ctypes.c_int32(N),
+                          _ptr(out, _f64p))
+    return out
 
 
 def gen_paths(pairs, utab):

@@ -28,6 +28,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define ORC_HALFPLANE 0
@@ -392,5 +393,125 @@ int orc_argmin(const double* v, int64_t groups, int32_t G, int32_t take_sqrt, in
         }
         best[q] = bi;
     }
+    return 0;
+}
+
+/* ---- volume mode (BASELINE config 5; no reference counterpart) --------------------------
+ * Restates the build's own definition (include/uampath.h uam_volume_build /
+ * uam_eval_generated3d): voxel [ny][nx][nz] {risk, psi_nfz, terrain, flags}. */
+#define ORC_FLAG_BELOW 8u
+
+typedef struct {
+    int32_t nx, ny, nz;
+    double x0, y_top, dx, dy, z0, dz;
+} orc_volume;
+
+int orc_volume_build(const orc_volume* v, const float* rec2, const double* layer_w, float* vol) {
+    for (int64_t col = 0; col < (int64_t)v->nx * v->ny; ++col) {
+        uint32_t f2;
+        memcpy(&f2, &rec2[4 * col + 3], 4);
+        float terrain = (f2 & ORC_FLAG_NODATA) ? 0.0f : rec2[4 * col + 2];
+        for (int iz = 0; iz < v->nz; ++iz) {
+            int64_t o = (col * v->nz + iz) * 4;
+            double hc = v->z0 + ((double)iz + 0.5) * v->dz;
+            uint32_t fl = f2 & (ORC_FLAG_NFZ | ORC_FLAG_MASK | ORC_FLAG_NODATA);
+            if (hc < (double)terrain) fl |= ORC_FLAG_BELOW;
+            vol[o + 0] = (float)((double)rec2[4 * col] * layer_w[iz]);
+            vol[o + 1] = rec2[4 * col + 1];
+            vol[o + 2] = terrain;
+            memcpy(&vol[o + 3], &fl, 4);
+        }
+    }
+    return 0;
+}
+
+/* pairs6 [Q][6] = (x0, y0, z0, xf, yf, zf) -> wp3 [Q*D][N+2][3]; x/y as orc_gen_paths,
+ * z_j = z0 + (zf - z0) * (j / (N+1)) */
+int orc_gen_paths3d(const double* pairs6, int64_t Q, const double* utab, int32_t D, int32_t N,
+                    double* out) {
+    int W = N + 2;
+    for (int64_t q = 0; q < Q; ++q) {
+        const double* pr6 = pairs6 + 6 * q;
+        double pr[4] = {pr6[0], pr6[1], pr6[3], pr6[4]};
+        for (int d = 0; d < D; ++d) {
+            double* o = out + ((q * D + d) * (int64_t)W) * 3;
+            for (int j = 0; j < W; ++j) {
+                double px, py;
+                if (j == 0) {
+                    px = pr[0];
+                    py = pr[1];
+                } else if (j == W - 1) {
+                    px = pr[2];
+                    py = pr[3];
+                } else {
+                    gen_point(pr, utab + ((int64_t)d * N + (j - 1)) * 2, &px, &py);
+                }
+                o[3 * j] = px;
+                o[3 * j + 1] = py;
+                o[3 * j + 2] = pr6[2] + (pr6[5] - pr6[2]) * ((double)j / (double)(W - 1));
+            }
+        }
+    }
+    return 0;
+}
+
+int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v,
+                     const float* vol, const double* wp3, int64_t P, double* cost, double* lq,
+                     double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
+                     int32_t* offmap, int32_t* below, int32_t* cells) {
+    const int N = p->N, W = N + 2;
+    double* xy = (double*)malloc(sizeof(double) * 2 * W);
+    const double idx = 1.0 / v->dx, idy = 1.0 / v->dy, idz = 1.0 / v->dz;
+    for (int64_t pi = 0; pi < P; ++pi) {
+        const double* z = wp3 + pi * (int64_t)W * 3;
+        for (int j = 0; j < W; ++j) {
+            xy[2 * j] = z[3 * j];
+            xy[2 * j + 1] = z[3 * j + 1];
+        }
+        /* geometry-only terms: the 2-D path evaluation in analytic mode with no shapes
+         * would recompute penalties; call the shared pieces through orc_eval_paths on a
+         * geometry-free copy instead */
+        orc_geom g0 = *g;
+        g0.n_regions = 0;
+        g0.n_obstacles = 0;
+        double c2, lq2, len2, k2, n2, mc2;
+        int32_t h2, o2;
+        orc_eval_paths(&g0, p, 0, NULL, NULL, xy, 1, &c2, &lq2, &len2, &k2, &n2, &h2, &mc2, &o2,
+                       NULL, NULL);
+        double c = (double)(N + 1) * lq2, ns = 0.0, cm = INFINITY;
+        int32_t nh = 0, off = 0, bel = 0;
+        for (int j = 0; j < W; ++j) {
+            double fx = floor((z[3 * j] - v->x0) * idx);
+            double fy = floor((v->y_top - z[3 * j + 1]) * idy);
+            double fz = floor((z[3 * j + 2] - v->z0) * idz);
+            int in = fx >= 0.0 && fx < (double)v->nx && fy >= 0.0 && fy < (double)v->ny &&
+                     fz >= 0.0 && fz < (double)v->nz;
+            if (!in) {
+                ++off;
+                if (cells) cells[pi * W + j] = -1;
+                continue;
+            }
+            int64_t vi = ((int64_t)fy * v->nx + (int64_t)fx) * v->nz + (int64_t)fz;
+            if (cells) cells[pi * W + j] = (int32_t)vi;
+            const float* r = vol + 4 * vi;
+            uint32_t fl;
+            memcpy(&fl, &r[3], 4);
+            c = c + (double)r[0] / (double)N;
+            ns = ns + (double)r[1];
+            nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
+            bel += (fl & ORC_FLAG_BELOW) ? 1 : 0;
+            cm = fmin(cm, z[3 * j + 2] - (double)r[2]);
+        }
+        if (cost) cost[pi] = c;
+        if (lq) lq[pi] = lq2;
+        if (length) length[pi] = len2;
+        if (kin) kin[pi] = k2;
+        if (nfz) nfz[pi] = ns;
+        if (hits) hits[pi] = nh;
+        if (minclr) minclr[pi] = cm;
+        if (offmap) offmap[pi] = off;
+        if (below) below[pi] = bel;
+    }
+    free(xy);
     return 0;
 }

@@ -404,3 +404,33 @@ def test_vrt_ingest_and_dem_mask(eng, oracle_mod, tmp_path, thr):
     np.testing.assert_array_equal(_np(r.rec), ref.view(np.int32))
     mask = dm.load_dem_mask(vrt, thr)
     np.testing.assert_array_equal(mask, (dem == -9999) if thr == -9999 else (dem > thr))
+
+
+def test_volume_mode_vs_oracle(eng, oracle_mod):
+    """Config 5 (3-D risk volume, build-defined semantics): volume build and the volume path
+    kernel bit-exact vs the oracle, incl. waypoints below/above the layer range."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import (canonical_spec, displacements, layer_weights,
+                                                raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs3d, synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=8)
+    orc = _setup(eng, oracle_mod, spec, 40, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"])
+    R, nz, z0, dz = 256, 64, 0.0, 10.0
+    geo = raster_geo(R)
+    dem = synthetic_dem(R)
+    r2 = eng.raster_build(geo, dem)
+    lw = layer_weights(nz)
+    vol = eng.volume_build(r2, nz, z0, dz, lw)
+    vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, z0, dz)
+    ref_vol = oracle_mod.volume_build(vd, _np(r2.rec).view(np.float32), lw)
+    np.testing.assert_array_equal(_np(vol.vox), ref_vol.view(np.int32))
+    pairs = random_pairs3d(300, seed=4, zmin=-50.0, zmax=700.0)   # some outside [0, 640)
+    ut = arc_table(40, displacements(5))
+    gpu = eng.eval_generated3d(pairs, ut, vol)
+    ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
+    for gk, ok in PATH_KEYS + (("below_terrain", "below"), ("min_clearance", "min_clearance")):
+        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+    assert (_np(gpu["offmap"]) > 0).any() and (_np(gpu["below_terrain"]) > 0).any()
+    np.testing.assert_array_equal(_np(gpu["best_fval_idx"]), oracle_mod.argmin(ref["cost"], 5, True))

@@ -16,8 +16,8 @@ RECORD_BYTES = 16
 
 UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
-MODE_ANALYTIC, MODE_RASTER = 0, 1
-FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4
+MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
+FLAG_NFZ, FLAG_MASK, FLAG_NODATA, FLAG_BELOW_TERRAIN = 1, 2, 4, 8
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _f64p = ctypes.POINTER(ctypes.c_double)
@@ -49,10 +49,17 @@ class RasterDesc(ctypes.Structure):
                 ("nodata", ctypes.c_float), ("dem_threshold", ctypes.c_float)]
 
 
+class VolumeDesc(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32),
+                ("x0", ctypes.c_double), ("y_top", ctypes.c_double), ("dx", ctypes.c_double),
+                ("dy", ctypes.c_double), ("z0", ctypes.c_double), ("dz", ctypes.c_double)]
+
+
 class PathOutputs(ctypes.Structure):
     _fields_ = [(name, _vp) for name in ("cost", "length_q", "length", "kin_sum", "nfz_sum",
                                          "nfz_hits", "min_clearance", "offmap", "cells",
-                                         "g_rows", "best_fval_idx", "best_length_idx")]
+                                         "g_rows", "best_fval_idx", "best_length_idx",
+                                         "below_terrain")]
 
 
 # name -> (restype, argtypes); the full exported surface of include/uampath.h
@@ -80,6 +87,10 @@ SIGNATURES = {
                                        ctypes.c_int32, _vp, _vp]),
     "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
     "uam_set_tuning": (ctypes.c_int, [_vp, ctypes.c_int32]),
+    "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
+    "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
+                                            ctypes.c_int64, _vp, ctypes.c_int32,
+                                            ctypes.POINTER(PathOutputs), _vp]),
 }
 
 _lib = None

@@ -94,6 +94,11 @@ struct KRaster {
     double x0, y_top, dx, dy, inv_dx, inv_dy;
 };
 
+struct KVolume {
+    int32_t nx, ny, nz;
+    double x0, y_top, z0, inv_dx, inv_dy, inv_dz;
+};
+
 struct KOut {
     double* cost;
     double* length_q;
@@ -105,6 +110,7 @@ struct KOut {
     int32_t* offmap;
     int32_t* cells;
     double* g_rows;
+    int32_t* below_terrain;
 };
 
 // ----------------------------------------------------------------------------------------
@@ -294,6 +300,29 @@ __global__ __launch_bounds__(256) void k_dem_mosaic(const float* __restrict__ ti
     }
 }
 
+// Volume build (config 5): voxel (ix, iy, iz), iz fastest, from the 2-D record of its column:
+// risk = Φ(column) * w[iz] (f64 product rounded to f32), psi_nfz and flags of the column,
+// terrain = column DEM (0 for nodata = sea), BELOW_TERRAIN when the layer centre
+// z0 + (iz + 0.5) dz lies below the terrain.
+__global__ __launch_bounds__(256) void k_volume_build(const uint4* __restrict__ rec2, int nx,
+                                                      int ny, int nz, double z0, double dz,
+                                                      const double* __restrict__ layer_w,
+                                                      uint4* __restrict__ vol) {
+    const int64_t total = (int64_t)nx * ny * nz;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total;
+         v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t col = v / nz;
+        const int iz = (int)(v - col * nz);
+        const uint4 r = rec2[col];
+        const float terrain = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+        const double hc = z0 + ((double)iz + 0.5) * dz;
+        uint32_t fl = r.w & (UAM_FLAG_NFZ | UAM_FLAG_MASK | UAM_FLAG_NODATA);
+        if (hc < (double)terrain) fl |= UAM_FLAG_BELOW_TERRAIN;
+        const float risk = (float)((double)__uint_as_float(r.x) * layer_w[iz]);
+        vol[v] = make_uint4(__float_as_uint(risk), r.y, __float_as_uint(terrain), fl);
+    }
+}
+
 // candidate point k (1..N) of pair pr: solver.py:121-136 restated as
 // p = C + 0.5*[[vx,-vy],[vy,vx]] u, v = x0 - xf, C = (xf + x0)/2
 __device__ __forceinline__ void arc_point(double x0, double y0, double xf, double yf, double ux,
@@ -310,7 +339,12 @@ struct PathSrc {
     const double* __restrict__ wp;  // explicit: this path's W points
     double x0, y0, xf, yf;          // generated: the pair
     const double* __restrict__ u;   // generated: u[d][0..N-1][2] (wave-uniform address)
+    double za, zb;                  // volume mode: altitude at p_0 and p_{N+1} (m)
     int W;
+    // volume mode altitude profile: z_j = za + (zb - za) * (j / (N+1))
+    __device__ __forceinline__ double alt(int j) const {
+        return za + (zb - za) * ((double)j / (double)(W - 1));
+    }
     __device__ __forceinline__ void at(int j, double& px, double& py) const {
         if (GEN) {
             if (j == 0) {
@@ -332,8 +366,8 @@ struct PathSrc {
 
 // Per-path results, in the reference's summation order (see eval_path).
 struct PathAcc {
-    double cost, L, len, ksum, nsum, hmax;
-    int32_t nh, off;
+    double cost, L, len, ksum, nsum, hmax, cmin;
+    int32_t nh, off, below;
 };
 
 // Gathers of one chunk of C consecutive waypoints (issued together, consumed together).
@@ -388,12 +422,61 @@ __device__ __forceinline__ void consume_chunk(const Chunk<C>& ch, int j0, int W,
     }
 }
 
+// Volume mode (BASELINE config 5, no reference counterpart): the waypoint's voxel
+// (ix, iy as in raster mode, iz = floor((z - z0) / dz)) holds {risk f32, psi_nfz f32,
+// terrain f32, flags}; risk already carries the altitude-layer weight.
+template <bool GEN, int C>
+__device__ __forceinline__ void issue_chunk_vol(const KVolume& vs, const uint4* __restrict__ vol,
+                                                const PathSrc<GEN>& src, int j0, int W,
+                                                int32_t* cells, Chunk<C>& ch) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        const int j = j0 + t;
+        ch.in[t] = false;
+        ch.r[t] = make_uint4(0, 0, 0, 0);
+        if (j < W) {
+            double x0, x1;
+            src.at(j, x0, x1);
+            const double z = src.alt(j);
+            const double fx = floor((x0 - vs.x0) * vs.inv_dx);
+            const double fy = floor((vs.y_top - x1) * vs.inv_dy);
+            const double fz = floor((z - vs.z0) * vs.inv_dz);
+            const bool in = (fx >= 0.0) && (fx < (double)vs.nx) && (fy >= 0.0) &&
+                            (fy < (double)vs.ny) && (fz >= 0.0) && (fz < (double)vs.nz);
+            const int64_t v =
+                in ? ((int64_t)fy * vs.nx + (int64_t)fx) * vs.nz + (int64_t)fz : (int64_t)0;
+            ch.in[t] = in;
+            ch.r[t] = vol[v];
+            if (cells) cells[j] = in ? (int32_t)v : -1;
+        }
+    }
+}
+
+template <bool GEN, int C>
+__device__ __forceinline__ void consume_chunk_vol(const Chunk<C>& ch, const PathSrc<GEN>& src,
+                                                  int j0, int W, double dN, PathAcc& a) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        const int j = j0 + t;
+        if (j >= W) break;
+        if (!ch.in[t]) {
+            ++a.off;
+            continue;
+        }
+        a.cost = a.cost + (double)__uint_as_float(ch.r[t].x) / dN;
+        a.nsum = a.nsum + (double)__uint_as_float(ch.r[t].y);
+        a.nh += (ch.r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+        a.below += (ch.r[t].w & UAM_FLAG_BELOW_TERRAIN) ? 1 : 0;
+        a.cmin = fmin(a.cmin, src.alt(j) - (double)__uint_as_float(ch.r[t].z));
+    }
+}
+
 // One path: pass 1 = geometry-only terms (length_of, true length, kinematic rows), pass 2 =
 // per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk,
 // PIPE = issue chunk k+1's gathers before consuming chunk k (two chunks in flight).
 template <int MODE, bool GEN, int C, bool PIPE>
 __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
-                                             const uint4* __restrict__ rec,
+                                             const KVolume& vs, const uint4* __restrict__ rec,
                                              const PathSrc<GEN>& src, int64_t path,
                                              const KOut& out) {
     const int N = p.N, W = N + 2;
@@ -461,9 +544,18 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
     a.nsum = 0.0;
     a.nh = 0;
     a.off = 0;
+    a.below = 0;
     a.hmax = -INFINITY;
+    a.cmin = INFINITY;
     const double dN = (double)N;
-    if (MODE == UAM_MODE_ANALYTIC) {
+    if (MODE == UAM_MODE_VOLUME) {
+        int32_t* cells = out.cells ? out.cells + path * W : nullptr;
+        for (int j0 = 0; j0 < W; j0 += C) {
+            Chunk<C> ch;
+            issue_chunk_vol<GEN, C>(vs, rec, src, j0, W, cells, ch);
+            consume_chunk_vol<GEN, C>(ch, src, j0, W, dN, a);
+        }
+    } else if (MODE == UAM_MODE_ANALYTIC) {
         for (int j = 0; j < W; ++j) {
             double x0, x1;
             src.at(j, x0, x1);
@@ -500,6 +592,13 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
     return a;
 }
 
+// raster: cruise altitude - highest terrain under the waypoints; volume: min over waypoints of
+// (waypoint altitude - terrain of its column); analytic: NaN (no DEM)
+__device__ __forceinline__ double clearance(const KParams& p, int mode, const PathAcc& a) {
+    return mode == UAM_MODE_RASTER ? p.altitude - a.hmax
+                                   : (mode == UAM_MODE_VOLUME ? a.cmin : (double)NAN);
+}
+
 __device__ __forceinline__ void write_path(const KOut& out, const KParams& p, int mode,
                                            int64_t path, const PathAcc& a) {
     if (out.cost) out.cost[path] = a.cost;
@@ -509,8 +608,8 @@ __device__ __forceinline__ void write_path(const KOut& out, const KParams& p, in
     if (out.nfz_sum) out.nfz_sum[path] = a.nsum;
     if (out.nfz_hits) out.nfz_hits[path] = a.nh;
     if (out.offmap) out.offmap[path] = a.off;
-    if (out.min_clearance)
-        out.min_clearance[path] = (mode == UAM_MODE_RASTER) ? p.altitude - a.hmax : NAN;
+    if (out.min_clearance) out.min_clearance[path] = clearance(p, mode, a);
+    if (out.below_terrain) out.below_terrain[path] = a.below;
 }
 
 // main.py:175-180 selection over D values (see uam_argmin)
@@ -539,7 +638,9 @@ __global__ __launch_bounds__(256) void k_eval_waypoints(KGeom g, KParams p, KRas
     src.wp = wp + path * (int64_t)src.W * 2;
     src.u = nullptr;
     src.x0 = src.y0 = src.xf = src.yf = 0.0;
-    const PathAcc a = eval_path<MODE, false, 8, false>(g, p, rs, rec, src, path, out);
+    src.za = src.zb = 0.0;
+    const KVolume vs{};
+    const PathAcc a = eval_path<MODE, false, 8, false>(g, p, rs, vs, rec, src, path, out);
     write_path(out, p, MODE, path, a);
 }
 
@@ -568,7 +669,9 @@ __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRas
     src.xf = pr.z;
     src.yf = pr.w;
     src.u = utab + (int64_t)d * p.N * 2;
-    const PathAcc a = eval_path<MODE, true, 8, false>(g, p, rs, rec, src, q * D + d, out);
+    src.za = src.zb = 0.0;
+    const KVolume vs{};
+    const PathAcc a = eval_path<MODE, true, 8, false>(g, p, rs, vs, rec, src, q * D + d, out);
     write_path(out, p, MODE, q * D + d, a);
 }
 
@@ -578,6 +681,7 @@ __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRas
 // (main.py:175-180) runs in the same launch on the staged costs / lengths.
 template <int MODE, int C, bool PIPE, int MINW>
 __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, KRaster rs,
+                                                           KVolume vs,
                                                            const uint4* __restrict__ rec,
                                                            const double* __restrict__ pairs,
                                                            int64_t n_pairs,
@@ -595,6 +699,7 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     double* s_clr = s_n + BP;
     int32_t* s_nh = reinterpret_cast<int32_t*>(s_clr + BP);
     int32_t* s_off = s_nh + BP;
+    int32_t* s_bel = s_off + BP;
 
     const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -602,24 +707,30 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     const int64_t q = q0 + lane;
     const int slot = d * 64 + lane;
     if (q < n_pairs) {
-        const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
         PathSrc<true> src;
         src.W = p.N + 2;
         src.wp = nullptr;
-        src.x0 = pr.x;
-        src.y0 = pr.y;
-        src.xf = pr.z;
-        src.yf = pr.w;
+        if (MODE == UAM_MODE_VOLUME) {  // pairs [Q][6] = (x0, y0, z0, xf, yf, zf)
+            const double* pr = pairs + 6 * q;
+            src.x0 = pr[0], src.y0 = pr[1], src.za = pr[2];
+            src.xf = pr[3], src.yf = pr[4], src.zb = pr[5];
+        } else {
+            const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+            src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+            src.za = src.zb = 0.0;
+        }
         src.u = utab + (int64_t)d * p.N * 2;
-        const PathAcc a = eval_path<MODE, true, C, PIPE>(g, p, rs, rec, src, q * D + d, out);
+        const PathAcc a =
+            eval_path<MODE, true, C, PIPE>(g, p, rs, vs, rec, src, q * D + d, out);
         s_cost[slot] = a.cost;
         s_L[slot] = a.L;
         s_len[slot] = a.len;
         s_k[slot] = a.ksum;
         s_n[slot] = a.nsum;
-        s_clr[slot] = (MODE == UAM_MODE_RASTER) ? p.altitude - a.hmax : NAN;
+        s_clr[slot] = clearance(p, MODE, a);
         s_nh[slot] = a.nh;
         s_off[slot] = a.off;
+        s_bel[slot] = a.below;
     }
     __syncthreads();
     // coalesced stores: thread t -> block-local path t = (pair t / D, displacement t % D)
@@ -636,6 +747,7 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         if (out.min_clearance) out.min_clearance[gp] = s_clr[s];
         if (out.nfz_hits) out.nfz_hits[gp] = s_nh[s];
         if (out.offmap) out.offmap[gp] = s_off[s];
+        if (out.below_terrain) out.below_terrain[gp] = s_bel[s];
     }
     if (d == 0 && q < n_pairs) {
         if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
@@ -873,6 +985,7 @@ KOut make_kout(const uam_path_outputs* o) {
     k.offmap = o->offmap;
     k.cells = o->cells;
     k.g_rows = o->g_rows;
+    k.below_terrain = o->below_terrain;
     return k;
 }
 
@@ -1177,11 +1290,12 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const dim3 grid((unsigned)blocks), block(64 * D);
-    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 2 * sizeof(int32_t));
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    const KVolume kv{};
 #define UAM_LAUNCH_PAIRS(MODE_, C_, PIPE_, MINW_)                                          \
     hipLaunchKernelGGL((k_eval_pairs<MODE_, C_, PIPE_, MINW_>), grid, block, lds, s, ctx->kg, \
-                       ctx->kp, kr, (const uint4*)rec, pairs, n_pairs, utab, D, ko, best_f,  \
-                       best_l)
+                       ctx->kp, kr, kv, (const uint4*)rec, pairs, n_pairs, utab, D, ko,      \
+                       best_f, best_l)
     if (mode == UAM_MODE_ANALYTIC) {
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
@@ -1196,6 +1310,65 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
         }
     }
 #undef UAM_LAUNCH_PAIRS
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+namespace {
+int make_kvolume(const uam_volume_desc* d, KVolume* k) {
+    if (!d) return fail(UAM_E_INVALID, "volume descriptor is NULL");
+    if (d->nx <= 0 || d->ny <= 0 || d->nz <= 0)
+        return fail(UAM_E_INVALID, "volume size %dx%dx%d", d->nx, d->ny, d->nz);
+    if ((int64_t)d->nx * d->ny * d->nz >= ((int64_t)1 << 31))
+        return fail(UAM_E_INVALID, "volume has more than 2^31 voxels");
+    if (!(d->dx > 0.0) || !(d->dy > 0.0) || !(d->dz > 0.0))
+        return fail(UAM_E_INVALID, "dx, dy, dz must be > 0");
+    k->nx = d->nx, k->ny = d->ny, k->nz = d->nz;
+    k->x0 = d->x0, k->y_top = d->y_top, k->z0 = d->z0;
+    k->inv_dx = 1.0 / d->dx, k->inv_dy = 1.0 / d->dy, k->inv_dz = 1.0 / d->dz;
+    return UAM_OK;
+}
+}  // namespace
+
+int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
+                     const double* layer_w, void* vol, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    KVolume kv;
+    int st = make_kvolume(vd, &kv);
+    if (st) return st;
+    if (!rec2d || !layer_w || !vol) return fail(UAM_E_INVALID, "volume build pointer is NULL");
+    DeviceGuard dg(ctx->device);
+    const int64_t total = (int64_t)vd->nx * vd->ny * vd->nz;
+    hipLaunchKernelGGL(k_volume_build, dim3(grid_for(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint4*)rec2d, vd->nx, vd->ny, vd->nz, vd->z0,
+                       vd->dz, layer_w, (uint4*)vol);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
+                         const double* pairs6, int64_t n_pairs, const double* utab, int32_t D,
+                         const uam_path_outputs* out, uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (n_pairs < 0 || D < 1 || D > 16)
+        return fail(UAM_E_INVALID, "n_pairs < 0 or D outside [1, 16]");
+    if (n_pairs == 0) return UAM_OK;
+    KVolume kv;
+    st = make_kvolume(vd, &kv);
+    if (st) return st;
+    if (!vol || !pairs6 || !utab) return fail(UAM_E_INVALID, "pointer is NULL");
+    const KOut ko = make_kout(out);
+    int32_t* best_f = out ? out->best_fval_idx : nullptr;
+    int32_t* best_l = out ? out->best_length_idx : nullptr;
+    DeviceGuard dg(ctx->device);
+    const int64_t blocks = (n_pairs + 63) / 64;
+    if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    const KRaster kr{};
+    hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
+                       dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
+                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }

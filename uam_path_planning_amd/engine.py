@@ -84,6 +84,31 @@ class CostRaster:
         return self.geo.nx * self.geo.ny * _lib.RECORD_BYTES
 
 
+@dataclass
+class VolumeGeo:
+    """3-D risk volume grid (config 5): the raster's x/y grid x nz altitude layers (m)."""
+    nx: int
+    ny: int
+    nz: int
+    x0: float
+    y_top: float
+    dx: float
+    dy: float
+    z0: float
+    dz: float
+
+    def as_struct(self):
+        return _lib.VolumeDesc(int(self.nx), int(self.ny), int(self.nz), float(self.x0),
+                               float(self.y_top), float(self.dx), float(self.dy),
+                               float(self.z0), float(self.dz))
+
+
+@dataclass
+class RiskVolume:
+    geo: VolumeGeo
+    vox: object = field(repr=False)     # [ny, nx, nz, 4] int32 view of 16-B voxels
+
+
 def _ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
@@ -209,6 +234,7 @@ class Engine:
                                                            "min_clearance")}
         o["nfz_hits"] = self.empty((P,), torch.int32)
         o["offmap"] = self.empty((P,), torch.int32)
+        o["below_terrain"] = self.empty((P,), torch.int32)
         if want_cells:
             o["cells"] = self.empty((P, W), torch.int32)
         if want_g:
@@ -256,6 +282,36 @@ class Engine:
         _lib.check(self.lib.uam_eval_generated(
             self._ctx, self._mode(raster), geo, _ptr(None if raster is None else raster.rec),
             _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated")
+        return o
+
+    # -- volume (config 5) -------------------------------------------------------------
+    def volume_build(self, raster, nz, z0, dz, layer_w):
+        torch = _torch()
+        g = raster.geo
+        vg = VolumeGeo(g.nx, g.ny, int(nz), g.x0, g.y_top, g.dx, g.dy, float(z0), float(dz))
+        lw = self.tensor(layer_w, torch.float64).reshape(-1)
+        if lw.numel() != nz:
+            raise ValueError(f"layer_w has {lw.numel()} entries, nz = {nz}")
+        vox = self.empty((g.ny, g.nx, int(nz), 4), torch.int32)
+        _lib.check(self.lib.uam_volume_build(self._ctx, ctypes.byref(vg.as_struct()),
+                                             _ptr(raster.rec), _ptr(lw), _ptr(vox),
+                                             self.stream), "uam_volume_build")
+        return RiskVolume(vg, vox)
+
+    def eval_generated3d(self, pairs6, utab, volume, outputs=None):
+        """pairs6 [Q, 6] = (x0, y0, z0, xf, yf, zf) (km, km, m); path p = q*D + d."""
+        torch = _torch()
+        pr = self.tensor(pairs6, torch.float64).reshape(-1, 6)
+        ut = self.tensor(utab, torch.float64)
+        D = ut.shape[0]
+        if ut.shape[1] != self.params.N:
+            raise ValueError(f"arc table has N={ut.shape[1]}, params N={self.params.N}")
+        Q = pr.shape[0]
+        o, s = outputs if outputs is not None else self._outputs(
+            Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False, n_pairs=Q)
+        _lib.check(self.lib.uam_eval_generated3d(
+            self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.vox), _ptr(pr), Q,
+            _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated3d")
         return o
 
     def gen_paths(self, pairs, utab):

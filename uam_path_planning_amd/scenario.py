@@ -84,7 +84,15 @@ CONFIGS = {
                  R=4096, pairs=100_000, D=5, N=80, nfz_polygons=64, mode="raster"),
     "cfg4": dict(name="1M candidate paths, 8192^2 DEM (synthetic GeoTIFF tiles), 8 GPUs",
                  R=8192, pairs=200_000, D=5, N=80, nfz_polygons=64, mode="raster"),
+    "cfg5": dict(name="3-D 1024x1024x64 (x,y,alt) altitude-dependent risk volume",
+                 R=1024, nz=64, z0=0.0, dz=10.0, pairs=100_000, D=5, N=80, nfz_polygons=64,
+                 mode="volume"),
 }
+
+
+def layer_weights(nz):
+    """Altitude weight of the ground risk per layer (config 5, build-defined): 1 / (1 + k)."""
+    return 1.0 / (1.0 + np.arange(nz, dtype=np.float64))
 
 
 def displacements(D):

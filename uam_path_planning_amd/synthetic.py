@@ -79,3 +79,10 @@ def random_convex_polygons(K, seed=2, bbox=LAND_BBOX, rmin=0.5, rmax=3.0, kmin=4
                         round(float(cy + x * np.sin(rot) + y * np.cos(rot)), 6)])
         out.append(pts)
     return out
+
+
+def random_pairs3d(Q, seed=0, bbox=LAND_BBOX, zmin=100.0, zmax=500.0):
+    """Q pairs with altitudes: [Q, 6] = (x0, y0, z0, xf, yf, zf), z in metres."""
+    xy = random_pairs(Q, seed=seed, bbox=bbox)
+    z = np.random.default_rng(seed + 1000).uniform(zmin, zmax, size=(Q, 2))
+    return np.stack([xy[:, 0], xy[:, 1], z[:, 0], xy[:, 2], xy[:, 3], z[:, 1]], axis=1)
