@@ -51,6 +51,20 @@ class _Volume(ctypes.Structure):
                 ("dy", ctypes.c_double), ("z0", ctypes.c_double), ("dz", ctypes.c_double)]
 
 
+class _RefineParams(ctypes.Structure):
+    _fields_ = [("n_outer", ctypes.c_int32), ("n_inner", ctypes.c_int32),
+                ("max_backtrack", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("c0", ctypes.c_double), ("rho", ctypes.c_double), ("c_max", ctypes.c_double),
+                ("alpha0", ctypes.c_double), ("armijo", ctypes.c_double),
+                ("theta", ctypes.c_double), ("max_step", ctypes.c_double)]
+
+
+def refine_params(n_outer=10, n_inner=20, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
+                  alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5):
+    return _RefineParams(n_outer, n_inner, max_backtrack, 0, c0, rho, c_max, alpha0, armijo,
+                         theta, max_step)
+
+
 def build():
     """Compile liboracle.so (gcc) if it is missing or older than its source."""
     src = os.path.join(HERE, "uam_oracle.c")
@@ -69,7 +83,8 @@ def lib():
             build()
         _lib = ctypes.CDLL(LIB_PATH)
         for name in ("orc_eval_points", "orc_gen_paths", "orc_raster_build", "orc_eval_paths",
-                     "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d"):
+                     "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d",
+                     "orc_refine"):
             getattr(_lib, name).restype = ctypes.c_int
     return _lib
 
@@ -105,6 +120,20 @@ class Oracle:
                          0.0 if anchor is None else float(anchor[0]),
                          0.0 if anchor is None else float(anchor[1]),
                          float(maxratio), float(maxalpha), float(enlargement), float(altitude), w)
+
+    # -- refinement (§8(f) rank 1) ---------------------------------------------------------
+    def refine(self, wp, rp):
+        W = self.N + 2
+        wp = np.array(wp, dtype=np.float64, copy=True).reshape(-1, W, 2)
+        P = wp.shape[0]
+        out = {"cost": np.zeros(P), "infeas": np.zeros(P), "iters": np.zeros(P, np.int32)}
+        st = lib().orc_refine(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.byref(rp),
+                              _ptr(wp, _f64p), ctypes.c_int64(P), _ptr(out["cost"], _f64p),
+                              _ptr(out["infeas"], _f64p), _ptr(out["iters"], _i32p))
+        if st != 0:
+            raise ValueError("refinement needs penalty_smooth and obstacle_smooth")
+        out["wp"] = wp
+        return out
 
     # -- volume (config 5) -----------------------------------------------------------------
     def eval_paths3d(self, wp3, vdesc, vol, want_cells=False):

@@ -515,3 +515,296 @@ int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v
     free(xy);
     return 0;
 }
+
+/* ---- batched refinement (no pinned reference output) ----------------
+ * Restates the build's ALM refinement (include/uampath.h uam_refine): the reference solves
+ *   min get_cost(z)  s.t.  get_nonlincon(z) in {0}            (solver.py:82-93)
+ * with OpEn's augmented Lagrangian; here per path: outer ALM updates y += c g, c *= rho when
+ * sum g^2 did not drop below theta * previous, inner gradient steps on
+ *   L = f + sum_i (c/2) (g_i + y_i/c)^2
+ * with Armijo backtracking.  Requires penalty_smooth and obstacle_smooth (the reference's
+ * main.py options).  Operation order is part of the definition (GPU == oracle bit for bit). */
+typedef struct {
+    int32_t n_outer, n_inner, max_backtrack, pad;
+    double c0, rho, c_max, alpha0, armijo, theta, max_step;
+} orc_refine_params;
+
+/* gradient of h_i */
+static void ineq_grad(const orc_geom* g, int i, double x0, double x1, double* gx, double* gy) {
+    const double* p = g->ineq_par + 6 * (int64_t)i;
+    switch (g->ineq_kind[i]) {
+        case ORC_HALFPLANE:
+            *gx = p[4] * p[3];
+            *gy = -(p[4] * p[2]);
+            return;
+        case ORC_ELLIPSE: {
+            double a = (x0 - p[0]) / p[2];
+            double b = (x1 - p[1]) / p[3];
+            *gx = (2.0 * a) / p[2];
+            *gy = (2.0 * b) / p[3];
+            return;
+        }
+        default:
+            *gx = (p[0] == 0.0) ? p[3] : 0.0;
+            *gy = (p[0] == 0.0) ? 0.0 : p[3];
+            return;
+    }
+}
+
+/* d psi / dx for the smooth psi = prod_i min(h_i - e, 0)^2 */
+static void psi_grad(const orc_geom* g, int s, double x0, double x1, double e, double* dx,
+                     double* dy) {
+    int f = g->shape_first[s], n = g->shape_count[s];
+    double m[64];
+    double ox = 0.0, oy = 0.0;
+    if (n > 64) n = 64;
+    for (int i = 0; i < n; ++i) m[i] = fmin(ineq_h(g, f + i, x0, x1) - e, 0.0);
+    for (int i = 0; i < n; ++i) {
+        if (m[i] == 0.0) continue;
+        double prod = 1.0;
+        for (int k = 0; k < n; ++k)
+            if (k != i) prod = prod * (m[k] * m[k]);
+        double coef = (2.0 * m[i]) * prod;
+        double hx, hy;
+        ineq_grad(g, f + i, x0, x1, &hx, &hy);
+        ox = ox + coef * hx;
+        oy = oy + coef * hy;
+    }
+    *dx = ox;
+    *dy = oy;
+}
+
+/* gradient of the total penalty Phi (smooth) */
+static void phi_grad(const orc_geom* g, const orc_params* p, double x0, double x1, double* dx,
+                     double* dy) {
+    double gx = 0.0, gy = 0.0;
+    for (int r = 0; r < g->n_regions; ++r) {
+        double tx = 0.0, ty = 0.0;
+        for (int s = g->region_first[r]; s < g->region_first[r + 1]; ++s) {
+            double cx = g->shape_center[2 * s], cy = g->shape_center[2 * s + 1];
+            double ex, ey;
+            psi_grad(g, s, x0, x1, p->enlargement, &ex, &ey);
+            if (isnan(cx) || isnan(cy)) {
+                tx = tx + ex;
+                ty = ty + ey;
+            } else {
+                double nrm = psi(g, s, cx, cy, 1, p->enlargement);
+                tx = tx + ex / nrm;
+                ty = ty + ey / nrm;
+            }
+        }
+        gx = gx + p->weights[r] * tx;
+        gy = gy + p->weights[r] * ty;
+    }
+    *dx = gx;
+    *dy = gy;
+}
+
+typedef struct {
+    double c1, c2, c3;          /* row values */
+    double d[3][6];             /* d row / d (p_k, p_k+1, p_k+2) as (x, y) triples */
+} kin_row;
+
+static void kin_eval(const double* pk, const double* pk1, const double* pk2, double r,
+                     double mincos, int ms, int want_grad, kin_row* o) {
+    double ax = pk1[0] - pk[0], ay = pk1[1] - pk[1];
+    double bx = pk2[0] - pk1[0], by = pk2[1] - pk1[1];
+    double sa = 0.0, sb = 0.0, dt = 0.0;
+    sa = sa + ax * ax;
+    sa = sa + ay * ay;
+    sb = sb + bx * bx;
+    sb = sb + by * by;
+    dt = dt + ax * bx;
+    dt = dt + ay * by;
+    double ra = sqrt(sa), rb = sqrt(sb);
+    double na = ms ? ra * ra : ra, nb = ms ? rb * rb : rb;
+    o->c1 = fmax(0.0, nb - r * na);
+    o->c2 = fmax(0.0, na / r - nb);
+    double den = na * nb;
+    o->c3 = fmax(0.0, mincos - dt / den);
+    if (!want_grad) return;
+    double gax = ms ? 2.0 * ax : ax / ra, gay = ms ? 2.0 * ay : ay / ra;
+    double gbx = ms ? 2.0 * bx : bx / rb, gby = ms ? 2.0 * by : by / rb;
+    double da[3][2], db[3][2];
+    /* c1 = nb - r na */
+    da[0][0] = -(r * gax), da[0][1] = -(r * gay), db[0][0] = gbx, db[0][1] = gby;
+    /* c2 = na / r - nb */
+    da[1][0] = gax / r, da[1][1] = gay / r, db[1][0] = -gbx, db[1][1] = -gby;
+    /* c3 = mincos - dt / den */
+    double d2 = den * den;
+    double qax = bx / den - ((dt * nb) * gax) / d2, qay = by / den - ((dt * nb) * gay) / d2;
+    double qbx = ax / den - ((dt * na) * gbx) / d2, qby = ay / den - ((dt * na) * gby) / d2;
+    da[2][0] = -qax, da[2][1] = -qay, db[2][0] = -qbx, db[2][1] = -qby;
+    for (int t = 0; t < 3; ++t) {
+        o->d[t][0] = -da[t][0];
+        o->d[t][1] = -da[t][1];
+        o->d[t][2] = da[t][0] - db[t][0];
+        o->d[t][3] = da[t][1] - db[t][1];
+        o->d[t][4] = db[t][0];
+        o->d[t][5] = db[t][1];
+    }
+}
+
+/* L(z) (and its gradient into gr[2N] when gr != NULL).  z: W points of this path.
+ * Summation order: f exactly as get_cost; then kinematic rows k ascending (c1, c2, c3); then
+ * obstacle rows s-major, j ascending. */
+static double refine_L(const orc_geom* g, const orc_params* p, const double* z, const double* y,
+                       double c, double* gr, double* fout) {
+    const int N = p->N, W = N + 2;
+    const int ls = p->length_smooth;
+    const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
+    const double mincos = cos(p->maxalpha);
+    if (gr)
+        for (int k = 0; k < 2 * N; ++k) gr[k] = 0.0;
+    /* length term (get_cost order) */
+    double ax = p->anchor_mode ? p->anchor_x : z[0], ay = p->anchor_mode ? p->anchor_y : z[1];
+    double L = 0.0;
+    if (p->quirk_length) {
+        double dx = z[0] - ax, dy = z[1] - ay, s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        L = L + nrm_of(s, ls);
+    }
+    int kend = p->quirk_length ? N : N + 1;
+    for (int k = 1; k <= kend; ++k) {
+        double dx = z[2 * k] - z[2 * k - 2], dy = z[2 * k + 1] - z[2 * k - 1], s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        double n = sqrt(s);
+        L = L + (ls ? n * n : n);
+        if (gr) {
+            double sc = (double)(N + 1);
+            double vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
+            double vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
+            if (k <= N) {
+                gr[2 * (k - 1)] = gr[2 * (k - 1)] + vx;
+                gr[2 * (k - 1) + 1] = gr[2 * (k - 1) + 1] + vy;
+            }
+            if (k - 1 >= 1) {
+                gr[2 * (k - 2)] = gr[2 * (k - 2)] - vx;
+                gr[2 * (k - 2) + 1] = gr[2 * (k - 2) + 1] - vy;
+            }
+        }
+    }
+    double f = (double)(N + 1) * L;
+    for (int j = 0; j < W; ++j) {
+        f = f + total_penalty(g, p, z[2 * j], z[2 * j + 1]) / (double)N;
+        if (gr && j >= 1 && j <= N) {
+            double gx, gy;
+            phi_grad(g, p, z[2 * j], z[2 * j + 1], &gx, &gy);
+            gr[2 * (j - 1)] = gr[2 * (j - 1)] + gx / (double)N;
+            gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + gy / (double)N;
+        }
+    }
+    double aug = 0.0;
+    const double hc = 0.5 * c;
+    for (int k = 0; k < N; ++k) {
+        kin_row kr;
+        kin_eval(&z[2 * k], &z[2 * (k + 1)], &z[2 * (k + 2)], r, mincos, p->maxratio_smooth,
+                 gr != NULL, &kr);
+        double gv[3] = {kr.c1, kr.c2, kr.c3};
+        for (int t = 0; t < 3; ++t) {
+            double tt = gv[t] + y[3 * k + t] / c;
+            aug = aug + hc * (tt * tt);
+            if (gr && gv[t] > 0.0) {
+                double coef = c * tt;
+                for (int q = 0; q < 3; ++q) {
+                    int j = k + q;
+                    if (j >= 1 && j <= N) {
+                        gr[2 * (j - 1)] = gr[2 * (j - 1)] + coef * kr.d[t][2 * q];
+                        gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + coef * kr.d[t][2 * q + 1];
+                    }
+                }
+            }
+        }
+    }
+    for (int s = 0; s < g->n_obstacles; ++s) {
+        for (int j = 0; j < W; ++j) {
+            double v = psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0);
+            double tt = v + y[3 * N + s * W + j] / c;
+            aug = aug + hc * (tt * tt);
+            if (gr && j >= 1 && j <= N) {
+                double coef = c * tt, ex, ey;
+                psi_grad(g, s, z[2 * j], z[2 * j + 1], 0.0, &ex, &ey);
+                gr[2 * (j - 1)] = gr[2 * (j - 1)] + coef * ex;
+                gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + coef * ey;
+            }
+        }
+    }
+    if (fout) *fout = f;
+    return f + aug;
+}
+
+/* constraint rows in canonical order (kinematic, then obstacles s-major) */
+static void refine_rows(const orc_geom* g, const orc_params* p, const double* z, double* rows) {
+    const int N = p->N, W = N + 2;
+    const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
+    const double mincos = cos(p->maxalpha);
+    for (int k = 0; k < N; ++k) {
+        kin_row kr;
+        kin_eval(&z[2 * k], &z[2 * (k + 1)], &z[2 * (k + 2)], r, mincos, p->maxratio_smooth, 0,
+                 &kr);
+        rows[3 * k] = kr.c1;
+        rows[3 * k + 1] = kr.c2;
+        rows[3 * k + 2] = kr.c3;
+    }
+    for (int s = 0; s < g->n_obstacles; ++s)
+        for (int j = 0; j < W; ++j) rows[3 * N + s * W + j] = psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0);
+}
+
+int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* rp, double* wp,
+               int64_t P, double* cost, double* infeas, int32_t* iters) {
+    const int N = p->N, W = N + 2, R = 3 * N + g->n_obstacles * W;
+    if (!p->penalty_smooth || !p->obstacle_smooth) return -1;
+    double* y = (double*)malloc(sizeof(double) * R);
+    double* rows = (double*)malloc(sizeof(double) * R);
+    double* gr = (double*)malloc(sizeof(double) * 2 * N);
+    double* zt = (double*)malloc(sizeof(double) * 2 * W);
+    for (int64_t pi = 0; pi < P; ++pi) {
+        double* z = wp + pi * (int64_t)W * 2;
+        for (int i = 0; i < R; ++i) y[i] = 0.0;
+        double c = rp->c0, alpha = rp->alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
+        int32_t it_used = 0;
+        for (int o = 0; o < rp->n_outer; ++o) {
+            for (int it = 0; it < rp->n_inner; ++it) {
+                double Lz = refine_L(g, p, z, y, c, gr, NULL);
+                double gn2 = 0.0;
+                for (int k = 0; k < 2 * N; ++k) gn2 = gn2 + gr[k] * gr[k];
+                if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;
+                double a = fmin(alpha * 2.0, rp->max_step / sqrt(gn2));
+                int ok = 0;
+                for (int b = 0; b < rp->max_backtrack; ++b) {
+                    for (int k = 0; k < 2 * W; ++k) zt[k] = z[k];
+                    for (int k = 0; k < 2 * N; ++k) zt[2 + k] = z[2 + k] - a * gr[k];
+                    double Lt = refine_L(g, p, zt, y, c, NULL, NULL);
+                    if (Lt <= Lz - (rp->armijo * a) * gn2) {
+                        ok = 1;
+                        break;
+                    }
+                    a = a * 0.5;
+                }
+                if (!ok) break;
+                for (int k = 0; k < 2 * N; ++k) z[2 + k] = z[2 + k] - a * gr[k];
+                alpha = a;
+                ++it_used;
+            }
+            refine_rows(g, p, z, rows);
+            inf = 0.0;
+            for (int i = 0; i < R; ++i) {
+                y[i] = y[i] + c * rows[i];
+                inf = inf + rows[i] * rows[i];
+            }
+            if (inf > rp->theta * prev) c = fmin(c * rp->rho, rp->c_max);
+            prev = inf;
+        }
+        refine_L(g, p, z, y, c, NULL, &f);
+        if (cost) cost[pi] = f;
+        if (infeas) infeas[pi] = inf;
+        if (iters) iters[pi] = it_used;
+    }
+    free(y);
+    free(rows);
+    free(gr);
+    free(zt);
+    return 0;
+}

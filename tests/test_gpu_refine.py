@@ -1,0 +1,96 @@
+"""GPU refinement (uam_refine) against the oracle's orc_refine: the
+refined waypoints, final cost, final infeasibility and step counts are compared with exact
+equality (tolerance 0: same float64 operation order, no FMA contraction).  The reference's
+OpEn solve itself is absent (parity unpinned vs the reference, see test_refine_cpu.py)."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from uam_path_planning_amd import build
+    from uam_path_planning_amd.engine import Engine
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    build.build_library()
+    return Engine(0)
+
+
+def _setup(eng, oracle_mod, spec, N, options, maxratio, maxalpha, enl, weights, anchor):
+    from uam_path_planning_amd.engine import PathParams
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import build_region_map
+
+    eng.set_geometry(compile_map(build_region_map(spec)))
+    eng.set_params(PathParams(N=N, **options, maxratio=maxratio, maxalpha=maxalpha,
+                              enlargement=enl, weights=tuple(weights), anchor=anchor))
+    return oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, options, maxratio, maxalpha, enl,
+                             weights, anchor=anchor)
+
+
+def _check(eng, orc, oracle_mod, wp, **kw):
+    gpu = eng.refine(wp, kw)
+    ref = orc.refine(wp, oracle_mod.refine_params(**kw))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gpu["iters"].cpu().numpy(), ref["iters"])
+    np.testing.assert_array_equal(gpu["wp"].cpu().numpy(), ref["wp"])
+    np.testing.assert_array_equal(gpu["cost"].cpu().numpy(), ref["cost"])
+    np.testing.assert_array_equal(gpu["infeas"].cpu().numpy(), ref["infeas"])
+    return gpu, ref
+
+
+def test_refine_canonical_bit_exact(eng, oracle_mod):
+    meta, arr = G.canonical()
+    orc = _setup(eng, oracle_mod, meta["map"], meta["N"], meta["options"], meta["maxratio"],
+                 meta["maxalpha"], meta["enlargement"], meta["weights"],
+                 tuple(meta["map"]["x_start"]))
+    wp = G.canonical_paths(meta, arr)
+    gpu, ref = _check(eng, orc, oracle_mod, wp, n_outer=4, n_inner=12)
+    assert (ref["iters"] > 0).all()
+    before = eng.eval_waypoints(wp)["cost"].cpu().numpy()
+    after = eng.eval_waypoints(gpu["wp"])["cost"].cpu().numpy()
+    assert (after < before).all()
+
+
+def test_refine_cfg3_geometry_bit_exact(eng, oracle_mod):
+    """Generated candidates on the config-3 map (64 extra polygon no-fly zones, 69
+    obstacle rows per waypoint) -- exercises the culled psi/psi_grad paths."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    spec = canonical_spec(nfz_polygons=64)
+    N = 40
+    opts = {"length_smooth": True, "penalty_smooth": True, "obstacle_smooth": True,
+            "maxratio_smooth": False}
+    orc = _setup(eng, oracle_mod, spec, N, opts, spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"], tuple(spec["x_start"]))
+    ut = arc_table(N, displacements(5))
+    wp = oracle_mod.gen_paths(random_pairs(24, seed=7), ut)
+    _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=8)
+
+
+def test_refine_edge_cases(eng, oracle_mod):
+    from uam_path_planning_amd._lib import UamError
+
+    meta, arr = G.canonical()
+    opts = dict(meta["options"], maxratio_smooth=True)
+    orc = _setup(eng, oracle_mod, meta["map"], meta["N"], opts, meta["maxratio"],
+                 meta["maxalpha"], meta["enlargement"], meta["weights"],
+                 tuple(meta["map"]["x_start"]))
+    wp = G.canonical_paths(meta, arr)
+    _check(eng, orc, oracle_mod, wp, n_outer=2, n_inner=6)          # smooth max-ratio rows
+    _check(eng, orc, oracle_mod, wp[:0], n_outer=2, n_inner=6)      # empty batch
+    _check(eng, orc, oracle_mod, wp, n_outer=0, n_inner=0)          # identity
+    eng.set_params(dataclasses.replace(eng.params, obstacle_smooth=False))
+    with pytest.raises((UamError, ValueError)):
+        eng.refine(wp, {"n_outer": 1, "n_inner": 1})

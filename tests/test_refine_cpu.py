@@ -1,0 +1,51 @@
+"""Refinement oracle (oracle/uam_oracle.c orc_refine) on the CPU.
+The reference's own optimiser (OpEn/CasADi, solver.py:82-93) is a Rust build that is absent
+here, so the refinement result is parity unpinned against the reference; what is pinned is
+(a) its objective -- get_cost of the refined path is the golden-pinned cost function -- and
+(b) GPU == oracle bit for bit (tests/test_gpu_refine.py).  These tests hold the optimiser's
+own contract: endpoints fixed, cost and the augmented objective go down, determinism."""
+import numpy as np
+import pytest
+
+import golden_io as G
+
+
+def _canonical(oracle_mod, options=None):
+    meta, arr = G.canonical()
+    opts = dict(meta["options"])
+    opts.update(options or {})
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(meta["map"]), meta["N"], opts,
+                            meta["maxratio"], meta["maxalpha"], meta["enlargement"],
+                            meta["weights"], anchor=tuple(meta["map"]["x_start"]))
+    return orc, G.canonical_paths(meta, arr), arr
+
+
+def test_refine_lowers_cost_and_keeps_endpoints(oracle_mod):
+    orc, wp, arr = _canonical(oracle_mod)
+    rp = oracle_mod.refine_params(n_outer=4, n_inner=10)
+    out = orc.refine(wp, rp)
+    z = out["wp"]
+    np.testing.assert_array_equal(z[:, 0], wp[:, 0])
+    np.testing.assert_array_equal(z[:, -1], wp[:, -1])
+    assert (out["iters"] > 0).all()
+    before = orc.eval_paths(wp)["cost"]
+    after = orc.eval_paths(z)["cost"]
+    np.testing.assert_array_equal(before, arr["cost"])        # the objective is the golden one
+    assert (after < before).all(), (before, after)
+    np.testing.assert_allclose(out["cost"], after, rtol=1e-12)
+    again = orc.refine(wp, rp)
+    np.testing.assert_array_equal(again["wp"], z)               # deterministic
+
+
+def test_refine_needs_smooth_options(oracle_mod):
+    orc, wp, _ = _canonical(oracle_mod, {"obstacle_smooth": False})
+    with pytest.raises(ValueError):
+        orc.refine(wp, oracle_mod.refine_params(n_outer=1, n_inner=1))
+
+
+def test_refine_zero_iterations_is_identity(oracle_mod):
+    orc, wp, arr = _canonical(oracle_mod)
+    out = orc.refine(wp, oracle_mod.refine_params(n_outer=0, n_inner=0))
+    np.testing.assert_array_equal(out["wp"], wp)
+    np.testing.assert_allclose(out["cost"], arr["cost"], rtol=1e-12)
+    assert (out["iters"] == 0).all()

@@ -1,0 +1,54 @@
+"""Time batched refinement (uam_refine) on generated candidates of the canonical map.
+usage: python tools/time_refine.py [--pairs Q] [--N N] [--outer O] [--inner I] [--nfz K]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=80)
+    ap.add_argument("--outer", type=int, default=10)
+    ap.add_argument("--inner", type=int, default=20)
+    ap.add_argument("--nfz", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import (build_region_map, canonical_params,
+                                                canonical_spec, displacements)
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    spec = canonical_spec(nfz_polygons=a.nfz)
+    eng = Engine(0)
+    eng.set_geometry(compile_map(build_region_map(spec)))
+    eng.set_params(canonical_params(spec, N=a.N, anchor=tuple(spec["x_start"])))
+    wp = eng.gen_paths(torch.tensor(random_pairs(a.pairs, seed=3), device="cuda"),
+                       arc_table(a.N, displacements(5)))
+    rp = {"n_outer": a.outer, "n_inner": a.inner}
+    eng.refine(wp[:64], rp)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0 = eng.eval_waypoints(wp)["cost"]
+    e0.record()
+    out = eng.refine(wp, rp)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    c1 = out["cost"]
+    P = wp.shape[0]
+    print(json.dumps({"paths": P, "N": a.N, "outer": a.outer, "inner": a.inner, "nfz": a.nfz,
+                      "ms": ms, "paths_per_s": P / (ms / 1e3),
+                      "steps_mean": float(out["iters"].double().mean()),
+                      "cost_before_mean": float(c0.mean()), "cost_after_mean": float(c1.mean()),
+                      "improved_frac": float((c1 < c0).double().mean()),
+                      "infeas_median": float(out["infeas"].median())}))
+
+
+if __name__ == "__main__":
+    main()

@@ -755,6 +755,325 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// K6: batched refinement.  One lane per path.  Definition and operation
+// order: oracle/uam_oracle.c orc_refine (GPU == oracle bit for bit).  The reference solves
+// min get_cost(z) s.t. get_nonlincon(z) in {0} with OpEn's ALM (solver.py:82-93).
+
+struct KRefine {
+    int32_t n_outer, n_inner, max_backtrack, pad;
+    double c0, rho, c_max, alpha0, armijo, theta, max_step;
+};
+
+__device__ __forceinline__ void ineq_grad(const DevIneq* __restrict__ q, double x0, double x1,
+                                          double& gx, double& gy) {
+    const int kind = q->kind;
+    if (kind == UAM_INEQ_HALFPLANE) {
+        gx = q->p[4] * q->p[3];
+        gy = -(q->p[4] * q->p[2]);
+    } else if (kind == UAM_INEQ_ELLIPSE) {
+        const double a = (x0 - q->p[0]) / q->p[2];
+        const double b = (x1 - q->p[1]) / q->p[3];
+        gx = (2.0 * a) / q->p[2];
+        gy = (2.0 * b) / q->p[3];
+    } else {
+        gx = (q->p[0] == 0.0) ? q->p[3] : 0.0;
+        gy = (q->p[0] == 0.0) ? 0.0 : q->p[3];
+    }
+}
+
+// d psi/dx of the smooth psi = prod_i min(h_i - e, 0)^2 (products recomputed, no arrays)
+__device__ __forceinline__ void psi_grad(const KGeom& g, const DevShape& sh, double x0,
+                                         double x1, double e, double& dx, double& dy) {
+    double ox = 0.0, oy = 0.0;
+    const int f = sh.first, n = sh.count;
+    for (int i = 0; i < n; ++i) {
+        const double mi = fmin(ineq_h(g.ineq + f + i, x0, x1) - e, 0.0);
+        if (mi == 0.0) continue;
+        double prod = 1.0;
+        for (int k = 0; k < n; ++k) {
+            if (k == i) continue;
+            const double mk = fmin(ineq_h(g.ineq + f + k, x0, x1) - e, 0.0);
+            prod = prod * (mk * mk);
+        }
+        const double coef = (2.0 * mi) * prod;
+        double hx, hy;
+        ineq_grad(g.ineq + f + i, x0, x1, hx, hy);
+        ox = ox + coef * hx;
+        oy = oy + coef * hy;
+    }
+    dx = ox;
+    dy = oy;
+}
+
+__device__ __forceinline__ void phi_grad(const KGeom& g, const KParams& p, double x0, double x1,
+                                         double& dx, double& dy) {
+    double gx = 0.0, gy = 0.0;
+    for (int r = 0; r < g.n_regions; ++r) {
+        double tx = 0.0, ty = 0.0;
+        const int s1 = g.region_first[r + 1];
+        for (int s = g.region_first[r]; s < s1; ++s) {
+            const DevShape& sh = g.shape[s];
+            if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;
+            double ex, ey;
+            psi_grad(g, sh, x0, x1, p.enlargement, ex, ey);
+            if (sh.has_center) {
+                tx = tx + ex / sh.norm_pen;
+                ty = ty + ey / sh.norm_pen;
+            } else {
+                tx = tx + ex;
+                ty = ty + ey;
+            }
+        }
+        gx = gx + p.weights[r] * tx;
+        gy = gy + p.weights[r] * ty;
+    }
+    dx = gx;
+    dy = gy;
+}
+
+struct KinRow {
+    double c[3];
+    double d[3][6];
+};
+
+__device__ __forceinline__ void kin_eval(double pkx, double pky, double p1x, double p1y,
+                                         double p2x, double p2y, double r, double mincos,
+                                         bool ms, bool want_grad, KinRow& o) {
+    const double ax = p1x - pkx, ay = p1y - pky;
+    const double bx = p2x - p1x, by = p2y - p1y;
+    double sa = 0.0, sb = 0.0, dt = 0.0;
+    sa = sa + ax * ax;
+    sa = sa + ay * ay;
+    sb = sb + bx * bx;
+    sb = sb + by * by;
+    dt = dt + ax * bx;
+    dt = dt + ay * by;
+    const double ra = sqrt(sa), rb = sqrt(sb);
+    const double na = ms ? ra * ra : ra, nb = ms ? rb * rb : rb;
+    o.c[0] = fmax(0.0, nb - r * na);
+    o.c[1] = fmax(0.0, na / r - nb);
+    const double den = na * nb;
+    o.c[2] = fmax(0.0, mincos - dt / den);
+    if (!want_grad) return;
+    const double gax = ms ? 2.0 * ax : ax / ra, gay = ms ? 2.0 * ay : ay / ra;
+    const double gbx = ms ? 2.0 * bx : bx / rb, gby = ms ? 2.0 * by : by / rb;
+    double da[3][2], db[3][2];
+    da[0][0] = -(r * gax), da[0][1] = -(r * gay), db[0][0] = gbx, db[0][1] = gby;
+    da[1][0] = gax / r, da[1][1] = gay / r, db[1][0] = -gbx, db[1][1] = -gby;
+    const double d2 = den * den;
+    const double qax = bx / den - ((dt * nb) * gax) / d2, qay = by / den - ((dt * nb) * gay) / d2;
+    const double qbx = ax / den - ((dt * na) * gbx) / d2, qby = ay / den - ((dt * na) * gby) / d2;
+    da[2][0] = -qax, da[2][1] = -qay, db[2][0] = -qbx, db[2][1] = -qby;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        o.d[t][0] = -da[t][0];
+        o.d[t][1] = -da[t][1];
+        o.d[t][2] = da[t][0] - db[t][0];
+        o.d[t][3] = da[t][1] - db[t][1];
+        o.d[t][4] = db[t][0];
+        o.d[t][5] = db[t][1];
+    }
+}
+
+// A path in refinement: points z[W][2] (path-major, in place), gradient gr[2N][P] and
+// multipliers y[R][P] strided by P (coalesced across lanes).  pt(j, a) is z_j, or the trial
+// point z_j - a * gr_j for interior j when a != 0.
+struct RefPath {
+    double* z;
+    double* gr;
+    const double* y;
+    int64_t P;
+    int N;
+    __device__ __forceinline__ double grv(int k) const { return gr[(int64_t)k * P]; }
+    __device__ __forceinline__ void pt(int j, double a, double& x, double& yv) const {
+        x = z[2 * j];
+        yv = z[2 * j + 1];
+        if (a != 0.0 && j >= 1 && j <= N) {
+            x = x - a * grv(2 * (j - 1));
+            yv = yv - a * grv(2 * (j - 1) + 1);
+        }
+    }
+    __device__ __forceinline__ void gadd(int j, double vx, double vy) const {
+        double* g0 = gr + (int64_t)(2 * (j - 1)) * P;
+        double* g1 = gr + (int64_t)(2 * (j - 1) + 1) * P;
+        *g0 = *g0 + vx;
+        *g1 = *g1 + vy;
+    }
+};
+
+// L(z - a gr) (a = 0: at z; want_grad only with a = 0 -> writes gr); order as refine_L.
+__device__ double refine_L(const KGeom& g, const KParams& p, const RefPath& rp, double a,
+                           double c, bool want_grad, double* fout) {
+    const int N = p.N, W = N + 2;
+    const bool ls = p.length_smooth != 0;
+    if (want_grad)
+        for (int k = 0; k < 2 * N; ++k) rp.gr[(int64_t)k * rp.P] = 0.0;
+    double x0, y0;
+    rp.pt(0, a, x0, y0);
+    const double ax = p.anchor_mode ? p.anchor_x : x0, ay = p.anchor_mode ? p.anchor_y : y0;
+    double L = 0.0;
+    if (p.quirk_length) {
+        const double dx = x0 - ax, dy = y0 - ay;
+        double s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        const double n = sqrt(s);
+        L = L + (ls ? n * n : n);
+    }
+    const int kend = p.quirk_length ? N : N + 1;
+    double px = x0, py = y0;
+    for (int k = 1; k <= kend; ++k) {
+        double qx, qy;
+        rp.pt(k, a, qx, qy);
+        const double dx = qx - px, dy = qy - py;
+        double s = 0.0;
+        s = s + dx * dx;
+        s = s + dy * dy;
+        const double n = sqrt(s);
+        L = L + (ls ? n * n : n);
+        if (want_grad) {
+            const double sc = (double)(N + 1);
+            const double vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
+            const double vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
+            if (k <= N) rp.gadd(k, vx, vy);
+            if (k - 1 >= 1) rp.gadd(k - 1, -vx, -vy);
+        }
+        px = qx;
+        py = qy;
+    }
+    double f = (double)(N + 1) * L;
+    const double dN = (double)N;
+    for (int j = 0; j < W; ++j) {
+        double x, yv;
+        rp.pt(j, a, x, yv);
+        f = f + total_penalty(g, p, x, yv) / dN;
+        if (want_grad && j >= 1 && j <= N) {
+            double gx, gy;
+            phi_grad(g, p, x, yv, gx, gy);
+            rp.gadd(j, gx / dN, gy / dN);
+        }
+    }
+    double aug = 0.0;
+    const double hc = 0.5 * c;
+    const bool ms = p.maxratio_smooth != 0;
+    for (int k = 0; k < N; ++k) {
+        double x0k, y0k, x1k, y1k, x2k, y2k;
+        rp.pt(k, a, x0k, y0k);
+        rp.pt(k + 1, a, x1k, y1k);
+        rp.pt(k + 2, a, x2k, y2k);
+        KinRow kr;
+        kin_eval(x0k, y0k, x1k, y1k, x2k, y2k, p.r_eff, p.mincos, ms, want_grad, kr);
+        for (int t = 0; t < 3; ++t) {
+            const double tt = kr.c[t] + rp.y[(int64_t)(3 * k + t) * rp.P] / c;
+            aug = aug + hc * (tt * tt);
+            if (want_grad && kr.c[t] > 0.0) {
+                const double coef = c * tt;
+                for (int q = 0; q < 3; ++q) {
+                    const int j = k + q;
+                    if (j >= 1 && j <= N)
+                        rp.gadd(j, coef * kr.d[t][2 * q], coef * kr.d[t][2 * q + 1]);
+                }
+            }
+        }
+    }
+    for (int s = 0; s < g.n_obstacles; ++s) {
+        const DevShape& sh = g.shape[s];
+        for (int j = 0; j < W; ++j) {
+            double x, yv;
+            rp.pt(j, a, x, yv);
+            const bool culled = (sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x, yv);
+            const double v = culled ? 0.0 : psi(g, sh, x, yv, true, 0.0);
+            const double tt = v + rp.y[(int64_t)(3 * N + s * W + j) * rp.P] / c;
+            aug = aug + hc * (tt * tt);
+            if (want_grad && j >= 1 && j <= N && !culled) {
+                const double coef = c * tt;
+                double ex, ey;
+                psi_grad(g, sh, x, yv, 0.0, ex, ey);
+                rp.gadd(j, coef * ex, coef * ey);
+            }
+        }
+    }
+    if (fout) *fout = f;
+    return f + aug;
+}
+
+__global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
+                                                double* __restrict__ wp, int64_t P,
+                                                double* __restrict__ yb, double* __restrict__ gb,
+                                                double* __restrict__ cost,
+                                                double* __restrict__ infeas,
+                                                int32_t* __restrict__ iters) {
+    const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (path >= P) return;
+    const int N = p.N, W = N + 2, R = 3 * N + g.n_obstacles * W;
+    RefPath rp;
+    rp.z = wp + path * (int64_t)W * 2;
+    rp.gr = gb + path;
+    rp.y = yb + path;
+    rp.P = P;
+    rp.N = N;
+    double* y = yb + path;
+    for (int i = 0; i < R; ++i) y[(int64_t)i * P] = 0.0;
+    double c = rf.c0, alpha = rf.alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
+    int32_t used = 0;
+    const bool ms = p.maxratio_smooth != 0;
+    for (int o = 0; o < rf.n_outer; ++o) {
+        for (int it = 0; it < rf.n_inner; ++it) {
+            const double Lz = refine_L(g, p, rp, 0.0, c, true, nullptr);
+            double gn2 = 0.0;
+            for (int k = 0; k < 2 * N; ++k) {
+                const double v = rp.grv(k);
+                gn2 = gn2 + v * v;
+            }
+            if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;
+            double a = fmin(alpha * 2.0, rf.max_step / sqrt(gn2));
+            bool ok = false;
+            for (int b = 0; b < rf.max_backtrack; ++b) {
+                const double Lt = refine_L(g, p, rp, a, c, false, nullptr);
+                if (Lt <= Lz - (rf.armijo * a) * gn2) {
+                    ok = true;
+                    break;
+                }
+                a = a * 0.5;
+            }
+            if (!ok) break;
+            for (int k = 0; k < 2 * N; ++k) rp.z[2 + k] = rp.z[2 + k] - a * rp.grv(k);
+            alpha = a;
+            ++used;
+        }
+        // multiplier update on the canonical rows (kinematic, then obstacles s-major)
+        inf = 0.0;
+        for (int k = 0; k < N; ++k) {
+            KinRow kr;
+            kin_eval(rp.z[2 * k], rp.z[2 * k + 1], rp.z[2 * k + 2], rp.z[2 * k + 3],
+                     rp.z[2 * k + 4], rp.z[2 * k + 5], p.r_eff, p.mincos, ms, false, kr);
+            for (int t = 0; t < 3; ++t) {
+                double* yi = y + (int64_t)(3 * k + t) * P;
+                *yi = *yi + c * kr.c[t];
+                inf = inf + kr.c[t] * kr.c[t];
+            }
+        }
+        for (int s = 0; s < g.n_obstacles; ++s) {
+            const DevShape& sh = g.shape[s];
+            for (int j = 0; j < W; ++j) {
+                const double x = rp.z[2 * j], yv = rp.z[2 * j + 1];
+                const bool culled = (sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x, yv);
+                const double v = culled ? 0.0 : psi(g, sh, x, yv, true, 0.0);
+                double* yi = y + (int64_t)(3 * N + s * W + j) * P;
+                *yi = *yi + c * v;
+                inf = inf + v * v;
+            }
+        }
+        if (inf > rf.theta * prev) c = fmin(c * rf.rho, rf.c_max);
+        prev = inf;
+    }
+    refine_L(g, p, rp, 0.0, c, false, &f);
+    if (cost) cost[path] = f;
+    if (infeas) infeas[path] = inf;
+    if (iters) iters[path] = used;
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -1369,6 +1688,45 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
                        (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths) {
+    if (!ctx || !ctx->have_params || n_paths < 0) return -1;
+    const int64_t N = ctx->kp.N, W = N + 2;
+    const int64_t R = 3 * N + (int64_t)ctx->kg.n_obstacles * W;
+    return (R + 2 * N) * n_paths * (int64_t)sizeof(double);
+}
+
+int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_params* rp,
+               void* workspace, int64_t workspace_bytes, double* cost, double* infeas,
+               int32_t* iters, uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    if (!rp) return fail(UAM_E_INVALID, "refine params are NULL");
+    if (!ctx->kp.penalty_smooth || !ctx->kp.obstacle_smooth)
+        return fail(UAM_E_INVALID, "refinement needs penalty_smooth and obstacle_smooth");
+    if (n_paths < 0) return fail(UAM_E_INVALID, "n_paths < 0");
+    if (n_paths == 0) return UAM_OK;
+    if (!wp || !workspace) return fail(UAM_E_INVALID, "wp/workspace is NULL");
+    if (rp->n_outer < 0 || rp->n_inner < 0 || rp->max_backtrack < 1 || !(rp->c0 > 0.0) ||
+        !(rp->max_step > 0.0))
+        return fail(UAM_E_INVALID, "bad refine params");
+    const int64_t need = uam_refine_workspace_bytes(ctx, n_paths);
+    if (workspace_bytes < need)
+        return fail(UAM_E_INVALID, "workspace %lld bytes < %lld", (long long)workspace_bytes,
+                    (long long)need);
+    const int64_t N = ctx->kp.N, W = N + 2;
+    const int64_t R = 3 * N + (int64_t)ctx->kg.n_obstacles * W;
+    double* yb = (double*)workspace;
+    double* gb = yb + R * n_paths;
+    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, 0, rp->c0, rp->rho, rp->c_max,
+               rp->alpha0, rp->armijo, rp->theta, rp->max_step};
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_refine, dim3(grid_for(n_paths, 256, INT32_MAX)), dim3(256), 0,
+                       (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp, n_paths, yb, gb, cost,
+                       infeas, iters);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }

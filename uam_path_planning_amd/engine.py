@@ -113,6 +113,11 @@ def _ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
+# refinement defaults (same as oracle.refine_params)
+REFINE_DEFAULTS = dict(n_outer=10, n_inner=20, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
+                       alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5)
+
+
 class Engine:
     """libuampath context bound to one GPU."""
 
@@ -345,6 +350,40 @@ class Engine:
         _lib.check(self.lib.uam_path_length(self._ctx, _ptr(p), P, n_points, int(n_segments),
                                             int(bool(smooth)), _ptr(out), self.stream),
                    "uam_path_length")
+        return out
+
+    def refine(self, wp, params=None, inplace=False):
+        """Batched ALM refinement of waypoint paths (the reference's
+        OpEn solve, solver.py:82-93).  wp: [P, N+2, 2] float64; endpoints stay fixed.
+        Returns {"wp", "cost", "infeas", "iters"} (device tensors).  Definition and
+        defaults: oracle/uam_oracle.c orc_refine, REFINE_DEFAULTS."""
+        torch = _torch()
+        W = self.params.N + 2
+        z = self.tensor(wp, torch.float64)
+        if z.dim() == 2:
+            z = z.unsqueeze(0)
+        if tuple(z.shape[1:]) != (W, 2):
+            raise ValueError(f"wp must be [P, {W}, 2], got {tuple(z.shape)}")
+        if not inplace:
+            z = z.clone(memory_format=torch.contiguous_format)
+        elif not z.is_contiguous():
+            raise ValueError("inplace refinement needs a contiguous tensor")
+        P = z.shape[0]
+        rp = dict(REFINE_DEFAULTS)
+        rp.update(params or {})
+        st = _lib.RefineParams(int(rp["n_outer"]), int(rp["n_inner"]), int(rp["max_backtrack"]),
+                               0, float(rp["c0"]), float(rp["rho"]), float(rp["c_max"]),
+                               float(rp["alpha0"]), float(rp["armijo"]), float(rp["theta"]),
+                               float(rp["max_step"]))
+        nbytes = self.lib.uam_refine_workspace_bytes(self._ctx, P)
+        if nbytes < 0:
+            raise _lib.UamError("uam_refine_workspace_bytes: set geometry and params first")
+        ws = self.empty((max(nbytes, 8) // 8,), torch.float64)
+        out = {"wp": z, "cost": self.empty((P,), torch.float64),
+               "infeas": self.empty((P,), torch.float64), "iters": self.empty((P,), torch.int32)}
+        _lib.check(self.lib.uam_refine(self._ctx, _ptr(z), P, ctypes.byref(st), _ptr(ws), nbytes,
+                                       _ptr(out["cost"]), _ptr(out["infeas"]), _ptr(out["iters"]),
+                                       self.stream), "uam_refine")
         return out
 
     def synchronize(self):
