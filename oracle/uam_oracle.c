@@ -551,53 +551,66 @@ static void ineq_grad(const orc_geom* g, int i, double x0, double x1, double* gx
     }
 }
 
-/* d psi / dx for the smooth psi = prod_i min(h_i - e, 0)^2 */
-static void psi_grad(const orc_geom* g, int s, double x0, double x1, double e, double* dx,
-                     double* dy) {
+/* smooth psi = prod_i m_i^2, m_i = min(h_i - e, 0), and (want != 0) its gradient
+ * sum_i (2 psi / m_i) grad h_i -- nonzero only where every m_i != 0, i.e. psi != 0.  The value
+ * is psi(g, s, x, 1, e) bit for bit. */
+static double psi_vg(const orc_geom* g, int s, double x0, double x1, double e, int want,
+                     double* dx, double* dy) {
     int f = g->shape_first[s], n = g->shape_count[s];
-    double m[64];
-    double ox = 0.0, oy = 0.0;
-    if (n > 64) n = 64;
-    for (int i = 0; i < n; ++i) m[i] = fmin(ineq_h(g, f + i, x0, x1) - e, 0.0);
-    for (int i = 0; i < n; ++i) {
-        if (m[i] == 0.0) continue;
-        double prod = 1.0;
-        for (int k = 0; k < n; ++k)
-            if (k != i) prod = prod * (m[k] * m[k]);
-        double coef = (2.0 * m[i]) * prod;
-        double hx, hy;
-        ineq_grad(g, f + i, x0, x1, &hx, &hy);
-        ox = ox + coef * hx;
-        oy = oy + coef * hy;
+    double v = 1.0;
+    for (int i = f; i < f + n; ++i) {
+        double m = fmin(ineq_h(g, i, x0, x1) - e, 0.0);
+        v = v * (m * m);
     }
-    *dx = ox;
-    *dy = oy;
+    *dx = 0.0;
+    *dy = 0.0;
+    if (want && v != 0.0) {
+        double ox = 0.0, oy = 0.0;
+        for (int i = f; i < f + n; ++i) {
+            double m = fmin(ineq_h(g, i, x0, x1) - e, 0.0);
+            double coef = (2.0 * v) / m, hx, hy;
+            ineq_grad(g, i, x0, x1, &hx, &hy);
+            ox = ox + coef * hx;
+            oy = oy + coef * hy;
+        }
+        *dx = ox;
+        *dy = oy;
+    }
+    return v;
 }
 
-/* gradient of the total penalty Phi (smooth) */
-static void phi_grad(const orc_geom* g, const orc_params* p, double x0, double x1, double* dx,
-                     double* dy) {
-    double gx = 0.0, gy = 0.0;
+/* Phi (total_penalty bit for bit, smooth) and, when want, its gradient */
+static double phi_vg(const orc_geom* g, const orc_params* p, double x0, double x1, int want,
+                     double* dx, double* dy) {
+    double pen = 0.0, gx = 0.0, gy = 0.0;
     for (int r = 0; r < g->n_regions; ++r) {
-        double tx = 0.0, ty = 0.0;
+        double t = 0.0, tx = 0.0, ty = 0.0;
         for (int s = g->region_first[r]; s < g->region_first[r + 1]; ++s) {
             double cx = g->shape_center[2 * s], cy = g->shape_center[2 * s + 1];
             double ex, ey;
-            psi_grad(g, s, x0, x1, p->enlargement, &ex, &ey);
+            double v = psi_vg(g, s, x0, x1, p->enlargement, want, &ex, &ey);
             if (isnan(cx) || isnan(cy)) {
-                tx = tx + ex;
-                ty = ty + ey;
+                t = t + v;
+                if (want && v != 0.0) {
+                    tx = tx + ex;
+                    ty = ty + ey;
+                }
             } else {
                 double nrm = psi(g, s, cx, cy, 1, p->enlargement);
-                tx = tx + ex / nrm;
-                ty = ty + ey / nrm;
+                t = t + v / nrm;
+                if (want && v != 0.0) {
+                    tx = tx + ex / nrm;
+                    ty = ty + ey / nrm;
+                }
             }
         }
+        pen = pen + p->weights[r] * t;
         gx = gx + p->weights[r] * tx;
         gy = gy + p->weights[r] * ty;
     }
     *dx = gx;
     *dy = gy;
+    return pen;
 }
 
 typedef struct {
@@ -645,138 +658,210 @@ static void kin_eval(const double* pk, const double* pk1, const double* pk2, dou
     }
 }
 
-/* L(z) (and its gradient into gr[2N] when gr != NULL).  z: W points of this path.
- * Summation order: f exactly as get_cost; then kinematic rows k ascending (c1, c2, c3); then
- * obstacle rows s-major, j ascending. */
-static double refine_L(const orc_geom* g, const orc_params* p, const double* z, const double* y,
-                       double c, double* gr, double* fout) {
-    const int N = p->N, W = N + 2;
-    const int ls = p->length_smooth;
-    const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
-    const double mincos = cos(p->maxalpha);
-    if (gr)
-        for (int k = 0; k < 2 * N; ++k) gr[k] = 0.0;
-    /* length term (get_cost order) */
-    double ax = p->anchor_mode ? p->anchor_x : z[0], ay = p->anchor_mode ? p->anchor_y : z[1];
-    double L = 0.0;
-    if (p->quirk_length) {
-        double dx = z[0] - ax, dy = z[1] - ay, s = 0.0;
-        s = s + dx * dx;
-        s = s + dy * dy;
-        L = L + nrm_of(s, ls);
+/* The GPU refines one path per 64-lane wavefront, lane l owning waypoints j = l, l+64, ...
+ * Path-level sums are therefore defined as: per lane, the sequential sum of its waypoints'
+ * terms (ascending j), then the xor butterfly over lanes (offsets 32, 16, ..., 1). */
+#define RF_LANES 64
+static double wsum(const double* t, int W) {
+    double v[RF_LANES], u[RF_LANES];
+    for (int l = 0; l < RF_LANES; ++l) {
+        v[l] = 0.0;
+        for (int j = l; j < W; j += RF_LANES) v[l] = v[l] + t[j];
     }
-    int kend = p->quirk_length ? N : N + 1;
-    for (int k = 1; k <= kend; ++k) {
-        double dx = z[2 * k] - z[2 * k - 2], dy = z[2 * k + 1] - z[2 * k - 1], s = 0.0;
-        s = s + dx * dx;
-        s = s + dy * dy;
-        double n = sqrt(s);
-        L = L + (ls ? n * n : n);
-        if (gr) {
-            double sc = (double)(N + 1);
-            double vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
-            double vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
-            if (k <= N) {
-                gr[2 * (k - 1)] = gr[2 * (k - 1)] + vx;
-                gr[2 * (k - 1) + 1] = gr[2 * (k - 1) + 1] + vy;
-            }
-            if (k - 1 >= 1) {
-                gr[2 * (k - 2)] = gr[2 * (k - 2)] - vx;
-                gr[2 * (k - 2) + 1] = gr[2 * (k - 2) + 1] - vy;
-            }
-        }
+    for (int off = RF_LANES / 2; off >= 1; off >>= 1) {
+        for (int l = 0; l < RF_LANES; ++l) u[l] = v[l] + v[l ^ off];
+        for (int l = 0; l < RF_LANES; ++l) v[l] = u[l];
     }
-    double f = (double)(N + 1) * L;
+    return v[0];
+}
+
+/* waypoint j of z, or of the trial point z - a gr (interior j, a != 0); gr is indexed by
+ * waypoint (gr[2j], gr[2j+1]; endpoints unused) */
+static void rpt(const double* z, const double* gr, double a, int N, int j, double* x,
+                double* y) {
+    *x = z[2 * j];
+    *y = z[2 * j + 1];
+    if (a != 0.0 && j >= 1 && j <= N) {
+        *x = *x - a * gr[2 * j];
+        *y = *y - a * gr[2 * j + 1];
+    }
+}
+
+/* norm of the segment (px,py) -> (qx,qy) as get_cost sums it; vx/vy: d/dq of (N+1) * term */
+static double seg_term(double px, double py, double qx, double qy, int ls, double sc,
+                       double* vx, double* vy) {
+    double dx = qx - px, dy = qy - py, s = 0.0;
+    s = s + dx * dx;
+    s = s + dy * dy;
+    double n = sqrt(s);
+    if (vx) {
+        *vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
+        *vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
+    }
+    return ls ? n * n : n;
+}
+
+/* L(z - a gr) = f + sum_i (c/2)(g_i + y_i/c)^2 with f = (N+1) * sum(length terms) +
+ * sum(Phi_j / N); per-waypoint terms as the GPU lanes form them; want (a = 0 only): the
+ * gradient into gr (waypoint-indexed) and *gn2 = |gr|^2.  Gradient accumulation order per
+ * waypoint j: segment ending at j (+), segment starting at j (-), grad Phi / N, kinematic
+ * rows k = j-2, j-1, j (c1, c2, c3), obstacle rows s ascending.  yk: kinematic multipliers
+ * [3N], yo: obstacle multipliers [S][W]. */
+static double refine_L(const orc_geom* g, const orc_params* p, const double* z, double* gr,
+                       double a, const double* yk, const double* yo, double c, int want,
+                       double* fout, double* gn2) {
+    const int N = p->N, W = N + 2, ls = p->length_smooth, ms = p->maxratio_smooth;
+    const double r = ms ? p->maxratio * p->maxratio : p->maxratio;
+    const double mincos = cos(p->maxalpha), hc = 0.5 * c, dN = (double)N;
+    const double sc = (double)(N + 1);
+    const int kend = p->quirk_length ? N : N + 1;
+    double* tl = (double*)malloc(sizeof(double) * 4 * W);
+    double *tphi = tl + W, *taug = tl + 2 * W, *tg = tl + 3 * W;
     for (int j = 0; j < W; ++j) {
-        f = f + total_penalty(g, p, z[2 * j], z[2 * j + 1]) / (double)N;
-        if (gr && j >= 1 && j <= N) {
-            double gx, gy;
-            phi_grad(g, p, z[2 * j], z[2 * j + 1], &gx, &gy);
-            gr[2 * (j - 1)] = gr[2 * (j - 1)] + gx / (double)N;
-            gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + gy / (double)N;
+        const int inner = want && j >= 1 && j <= N;
+        double xj, yj;
+        rpt(z, gr, a, N, j, &xj, &yj);
+        /* length term of the segment ending at j (anchor segment for j = 0) */
+        double lj = 0.0, vx0 = 0.0, vy0 = 0.0;
+        if (j == 0) {
+            if (p->quirk_length) {
+                double ax = p->anchor_mode ? p->anchor_x : xj;
+                double ay = p->anchor_mode ? p->anchor_y : yj;
+                lj = seg_term(ax, ay, xj, yj, ls, sc, NULL, NULL);
+            }
+        } else if (j <= kend) {
+            double px, py;
+            rpt(z, gr, a, N, j - 1, &px, &py);
+            lj = seg_term(px, py, xj, yj, ls, sc, inner ? &vx0 : NULL, &vy0);
         }
-    }
-    double aug = 0.0;
-    const double hc = 0.5 * c;
-    for (int k = 0; k < N; ++k) {
-        kin_row kr;
-        kin_eval(&z[2 * k], &z[2 * (k + 1)], &z[2 * (k + 2)], r, mincos, p->maxratio_smooth,
-                 gr != NULL, &kr);
-        double gv[3] = {kr.c1, kr.c2, kr.c3};
-        for (int t = 0; t < 3; ++t) {
-            double tt = gv[t] + y[3 * k + t] / c;
-            aug = aug + hc * (tt * tt);
-            if (gr && gv[t] > 0.0) {
-                double coef = c * tt;
-                for (int q = 0; q < 3; ++q) {
-                    int j = k + q;
-                    if (j >= 1 && j <= N) {
-                        gr[2 * (j - 1)] = gr[2 * (j - 1)] + coef * kr.d[t][2 * q];
-                        gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + coef * kr.d[t][2 * q + 1];
-                    }
+        tl[j] = lj;
+        double ex, ey;
+        tphi[j] = phi_vg(g, p, xj, yj, inner, &ex, &ey) / dN;
+        double aj = 0.0, gx = 0.0, gy = 0.0;
+        if (j < N) {
+            double q1[2], q2[2], q0[2] = {xj, yj};
+            rpt(z, gr, a, N, j + 1, &q1[0], &q1[1]);
+            rpt(z, gr, a, N, j + 2, &q2[0], &q2[1]);
+            kin_row kr;
+            kin_eval(q0, q1, q2, r, mincos, ms, 0, &kr);
+            double gv[3] = {kr.c1, kr.c2, kr.c3};
+            for (int t = 0; t < 3; ++t) {
+                double tt = gv[t] + yk[3 * j + t] / c;
+                aj = aj + hc * (tt * tt);
+            }
+        }
+        if (inner) {
+            if (j <= kend) {
+                gx = gx + vx0;
+                gy = gy + vy0;
+            }
+            if (j + 1 <= kend) {
+                double qx, qy, vx, vy;
+                rpt(z, gr, a, N, j + 1, &qx, &qy);
+                seg_term(xj, yj, qx, qy, ls, sc, &vx, &vy);
+                gx = gx - vx;
+                gy = gy - vy;
+            }
+            gx = gx + ex / dN;
+            gy = gy + ey / dN;
+            for (int k = j - 2; k <= j; ++k) {
+                if (k < 0 || k >= N) continue;
+                double q0[2], q1[2], q2[2];
+                rpt(z, gr, a, N, k, &q0[0], &q0[1]);
+                rpt(z, gr, a, N, k + 1, &q1[0], &q1[1]);
+                rpt(z, gr, a, N, k + 2, &q2[0], &q2[1]);
+                kin_row kr;
+                kin_eval(q0, q1, q2, r, mincos, ms, 1, &kr);
+                double gv[3] = {kr.c1, kr.c2, kr.c3};
+                const int q = j - k;
+                for (int t = 0; t < 3; ++t) {
+                    if (!(gv[t] > 0.0)) continue;
+                    double coef = c * (gv[t] + yk[3 * k + t] / c);
+                    gx = gx + coef * kr.d[t][2 * q];
+                    gy = gy + coef * kr.d[t][2 * q + 1];
                 }
             }
         }
-    }
-    for (int s = 0; s < g->n_obstacles; ++s) {
-        for (int j = 0; j < W; ++j) {
-            double v = psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0);
-            double tt = v + y[3 * N + s * W + j] / c;
-            aug = aug + hc * (tt * tt);
-            if (gr && j >= 1 && j <= N) {
-                double coef = c * tt, ex, ey;
-                psi_grad(g, s, z[2 * j], z[2 * j + 1], 0.0, &ex, &ey);
-                gr[2 * (j - 1)] = gr[2 * (j - 1)] + coef * ex;
-                gr[2 * (j - 1) + 1] = gr[2 * (j - 1) + 1] + coef * ey;
+        for (int s = 0; s < g->n_obstacles; ++s) {
+            double ox, oy;
+            double v = psi_vg(g, s, xj, yj, 0.0, inner, &ox, &oy);
+            double tt = v + yo[(int64_t)s * W + j] / c;
+            aj = aj + hc * (tt * tt);
+            if (inner && v != 0.0) {
+                double coef = c * tt;
+                gx = gx + coef * ox;
+                gy = gy + coef * oy;
             }
         }
+        taug[j] = aj;
+        tg[j] = 0.0;
+        if (inner) {
+            gr[2 * j] = gx;
+            gr[2 * j + 1] = gy;
+            tg[j] = gx * gx + gy * gy;
+        }
     }
+    double f = sc * wsum(tl, W) + wsum(tphi, W);
+    double L = f + wsum(taug, W);
+    if (want && gn2) *gn2 = wsum(tg, W);
     if (fout) *fout = f;
-    return f + aug;
+    free(tl);
+    return L;
 }
 
-/* constraint rows in canonical order (kinematic, then obstacles s-major) */
-static void refine_rows(const orc_geom* g, const orc_params* p, const double* z, double* rows) {
-    const int N = p->N, W = N + 2;
-    const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
+/* outer ALM update: y += c * row for every row; returns sum of row^2 (lane-tree order) */
+static double refine_update(const orc_geom* g, const orc_params* p, const double* z,
+                            double* yk, double* yo, double c) {
+    const int N = p->N, W = N + 2, ms = p->maxratio_smooth;
+    const double r = ms ? p->maxratio * p->maxratio : p->maxratio;
     const double mincos = cos(p->maxalpha);
-    for (int k = 0; k < N; ++k) {
-        kin_row kr;
-        kin_eval(&z[2 * k], &z[2 * (k + 1)], &z[2 * (k + 2)], r, mincos, p->maxratio_smooth, 0,
-                 &kr);
-        rows[3 * k] = kr.c1;
-        rows[3 * k + 1] = kr.c2;
-        rows[3 * k + 2] = kr.c3;
+    double* ti = (double*)malloc(sizeof(double) * W);
+    for (int j = 0; j < W; ++j) {
+        double sj = 0.0;
+        if (j < N) {
+            kin_row kr;
+            kin_eval(&z[2 * j], &z[2 * (j + 1)], &z[2 * (j + 2)], r, mincos, ms, 0, &kr);
+            double gv[3] = {kr.c1, kr.c2, kr.c3};
+            for (int t = 0; t < 3; ++t) {
+                yk[3 * j + t] = yk[3 * j + t] + c * gv[t];
+                sj = sj + gv[t] * gv[t];
+            }
+        }
+        for (int s = 0; s < g->n_obstacles; ++s) {
+            double v = psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0);
+            yo[(int64_t)s * W + j] = yo[(int64_t)s * W + j] + c * v;
+            sj = sj + v * v;
+        }
+        ti[j] = sj;
     }
-    for (int s = 0; s < g->n_obstacles; ++s)
-        for (int j = 0; j < W; ++j) rows[3 * N + s * W + j] = psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0);
+    double inf = wsum(ti, W);
+    free(ti);
+    return inf;
 }
 
 int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* rp, double* wp,
                int64_t P, double* cost, double* infeas, int32_t* iters) {
-    const int N = p->N, W = N + 2, R = 3 * N + g->n_obstacles * W;
+    const int N = p->N, W = N + 2;
+    const int64_t R = 3 * (int64_t)N + (int64_t)g->n_obstacles * W;
     if (!p->penalty_smooth || !p->obstacle_smooth) return -1;
-    double* y = (double*)malloc(sizeof(double) * R);
-    double* rows = (double*)malloc(sizeof(double) * R);
-    double* gr = (double*)malloc(sizeof(double) * 2 * N);
-    double* zt = (double*)malloc(sizeof(double) * 2 * W);
+    double* y = (double*)malloc(sizeof(double) * (R > 0 ? R : 1));
+    double* gr = (double*)malloc(sizeof(double) * 2 * W);
     for (int64_t pi = 0; pi < P; ++pi) {
         double* z = wp + pi * (int64_t)W * 2;
-        for (int i = 0; i < R; ++i) y[i] = 0.0;
+        double *yk = y, *yo = y + 3 * N;
+        for (int64_t i = 0; i < R; ++i) y[i] = 0.0;
+        for (int k = 0; k < 2 * W; ++k) gr[k] = 0.0;
         double c = rp->c0, alpha = rp->alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
         int32_t it_used = 0;
         for (int o = 0; o < rp->n_outer; ++o) {
             for (int it = 0; it < rp->n_inner; ++it) {
-                double Lz = refine_L(g, p, z, y, c, gr, NULL);
                 double gn2 = 0.0;
-                for (int k = 0; k < 2 * N; ++k) gn2 = gn2 + gr[k] * gr[k];
+                double Lz = refine_L(g, p, z, gr, 0.0, yk, yo, c, 1, NULL, &gn2);
                 if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;
                 double a = fmin(alpha * 2.0, rp->max_step / sqrt(gn2));
                 int ok = 0;
                 for (int b = 0; b < rp->max_backtrack; ++b) {
-                    for (int k = 0; k < 2 * W; ++k) zt[k] = z[k];
-                    for (int k = 0; k < 2 * N; ++k) zt[2 + k] = z[2 + k] - a * gr[k];
-                    double Lt = refine_L(g, p, zt, y, c, NULL, NULL);
+                    double Lt = refine_L(g, p, z, gr, a, yk, yo, c, 0, NULL, NULL);
                     if (Lt <= Lz - (rp->armijo * a) * gn2) {
                         ok = 1;
                         break;
@@ -784,27 +869,23 @@ int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* 
                     a = a * 0.5;
                 }
                 if (!ok) break;
-                for (int k = 0; k < 2 * N; ++k) z[2 + k] = z[2 + k] - a * gr[k];
+                for (int j = 1; j <= N; ++j) {
+                    z[2 * j] = z[2 * j] - a * gr[2 * j];
+                    z[2 * j + 1] = z[2 * j + 1] - a * gr[2 * j + 1];
+                }
                 alpha = a;
                 ++it_used;
             }
-            refine_rows(g, p, z, rows);
-            inf = 0.0;
-            for (int i = 0; i < R; ++i) {
-                y[i] = y[i] + c * rows[i];
-                inf = inf + rows[i] * rows[i];
-            }
+            inf = refine_update(g, p, z, yk, yo, c);
             if (inf > rp->theta * prev) c = fmin(c * rp->rho, rp->c_max);
             prev = inf;
         }
-        refine_L(g, p, z, y, c, NULL, &f);
+        refine_L(g, p, z, gr, 0.0, yk, yo, c, 0, &f, NULL);
         if (cost) cost[pi] = f;
         if (infeas) infeas[pi] = inf;
         if (iters) iters[pi] = it_used;
     }
     free(y);
-    free(rows);
     free(gr);
-    free(zt);
     return 0;
 }

@@ -756,9 +756,12 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
 }
 
 // ----------------------------------------------------------------------------------------
-// K6: batched refinement.  One lane per path.  Definition and operation
-// order: oracle/uam_oracle.c orc_refine (GPU == oracle bit for bit).  The reference solves
-// min get_cost(z) s.t. get_nonlincon(z) in {0} with OpEn's ALM (solver.py:82-93).
+// K6: batched refinement.  One 64-lane wavefront per path, lane l owning
+// waypoints j = l, l+64, ...; the path's points z, gradient gr and kinematic multipliers live
+// in the wave's LDS slice, obstacle multipliers [S][W] in the workspace (row s*W + j touched
+// only by the lane owning j).  Definition and operation order: oracle/uam_oracle.c
+// orc_refine (GPU == oracle bit for bit; path sums = per-lane sums + xor butterfly).  The
+// reference solves min get_cost(z) s.t. get_nonlincon(z) in {0} with OpEn (solver.py:82-93).
 
 struct KRefine {
     int32_t n_outer, n_inner, max_backtrack, pad;
@@ -782,64 +785,74 @@ __device__ __forceinline__ void ineq_grad(const DevIneq* __restrict__ q, double 
     }
 }
 
-// d psi/dx of the smooth psi = prod_i min(h_i - e, 0)^2 (products recomputed, no arrays)
-__device__ __forceinline__ void psi_grad(const KGeom& g, const DevShape& sh, double x0,
-                                         double x1, double e, double& dx, double& dy) {
-    double ox = 0.0, oy = 0.0;
-    const int f = sh.first, n = sh.count;
-    for (int i = 0; i < n; ++i) {
-        const double mi = fmin(ineq_h(g.ineq + f + i, x0, x1) - e, 0.0);
-        if (mi == 0.0) continue;
-        double prod = 1.0;
-        for (int k = 0; k < n; ++k) {
-            if (k == i) continue;
-            const double mk = fmin(ineq_h(g.ineq + f + k, x0, x1) - e, 0.0);
-            prod = prod * (mk * mk);
-        }
-        const double coef = (2.0 * mi) * prod;
-        double hx, hy;
-        ineq_grad(g.ineq + f + i, x0, x1, hx, hy);
-        ox = ox + coef * hx;
-        oy = oy + coef * hy;
+// smooth psi = prod m_i^2 (== psi(.., smooth, e) bit for bit) and, when want, its gradient
+// sum_i (2 psi / m_i) grad h_i (nonzero only where psi != 0)
+__device__ __forceinline__ double psi_vg(const KGeom& g, const DevShape& sh, double x0,
+                                         double x1, double e, bool want, double& dx,
+                                         double& dy) {
+    double v = 1.0;
+    const int end = sh.first + sh.count;
+    for (int i = sh.first; i < end; ++i) {
+        const double m = fmin(ineq_h(g.ineq + i, x0, x1) - e, 0.0);
+        v = v * (m * m);
     }
-    dx = ox;
-    dy = oy;
+    dx = 0.0;
+    dy = 0.0;
+    if (want && v != 0.0) {
+        double ox = 0.0, oy = 0.0;
+        for (int i = sh.first; i < end; ++i) {
+            const double m = fmin(ineq_h(g.ineq + i, x0, x1) - e, 0.0);
+            const double coef = (2.0 * v) / m;
+            double hx, hy;
+            ineq_grad(g.ineq + i, x0, x1, hx, hy);
+            ox = ox + coef * hx;
+            oy = oy + coef * hy;
+        }
+        dx = ox;
+        dy = oy;
+    }
+    return v;
 }
 
-__device__ __forceinline__ void phi_grad(const KGeom& g, const KParams& p, double x0, double x1,
-                                         double& dx, double& dy) {
-    double gx = 0.0, gy = 0.0;
+// Phi (== total_penalty bit for bit) and, when want, grad Phi
+__device__ double phi_vg(const KGeom& g, const KParams& p, double x0, double x1, bool want,
+                         double& dx, double& dy) {
+    double pen = 0.0, gx = 0.0, gy = 0.0;
     for (int r = 0; r < g.n_regions; ++r) {
-        double tx = 0.0, ty = 0.0;
+        double t = 0.0, tx = 0.0, ty = 0.0;
         const int s1 = g.region_first[r + 1];
         for (int s = g.region_first[r]; s < s1; ++s) {
             const DevShape& sh = g.shape[s];
-            if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;
+            if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;  // psi = 0
             double ex, ey;
-            psi_grad(g, sh, x0, x1, p.enlargement, ex, ey);
+            const double v = psi_vg(g, sh, x0, x1, p.enlargement, want, ex, ey);
             if (sh.has_center) {
-                tx = tx + ex / sh.norm_pen;
-                ty = ty + ey / sh.norm_pen;
+                t = t + v / sh.norm_pen;
+                if (want && v != 0.0) {
+                    tx = tx + ex / sh.norm_pen;
+                    ty = ty + ey / sh.norm_pen;
+                }
             } else {
-                tx = tx + ex;
-                ty = ty + ey;
+                t = t + v;
+                if (want && v != 0.0) {
+                    tx = tx + ex;
+                    ty = ty + ey;
+                }
             }
         }
+        pen = pen + p.weights[r] * t;
         gx = gx + p.weights[r] * tx;
         gy = gy + p.weights[r] * ty;
     }
     dx = gx;
     dy = gy;
+    return pen;
 }
 
-struct KinRow {
-    double c[3];
-    double d[3][6];
-};
-
-__device__ __forceinline__ void kin_eval(double pkx, double pky, double p1x, double p1y,
-                                         double p2x, double p2y, double r, double mincos,
-                                         bool ms, bool want_grad, KinRow& o) {
+// kinematic rows of (p_k, p_k+1, p_k+2); q in {0,1,2}: d row / d p_k+q, q < 0: values only
+__device__ __forceinline__ void kin_col(double pkx, double pky, double p1x, double p1y,
+                                        double p2x, double p2y, double r, double mincos,
+                                        bool ms, int q, double (&cv)[3], double (&dq)[3][2]) {
     const double ax = p1x - pkx, ay = p1y - pky;
     const double bx = p2x - p1x, by = p2y - p1y;
     double sa = 0.0, sb = 0.0, dt = 0.0;
@@ -851,11 +864,11 @@ __device__ __forceinline__ void kin_eval(double pkx, double pky, double p1x, dou
     dt = dt + ay * by;
     const double ra = sqrt(sa), rb = sqrt(sb);
     const double na = ms ? ra * ra : ra, nb = ms ? rb * rb : rb;
-    o.c[0] = fmax(0.0, nb - r * na);
-    o.c[1] = fmax(0.0, na / r - nb);
+    cv[0] = fmax(0.0, nb - r * na);
+    cv[1] = fmax(0.0, na / r - nb);
     const double den = na * nb;
-    o.c[2] = fmax(0.0, mincos - dt / den);
-    if (!want_grad) return;
+    cv[2] = fmax(0.0, mincos - dt / den);
+    if (q < 0) return;
     const double gax = ms ? 2.0 * ax : ax / ra, gay = ms ? 2.0 * ay : ay / ra;
     const double gbx = ms ? 2.0 * bx : bx / rb, gby = ms ? 2.0 * by : by / rb;
     double da[3][2], db[3][2];
@@ -867,170 +880,201 @@ __device__ __forceinline__ void kin_eval(double pkx, double pky, double p1x, dou
     da[2][0] = -qax, da[2][1] = -qay, db[2][0] = -qbx, db[2][1] = -qby;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
-        o.d[t][0] = -da[t][0];
-        o.d[t][1] = -da[t][1];
-        o.d[t][2] = da[t][0] - db[t][0];
-        o.d[t][3] = da[t][1] - db[t][1];
-        o.d[t][4] = db[t][0];
-        o.d[t][5] = db[t][1];
+        if (q == 0) {
+            dq[t][0] = -da[t][0];
+            dq[t][1] = -da[t][1];
+        } else if (q == 1) {
+            dq[t][0] = da[t][0] - db[t][0];
+            dq[t][1] = da[t][1] - db[t][1];
+        } else {
+            dq[t][0] = db[t][0];
+            dq[t][1] = db[t][1];
+        }
     }
 }
 
-// A path in refinement: points z[W][2] (path-major, in place), gradient gr[2N][P] and
-// multipliers y[R][P] strided by P (coalesced across lanes).  pt(j, a) is z_j, or the trial
-// point z_j - a * gr_j for interior j when a != 0.
-struct RefPath {
-    double* z;
-    double* gr;
-    const double* y;
-    int64_t P;
-    int N;
-    __device__ __forceinline__ double grv(int k) const { return gr[(int64_t)k * P]; }
-    __device__ __forceinline__ void pt(int j, double a, double& x, double& yv) const {
+// LDS visibility between the lanes of one wave (wave-private slice, no block barrier)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+struct RfPath {
+    const double* z;   // LDS [W][2]
+    double* gr;        // LDS [W][2] (waypoint-indexed; endpoints unused)
+    const double* yk;  // LDS [3N]
+    const double* yo;  // global [S][W]
+    int N, W;
+    __device__ __forceinline__ void pt(int j, double a, double& x, double& y) const {
         x = z[2 * j];
-        yv = z[2 * j + 1];
+        y = z[2 * j + 1];
         if (a != 0.0 && j >= 1 && j <= N) {
-            x = x - a * grv(2 * (j - 1));
-            yv = yv - a * grv(2 * (j - 1) + 1);
+            x = x - a * gr[2 * j];
+            y = y - a * gr[2 * j + 1];
         }
-    }
-    __device__ __forceinline__ void gadd(int j, double vx, double vy) const {
-        double* g0 = gr + (int64_t)(2 * (j - 1)) * P;
-        double* g1 = gr + (int64_t)(2 * (j - 1) + 1) * P;
-        *g0 = *g0 + vx;
-        *g1 = *g1 + vy;
     }
 };
 
-// L(z - a gr) (a = 0: at z; want_grad only with a = 0 -> writes gr); order as refine_L.
-__device__ double refine_L(const KGeom& g, const KParams& p, const RefPath& rp, double a,
-                           double c, bool want_grad, double* fout) {
-    const int N = p.N, W = N + 2;
-    const bool ls = p.length_smooth != 0;
-    if (want_grad)
-        for (int k = 0; k < 2 * N; ++k) rp.gr[(int64_t)k * rp.P] = 0.0;
-    double x0, y0;
-    rp.pt(0, a, x0, y0);
-    const double ax = p.anchor_mode ? p.anchor_x : x0, ay = p.anchor_mode ? p.anchor_y : y0;
-    double L = 0.0;
-    if (p.quirk_length) {
-        const double dx = x0 - ax, dy = y0 - ay;
-        double s = 0.0;
-        s = s + dx * dx;
-        s = s + dy * dy;
-        const double n = sqrt(s);
-        L = L + (ls ? n * n : n);
+__device__ __forceinline__ double seg_term(double px, double py, double qx, double qy, bool ls,
+                                           double sc, bool want, double& vx, double& vy) {
+    const double dx = qx - px, dy = qy - py;
+    double s = 0.0;
+    s = s + dx * dx;
+    s = s + dy * dy;
+    const double n = sqrt(s);
+    if (want) {
+        vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
+        vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
     }
+    return ls ? n * n : n;
+}
+
+// L(z - a gr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
+// gradient accumulation order as oracle refine_L.
+__device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int lane, double a,
+                       double c, bool want, double* fout, double* gn2) {
+    const int N = rp.N, W = rp.W;
+    const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
+    const double hc = 0.5 * c, dN = (double)N, sc = (double)(N + 1);
     const int kend = p.quirk_length ? N : N + 1;
-    double px = x0, py = y0;
-    for (int k = 1; k <= kend; ++k) {
-        double qx, qy;
-        rp.pt(k, a, qx, qy);
-        const double dx = qx - px, dy = qy - py;
-        double s = 0.0;
-        s = s + dx * dx;
-        s = s + dy * dy;
-        const double n = sqrt(s);
-        L = L + (ls ? n * n : n);
-        if (want_grad) {
-            const double sc = (double)(N + 1);
-            const double vx = ls ? sc * (2.0 * dx) : sc * (dx / n);
-            const double vy = ls ? sc * (2.0 * dy) : sc * (dy / n);
-            if (k <= N) rp.gadd(k, vx, vy);
-            if (k - 1 >= 1) rp.gadd(k - 1, -vx, -vy);
+    double sl = 0.0, sphi = 0.0, saug = 0.0, sg = 0.0;
+    for (int j = lane; j < W; j += 64) {
+        const bool inner = want && j >= 1 && j <= N;
+        double xj, yj;
+        rp.pt(j, a, xj, yj);
+        double lj = 0.0, vx0 = 0.0, vy0 = 0.0;
+        if (j == 0) {
+            if (p.quirk_length) {
+                const double ax = p.anchor_mode ? p.anchor_x : xj;
+                const double ay = p.anchor_mode ? p.anchor_y : yj;
+                lj = seg_term(ax, ay, xj, yj, ls, sc, false, vx0, vy0);
+            }
+        } else if (j <= kend) {
+            double px, py;
+            rp.pt(j - 1, a, px, py);
+            lj = seg_term(px, py, xj, yj, ls, sc, inner, vx0, vy0);
         }
-        px = qx;
-        py = qy;
-    }
-    double f = (double)(N + 1) * L;
-    const double dN = (double)N;
-    for (int j = 0; j < W; ++j) {
-        double x, yv;
-        rp.pt(j, a, x, yv);
-        f = f + total_penalty(g, p, x, yv) / dN;
-        if (want_grad && j >= 1 && j <= N) {
-            double gx, gy;
-            phi_grad(g, p, x, yv, gx, gy);
-            rp.gadd(j, gx / dN, gy / dN);
+        sl = sl + lj;
+        double ex, ey;
+        sphi = sphi + phi_vg(g, p, xj, yj, inner, ex, ey) / dN;
+        double aj = 0.0, gx = 0.0, gy = 0.0;
+        if (j < N) {
+            double q1x, q1y, q2x, q2y, cv[3], dq[3][2];
+            rp.pt(j + 1, a, q1x, q1y);
+            rp.pt(j + 2, a, q2x, q2y);
+            kin_col(xj, yj, q1x, q1y, q2x, q2y, p.r_eff, p.mincos, ms, -1, cv, dq);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const double tt = cv[t] + rp.yk[3 * j + t] / c;
+                aj = aj + hc * (tt * tt);
+            }
         }
-    }
-    double aug = 0.0;
-    const double hc = 0.5 * c;
-    const bool ms = p.maxratio_smooth != 0;
-    for (int k = 0; k < N; ++k) {
-        double x0k, y0k, x1k, y1k, x2k, y2k;
-        rp.pt(k, a, x0k, y0k);
-        rp.pt(k + 1, a, x1k, y1k);
-        rp.pt(k + 2, a, x2k, y2k);
-        KinRow kr;
-        kin_eval(x0k, y0k, x1k, y1k, x2k, y2k, p.r_eff, p.mincos, ms, want_grad, kr);
-        for (int t = 0; t < 3; ++t) {
-            const double tt = kr.c[t] + rp.y[(int64_t)(3 * k + t) * rp.P] / c;
-            aug = aug + hc * (tt * tt);
-            if (want_grad && kr.c[t] > 0.0) {
-                const double coef = c * tt;
-                for (int q = 0; q < 3; ++q) {
-                    const int j = k + q;
-                    if (j >= 1 && j <= N)
-                        rp.gadd(j, coef * kr.d[t][2 * q], coef * kr.d[t][2 * q + 1]);
+        if (inner) {
+            if (j <= kend) {
+                gx = gx + vx0;
+                gy = gy + vy0;
+            }
+            if (j + 1 <= kend) {
+                double qx, qy, vx, vy;
+                rp.pt(j + 1, a, qx, qy);
+                seg_term(xj, yj, qx, qy, ls, sc, true, vx, vy);
+                gx = gx - vx;
+                gy = gy - vy;
+            }
+            gx = gx + ex / dN;
+            gy = gy + ey / dN;
+            for (int q = 2; q >= 0; --q) {  // k = j - q ascending
+                const int k = j - q;
+                if (k < 0 || k >= N) continue;
+                double k0x, k0y, k1x, k1y, k2x, k2y, cv[3], dq[3][2];
+                rp.pt(k, a, k0x, k0y);
+                rp.pt(k + 1, a, k1x, k1y);
+                rp.pt(k + 2, a, k2x, k2y);
+                kin_col(k0x, k0y, k1x, k1y, k2x, k2y, p.r_eff, p.mincos, ms, q, cv, dq);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    if (!(cv[t] > 0.0)) continue;
+                    const double coef = c * (cv[t] + rp.yk[3 * k + t] / c);
+                    gx = gx + coef * dq[t][0];
+                    gy = gy + coef * dq[t][1];
                 }
             }
         }
-    }
-    for (int s = 0; s < g.n_obstacles; ++s) {
-        const DevShape& sh = g.shape[s];
-        for (int j = 0; j < W; ++j) {
-            double x, yv;
-            rp.pt(j, a, x, yv);
-            const bool culled = (sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x, yv);
-            const double v = culled ? 0.0 : psi(g, sh, x, yv, true, 0.0);
-            const double tt = v + rp.y[(int64_t)(3 * N + s * W + j) * rp.P] / c;
-            aug = aug + hc * (tt * tt);
-            if (want_grad && j >= 1 && j <= N && !culled) {
+        for (int s = 0; s < g.n_obstacles; ++s) {
+            const DevShape& sh = g.shape[s];
+            double v = 0.0, ox = 0.0, oy = 0.0;
+            if (!((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)))
+                v = psi_vg(g, sh, xj, yj, 0.0, inner, ox, oy);
+            const double tt = v + rp.yo[(int64_t)s * W + j] / c;
+            aj = aj + hc * (tt * tt);
+            if (inner && v != 0.0) {
                 const double coef = c * tt;
-                double ex, ey;
-                psi_grad(g, sh, x, yv, 0.0, ex, ey);
-                rp.gadd(j, coef * ex, coef * ey);
+                gx = gx + coef * ox;
+                gy = gy + coef * oy;
             }
         }
+        saug = saug + aj;
+        double tg = 0.0;
+        if (inner) {
+            rp.gr[2 * j] = gx;
+            rp.gr[2 * j + 1] = gy;
+            tg = gx * gx + gy * gy;
+        }
+        sg = sg + tg;
     }
+    sl = wave_sum(sl);
+    sphi = wave_sum(sphi);
+    saug = wave_sum(saug);
+    const double f = sc * sl + sphi;
+    if (want) *gn2 = wave_sum(sg);
     if (fout) *fout = f;
-    return f + aug;
+    return f + saug;
 }
 
 __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
                                                 double* __restrict__ wp, int64_t P,
-                                                double* __restrict__ yb, double* __restrict__ gb,
+                                                double* __restrict__ yo_all,
                                                 double* __restrict__ cost,
                                                 double* __restrict__ infeas,
                                                 int32_t* __restrict__ iters) {
-    const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (path >= P) return;
-    const int N = p.N, W = N + 2, R = 3 * N + g.n_obstacles * W;
-    RefPath rp;
-    rp.z = wp + path * (int64_t)W * 2;
-    rp.gr = gb + path;
-    rp.y = yb + path;
-    rp.P = P;
-    rp.N = N;
-    double* y = yb + path;
-    for (int i = 0; i < R; ++i) y[(int64_t)i * P] = 0.0;
+    extern __shared__ double rf_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int64_t path = (int64_t)blockIdx.x * wpb + wave;
+    if (path >= P) return;  // whole wave
+    const int N = p.N, W = N + 2, S = g.n_obstacles;
+    double* z = rf_lds + (int64_t)wave * (4 * W + 3 * N);
+    double* gr = z + 2 * W;
+    double* yk = gr + 2 * W;
+    double* zg = wp + path * (int64_t)W * 2;
+    double* yo = yo_all + path * (int64_t)S * W;
+    for (int k = lane; k < 2 * W; k += 64) {
+        z[k] = zg[k];
+        gr[k] = 0.0;
+    }
+    for (int k = lane; k < 3 * N; k += 64) yk[k] = 0.0;
+    for (int s = 0; s < S; ++s)
+        for (int j = lane; j < W; j += 64) yo[(int64_t)s * W + j] = 0.0;
+    wave_sync();
+    RfPath rp{z, gr, yk, yo, N, W};
+    const bool ms = p.maxratio_smooth != 0;
     double c = rf.c0, alpha = rf.alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
     int32_t used = 0;
-    const bool ms = p.maxratio_smooth != 0;
     for (int o = 0; o < rf.n_outer; ++o) {
         for (int it = 0; it < rf.n_inner; ++it) {
-            const double Lz = refine_L(g, p, rp, 0.0, c, true, nullptr);
             double gn2 = 0.0;
-            for (int k = 0; k < 2 * N; ++k) {
-                const double v = rp.grv(k);
-                gn2 = gn2 + v * v;
-            }
-            if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;
+            const double Lz = rf_L(g, p, rp, lane, 0.0, c, true, nullptr, &gn2);
+            wave_sync();
+            if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;  // wave-uniform
             double a = fmin(alpha * 2.0, rf.max_step / sqrt(gn2));
             bool ok = false;
             for (int b = 0; b < rf.max_backtrack; ++b) {
-                const double Lt = refine_L(g, p, rp, a, c, false, nullptr);
+                const double Lt = rf_L(g, p, rp, lane, a, c, false, nullptr, nullptr);
                 if (Lt <= Lz - (rf.armijo * a) * gn2) {
                     ok = true;
                     break;
@@ -1038,40 +1082,54 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
                 a = a * 0.5;
             }
             if (!ok) break;
-            for (int k = 0; k < 2 * N; ++k) rp.z[2 + k] = rp.z[2 + k] - a * rp.grv(k);
+            wave_sync();
+            for (int j = lane; j < W; j += 64) {
+                if (j >= 1 && j <= N) {
+                    z[2 * j] = z[2 * j] - a * gr[2 * j];
+                    z[2 * j + 1] = z[2 * j + 1] - a * gr[2 * j + 1];
+                }
+            }
+            wave_sync();
             alpha = a;
             ++used;
         }
-        // multiplier update on the canonical rows (kinematic, then obstacles s-major)
-        inf = 0.0;
-        for (int k = 0; k < N; ++k) {
-            KinRow kr;
-            kin_eval(rp.z[2 * k], rp.z[2 * k + 1], rp.z[2 * k + 2], rp.z[2 * k + 3],
-                     rp.z[2 * k + 4], rp.z[2 * k + 5], p.r_eff, p.mincos, ms, false, kr);
-            for (int t = 0; t < 3; ++t) {
-                double* yi = y + (int64_t)(3 * k + t) * P;
-                *yi = *yi + c * kr.c[t];
-                inf = inf + kr.c[t] * kr.c[t];
+        // outer update: y += c * row, inf = sum row^2 (kinematic rows of j, then obstacles)
+        double si = 0.0;
+        for (int j = lane; j < W; j += 64) {
+            const double xj = z[2 * j], yj = z[2 * j + 1];
+            double sj = 0.0;
+            if (j < N) {
+                double cv[3], dq[3][2];
+                kin_col(xj, yj, z[2 * j + 2], z[2 * j + 3], z[2 * j + 4], z[2 * j + 5], p.r_eff,
+                        p.mincos, ms, -1, cv, dq);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    yk[3 * j + t] = yk[3 * j + t] + c * cv[t];
+                    sj = sj + cv[t] * cv[t];
+                }
             }
-        }
-        for (int s = 0; s < g.n_obstacles; ++s) {
-            const DevShape& sh = g.shape[s];
-            for (int j = 0; j < W; ++j) {
-                const double x = rp.z[2 * j], yv = rp.z[2 * j + 1];
-                const bool culled = (sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x, yv);
-                const double v = culled ? 0.0 : psi(g, sh, x, yv, true, 0.0);
-                double* yi = y + (int64_t)(3 * N + s * W + j) * P;
+            for (int s = 0; s < S; ++s) {
+                const DevShape& sh = g.shape[s];
+                if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)) continue;  // +0
+                const double v = psi(g, sh, xj, yj, true, 0.0);
+                double* yi = yo + (int64_t)s * W + j;
                 *yi = *yi + c * v;
-                inf = inf + v * v;
+                sj = sj + v * v;
             }
+            si = si + sj;
         }
+        inf = wave_sum(si);
+        wave_sync();
         if (inf > rf.theta * prev) c = fmin(c * rf.rho, rf.c_max);
         prev = inf;
     }
-    refine_L(g, p, rp, 0.0, c, false, &f);
-    if (cost) cost[path] = f;
-    if (infeas) infeas[path] = inf;
-    if (iters) iters[path] = used;
+    rf_L(g, p, rp, lane, 0.0, c, false, &f, nullptr);
+    for (int k = lane; k < 2 * W; k += 64) zg[k] = z[k];
+    if (lane == 0) {
+        if (cost) cost[path] = f;
+        if (infeas) infeas[path] = inf;
+        if (iters) iters[path] = used;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
@@ -1694,9 +1752,8 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
 
 int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths) {
     if (!ctx || !ctx->have_params || n_paths < 0) return -1;
-    const int64_t N = ctx->kp.N, W = N + 2;
-    const int64_t R = 3 * N + (int64_t)ctx->kg.n_obstacles * W;
-    return (R + 2 * N) * n_paths * (int64_t)sizeof(double);
+    const int64_t W = ctx->kp.N + 2;
+    return (int64_t)ctx->kg.n_obstacles * W * n_paths * (int64_t)sizeof(double);
 }
 
 int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_params* rp,
@@ -1708,25 +1765,28 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
     if (!ctx->kp.penalty_smooth || !ctx->kp.obstacle_smooth)
         return fail(UAM_E_INVALID, "refinement needs penalty_smooth and obstacle_smooth");
     if (n_paths < 0) return fail(UAM_E_INVALID, "n_paths < 0");
-    if (n_paths == 0) return UAM_OK;
-    if (!wp || !workspace) return fail(UAM_E_INVALID, "wp/workspace is NULL");
     if (rp->n_outer < 0 || rp->n_inner < 0 || rp->max_backtrack < 1 || !(rp->c0 > 0.0) ||
         !(rp->max_step > 0.0))
         return fail(UAM_E_INVALID, "bad refine params");
+    const int64_t N = ctx->kp.N, W = N + 2;
+    const int64_t per_wave = (4 * W + 3 * N) * (int64_t)sizeof(double);
+    if (per_wave > 65536)
+        return fail(UAM_E_INVALID, "N = %lld too large for refinement (LDS)", (long long)N);
+    if (n_paths == 0) return UAM_OK;
     const int64_t need = uam_refine_workspace_bytes(ctx, n_paths);
+    if (!wp || (need > 0 && !workspace)) return fail(UAM_E_INVALID, "wp/workspace is NULL");
     if (workspace_bytes < need)
         return fail(UAM_E_INVALID, "workspace %lld bytes < %lld", (long long)workspace_bytes,
                     (long long)need);
-    const int64_t N = ctx->kp.N, W = N + 2;
-    const int64_t R = 3 * N + (int64_t)ctx->kg.n_obstacles * W;
-    double* yb = (double*)workspace;
-    double* gb = yb + R * n_paths;
-    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, 0, rp->c0, rp->rho, rp->c_max,
-               rp->alpha0, rp->armijo, rp->theta, rp->max_step};
+    const int wpb = (int)std::min<int64_t>(4, 65536 / per_wave);
+    const int64_t blocks = (n_paths + wpb - 1) / wpb;
+    if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "too many paths");
+    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, 0,     rp->c0,     rp->rho,
+               rp->c_max,   rp->alpha0, rp->armijo,        rp->theta, rp->max_step};
     DeviceGuard dg(ctx->device);
-    hipLaunchKernelGGL(k_refine, dim3(grid_for(n_paths, 256, INT32_MAX)), dim3(256), 0,
-                       (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp, n_paths, yb, gb, cost,
-                       infeas, iters);
+    hipLaunchKernelGGL(k_refine, dim3((unsigned)blocks), dim3(64 * wpb),
+                       (size_t)(wpb * per_wave), (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp,
+                       n_paths, (double*)workspace, cost, infeas, iters);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
