@@ -94,3 +94,53 @@ def test_refine_edge_cases(eng, oracle_mod):
     eng.set_params(dataclasses.replace(eng.params, obstacle_smooth=False))
     with pytest.raises((UamError, ValueError)):
         eng.refine(wp, {"n_outer": 1, "n_inner": 1})
+
+
+def test_dropin_solver_solve(eng, oracle_mod):
+    """Solver.solve(x_init, p) (solver.py:19-56 contract) = refinement of [x_start, x_init,
+    x_goal] under p; fval = sqrt(get_cost(x)), length = length_of(x); bit-exact vs the oracle
+    on the refined waypoints."""
+    from uam_path_planning_amd.path_generation import Solver
+    from uam_path_planning_amd.scenario import canonical_problem, canonical_spec
+
+    spec = canonical_spec()
+    prob = canonical_problem()
+    solver = Solver(prob, {"refine": {"n_outer": 3, "n_inner": 10}})
+    x_init = solver.create_x_init(0.25)
+    params = list(spec["x_start"]) + list(spec["x_goal"]) + [
+        spec["maxratio"], spec["maxalpha"], spec["enlargement"]] + list(spec["weights"])
+    res = solver.solve(x_init, params)
+    assert set(res) == {"x", "time", "fval", "length", "exit_status"}
+    assert len(res["x"]) == 2 * prob.N
+    z = np.concatenate([spec["x_start"], res["x"], spec["x_goal"]])
+    assert res["fval"] == np.sqrt(prob.get_cost(z))
+    assert res["length"] == prob.length_of(res["x"])
+    assert res["exit_status"] in ("Converged", "NotConvergedIterations")
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), prob.N, spec["options"],
+                            spec["maxratio"], spec["maxalpha"], spec["enlargement"],
+                            spec["weights"], anchor=tuple(spec["x_start"]))
+    wp0 = np.concatenate([spec["x_start"], x_init, spec["x_goal"]]).reshape(1, -1, 2)
+    ref = orc.refine(wp0, oracle_mod.refine_params(n_outer=3, n_inner=10))
+    np.testing.assert_array_equal(np.asarray(res["x"]), ref["wp"][0, 1:-1].reshape(-1))
+    assert res["fval"] < np.sqrt(prob.get_cost(wp0.reshape(-1)))
+    with pytest.raises(ValueError):
+        solver.solve(x_init, params[:-1])
+
+
+def test_dropin_solve_candidates_selection(eng):
+    from uam_path_planning_amd.path_generation import Solver
+    from uam_path_planning_amd.path_generation.solver import _select
+    from uam_path_planning_amd.scenario import canonical_problem, canonical_spec
+
+    spec = canonical_spec()
+    prob = canonical_problem()
+    solver = Solver(prob, {"refine": {"n_outer": 2, "n_inner": 8}})
+    params = list(spec["x_start"]) + list(spec["x_goal"]) + [
+        spec["maxratio"], spec["maxalpha"], spec["enlargement"]] + list(spec["weights"])
+    res = solver.solve_candidates(params)
+    assert res["x"].shape == (5, 2 * prob.N)
+    assert res["min_fval_index"] == int(np.argmin(res["fval"]))
+    assert res["min_length_index"] == int(np.argmin(res["length"]))
+    one = solver.solve(solver.create_x_init(res["displacements"][2]), params)
+    np.testing.assert_array_equal(np.asarray(one["x"]), res["x"][2])   # batch == single
+    assert _select([3.0, 1.0, 1.0, 2.0]) == 1 and _select([0.0, 2.0]) == 1

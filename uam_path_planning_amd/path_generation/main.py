@@ -2,11 +2,15 @@
 the canonical Nagasaki map (setup_map 21-49, from the data files via the safe loader), the
 N=80 problem (setup_problem 53-61), the parameter vector (main.py:128-150), and the candidate
 loop + selection (run 158-196) -- except that every displacement is evaluated in ONE device
-launch and no OpEn solve runs (out of scope): the printed fval/length are those of the initial
-candidates.  Shapefile export and plotting (main.py:92-116) are out of scope.
+launch.  With --solve (main.py:168-193 solve loop) every candidate is refined in one launch by
+the GPU ALM refinement (Solver.solve_candidates) and the printed fval/length are those of the
+refined paths; without it they are those of the initial candidates.  Shapefile export and
+plotting (main.py:92-116) are out of scope.
 
-    python -m uam_path_planning_amd.path_generation.main
+    python -m uam_path_planning_amd.path_generation.main [--solve]
 """
+import sys
+
 import numpy as np
 
 from ..arcs import REFERENCE_DISPLACEMENTS
@@ -37,7 +41,7 @@ class Main:
         assert maxratio >= 1
         assert 0 <= maxalpha <= np.pi
 
-    def run(self, displacements=REFERENCE_DISPLACEMENTS, verbose=True):
+    def run(self, displacements=REFERENCE_DISPLACEMENTS, verbose=True, solve=False):
         self.setup_map()
         self.setup_problem()
         self.setup_solver_options()
@@ -50,15 +54,25 @@ class Main:
                                     "enlargement": enlargement})
         for name, w in zip(self.map.region_names(), self.spec["weights"]):
             self.problem.set_weight(name, w)
-        res = self.solver.evaluate_candidates(displacements)
+        if solve:
+            params = x_start + x_goal + [maxratio, maxalpha, enlargement] + \
+                [self.problem.weights[n] for n in self.map.region_names()]
+            res = self.solver.solve_candidates(params, displacements)
+        else:
+            res = self.solver.evaluate_candidates(displacements)
         if verbose:
             print("Start simulation: N =", self.problem.N)
-            print("Candidates", self.solver.optimizer_name, "(initial paths, no OpEn solve)")
+            print("Solver" if solve else "Candidates", self.solver.optimizer_name,
+                  "(GPU ALM refinement)" if solve else "(initial paths, no solve)")
             print("-------------------------------------")
             for i in range(len(displacements)):
                 print("line", i + 1)
-                print(f"fval: {res['fval'][i]}\nlength: {res['length'][i]} km\n"
-                      f"nfz waypoints: {res['nfz_hits'][i]}\nkinematic violation: "
+                if solve:
+                    print(f"time: {res['time']} s (all lines)")
+                print(f"fval: {res['fval'][i]}\nlength: {res['length'][i]} km")
+                if solve:
+                    print(f"exit_status: {res['exit_status'][i]}")
+                print(f"nfz waypoints: {res['nfz_hits'][i]}\nkinematic violation: "
                       f"{res['kin_sum'][i]}")
                 print("-------------------------------------")
             print("Min fval result: line", res["min_fval_index"] + 1)
@@ -67,4 +81,4 @@ class Main:
 
 
 if __name__ == "__main__":
-    Main().run()
+    Main().run(solve="--solve" in sys.argv[1:])
