@@ -150,15 +150,16 @@ typedef struct {
 } uam_path_outputs;
 
 /* Batched refinement: the reference's OpEn ALM problem
- * min get_cost s.t. get_nonlincon in {0} (solver.py:82-93), solved per path by outer ALM
- * updates (y += c g; c = min(c rho, c_max) when sum g^2 > theta * previous) around n_inner
- * gradient steps with Armijo backtracking on L = f + sum (c/2)(g + y/c)^2; the first trial
- * step is min(2 alpha_prev, max_step / |grad|) (max_step bounds the waypoint move, km).
- * Definition:
- * oracle/uam_oracle.c orc_refine.  Needs penalty_smooth and obstacle_smooth. */
+ * min get_cost s.t. get_nonlincon in {0} (solver.py:82-93), solved per path by n_outer ALM
+ * updates (y += c g; c = min(c rho, c_max) when sum g^2 > theta * previous; stop when
+ * sqrt(sum g^2) <= delta) around up to n_inner L-BFGS steps (memory pairs, 0..8; 0 = steepest
+ * descent) on L = f + sum (c/2)(g + y/c)^2 with Armijo backtracking, stopping when
+ * |grad L| <= inner_tol.  First trial step: 1 (L-BFGS) or 2 * previous step (steepest),
+ * capped so the waypoint move is <= max_step (km).  Definition: oracle/uam_oracle.c
+ * orc_refine.  Needs penalty_smooth and obstacle_smooth. */
 typedef struct {
-    int32_t n_outer, n_inner, max_backtrack, pad;
-    double c0, rho, c_max, alpha0, armijo, theta, max_step;
+    int32_t n_outer, n_inner, max_backtrack, memory;
+    double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
 } uam_refine_params;
 
 int uam_abi_version(void);
@@ -235,7 +236,8 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */
-int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths);
+int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,
+                                   const uam_refine_params* params);
 /* Refines wp_dev [P][N+2][2] in place (endpoints fixed); per path: final cost (get_cost),
  * final sum of squared constraint rows, gradient steps taken.  Any output may be NULL. */
 int uam_refine(uam_ctx* ctx, double* wp_dev, int64_t n_paths, const uam_refine_params* params,

@@ -53,16 +53,18 @@ class _Volume(ctypes.Structure):
 
 class _RefineParams(ctypes.Structure):
     _fields_ = [("n_outer", ctypes.c_int32), ("n_inner", ctypes.c_int32),
-                ("max_backtrack", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("max_backtrack", ctypes.c_int32), ("memory", ctypes.c_int32),
                 ("c0", ctypes.c_double), ("rho", ctypes.c_double), ("c_max", ctypes.c_double),
                 ("alpha0", ctypes.c_double), ("armijo", ctypes.c_double),
-                ("theta", ctypes.c_double), ("max_step", ctypes.c_double)]
+                ("theta", ctypes.c_double), ("max_step", ctypes.c_double),
+                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double)]
 
 
-def refine_params(n_outer=10, n_inner=20, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
-                  alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5):
-    return _RefineParams(n_outer, n_inner, max_backtrack, 0, c0, rho, c_max, alpha0, armijo,
-                         theta, max_step)
+def refine_params(n_outer=15, n_inner=50, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
+                  alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5, memory=8, inner_tol=1e-3,
+                  delta=1e-4):
+    return _RefineParams(n_outer, n_inner, max_backtrack, memory, c0, rho, c_max, alpha0,
+                         armijo, theta, max_step, inner_tol, delta)
 
 
 def build():

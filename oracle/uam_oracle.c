@@ -525,9 +525,10 @@ int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v
  * with Armijo backtracking.  Requires penalty_smooth and obstacle_smooth (the reference's
  * main.py options).  Operation order is part of the definition (GPU == oracle bit for bit). */
 typedef struct {
-    int32_t n_outer, n_inner, max_backtrack, pad;
-    double c0, rho, c_max, alpha0, armijo, theta, max_step;
+    int32_t n_outer, n_inner, max_backtrack, memory;
+    double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
 } orc_refine_params;
+#define RF_MAXM 8
 
 /* gradient of h_i */
 static void ineq_grad(const orc_geom* g, int i, double x0, double x1, double* gx, double* gy) {
@@ -675,16 +676,24 @@ static double wsum(const double* t, int W) {
     return v[0];
 }
 
-/* waypoint j of z, or of the trial point z - a gr (interior j, a != 0); gr is indexed by
- * waypoint (gr[2j], gr[2j+1]; endpoints unused) */
-static void rpt(const double* z, const double* gr, double a, int N, int j, double* x,
+/* waypoint j of z, or of the trial point z + a dr (interior j, a != 0); vectors over the
+ * path are indexed by waypoint (v[2j], v[2j+1]; endpoint entries unused) */
+static void rpt(const double* z, const double* dr, double a, int N, int j, double* x,
                 double* y) {
     *x = z[2 * j];
     *y = z[2 * j + 1];
     if (a != 0.0 && j >= 1 && j <= N) {
-        *x = *x - a * gr[2 * j];
-        *y = *y - a * gr[2 * j + 1];
+        *x = *x + a * dr[2 * j];
+        *y = *y + a * dr[2 * j + 1];
     }
+}
+
+/* path dot product over the interior waypoints, lane-tree order */
+static double wdot(const double* u, const double* v, int N, double* tmp) {
+    const int W = N + 2;
+    for (int j = 0; j < W; ++j)
+        tmp[j] = (j >= 1 && j <= N) ? u[2 * j] * v[2 * j] + u[2 * j + 1] * v[2 * j + 1] : 0.0;
+    return wsum(tmp, W);
 }
 
 /* norm of the segment (px,py) -> (qx,qy) as get_cost sums it; vx/vy: d/dq of (N+1) * term */
@@ -701,15 +710,15 @@ static double seg_term(double px, double py, double qx, double qy, int ls, doubl
     return ls ? n * n : n;
 }
 
-/* L(z - a gr) = f + sum_i (c/2)(g_i + y_i/c)^2 with f = (N+1) * sum(length terms) +
+/* L(z + a dr) = f + sum_i (c/2)(g_i + y_i/c)^2 with f = (N+1) * sum(length terms) +
  * sum(Phi_j / N); per-waypoint terms as the GPU lanes form them; want (a = 0 only): the
  * gradient into gr (waypoint-indexed) and *gn2 = |gr|^2.  Gradient accumulation order per
  * waypoint j: segment ending at j (+), segment starting at j (-), grad Phi / N, kinematic
  * rows k = j-2, j-1, j (c1, c2, c3), obstacle rows s ascending.  yk: kinematic multipliers
  * [3N], yo: obstacle multipliers [S][W]. */
-static double refine_L(const orc_geom* g, const orc_params* p, const double* z, double* gr,
-                       double a, const double* yk, const double* yo, double c, int want,
-                       double* fout, double* gn2) {
+static double refine_L(const orc_geom* g, const orc_params* p, const double* z,
+                       const double* dr, double a, double* gr, const double* yk,
+                       const double* yo, double c, int want, double* fout, double* gn2) {
     const int N = p->N, W = N + 2, ls = p->length_smooth, ms = p->maxratio_smooth;
     const double r = ms ? p->maxratio * p->maxratio : p->maxratio;
     const double mincos = cos(p->maxalpha), hc = 0.5 * c, dN = (double)N;
@@ -720,7 +729,7 @@ static double refine_L(const orc_geom* g, const orc_params* p, const double* z, 
     for (int j = 0; j < W; ++j) {
         const int inner = want && j >= 1 && j <= N;
         double xj, yj;
-        rpt(z, gr, a, N, j, &xj, &yj);
+        rpt(z, dr, a, N, j, &xj, &yj);
         /* length term of the segment ending at j (anchor segment for j = 0) */
         double lj = 0.0, vx0 = 0.0, vy0 = 0.0;
         if (j == 0) {
@@ -731,7 +740,7 @@ static double refine_L(const orc_geom* g, const orc_params* p, const double* z, 
             }
         } else if (j <= kend) {
             double px, py;
-            rpt(z, gr, a, N, j - 1, &px, &py);
+            rpt(z, dr, a, N, j - 1, &px, &py);
             lj = seg_term(px, py, xj, yj, ls, sc, inner ? &vx0 : NULL, &vy0);
         }
         tl[j] = lj;
@@ -740,8 +749,8 @@ static double refine_L(const orc_geom* g, const orc_params* p, const double* z, 
         double aj = 0.0, gx = 0.0, gy = 0.0;
         if (j < N) {
             double q1[2], q2[2], q0[2] = {xj, yj};
-            rpt(z, gr, a, N, j + 1, &q1[0], &q1[1]);
-            rpt(z, gr, a, N, j + 2, &q2[0], &q2[1]);
+            rpt(z, dr, a, N, j + 1, &q1[0], &q1[1]);
+            rpt(z, dr, a, N, j + 2, &q2[0], &q2[1]);
             kin_row kr;
             kin_eval(q0, q1, q2, r, mincos, ms, 0, &kr);
             double gv[3] = {kr.c1, kr.c2, kr.c3};
@@ -757,7 +766,7 @@ static double refine_L(const orc_geom* g, const orc_params* p, const double* z, 
             }
             if (j + 1 <= kend) {
                 double qx, qy, vx, vy;
-                rpt(z, gr, a, N, j + 1, &qx, &qy);
+                rpt(z, dr, a, N, j + 1, &qx, &qy);
                 seg_term(xj, yj, qx, qy, ls, sc, &vx, &vy);
                 gx = gx - vx;
                 gy = gy - vy;
@@ -767,9 +776,9 @@ static double refine_L(const orc_geom* g, const orc_params* p, const double* z, 
             for (int k = j - 2; k <= j; ++k) {
                 if (k < 0 || k >= N) continue;
                 double q0[2], q1[2], q2[2];
-                rpt(z, gr, a, N, k, &q0[0], &q0[1]);
-                rpt(z, gr, a, N, k + 1, &q1[0], &q1[1]);
-                rpt(z, gr, a, N, k + 2, &q2[0], &q2[1]);
+                rpt(z, dr, a, N, k, &q0[0], &q0[1]);
+                rpt(z, dr, a, N, k + 1, &q1[0], &q1[1]);
+                rpt(z, dr, a, N, k + 2, &q2[0], &q2[1]);
                 kin_row kr;
                 kin_eval(q0, q1, q2, r, mincos, ms, 1, &kr);
                 double gv[3] = {kr.c1, kr.c2, kr.c3};
@@ -839,53 +848,149 @@ static double refine_update(const orc_geom* g, const orc_params* p, const double
     return inf;
 }
 
+/* L-BFGS direction dr = -H g (two-loop recursion over the cnt newest pairs of the ring
+ * hs/hy [m][2W], newest at slot head-1) */
+static void lbfgs_dir(const double* gr, double* dr, const double* hs, const double* hy,
+                      const double* rho, double gamma, int m, int cnt, int head, int N,
+                      double* tmp) {
+    const int W = N + 2;
+    double ai[RF_MAXM];
+    for (int j = 1; j <= N; ++j) {
+        dr[2 * j] = gr[2 * j];
+        dr[2 * j + 1] = gr[2 * j + 1];
+    }
+    for (int i = 0; i < cnt; ++i) {
+        const int sl = (head - 1 - i + m) % m;
+        const double* s = hs + (int64_t)sl * 2 * W;
+        const double* y = hy + (int64_t)sl * 2 * W;
+        ai[i] = rho[sl] * wdot(s, dr, N, tmp);
+        for (int j = 1; j <= N; ++j) {
+            dr[2 * j] = dr[2 * j] - ai[i] * y[2 * j];
+            dr[2 * j + 1] = dr[2 * j + 1] - ai[i] * y[2 * j + 1];
+        }
+    }
+    for (int j = 1; j <= N; ++j) {
+        dr[2 * j] = gamma * dr[2 * j];
+        dr[2 * j + 1] = gamma * dr[2 * j + 1];
+    }
+    for (int i = cnt - 1; i >= 0; --i) {
+        const int sl = (head - 1 - i + m) % m;
+        const double* s = hs + (int64_t)sl * 2 * W;
+        const double* y = hy + (int64_t)sl * 2 * W;
+        const double b = rho[sl] * wdot(y, dr, N, tmp);
+        for (int j = 1; j <= N; ++j) {
+            dr[2 * j] = dr[2 * j] + s[2 * j] * (ai[i] - b);
+            dr[2 * j + 1] = dr[2 * j + 1] + s[2 * j + 1] * (ai[i] - b);
+        }
+    }
+    for (int j = 1; j <= N; ++j) {
+        dr[2 * j] = -dr[2 * j];
+        dr[2 * j + 1] = -dr[2 * j + 1];
+    }
+}
+
 int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* rp, double* wp,
                int64_t P, double* cost, double* infeas, int32_t* iters) {
     const int N = p->N, W = N + 2;
     const int64_t R = 3 * (int64_t)N + (int64_t)g->n_obstacles * W;
+    const int m = rp->memory < 0 ? 0 : (rp->memory > RF_MAXM ? RF_MAXM : rp->memory);
     if (!p->penalty_smooth || !p->obstacle_smooth) return -1;
     double* y = (double*)malloc(sizeof(double) * (R > 0 ? R : 1));
-    double* gr = (double*)malloc(sizeof(double) * 2 * W);
+    double* gr = (double*)calloc(2 * (size_t)W, sizeof(double));
+    double* dr = (double*)calloc(2 * (size_t)W, sizeof(double));
+    double* hs = (double*)calloc((size_t)(m > 0 ? m : 1) * 2 * W, sizeof(double));
+    double* hy = (double*)calloc((size_t)(m > 0 ? m : 1) * 2 * W, sizeof(double));
+    double* tmp = (double*)malloc(sizeof(double) * W);
     for (int64_t pi = 0; pi < P; ++pi) {
         double* z = wp + pi * (int64_t)W * 2;
         double *yk = y, *yo = y + 3 * N;
         for (int64_t i = 0; i < R; ++i) y[i] = 0.0;
-        for (int k = 0; k < 2 * W; ++k) gr[k] = 0.0;
+        for (int k = 0; k < 2 * W; ++k) gr[k] = dr[k] = 0.0;
         double c = rp->c0, alpha = rp->alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
-        int32_t it_used = 0;
+        int32_t used = 0;
         for (int o = 0; o < rp->n_outer; ++o) {
+            int cnt = 0, head = 0;
+            double rho[RF_MAXM], gamma = 1.0, gn2 = 0.0;
+            double Lz = refine_L(g, p, z, dr, 0.0, gr, yk, yo, c, 1, NULL, &gn2);
             for (int it = 0; it < rp->n_inner; ++it) {
-                double gn2 = 0.0;
-                double Lz = refine_L(g, p, z, gr, 0.0, yk, yo, c, 1, NULL, &gn2);
                 if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;
-                double a = fmin(alpha * 2.0, rp->max_step / sqrt(gn2));
+                if (sqrt(gn2) <= rp->inner_tol) break;
+                double gd = 0.0, dn2 = gn2;
+                if (cnt > 0) {
+                    lbfgs_dir(gr, dr, hs, hy, rho, gamma, m, cnt, head, N, tmp);
+                    gd = wdot(gr, dr, N, tmp);
+                    if (!(gd < 0.0)) cnt = 0;
+                    else dn2 = wdot(dr, dr, N, tmp);
+                }
+                if (cnt == 0) {
+                    for (int j = 1; j <= N; ++j) {
+                        dr[2 * j] = -gr[2 * j];
+                        dr[2 * j + 1] = -gr[2 * j + 1];
+                    }
+                    gd = -gn2;
+                    dn2 = gn2;
+                }
+                double a = fmin(cnt > 0 ? 1.0 : alpha * 2.0, rp->max_step / sqrt(dn2));
                 int ok = 0;
                 for (int b = 0; b < rp->max_backtrack; ++b) {
-                    double Lt = refine_L(g, p, z, gr, a, yk, yo, c, 0, NULL, NULL);
-                    if (Lt <= Lz - (rp->armijo * a) * gn2) {
+                    double Lt = refine_L(g, p, z, dr, a, NULL, yk, yo, c, 0, NULL, NULL);
+                    if (Lt <= Lz + (rp->armijo * a) * gd) {
                         ok = 1;
                         break;
                     }
                     a = a * 0.5;
                 }
-                if (!ok) break;
+                if (!ok) {
+                    if (cnt > 0) {  /* retry along -g */
+                        cnt = 0;
+                        continue;
+                    }
+                    break;
+                }
+                double* hsl = hs + (int64_t)head * 2 * W;
+                double* hyl = hy + (int64_t)head * 2 * W;
                 for (int j = 1; j <= N; ++j) {
-                    z[2 * j] = z[2 * j] - a * gr[2 * j];
-                    z[2 * j + 1] = z[2 * j + 1] - a * gr[2 * j + 1];
+                    for (int e = 0; e < 2; ++e) {
+                        const double st = a * dr[2 * j + e];
+                        if (m > 0) {
+                            hsl[2 * j + e] = st;
+                            hyl[2 * j + e] = gr[2 * j + e];
+                        }
+                        z[2 * j + e] = z[2 * j + e] + st;
+                    }
                 }
                 alpha = a;
-                ++it_used;
+                ++used;
+                Lz = refine_L(g, p, z, dr, 0.0, gr, yk, yo, c, 1, NULL, &gn2);
+                if (m > 0) {
+                    for (int j = 1; j <= N; ++j) {
+                        hyl[2 * j] = gr[2 * j] - hyl[2 * j];
+                        hyl[2 * j + 1] = gr[2 * j + 1] - hyl[2 * j + 1];
+                    }
+                    const double sy = wdot(hsl, hyl, N, tmp), yy = wdot(hyl, hyl, N, tmp);
+                    if (sy > 0.0 && yy > 0.0) {
+                        rho[head] = 1.0 / sy;
+                        gamma = sy / yy;
+                        head = (head + 1) % m;
+                        if (cnt < m) ++cnt;
+                    }
+                }
             }
             inf = refine_update(g, p, z, yk, yo, c);
             if (inf > rp->theta * prev) c = fmin(c * rp->rho, rp->c_max);
             prev = inf;
+            if (sqrt(inf) <= rp->delta) break;
         }
-        refine_L(g, p, z, gr, 0.0, yk, yo, c, 0, &f, NULL);
+        refine_L(g, p, z, dr, 0.0, NULL, yk, yo, c, 0, &f, NULL);
         if (cost) cost[pi] = f;
         if (infeas) infeas[pi] = inf;
-        if (iters) iters[pi] = it_used;
+        if (iters) iters[pi] = used;
     }
     free(y);
     free(gr);
+    free(dr);
+    free(hs);
+    free(hy);
+    free(tmp);
     return 0;
 }

@@ -91,6 +91,9 @@ def test_refine_edge_cases(eng, oracle_mod):
     _check(eng, orc, oracle_mod, wp, n_outer=2, n_inner=6)          # smooth max-ratio rows
     _check(eng, orc, oracle_mod, wp[:0], n_outer=2, n_inner=6)      # empty batch
     _check(eng, orc, oracle_mod, wp, n_outer=0, n_inner=0)          # identity
+    _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=10, memory=0)   # steepest descent
+    _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=10, memory=3)   # ring wrap-around
+    _check(eng, orc, oracle_mod, wp, n_outer=30, n_inner=60, inner_tol=1.0, delta=0.5)
     eng.set_params(dataclasses.replace(eng.params, obstacle_smooth=False))
     with pytest.raises((UamError, ValueError)):
         eng.refine(wp, {"n_outer": 1, "n_inner": 1})

@@ -64,10 +64,11 @@ class PathOutputs(ctypes.Structure):
 
 class RefineParams(ctypes.Structure):
     _fields_ = [("n_outer", ctypes.c_int32), ("n_inner", ctypes.c_int32),
-                ("max_backtrack", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("max_backtrack", ctypes.c_int32), ("memory", ctypes.c_int32),
                 ("c0", ctypes.c_double), ("rho", ctypes.c_double), ("c_max", ctypes.c_double),
                 ("alpha0", ctypes.c_double), ("armijo", ctypes.c_double),
-                ("theta", ctypes.c_double), ("max_step", ctypes.c_double)]
+                ("theta", ctypes.c_double), ("max_step", ctypes.c_double),
+                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/uampath.h
@@ -99,7 +100,8 @@ SIGNATURES = {
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,
                                             ctypes.POINTER(PathOutputs), _vp]),
-    "uam_refine_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64]),
+    "uam_refine_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64,
+                                                    ctypes.POINTER(RefineParams)]),
     "uam_refine": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(RefineParams), _vp,
                                   ctypes.c_int64, _vp, _vp, _vp, _vp]),
 }

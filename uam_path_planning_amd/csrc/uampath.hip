@@ -764,9 +764,10 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
 // reference solves min get_cost(z) s.t. get_nonlincon(z) in {0} with OpEn (solver.py:82-93).
 
 struct KRefine {
-    int32_t n_outer, n_inner, max_backtrack, pad;
-    double c0, rho, c_max, alpha0, armijo, theta, max_step;
+    int32_t n_outer, n_inner, max_backtrack, memory;
+    double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
 };
+constexpr int RF_MAXM = 8;  // L-BFGS memory bound (uam_refine_params.memory)
 
 __device__ __forceinline__ void ineq_grad(const DevIneq* __restrict__ q, double x0, double x1,
                                           double& gx, double& gy) {
@@ -907,7 +908,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 struct RfPath {
     const double* z;   // LDS [W][2]
-    double* gr;        // LDS [W][2] (waypoint-indexed; endpoints unused)
+    double* gr;        // LDS [W][2] gradient (waypoint-indexed; endpoints unused)
+    const double* dr;  // LDS [W][2] search direction
     const double* yk;  // LDS [3N]
     const double* yo;  // global [S][W]
     int N, W;
@@ -915,11 +917,22 @@ struct RfPath {
         x = z[2 * j];
         y = z[2 * j + 1];
         if (a != 0.0 && j >= 1 && j <= N) {
-            x = x - a * gr[2 * j];
-            y = y - a * gr[2 * j + 1];
+            x = x + a * dr[2 * j];
+            y = y + a * dr[2 * j + 1];
         }
     }
 };
+
+// path dot product over interior waypoints (lane-owned entries), lane-tree order
+__device__ __forceinline__ double wdot(const double* u, const double* v, int N, int lane) {
+    double s = 0.0;
+    for (int j = lane; j < N + 2; j += 64) {
+        const double t = (j >= 1 && j <= N) ? u[2 * j] * v[2 * j] + u[2 * j + 1] * v[2 * j + 1]
+                                             : 0.0;
+        s = s + t;
+    }
+    return wave_sum(s);
+}
 
 __device__ __forceinline__ double seg_term(double px, double py, double qx, double qy, bool ls,
                                            double sc, bool want, double& vx, double& vy) {
@@ -935,7 +948,7 @@ __device__ __forceinline__ double seg_term(double px, double py, double qx, doub
     return ls ? n * n : n;
 }
 
-// L(z - a gr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
+// L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
 // gradient accumulation order as oracle refine_L.
 __device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int lane, double a,
                        double c, bool want, double* fout, double* gn2) {
@@ -1037,9 +1050,62 @@ __device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int l
     return f + saug;
 }
 
+// L-BFGS two-loop recursion: dr = -H gr over the cnt newest (s, y) pairs of the ring
+__device__ void lbfgs_dir(const double* gr, double* dr, const double* hs, const double* hy,
+                          const double* rho, double gamma, int m, int cnt, int head, int N,
+                          int W, int lane) {
+    double ai[RF_MAXM];
+    for (int j = lane; j < W; j += 64) {
+        if (j >= 1 && j <= N) {
+            dr[2 * j] = gr[2 * j];
+            dr[2 * j + 1] = gr[2 * j + 1];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RF_MAXM; ++i) {
+        if (i >= cnt) break;
+        const int sl = (head - 1 - i + m) % m;
+        const double* sv = hs + (int64_t)sl * 2 * W;
+        const double* yv = hy + (int64_t)sl * 2 * W;
+        ai[i] = rho[sl] * wdot(sv, dr, N, lane);
+        for (int j = lane; j < W; j += 64) {
+            if (j >= 1 && j <= N) {
+                dr[2 * j] = dr[2 * j] - ai[i] * yv[2 * j];
+                dr[2 * j + 1] = dr[2 * j + 1] - ai[i] * yv[2 * j + 1];
+            }
+        }
+    }
+    for (int j = lane; j < W; j += 64) {
+        if (j >= 1 && j <= N) {
+            dr[2 * j] = gamma * dr[2 * j];
+            dr[2 * j + 1] = gamma * dr[2 * j + 1];
+        }
+    }
+#pragma unroll
+    for (int i = RF_MAXM - 1; i >= 0; --i) {
+        if (i >= cnt) continue;
+        const int sl = (head - 1 - i + m) % m;
+        const double* sv = hs + (int64_t)sl * 2 * W;
+        const double* yv = hy + (int64_t)sl * 2 * W;
+        const double b = rho[sl] * wdot(yv, dr, N, lane);
+        for (int j = lane; j < W; j += 64) {
+            if (j >= 1 && j <= N) {
+                dr[2 * j] = dr[2 * j] + sv[2 * j] * (ai[i] - b);
+                dr[2 * j + 1] = dr[2 * j + 1] + sv[2 * j + 1] * (ai[i] - b);
+            }
+        }
+    }
+    for (int j = lane; j < W; j += 64) {
+        if (j >= 1 && j <= N) {
+            dr[2 * j] = -dr[2 * j];
+            dr[2 * j + 1] = -dr[2 * j + 1];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
                                                 double* __restrict__ wp, int64_t P,
-                                                double* __restrict__ yo_all,
+                                                double* __restrict__ ws,
                                                 double* __restrict__ cost,
                                                 double* __restrict__ infeas,
                                                 int32_t* __restrict__ iters) {
@@ -1048,50 +1114,111 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
     const int64_t path = (int64_t)blockIdx.x * wpb + wave;
     if (path >= P) return;  // whole wave
     const int N = p.N, W = N + 2, S = g.n_obstacles;
-    double* z = rf_lds + (int64_t)wave * (4 * W + 3 * N);
+    const int m = rf.memory < 0 ? 0 : (rf.memory > RF_MAXM ? RF_MAXM : rf.memory);
+    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM);
     double* gr = z + 2 * W;
-    double* yk = gr + 2 * W;
+    double* dr = gr + 2 * W;
+    double* yk = dr + 2 * W;
+    double* rho = yk + 3 * N;
     double* zg = wp + path * (int64_t)W * 2;
-    double* yo = yo_all + path * (int64_t)S * W;
+    double* yo = ws + path * ((int64_t)S * W + (int64_t)m * 4 * W);
+    double* hs = yo + (int64_t)S * W;
+    double* hy = hs + (int64_t)m * 2 * W;
     for (int k = lane; k < 2 * W; k += 64) {
         z[k] = zg[k];
         gr[k] = 0.0;
+        dr[k] = 0.0;
     }
     for (int k = lane; k < 3 * N; k += 64) yk[k] = 0.0;
     for (int s = 0; s < S; ++s)
         for (int j = lane; j < W; j += 64) yo[(int64_t)s * W + j] = 0.0;
     wave_sync();
-    RfPath rp{z, gr, yk, yo, N, W};
+    RfPath rp{z, gr, dr, yk, yo, N, W};
     const bool ms = p.maxratio_smooth != 0;
     double c = rf.c0, alpha = rf.alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
     int32_t used = 0;
     for (int o = 0; o < rf.n_outer; ++o) {
+        int cnt = 0, head = 0;
+        double gamma = 1.0, gn2 = 0.0;
+        double Lz = rf_L(g, p, rp, lane, 0.0, c, true, nullptr, &gn2);
+        wave_sync();
         for (int it = 0; it < rf.n_inner; ++it) {
-            double gn2 = 0.0;
-            const double Lz = rf_L(g, p, rp, lane, 0.0, c, true, nullptr, &gn2);
-            wave_sync();
             if (!(gn2 > 0.0) || !(gn2 < INFINITY)) break;  // wave-uniform
-            double a = fmin(alpha * 2.0, rf.max_step / sqrt(gn2));
+            if (sqrt(gn2) <= rf.inner_tol) break;
+            double gd = 0.0, dn2 = gn2;
+            if (cnt > 0) {
+                lbfgs_dir(gr, dr, hs, hy, rho, gamma, m, cnt, head, N, W, lane);
+                gd = wdot(gr, dr, N, lane);
+                if (!(gd < 0.0))
+                    cnt = 0;
+                else
+                    dn2 = wdot(dr, dr, N, lane);
+            }
+            if (cnt == 0) {
+                for (int j = lane; j < W; j += 64) {
+                    if (j >= 1 && j <= N) {
+                        dr[2 * j] = -gr[2 * j];
+                        dr[2 * j + 1] = -gr[2 * j + 1];
+                    }
+                }
+                gd = -gn2;
+                dn2 = gn2;
+            }
+            wave_sync();
+            double a = fmin(cnt > 0 ? 1.0 : alpha * 2.0, rf.max_step / sqrt(dn2));
             bool ok = false;
             for (int b = 0; b < rf.max_backtrack; ++b) {
                 const double Lt = rf_L(g, p, rp, lane, a, c, false, nullptr, nullptr);
-                if (Lt <= Lz - (rf.armijo * a) * gn2) {
+                if (Lt <= Lz + (rf.armijo * a) * gd) {
                     ok = true;
                     break;
                 }
                 a = a * 0.5;
             }
-            if (!ok) break;
+            if (!ok) {
+                if (cnt > 0) {  // retry along -g
+                    cnt = 0;
+                    continue;
+                }
+                break;
+            }
             wave_sync();
+            double* hsl = hs + (int64_t)head * 2 * W;
+            double* hyl = hy + (int64_t)head * 2 * W;
             for (int j = lane; j < W; j += 64) {
                 if (j >= 1 && j <= N) {
-                    z[2 * j] = z[2 * j] - a * gr[2 * j];
-                    z[2 * j + 1] = z[2 * j + 1] - a * gr[2 * j + 1];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const double st = a * dr[2 * j + e];
+                        if (m > 0) {
+                            hsl[2 * j + e] = st;
+                            hyl[2 * j + e] = gr[2 * j + e];
+                        }
+                        z[2 * j + e] = z[2 * j + e] + st;
+                    }
                 }
             }
             wave_sync();
             alpha = a;
             ++used;
+            Lz = rf_L(g, p, rp, lane, 0.0, c, true, nullptr, &gn2);
+            wave_sync();
+            if (m > 0) {
+                for (int j = lane; j < W; j += 64) {
+                    if (j >= 1 && j <= N) {
+                        hyl[2 * j] = gr[2 * j] - hyl[2 * j];
+                        hyl[2 * j + 1] = gr[2 * j + 1] - hyl[2 * j + 1];
+                    }
+                }
+                const double sy = wdot(hsl, hyl, N, lane), yy = wdot(hyl, hyl, N, lane);
+                if (sy > 0.0 && yy > 0.0) {
+                    rho[head] = 1.0 / sy;  // same value from every lane
+                    gamma = sy / yy;
+                    head = (head + 1) % m;
+                    if (cnt < m) ++cnt;
+                }
+                wave_sync();
+            }
         }
         // outer update: y += c * row, inf = sum row^2 (kinematic rows of j, then obstacles)
         double si = 0.0;
@@ -1122,6 +1249,7 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
         wave_sync();
         if (inf > rf.theta * prev) c = fmin(c * rf.rho, rf.c_max);
         prev = inf;
+        if (sqrt(inf) <= rf.delta) break;
     }
     rf_L(g, p, rp, lane, 0.0, c, false, &f, nullptr);
     for (int k = lane; k < 2 * W; k += 64) zg[k] = z[k];
@@ -1750,10 +1878,15 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     return UAM_OK;
 }
 
-int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths) {
-    if (!ctx || !ctx->have_params || n_paths < 0) return -1;
-    const int64_t W = ctx->kp.N + 2;
-    return (int64_t)ctx->kg.n_obstacles * W * n_paths * (int64_t)sizeof(double);
+static int refine_memory(const uam_refine_params* rp) {
+    return rp->memory < 0 ? 0 : (rp->memory > RF_MAXM ? RF_MAXM : rp->memory);
+}
+
+int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,
+                                   const uam_refine_params* params) {
+    if (!ctx || !ctx->have_params || n_paths < 0 || !params) return -1;
+    const int64_t W = ctx->kp.N + 2, m = refine_memory(params);
+    return ((int64_t)ctx->kg.n_obstacles * W + m * 4 * W) * n_paths * (int64_t)sizeof(double);
 }
 
 int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_params* rp,
@@ -1766,14 +1899,14 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
         return fail(UAM_E_INVALID, "refinement needs penalty_smooth and obstacle_smooth");
     if (n_paths < 0) return fail(UAM_E_INVALID, "n_paths < 0");
     if (rp->n_outer < 0 || rp->n_inner < 0 || rp->max_backtrack < 1 || !(rp->c0 > 0.0) ||
-        !(rp->max_step > 0.0))
-        return fail(UAM_E_INVALID, "bad refine params");
+        !(rp->max_step > 0.0) || rp->memory < 0 || rp->memory > RF_MAXM)
+        return fail(UAM_E_INVALID, "bad refine params (memory must be 0..%d)", RF_MAXM);
     const int64_t N = ctx->kp.N, W = N + 2;
-    const int64_t per_wave = (4 * W + 3 * N) * (int64_t)sizeof(double);
+    const int64_t per_wave = (6 * W + 3 * N + RF_MAXM) * (int64_t)sizeof(double);
     if (per_wave > 65536)
         return fail(UAM_E_INVALID, "N = %lld too large for refinement (LDS)", (long long)N);
     if (n_paths == 0) return UAM_OK;
-    const int64_t need = uam_refine_workspace_bytes(ctx, n_paths);
+    const int64_t need = uam_refine_workspace_bytes(ctx, n_paths, rp);
     if (!wp || (need > 0 && !workspace)) return fail(UAM_E_INVALID, "wp/workspace is NULL");
     if (workspace_bytes < need)
         return fail(UAM_E_INVALID, "workspace %lld bytes < %lld", (long long)workspace_bytes,
@@ -1781,8 +1914,9 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
     const int wpb = (int)std::min<int64_t>(4, 65536 / per_wave);
     const int64_t blocks = (n_paths + wpb - 1) / wpb;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "too many paths");
-    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, 0,     rp->c0,     rp->rho,
-               rp->c_max,   rp->alpha0, rp->armijo,        rp->theta, rp->max_step};
+    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, rp->memory, rp->c0,
+               rp->rho,     rp->c_max,   rp->alpha0,        rp->armijo, rp->theta,
+               rp->max_step, rp->inner_tol, rp->delta};
     DeviceGuard dg(ctx->device);
     hipLaunchKernelGGL(k_refine, dim3((unsigned)blocks), dim3(64 * wpb),
                        (size_t)(wpb * per_wave), (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp,

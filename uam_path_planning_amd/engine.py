@@ -114,8 +114,9 @@ def _ptr(t):
 
 
 # refinement defaults (same as oracle.refine_params)
-REFINE_DEFAULTS = dict(n_outer=10, n_inner=20, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
-                       alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5)
+REFINE_DEFAULTS = dict(n_outer=15, n_inner=50, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
+                       alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5, memory=8,
+                       inner_tol=1e-3, delta=1e-4)
 
 
 class Engine:
@@ -371,11 +372,15 @@ class Engine:
         P = z.shape[0]
         rp = dict(REFINE_DEFAULTS)
         rp.update(params or {})
+        unknown = set(rp) - set(REFINE_DEFAULTS)
+        if unknown:
+            raise ValueError(f"unknown refine settings {sorted(unknown)}")
         st = _lib.RefineParams(int(rp["n_outer"]), int(rp["n_inner"]), int(rp["max_backtrack"]),
-                               0, float(rp["c0"]), float(rp["rho"]), float(rp["c_max"]),
-                               float(rp["alpha0"]), float(rp["armijo"]), float(rp["theta"]),
-                               float(rp["max_step"]))
-        nbytes = self.lib.uam_refine_workspace_bytes(self._ctx, P)
+                               int(rp["memory"]), float(rp["c0"]), float(rp["rho"]),
+                               float(rp["c_max"]), float(rp["alpha0"]), float(rp["armijo"]),
+                               float(rp["theta"]), float(rp["max_step"]),
+                               float(rp["inner_tol"]), float(rp["delta"]))
+        nbytes = self.lib.uam_refine_workspace_bytes(self._ctx, P, ctypes.byref(st))
         if nbytes < 0:
             raise _lib.UamError("uam_refine_workspace_bytes: set geometry and params first")
         ws = self.empty((max(nbytes, 8) // 8,), torch.float64)
