@@ -199,6 +199,12 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # which kernel the library picks (uampath.hip want_wave: tuning 9, or auto for batches of
+    # at most 16384 paths in raster / volume mode; 10 = never)
+    wave = args.mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
+    kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
+                   f"k_eval_pairs<{mode}>" + (f" (variant {args.variant or 2})"
+                                              if raster_mode else ""))
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -223,8 +229,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": f"k_eval_pairs<{mode}>" + (
-                         f" (variant {args.variant or 2})" if raster_mode else ""),
+                     "kernel": kernel_name,
                      "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_path": bytes_per_path,
                      "algorithmic_bytes_per_launch": launch_bytes,

@@ -229,10 +229,13 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);
 
-/* Kernel variant for uam_eval_generated (0 = default).  1 = one wave per (displacement,
- * 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup per 64 pairs x D
- * (D <= 16) with LDS-staged coalesced stores and the selection fused, differing in gathers per
- * chunk / software pipelining / occupancy.  All variants return bit-identical results. */
+/* Kernel variant for the raster/volume evaluations (0 = automatic).  1 = one wave per
+ * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
+ * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,
+ * differing in gathers per chunk / software pipelining / occupancy; 9 = one wave per path
+ * (lanes over waypoints; small batches); 10 = never one wave per path.  0 picks the wave
+ * per path kernel for batches up to 16384 paths and variant 2 above.  All variants return
+ * bit-identical results. */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */

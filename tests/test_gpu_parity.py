@@ -191,16 +191,27 @@ def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5):
 
 @pytest.mark.parametrize("R,Q,N", [(256, 300, 80), (2048, 200, 254), (512, 64, 1)])
 def test_raster_eval_generated_vs_oracle(eng, oracle_mod, R, Q, N):
+    """Both the wave-per-path kernel (tuning 9, what 0 picks for these batch sizes) and the
+    lane-per-path kernels (tuning 10) against the oracle, generated and explicit paths."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, R, Q, N, nfz=4)
-    gpu = eng.eval_generated(pairs, ut, raster=raster, want_cells=True)
     wp = oracle_mod.gen_paths(pairs, ut)
     ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, want_cells=True)
-    _assert_paths_equal(gpu, ref, raster=True)
-    np.testing.assert_array_equal(_np(gpu["cells"]), ref["cells"])
-    # explicit-waypoint kernel on the same paths gives the same bits
-    gpu2 = eng.eval_waypoints(wp, raster=raster, want_cells=True)
-    _assert_paths_equal(gpu2, ref, raster=True)
-    np.testing.assert_array_equal(_np(gpu2["cells"]), ref["cells"])
+    try:
+        for v in (9, 10):
+            eng.set_tuning(v)
+            gpu = eng.eval_generated(pairs, ut, raster=raster, want_cells=True)
+            _assert_paths_equal(gpu, ref, raster=True)
+            np.testing.assert_array_equal(_np(gpu["cells"]), ref["cells"])
+            np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                          oracle_mod.argmin(ref["cost"], 5, True))
+            np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
+                                          oracle_mod.argmin(ref["length"], 5, False))
+            # explicit-waypoint kernel on the same paths gives the same bits
+            gpu2 = eng.eval_waypoints(wp, raster=raster, want_cells=True)
+            _assert_paths_equal(gpu2, ref, raster=True)
+            np.testing.assert_array_equal(_np(gpu2["cells"]), ref["cells"])
+    finally:
+        eng.set_tuning(0)
 
 
 def test_raster_matches_reference_at_snapped_centres(eng, oracle_mod):
@@ -305,8 +316,8 @@ def test_dropin_problem_and_solver(eng):
     assert res["min_fval_index"] == 3
     with pytest.raises(ValueError):
         solver.create_x_init(1.5)
-    with pytest.raises(NotImplementedError):
-        solver.solve(None, None)
+    with pytest.raises(ValueError):        # p vector of the wrong length (OpEn error 3003)
+        solver.solve(np.zeros(2 * prob.N), [0.0])
     # shape primitives on the device
     m = prob.map
     assert m.collides(np.array([38.66652661075855, -9.203164091309498]))
@@ -323,7 +334,7 @@ def test_kernel_variants_bit_identical(eng, oracle_mod, D):
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 333, 80, nfz=4, D=D)
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
     try:
-        for v in range(0, 9):
+        for v in range(0, 11):
             eng.set_tuning(v)
             gpu = eng.eval_generated(pairs, ut, raster=raster)
             _assert_paths_equal(gpu, ref, raster=True)
@@ -428,9 +439,15 @@ def test_volume_mode_vs_oracle(eng, oracle_mod):
     np.testing.assert_array_equal(_np(vol.vox), ref_vol.view(np.int32))
     pairs = random_pairs3d(300, seed=4, zmin=-50.0, zmax=700.0)   # some outside [0, 640)
     ut = arc_table(40, displacements(5))
-    gpu = eng.eval_generated3d(pairs, ut, vol)
     ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
-    for gk, ok in PATH_KEYS + (("below_terrain", "below"), ("min_clearance", "min_clearance")):
-        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+    try:
+        for v in (10, 9):   # lane-per-path, then wave-per-path (the auto pick at this size)
+            eng.set_tuning(v)
+            gpu = eng.eval_generated3d(pairs, ut, vol)
+            for gk, ok in PATH_KEYS + (("below_terrain", "below"),
+                                       ("min_clearance", "min_clearance")):
+                np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=f"{gk} v{v}")
+    finally:
+        eng.set_tuning(0)
     assert (_np(gpu["offmap"]) > 0).any() and (_np(gpu["below_terrain"]) > 0).any()
     np.testing.assert_array_equal(_np(gpu["best_fval_idx"]), oracle_mod.argmin(ref["cost"], 5, True))

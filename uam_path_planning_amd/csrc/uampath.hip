@@ -30,7 +30,10 @@
 
 #include "../../include/uampath.h"
 
-#define UAM_TUNING_MAX 8
+#define UAM_TUNING_MAX 10
+#define UAM_TUNING_WAVE 9       // force the wave-per-path kernel (K2w)
+#define UAM_TUNING_LANE 10      // never pick K2w automatically
+#define UAM_WAVE_AUTO_PATHS 16384  // auto: K2w up to here (tools/probe_wave.py crossover)
 #define UAM_TUNING_DEFAULT 2
 
 namespace {
@@ -1260,6 +1263,221 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// K2w: wave-per-path evaluation for small batches (raster / volume modes).  The lane-per-path
+// kernels walk a path serially, so a batch of 1k paths is 16 waves on a 256-CU chip and runs
+// at the latency of one 256-waypoint walk.  Here lane l owns waypoints l, l+64, ...: points,
+// segment norms, kinematic rows and record gathers run across the wave; the per-waypoint terms
+// are staged in LDS and lane 0 forms every reference-ordered sum (L, length, kinematic sum,
+// cost, no-fly sum) in exactly eval_path's order, so outputs are bit-identical to the
+// lane-per-path kernels.  max terrain / min clearance / counts are order-free (shuffles).
+__host__ __device__ constexpr int64_t ewave_doubles(int N) {
+    return 6 * (int64_t)(N + 2) + 3 * (int64_t)N;
+}
+
+__device__ __forceinline__ double wave_fmax(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_fmin(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int MODE, bool GEN>
+__global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster rs, KVolume vs,
+                                                   const uint4* __restrict__ rec,
+                                                   const double* __restrict__ wp,
+                                                   const double* __restrict__ pairs,
+                                                   const double* __restrict__ utab, int D,
+                                                   int64_t n_paths, KOut out) {
+    extern __shared__ double ew_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int64_t path = (int64_t)blockIdx.x * wpb + wave;
+    if (path >= n_paths) return;  // whole wave
+    const int N = p.N, W = N + 2;
+    const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
+    double* px = ew_lds + (int64_t)wave * ewave_doubles(N);
+    double* py = px + W;
+    double* lq = py + W;  // get_cost length term of the segment ending at j (anchor for j=0)
+    double* sg = lq + W;  // true segment norm
+    double* ph = sg + W;  // Phi_j / N
+    double* ps = ph + W;  // no-fly psi_j
+    double* kn = ps + W;  // kinematic rows [N][3]
+    PathSrc<GEN> src;
+    src.W = W;
+    src.wp = nullptr;
+    src.u = nullptr;
+    src.x0 = src.y0 = src.xf = src.yf = 0.0;
+    src.za = src.zb = 0.0;
+    if (GEN) {
+        const int64_t q = path / D;
+        const int d = (int)(path - q * D);
+        if (MODE == UAM_MODE_VOLUME) {
+            const double* pr = pairs + 6 * q;
+            src.x0 = pr[0], src.y0 = pr[1], src.za = pr[2];
+            src.xf = pr[3], src.yf = pr[4], src.zb = pr[5];
+        } else {
+            const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+            src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+        }
+        src.u = utab + (int64_t)d * N * 2;
+    } else {
+        src.wp = wp + path * (int64_t)W * 2;
+    }
+    for (int j = lane; j < W; j += 64) {
+        double x, y;
+        src.at(j, x, y);
+        px[j] = x;
+        py[j] = y;
+    }
+    wave_sync();
+    // geometry terms: lq = get_cost length term of the segment ending at j (anchor segment
+    // for j = 0; +0.0 where eval_path adds nothing), sg = true segment norm, kinematic rows
+    for (int j = lane; j < W; j += 64) {
+        const double x = px[j], y = py[j];
+        if (j == 0) {
+            double t = 0.0;
+            if (p.quirk_length) {
+                const double ax = p.anchor_mode ? p.anchor_x : x;
+                const double ay = p.anchor_mode ? p.anchor_y : y;
+                const double dx = x - ax, dy = y - ay;
+                double s = 0.0;
+                s = s + dx * dx;
+                s = s + dy * dy;
+                const double n = sqrt(s);
+                t = ls ? n * n : n;
+            }
+            lq[0] = t;
+            sg[0] = 0.0;
+        } else {
+            const double dx = x - px[j - 1], dy = y - py[j - 1];
+            double s = 0.0;
+            s = s + dx * dx;
+            s = s + dy * dy;
+            const double n = sqrt(s);
+            sg[j] = n;
+            lq[j] = (!p.quirk_length || j <= N) ? (ls ? n * n : n) : 0.0;
+            if (j >= 2) {  // kinematic row k = j-2, recomputing the previous segment
+                const double pdx = px[j - 1] - px[j - 2], pdy = py[j - 1] - py[j - 2];
+                double s2 = 0.0;
+                s2 = s2 + pdx * pdx;
+                s2 = s2 + pdy * pdy;
+                const double n2 = sqrt(s2);
+                const double pn = ms ? n2 * n2 : n2, nk = ms ? n * n : n;
+                double dt = 0.0;
+                dt = dt + pdx * dx;
+                dt = dt + pdy * dy;
+                kn[3 * (j - 2)] = fmax(0.0, nk - p.r_eff * pn);
+                kn[3 * (j - 2) + 1] = fmax(0.0, pn / p.r_eff - nk);
+                kn[3 * (j - 2) + 2] = fmax(0.0, p.mincos - dt / (pn * nk));
+            }
+        }
+    }
+    // record gathers, up to 4 per lane in flight; ph / ps = +0.0 for off-grid waypoints
+    double hmax = -INFINITY, cmin = INFINITY;
+    int nh = 0, off = 0, below = 0;
+    int32_t* cells = out.cells ? out.cells + path * W : nullptr;
+    const double dN = (double)N;
+    for (int jb = lane; jb < W; jb += 256) {
+        uint4 r[4];
+        bool in[4];
+        double zz[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = jb + 64 * t;
+            in[t] = false;
+            r[t] = make_uint4(0, 0, 0, 0);
+            zz[t] = 0.0;
+            if (j >= W) continue;
+            const double x = px[j], y = py[j];
+            int64_t cell;
+            if (MODE == UAM_MODE_VOLUME) {
+                const double z = src.alt(j);
+                const double fx = floor((x - vs.x0) * vs.inv_dx);
+                const double fy = floor((vs.y_top - y) * vs.inv_dy);
+                const double fz = floor((z - vs.z0) * vs.inv_dz);
+                in[t] = (fx >= 0.0) && (fx < (double)vs.nx) && (fy >= 0.0) &&
+                        (fy < (double)vs.ny) && (fz >= 0.0) && (fz < (double)vs.nz);
+                cell = in[t] ? ((int64_t)fy * vs.nx + (int64_t)fx) * vs.nz + (int64_t)fz
+                             : (int64_t)0;
+                zz[t] = z;
+            } else {
+                const double fx = floor((x - rs.x0) * rs.inv_dx);
+                const double fy = floor((rs.y_top - y) * rs.inv_dy);
+                in[t] = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) &&
+                        (fy < (double)rs.ny);
+                cell = in[t] ? (int64_t)fy * rs.nx + (int64_t)fx : (int64_t)0;
+            }
+            r[t] = rec[cell];
+            if (cells) cells[j] = in[t] ? (int32_t)cell : -1;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = jb + 64 * t;
+            if (j >= W) continue;
+            if (MODE == UAM_MODE_VOLUME) {
+                if (in[t]) {
+                    below += (r[t].w & UAM_FLAG_BELOW_TERRAIN) ? 1 : 0;
+                    cmin = fmin(cmin, zz[t] - (double)__uint_as_float(r[t].z));
+                }
+            } else {
+                const double terrain = (!in[t] || (r[t].w & UAM_FLAG_NODATA))
+                                           ? 0.0
+                                           : (double)__uint_as_float(r[t].z);
+                hmax = fmax(hmax, terrain);  // off-raster counts as sea level
+            }
+            if (in[t]) {
+                ph[j] = (double)__uint_as_float(r[t].x) / dN;
+                ps[j] = (double)__uint_as_float(r[t].y);
+                nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+            } else {
+                ph[j] = 0.0;
+                ps[j] = 0.0;
+                ++off;
+            }
+        }
+    }
+    hmax = wave_fmax(hmax);
+    cmin = wave_fmin(cmin);
+    nh = wave_isum(nh);
+    off = wave_isum(off);
+    below = wave_isum(below);
+    wave_sync();
+    // eval_path's sequential sums, same order, four chains on four lanes at once (L, length,
+    // no-fly sum, kinematic sum), then the cost chain seeded with (N+1) L.  Every accumulator
+    // starts at +0.0, so the +0.0 entries are exact no-ops.
+    const double* arr = lane == 0 ? lq : (lane == 1 ? sg : (lane == 2 ? ps : kn));
+    const int cnt = lane < 3 ? W : (lane == 3 ? 3 * N : 0);
+    double acc = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < cnt; ++i) acc = acc + arr[i];
+    const double L = __shfl(acc, 0, 64), len = __shfl(acc, 1, 64);
+    const double nsum = __shfl(acc, 2, 64), ksum = __shfl(acc, 3, 64);
+    if (lane == 0) {
+        double cost = (double)(N + 1) * L;
+#pragma unroll 8
+        for (int j = 0; j < W; ++j) cost = cost + ph[j];
+        if (out.cost) out.cost[path] = cost;
+        if (out.length_q) out.length_q[path] = L;
+        if (out.length) out.length[path] = len;
+        if (out.kin_sum) out.kin_sum[path] = ksum;
+        if (out.nfz_sum) out.nfz_sum[path] = nsum;
+        if (out.nfz_hits) out.nfz_hits[path] = nh;
+        if (out.offmap) out.offmap[path] = off;
+        if (out.min_clearance)
+            out.min_clearance[path] = MODE == UAM_MODE_RASTER ? p.altitude - hmax : cmin;
+        if (out.below_terrain) out.below_terrain[path] = below;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -1705,6 +1923,47 @@ int uam_gen_paths(uam_ctx* ctx, const double* pairs, int64_t n_pairs, const doub
     return UAM_OK;
 }
 
+// K2w launch (raster / volume, explicit or generated); returns 1 if launched, 0 if the
+// shape does not fit (caller falls back to the lane-per-path kernels), <0 on error.
+static int launch_wave(uam_ctx* ctx, int mode, bool gen, const KRaster& kr, const KVolume& kv,
+                       const void* rec, const double* wp, const double* pairs,
+                       const double* utab, int D, int64_t n_paths, const KOut& ko,
+                       int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    const int64_t per_wave = ewave_doubles(ctx->kp.N) * (int64_t)sizeof(double);
+    if (per_wave > 65536) return 0;
+    if ((best_f && !ko.cost) || (best_l && !ko.length)) return 0;
+    const int wpb = (int)std::min<int64_t>(4, 65536 / per_wave);
+    const int64_t blocks = (n_paths + wpb - 1) / wpb;
+    if (blocks > INT32_MAX) return 0;
+    const dim3 grid((unsigned)blocks), block(64 * wpb);
+    const size_t lds = (size_t)(wpb * per_wave);
+    const uint4* r = (const uint4*)rec;
+    if (mode == UAM_MODE_VOLUME)
+        hipLaunchKernelGGL((k_eval_wave<UAM_MODE_VOLUME, true>), grid, block, lds, s, ctx->kg,
+                           ctx->kp, kr, kv, r, wp, pairs, utab, D, n_paths, ko);
+    else if (gen)
+        hipLaunchKernelGGL((k_eval_wave<UAM_MODE_RASTER, true>), grid, block, lds, s, ctx->kg,
+                           ctx->kp, kr, kv, r, wp, pairs, utab, D, n_paths, ko);
+    else
+        hipLaunchKernelGGL((k_eval_wave<UAM_MODE_RASTER, false>), grid, block, lds, s, ctx->kg,
+                           ctx->kp, kr, kv, r, wp, pairs, utab, D, n_paths, ko);
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "k_eval_wave launch failed");
+    if (gen && (best_f || best_l)) {
+        const int64_t n_pairs = n_paths / D;
+        const dim3 g2(grid_for(n_pairs, 256, INT32_MAX));
+        if (best_f) hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.cost, n_pairs, D, 1, best_f);
+        if (best_l)
+            hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.length, n_pairs, D, 0, best_l);
+        if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "k_argmin launch failed");
+    }
+    return 1;
+}
+
+static bool want_wave(const uam_ctx* ctx, int64_t n_paths) {
+    if (ctx->variant == UAM_TUNING_WAVE) return true;
+    return ctx->variant == 0 && n_paths <= UAM_WAVE_AUTO_PATHS;
+}
+
 int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec, const double* wp, int64_t n_paths,
                        const uam_path_outputs* out, uam_stream stream) {
@@ -1723,6 +1982,13 @@ int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     }
     const KOut ko = make_kout(out);
     DeviceGuard dg(ctx->device);
+    if (mode == UAM_MODE_RASTER && want_wave(ctx, n_paths)) {
+        const KVolume kv{};
+        st = launch_wave(ctx, mode, false, kr, kv, rec, wp, nullptr, nullptr, 1, n_paths, ko,
+                         nullptr, nullptr, (hipStream_t)stream);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
     const dim3 grid(grid_for(n_paths, 256, INT32_MAX)), block(256);
     if (mode == UAM_MODE_RASTER)
         hipLaunchKernelGGL(k_eval_waypoints<UAM_MODE_RASTER>, grid, block, 0, (hipStream_t)stream,
@@ -1766,7 +2032,15 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     int32_t* best_l = out ? out->best_length_idx : nullptr;
     DeviceGuard dg(ctx->device);
     hipStream_t s = (hipStream_t)stream;
-    int v = ctx->variant == 0 ? UAM_TUNING_DEFAULT : ctx->variant;
+    if (mode == UAM_MODE_RASTER && n_pairs <= INT64_MAX / D && want_wave(ctx, n_pairs * D)) {
+        const KVolume kv{};
+        st = launch_wave(ctx, mode, true, kr, kv, rec, nullptr, pairs, utab, D, n_pairs * D, ko,
+                         best_f, best_l, s);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
+    int v = (ctx->variant == 0 || ctx->variant >= UAM_TUNING_WAVE) ? UAM_TUNING_DEFAULT
+                                                                   : ctx->variant;
     if (D > 16) v = 1;  // the block-of-pairs kernels hold all D waves in one workgroup
     if (v == 1) {
         const int64_t n_waves = ((n_pairs + 63) / 64) * D;
@@ -1867,10 +2141,16 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     int32_t* best_f = out ? out->best_fval_idx : nullptr;
     int32_t* best_l = out ? out->best_length_idx : nullptr;
     DeviceGuard dg(ctx->device);
+    const KRaster kr{};
+    if (want_wave(ctx, n_pairs * D)) {
+        st = launch_wave(ctx, UAM_MODE_VOLUME, true, kr, kv, vol, nullptr, pairs6, utab, D,
+                         n_pairs * D, ko, best_f, best_l, (hipStream_t)stream);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
-    const KRaster kr{};
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
                        (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l);
