@@ -229,6 +229,36 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);
 
+/* ---- Coordinate reference systems ------------------------------
+ * Transverse Mercator on an ellipsoid (Krueger series to n^6, Karney 2011) between geographic
+ * (lon, lat) degrees and plane (x = easting, y = northing) metres -- what pyproj's to_crs does
+ * for EPSG:4612/6668 <-> EPSG:2443..2461 in the reference (map_generation/data_manager.py:24-26
+ * and 84-85, path_generation/main.py:106-115).  Definition: oracle/uam_oracle.c tm_*. */
+typedef struct {
+    double a, f, k0, lat0_deg, lon0_deg, false_easting, false_northing;
+} uam_tm_params;
+/* GRS80 / k0 0.9999 / origin of Japan Plane Rectangular CS zone 1..19 (EPSG:2442 + zone). */
+int uam_tm_jprcs(int32_t zone, uam_tm_params* out);
+/* Batched transforms of interleaved device arrays [n][2]: lon,lat -> x,y and back. */
+int uam_geo_to_plane(uam_ctx* ctx, const uam_tm_params* tm, const double* lonlat_dev,
+                     int64_t n, double* xy_dev, uam_stream stream);
+int uam_plane_to_geo(uam_ctx* ctx, const uam_tm_params* tm, const double* xy_dev, int64_t n,
+                     double* lonlat_dev, uam_stream stream);
+/* North-up geographic grid (the mergeLL.vrt mosaic, mergeLL.vrt:1-3): pixel (i, j) covers
+ * lon in lon0 + [i, i+1) dlon, lat in lat_top - [j, j+1) dlat. */
+typedef struct {
+    int32_t nx, ny;
+    double lon0, lat_top, dlon, dlat;
+    float nodata;
+    int32_t pad;
+} uam_geo_grid_desc;
+/* Reproject a geographic DEM onto the plane raster grid dst (units of dst: unit_m metres):
+ * each output cell centre -> inverse TM -> source pixel; resample 0 = nearest, 1 = bilinear
+ * when all four neighbours are valid (else nearest); outside / nodata -> src nodata. */
+int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* tm, const float* src_dev,
+                      const uam_geo_grid_desc* src, const uam_raster_desc* dst, double unit_m,
+                      int32_t resample, float* dst_dev, uam_stream stream);
+
 /* Kernel variant for the raster/volume evaluations (0 = automatic).  1 = one wave per
  * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
  * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,

@@ -67,6 +67,64 @@ def refine_params(n_outer=15, n_inner=50, max_backtrack=30, c0=10.0, rho=5.0, c_
                          armijo, theta, max_step, inner_tol, delta)
 
 
+class _TM(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("a", "f", "k0", "lat0_deg", "lon0_deg", "fe",
+                                                "fn")]
+
+
+class _GeoGrid(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("lon0", ctypes.c_double),
+                ("lat_top", ctypes.c_double), ("dlon", ctypes.c_double),
+                ("dlat", ctypes.c_double), ("nodata", ctypes.c_float), ("pad", ctypes.c_int32)]
+
+
+# Japan Plane Rectangular CS origins (lat0, lon0) in degrees, zones I..XIX (EPSG:2443..2461)
+JPRCS_ORIGINS = [(33.0, 129.5), (33.0, 131.0), (36.0, 132.0 + 10 / 60), (33.0, 133.5),
+                 (36.0, 134.0 + 20 / 60), (36.0, 136.0), (36.0, 137.0 + 10 / 60),
+                 (36.0, 138.5), (36.0, 139.0 + 50 / 60), (40.0, 140.0 + 50 / 60),
+                 (44.0, 140.25), (44.0, 142.25), (44.0, 144.25), (26.0, 142.0), (26.0, 127.5),
+                 (26.0, 124.0), (26.0, 131.0), (20.0, 136.0), (26.0, 154.0)]
+
+
+def tm_zone(zone=1):
+    """GRS80, k0 = 0.9999, no false origin: JGD2000 / Japan Plane Rectangular CS zone."""
+    lat0, lon0 = JPRCS_ORIGINS[zone - 1]
+    return _TM(6378137.0, 1 / 298.257222101, 0.9999, lat0, lon0, 0.0, 0.0)
+
+
+def tm_fwd(lonlat, tm=None):
+    tm = tm or tm_zone(1)
+    ll = np.ascontiguousarray(lonlat, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros_like(ll)
+    lib().orc_tm_fwd(ctypes.byref(tm), _ptr(ll, _f64p), ctypes.c_int64(ll.shape[0]),
+                     _ptr(out, _f64p))
+    return out
+
+
+def tm_inv(xy, tm=None):
+    tm = tm or tm_zone(1)
+    p = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros_like(p)
+    lib().orc_tm_inv(ctypes.byref(tm), _ptr(p, _f64p), ctypes.c_int64(p.shape[0]),
+                     _ptr(out, _f64p))
+    return out
+
+
+def geo_grid(nx, ny, lon0, lat_top, dlon, dlat, nodata=-9999.0):
+    return _GeoGrid(int(nx), int(ny), float(lon0), float(lat_top), float(dlon), float(dlat),
+                    float(nodata), 0)
+
+
+def reproject(src, ggrid, rdesc, unit=1000.0, resample=0, tm=None):
+    tm = tm or tm_zone(1)
+    s = np.ascontiguousarray(src, dtype=np.float32)
+    out = np.zeros((rdesc.ny, rdesc.nx), dtype=np.float32)
+    lib().orc_reproject(ctypes.byref(tm), _ptr(s, _f32p), ctypes.byref(ggrid),
+                        ctypes.byref(rdesc), ctypes.c_double(unit), ctypes.c_int(resample),
+                        _ptr(out, _f32p))
+    return out
+
+
 def build():
     """Compile liboracle.so (gcc) if it is missing or older than its source."""
     src = os.path.join(HERE, "uam_oracle.c")

@@ -994,3 +994,161 @@ int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* 
     free(tmp);
     return 0;
 }
+
+/* ======================================================================================
+ * Transverse Mercator: geographic JGD2000 / JGD2011 (EPSG:4612 /
+ * 6668, lon-lat order as geopandas' to_crs uses) <-> Japan Plane Rectangular CS (EPSG:2443 +
+ * zone - 1), the transform pyproj applies at data_manager.py:24-26 / 84-85 and
+ * path_generation/main.py:106-115.  Krueger series in n to order 6 (Karney 2011), geodetic
+ * from conformal latitude by 5 Newton steps on tau = tan(phi).  Pinned: the reference's own
+ * shapefiles (data/processed/{land,populated_area,no_fly_zone}/ .shp) against the plane
+ * coordinates they were written from (tests/golden/make_crs_golden.py), <= 3e-14 deg. */
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+typedef struct {
+    double a, f, k0, lat0_deg, lon0_deg, fe, fn;
+} orc_tm;
+
+typedef struct {
+    double n, e, e2, A, xi0, lon0, alpha[6], beta[6];
+} tm_k;
+
+static void tm_prepare(const orc_tm* t, tm_k* k) {
+    const double n = t->f / (2.0 - t->f), n2 = n * n, n3 = n2 * n, n4 = n3 * n, n5 = n4 * n,
+                 n6 = n5 * n;
+    k->n = n;
+    k->e2 = t->f * (2.0 - t->f);
+    k->e = sqrt(k->e2);
+    k->A = t->a / (1.0 + n) * (1.0 + n2 / 4.0 + n4 / 64.0 + n6 / 256.0);
+    k->alpha[0] = n / 2 - 2 * n2 / 3 + 5 * n3 / 16 + 41 * n4 / 180 - 127 * n5 / 288 +
+                  7891 * n6 / 37800;
+    k->alpha[1] = 13 * n2 / 48 - 3 * n3 / 5 + 557 * n4 / 1440 + 281 * n5 / 630 -
+                  1983433 * n6 / 1935360;
+    k->alpha[2] = 61 * n3 / 240 - 103 * n4 / 140 + 15061 * n5 / 26880 + 167603 * n6 / 181440;
+    k->alpha[3] = 49561 * n4 / 161280 - 179 * n5 / 168 + 6601661 * n6 / 7257600;
+    k->alpha[4] = 34729 * n5 / 80640 - 3418889 * n6 / 1995840;
+    k->alpha[5] = 212378941 * n6 / 319334400;
+    k->beta[0] = n / 2 - 2 * n2 / 3 + 37 * n3 / 96 - n4 / 360 - 81 * n5 / 512 +
+                 96199 * n6 / 604800;
+    k->beta[1] = n2 / 48 + n3 / 15 - 437 * n4 / 1440 + 46 * n5 / 105 - 1118711 * n6 / 3870720;
+    k->beta[2] = 17 * n3 / 480 - 37 * n4 / 840 - 209 * n5 / 4480 + 5569 * n6 / 90720;
+    k->beta[3] = 4397 * n4 / 161280 - 11 * n5 / 504 - 830251 * n6 / 7257600;
+    k->beta[4] = 4583 * n5 / 161280 - 108847 * n6 / 3991680;
+    k->beta[5] = 20648693 * n6 / 638668800;
+    k->lon0 = t->lon0_deg * (M_PI / 180.0);
+    /* xi of the origin latitude on the central meridian */
+    const double phi0 = t->lat0_deg * (M_PI / 180.0), s0 = sin(phi0);
+    const double tt = sinh(atanh(s0) - k->e * atanh(k->e * s0));
+    const double xp = atan2(tt, 1.0);
+    double xi = xp;
+    for (int j = 0; j < 6; ++j) xi = xi + k->alpha[j] * sin(2.0 * (j + 1) * xp);
+    k->xi0 = xi;
+}
+
+static void tm_fwd1(const orc_tm* t, const tm_k* k, double lon, double lat, double* x,
+                    double* y) {
+    const double phi = lat * (M_PI / 180.0), dl = lon * (M_PI / 180.0) - k->lon0;
+    const double s = sin(phi);
+    const double tt = sinh(atanh(s) - k->e * atanh(k->e * s));
+    const double xp = atan2(tt, cos(dl));
+    const double ep = atanh(sin(dl) / sqrt(1.0 + tt * tt));
+    double xi = xp, eta = ep;
+    for (int j = 0; j < 6; ++j) {
+        const double c = 2.0 * (j + 1);
+        xi = xi + k->alpha[j] * (sin(c * xp) * cosh(c * ep));
+        eta = eta + k->alpha[j] * (cos(c * xp) * sinh(c * ep));
+    }
+    *x = t->k0 * k->A * eta + t->fe;
+    *y = t->k0 * k->A * (xi - k->xi0) + t->fn;
+}
+
+static void tm_inv1(const orc_tm* t, const tm_k* k, double x, double y, double* lon,
+                    double* lat) {
+    const double kA = t->k0 * k->A;
+    const double xi = (y - t->fn) / kA + k->xi0, eta = (x - t->fe) / kA;
+    double xp = xi, ep = eta;
+    for (int j = 0; j < 6; ++j) {
+        const double c = 2.0 * (j + 1);
+        xp = xp - k->beta[j] * (sin(c * xi) * cosh(c * eta));
+        ep = ep - k->beta[j] * (cos(c * xi) * sinh(c * eta));
+    }
+    const double se = sinh(ep), cx = cos(xp);
+    const double taup = sin(xp) / sqrt(se * se + cx * cx);
+    const double lam = atan2(se, cx);
+    const double e = k->e, e2m = 1.0 - k->e2;
+    double tau = taup;
+    for (int it = 0; it < 5; ++it) {
+        const double r = sqrt(1.0 + tau * tau);
+        const double sg = sinh(e * atanh(e * tau / r));
+        const double tp = tau * sqrt(1.0 + sg * sg) - sg * r;
+        tau = tau + (taup - tp) * (1.0 + e2m * tau * tau) / (e2m * sqrt(1.0 + tp * tp) * r);
+    }
+    *lat = atan(tau) * (180.0 / M_PI);
+    *lon = (lam + k->lon0) * (180.0 / M_PI);
+}
+
+void orc_tm_fwd(const orc_tm* t, const double* lonlat, int64_t n, double* xy) {
+    tm_k k;
+    tm_prepare(t, &k);
+    for (int64_t i = 0; i < n; ++i)
+        tm_fwd1(t, &k, lonlat[2 * i], lonlat[2 * i + 1], &xy[2 * i], &xy[2 * i + 1]);
+}
+
+void orc_tm_inv(const orc_tm* t, const double* xy, int64_t n, double* lonlat) {
+    tm_k k;
+    tm_prepare(t, &k);
+    for (int64_t i = 0; i < n; ++i)
+        tm_inv1(t, &k, xy[2 * i], xy[2 * i + 1], &lonlat[2 * i], &lonlat[2 * i + 1]);
+}
+
+/* DEM reprojection (build-defined; the reference's merge_test.tif is a
+ * plane-CS DEM made outside the repository from the lat/lon mosaic mergeLL.vrt):
+ * output cell (ix, iy) centre in plane units -> metres (* unit) -> inverse TM -> source pixel
+ * u = (lon - lon0) / dlon, v = (lat_top - lat) / dlat.  resample 0 = nearest (GDAL's default:
+ * pixel floor(u), floor(v)); 1 = bilinear on pixel centres when all four neighbours are valid
+ * (else nearest).  Outside the source or nodata -> nodata. */
+typedef struct {
+    int32_t nx, ny;
+    double lon0, lat_top, dlon, dlat;
+    float nodata;
+    int32_t pad;
+} orc_geo_grid;
+
+void orc_reproject(const orc_tm* t, const float* src, const orc_geo_grid* g,
+                   const orc_raster* dst, double unit, int resample, float* out) {
+    tm_k k;
+    tm_prepare(t, &k);
+    for (int64_t iy = 0; iy < dst->ny; ++iy) {
+        for (int64_t ix = 0; ix < dst->nx; ++ix) {
+            const double xc = dst->x0 + ((double)ix + 0.5) * dst->dx;
+            const double yc = dst->y_top - ((double)iy + 0.5) * dst->dy;
+            double lon, lat;
+            tm_inv1(t, &k, xc * unit, yc * unit, &lon, &lat);
+            const double u = (lon - g->lon0) / g->dlon, v = (g->lat_top - lat) / g->dlat;
+            float val = g->nodata;
+            const double fu = floor(u), fv = floor(v);
+            if (fu >= 0.0 && fu < (double)g->nx && fv >= 0.0 && fv < (double)g->ny) {
+                val = src[(int64_t)fv * g->nx + (int64_t)fu];
+                if (resample == 1) {
+                    const double uu = u - 0.5, vv = v - 0.5;
+                    const double bu = floor(uu), bv = floor(vv);
+                    if (bu >= 0.0 && bu + 1.0 < (double)g->nx && bv >= 0.0 &&
+                        bv + 1.0 < (double)g->ny) {
+                        const int64_t i0 = (int64_t)bv * g->nx + (int64_t)bu;
+                        const float a00 = src[i0], a01 = src[i0 + 1], a10 = src[i0 + g->nx],
+                                    a11 = src[i0 + g->nx + 1];
+                        if (a00 != g->nodata && a01 != g->nodata && a10 != g->nodata &&
+                            a11 != g->nodata) {
+                            const double wu = uu - bu, wv = vv - bv;
+                            const double top = (double)a00 + wu * ((double)a01 - (double)a00);
+                            const double bot = (double)a10 + wu * ((double)a11 - (double)a10);
+                            val = (float)(top + wv * (bot - top));
+                        }
+                    }
+                }
+            }
+            out[iy * dst->nx + ix] = val;
+        }
+    }
+}

@@ -71,6 +71,17 @@ class RefineParams(ctypes.Structure):
                 ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double)]
 
 
+class TmParams(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("a", "f", "k0", "lat0_deg", "lon0_deg",
+                                                "false_easting", "false_northing")]
+
+
+class GeoGridDesc(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("lon0", ctypes.c_double),
+                ("lat_top", ctypes.c_double), ("dlon", ctypes.c_double),
+                ("dlat", ctypes.c_double), ("nodata", ctypes.c_float), ("pad", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes); the full exported surface of include/uampath.h
 SIGNATURES = {
     "uam_abi_version": (ctypes.c_int, []),
@@ -100,6 +111,14 @@ SIGNATURES = {
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,
                                             ctypes.POINTER(PathOutputs), _vp]),
+    "uam_tm_jprcs": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(TmParams)]),
+    "uam_geo_to_plane": (ctypes.c_int, [_vp, ctypes.POINTER(TmParams), _vp, ctypes.c_int64, _vp,
+                                        _vp]),
+    "uam_plane_to_geo": (ctypes.c_int, [_vp, ctypes.POINTER(TmParams), _vp, ctypes.c_int64, _vp,
+                                        _vp]),
+    "uam_reproject_dem": (ctypes.c_int, [_vp, ctypes.POINTER(TmParams), _vp,
+                                         ctypes.POINTER(GeoGridDesc), ctypes.POINTER(RasterDesc),
+                                         ctypes.c_double, ctypes.c_int32, _vp, _vp]),
     "uam_refine_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64,
                                                     ctypes.POINTER(RefineParams)]),
     "uam_refine": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(RefineParams), _vp,

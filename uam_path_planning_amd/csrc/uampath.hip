@@ -1478,6 +1478,119 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// K7: coordinate reference systems.  Transverse Mercator between
+// geographic JGD2000/JGD2011 (lon, lat degrees) and the Japan Plane Rectangular CS (metres),
+// the transform pyproj applies at data_manager.py:24-26 / 84-85 and main.py:106-115.  Krueger
+// series to n^6, geodetic latitude from conformal latitude by 5 Newton steps; definition and
+// coefficient formulas as oracle/uam_oracle.c (tm_prepare / tm_fwd1 / tm_inv1); the host
+// computes the coefficients once (KTm) so device and oracle share them.
+struct KTm {
+    double k0, A, e, e2, xi0, lon0, fe, fn;
+    double alpha[6], beta[6];
+};
+
+__device__ __forceinline__ void tm_fwd(const KTm& k, double lon, double lat, double& x,
+                                       double& y) {
+    const double phi = lat * (M_PI / 180.0), dl = lon * (M_PI / 180.0) - k.lon0;
+    const double s = sin(phi);
+    const double tt = sinh(atanh(s) - k.e * atanh(k.e * s));
+    const double xp = atan2(tt, cos(dl));
+    const double ep = atanh(sin(dl) / sqrt(1.0 + tt * tt));
+    double xi = xp, eta = ep;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double c = 2.0 * (j + 1);
+        xi = xi + k.alpha[j] * (sin(c * xp) * cosh(c * ep));
+        eta = eta + k.alpha[j] * (cos(c * xp) * sinh(c * ep));
+    }
+    x = k.k0 * k.A * eta + k.fe;
+    y = k.k0 * k.A * (xi - k.xi0) + k.fn;
+}
+
+__device__ __forceinline__ void tm_inv(const KTm& k, double x, double y, double& lon,
+                                       double& lat) {
+    const double kA = k.k0 * k.A;
+    const double xi = (y - k.fn) / kA + k.xi0, eta = (x - k.fe) / kA;
+    double xp = xi, ep = eta;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double c = 2.0 * (j + 1);
+        xp = xp - k.beta[j] * (sin(c * xi) * cosh(c * eta));
+        ep = ep - k.beta[j] * (cos(c * xi) * sinh(c * eta));
+    }
+    const double se = sinh(ep), cx = cos(xp);
+    const double taup = sin(xp) / sqrt(se * se + cx * cx);
+    const double lam = atan2(se, cx);
+    const double e = k.e, e2m = 1.0 - k.e2;
+    double tau = taup;
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {
+        const double r = sqrt(1.0 + tau * tau);
+        const double sg = sinh(e * atanh(e * tau / r));
+        const double tp = tau * sqrt(1.0 + sg * sg) - sg * r;
+        tau = tau + (taup - tp) * (1.0 + e2m * tau * tau) / (e2m * sqrt(1.0 + tp * tp) * r);
+    }
+    lat = atan(tau) * (180.0 / M_PI);
+    lon = (lam + k.lon0) * (180.0 / M_PI);
+}
+
+__global__ __launch_bounds__(256) void k_tm_points(KTm k, int inverse,
+                                                   const double* __restrict__ in, int64_t n,
+                                                   double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double2 v = reinterpret_cast<const double2*>(in)[i];
+    double a, b;
+    if (inverse)
+        tm_inv(k, v.x, v.y, a, b);
+    else
+        tm_fwd(k, v.x, v.y, a, b);
+    reinterpret_cast<double2*>(out)[i] = make_double2(a, b);
+}
+
+struct KGeoGrid {
+    int32_t nx, ny;
+    double lon0, lat_top, dlon, dlat;
+    float nodata;
+};
+
+// DEM reprojection (definition: oracle orc_reproject).  One lane per output cell, rows
+// contiguous (coalesced 4-B stores); neighbouring cells read neighbouring source pixels.
+__global__ __launch_bounds__(256) void k_reproject(KTm k, KGeoGrid g, KRaster r, double unit,
+                                                   int resample, const float* __restrict__ src,
+                                                   float* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)r.nx * r.ny) return;
+    const int64_t iy = i / r.nx, ix = i - iy * r.nx;
+    const double xc = r.x0 + ((double)ix + 0.5) * r.dx;
+    const double yc = r.y_top - ((double)iy + 0.5) * r.dy;
+    double lon, lat;
+    tm_inv(k, xc * unit, yc * unit, lon, lat);
+    const double u = (lon - g.lon0) / g.dlon, v = (g.lat_top - lat) / g.dlat;
+    float val = g.nodata;
+    const double fu = floor(u), fv = floor(v);
+    if (fu >= 0.0 && fu < (double)g.nx && fv >= 0.0 && fv < (double)g.ny) {
+        val = src[(int64_t)fv * g.nx + (int64_t)fu];
+        if (resample == 1) {
+            const double uu = u - 0.5, vv = v - 0.5;
+            const double bu = floor(uu), bv = floor(vv);
+            if (bu >= 0.0 && bu + 1.0 < (double)g.nx && bv >= 0.0 && bv + 1.0 < (double)g.ny) {
+                const int64_t i0 = (int64_t)bv * g.nx + (int64_t)bu;
+                const float a00 = src[i0], a01 = src[i0 + 1], a10 = src[i0 + g.nx],
+                            a11 = src[i0 + g.nx + 1];
+                if (a00 != g.nodata && a01 != g.nodata && a10 != g.nodata && a11 != g.nodata) {
+                    const double wu = uu - bu, wv = vv - bv;
+                    const double top = (double)a00 + wu * ((double)a01 - (double)a00);
+                    const double bot = (double)a10 + wu * ((double)a11 - (double)a10);
+                    val = (float)(top + wv * (bot - top));
+                }
+            }
+        }
+    }
+    dst[i] = val;
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -2201,6 +2314,111 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
     hipLaunchKernelGGL(k_refine, dim3((unsigned)blocks), dim3(64 * wpb),
                        (size_t)(wpb * per_wave), (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp,
                        n_paths, (double*)workspace, cost, infeas, iters);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+// ---- CRS (K7) ----------------------------------------------------------------------------
+static const double kJprcsOrigin[19][2] = {
+    {33.0, 129.5}, {33.0, 131.0}, {36.0, 132.0 + 10.0 / 60}, {33.0, 133.5},
+    {36.0, 134.0 + 20.0 / 60}, {36.0, 136.0}, {36.0, 137.0 + 10.0 / 60}, {36.0, 138.5},
+    {36.0, 139.0 + 50.0 / 60}, {40.0, 140.0 + 50.0 / 60}, {44.0, 140.25}, {44.0, 142.25},
+    {44.0, 144.25}, {26.0, 142.0}, {26.0, 127.5}, {26.0, 124.0}, {26.0, 131.0}, {20.0, 136.0},
+    {26.0, 154.0}};
+
+int uam_tm_jprcs(int32_t zone, uam_tm_params* out) {
+    if (!out) return fail(UAM_E_INVALID, "out is NULL");
+    if (zone < 1 || zone > 19) return fail(UAM_E_INVALID, "JPRCS zone %d outside [1, 19]", zone);
+    *out = uam_tm_params{6378137.0, 1.0 / 298.257222101, 0.9999, kJprcsOrigin[zone - 1][0],
+                         kJprcsOrigin[zone - 1][1], 0.0, 0.0};
+    return UAM_OK;
+}
+
+static int make_ktm(const uam_tm_params* t, KTm* k) {
+    if (!t) return fail(UAM_E_INVALID, "tm params are NULL");
+    if (!(t->a > 0.0) || !(t->f >= 0.0 && t->f < 1.0) || !(t->k0 > 0.0))
+        return fail(UAM_E_INVALID, "bad ellipsoid / scale");
+    const double n = t->f / (2.0 - t->f), n2 = n * n, n3 = n2 * n, n4 = n3 * n, n5 = n4 * n,
+                 n6 = n5 * n;
+    k->e2 = t->f * (2.0 - t->f);
+    k->e = sqrt(k->e2);
+    k->A = t->a / (1.0 + n) * (1.0 + n2 / 4.0 + n4 / 64.0 + n6 / 256.0);
+    k->alpha[0] = n / 2 - 2 * n2 / 3 + 5 * n3 / 16 + 41 * n4 / 180 - 127 * n5 / 288 +
+                  7891 * n6 / 37800;
+    k->alpha[1] = 13 * n2 / 48 - 3 * n3 / 5 + 557 * n4 / 1440 + 281 * n5 / 630 -
+                  1983433 * n6 / 1935360;
+    k->alpha[2] = 61 * n3 / 240 - 103 * n4 / 140 + 15061 * n5 / 26880 + 167603 * n6 / 181440;
+    k->alpha[3] = 49561 * n4 / 161280 - 179 * n5 / 168 + 6601661 * n6 / 7257600;
+    k->alpha[4] = 34729 * n5 / 80640 - 3418889 * n6 / 1995840;
+    k->alpha[5] = 212378941 * n6 / 319334400;
+    k->beta[0] = n / 2 - 2 * n2 / 3 + 37 * n3 / 96 - n4 / 360 - 81 * n5 / 512 +
+                 96199 * n6 / 604800;
+    k->beta[1] = n2 / 48 + n3 / 15 - 437 * n4 / 1440 + 46 * n5 / 105 - 1118711 * n6 / 3870720;
+    k->beta[2] = 17 * n3 / 480 - 37 * n4 / 840 - 209 * n5 / 4480 + 5569 * n6 / 90720;
+    k->beta[3] = 4397 * n4 / 161280 - 11 * n5 / 504 - 830251 * n6 / 7257600;
+    k->beta[4] = 4583 * n5 / 161280 - 108847 * n6 / 3991680;
+    k->beta[5] = 20648693 * n6 / 638668800;
+    k->lon0 = t->lon0_deg * (M_PI / 180.0);
+    k->k0 = t->k0;
+    k->fe = t->false_easting;
+    k->fn = t->false_northing;
+    const double phi0 = t->lat0_deg * (M_PI / 180.0), s0 = sin(phi0);
+    const double tt = sinh(atanh(s0) - k->e * atanh(k->e * s0));
+    const double xp = atan2(tt, 1.0);
+    double xi = xp;
+    for (int j = 0; j < 6; ++j) xi = xi + k->alpha[j] * sin(2.0 * (j + 1) * xp);
+    k->xi0 = xi;
+    return UAM_OK;
+}
+
+static int tm_points(uam_ctx* ctx, const uam_tm_params* t, int inverse, const double* in,
+                     int64_t n, double* out, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    int st;
+    KTm k;
+    st = make_ktm(t, &k);
+    if (st) return st;
+    if (n < 0) return fail(UAM_E_INVALID, "n < 0");
+    if (n == 0) return UAM_OK;
+    if (!in || !out) return fail(UAM_E_INVALID, "in/out is NULL");
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_tm_points, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0,
+                       (hipStream_t)stream, k, inverse, in, n, out);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_geo_to_plane(uam_ctx* ctx, const uam_tm_params* t, const double* lonlat, int64_t n,
+                     double* xy, uam_stream stream) {
+    return tm_points(ctx, t, 0, lonlat, n, xy, stream);
+}
+
+int uam_plane_to_geo(uam_ctx* ctx, const uam_tm_params* t, const double* xy, int64_t n,
+                     double* lonlat, uam_stream stream) {
+    return tm_points(ctx, t, 1, xy, n, lonlat, stream);
+}
+
+int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* t, const float* src,
+                      const uam_geo_grid_desc* sg, const uam_raster_desc* dst, double unit_m,
+                      int32_t resample, float* out, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    int st;
+    KTm k;
+    st = make_ktm(t, &k);
+    if (st) return st;
+    if (!sg || !src || !out) return fail(UAM_E_INVALID, "src/grid/out is NULL");
+    if (sg->nx < 1 || sg->ny < 1 || !(sg->dlon > 0.0) || !(sg->dlat > 0.0))
+        return fail(UAM_E_INVALID, "bad source grid");
+    if (resample != 0 && resample != 1) return fail(UAM_E_INVALID, "resample must be 0 or 1");
+    if (!(unit_m > 0.0)) return fail(UAM_E_INVALID, "unit_m must be > 0");
+    KRaster kr;
+    st = make_kraster(dst, &kr);
+    if (st) return st;
+    const KGeoGrid g{sg->nx, sg->ny, sg->lon0, sg->lat_top, sg->dlon, sg->dlat, sg->nodata};
+    const int64_t cells = (int64_t)kr.nx * kr.ny;
+    DeviceGuard dg(ctx->device);
+    hipLaunchKernelGGL(k_reproject, dim3(grid_for(cells, 256, INT32_MAX)), dim3(256), 0,
+                       (hipStream_t)stream, k, g, kr, unit_m, resample, src, out);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }

@@ -391,6 +391,46 @@ class Engine:
                                        self.stream), "uam_refine")
         return out
 
+    # -- coordinate reference systems (K7; SURVEY §8(f) ranks 3-4) --------------------------
+    def _tm(self, tm):
+        if tm is None or isinstance(tm, int):
+            out = _lib.TmParams()
+            _lib.check(self.lib.uam_tm_jprcs(1 if tm is None else int(tm), ctypes.byref(out)),
+                       "uam_tm_jprcs")
+            return out
+        return tm
+
+    def _points(self, fn, name, pts, tm):
+        torch = _torch()
+        p = self.tensor(pts, torch.float64).reshape(-1, 2).contiguous()
+        out = self.empty(tuple(p.shape), torch.float64)
+        _lib.check(fn(self._ctx, ctypes.byref(self._tm(tm)), _ptr(p), p.shape[0], _ptr(out),
+                      self.stream), name)
+        return out
+
+    def geo_to_plane(self, lonlat, tm=None):
+        """[n, 2] lon, lat (deg) -> x (easting), y (northing) in metres; tm = JPRCS zone
+        number (default 1 = EPSG:2443) or a TmParams."""
+        return self._points(self.lib.uam_geo_to_plane, "uam_geo_to_plane", lonlat, tm)
+
+    def plane_to_geo(self, xy, tm=None):
+        """[n, 2] x, y metres -> lon, lat (deg)."""
+        return self._points(self.lib.uam_plane_to_geo, "uam_plane_to_geo", xy, tm)
+
+    def reproject_dem(self, src, src_grid, dst_geo, unit_m=1000.0, resample=0, tm=None):
+        """Geographic DEM [ny, nx] float32 on src_grid (GeoGridDesc) -> plane DEM on the
+        RasterGeo dst_geo (coordinates in units of unit_m metres)."""
+        torch = _torch()
+        s = self.tensor(src, torch.float32).contiguous()
+        if tuple(s.shape) != (src_grid.ny, src_grid.nx):
+            raise ValueError(f"src must be [{src_grid.ny}, {src_grid.nx}]")
+        out = self.empty((dst_geo.ny, dst_geo.nx), torch.float32)
+        _lib.check(self.lib.uam_reproject_dem(
+            self._ctx, ctypes.byref(self._tm(tm)), _ptr(s), ctypes.byref(src_grid),
+            ctypes.byref(dst_geo.as_struct()), float(unit_m), int(resample), _ptr(out),
+            self.stream), "uam_reproject_dem")
+        return out
+
     def synchronize(self):
         _lib.check(self.lib.uam_synchronize(self._ctx, self.stream), "uam_synchronize")
 

@@ -7,10 +7,13 @@ map_generation/data_manager.py (DataManager, 8-86).
   (data_manager.py:14-17): ``dem == -9999`` when threshold_dem == -9999, else ``dem > thr``,
   computed on the GPU as the MASK flag bit of the cost-raster build (K1).
 * ``build_cost_raster(...)``: DEM -> device record raster {Φ, Σψ_nfz, dem, flags} (K1).
+* ``load_dem_geographic(vrt, dst_geo)``: the full-scale ingest of SURVEY §8(f) rank 3 -- a
+  lat/lon tile mosaic (mergeLL.vrt: JGD2011, 0.2" pixels, mergeLL.vrt:1-3) placed on the
+  device (K0) and reprojected onto the plane cost-raster grid (K7, EPSG:2443 via the TM
+  transform the reference delegates to pyproj, data_manager.py:24-26).
 * ``save_polygons(vertex_lists, path)``: the D1 text format of data_manager.py:56-81
   (coordinates / 1000, m -> km), readable by path_generation.utils.get_var_from_file.
-Polygonisation (rasterio.features.shapes + shapely, data_manager.py:18-19) and shapefile IO
-(geopandas) are out of scope.
+Shapefile output: ``uam_path_planning_amd.geo.export`` (save_polygons_to_shapefile).
 """
 from ..engine import RasterGeo, default_engine
 from .geotiff import read_geotiff
@@ -53,6 +56,33 @@ class DataManager:
         dem = eng.tensor(data, torch.float32)
         gt = gt or (0.0, 1.0, 0.0, float(data.shape[0]), 0.0, -1.0)
         return dem, geo_from_geotransform(data.shape[1], data.shape[0], gt, nod, dem_threshold)
+
+    def load_dem_geographic(self, input_file, dst_geo, resample=0, zone=1, unit_m=1000.0):
+        """Geographic (lon/lat) DEM mosaic -> plane DEM on ``dst_geo`` (RasterGeo in units of
+        unit_m metres, JPRCS zone): device mosaic (K0) + reprojection (K7)."""
+        from .._lib import GeoGridDesc
+
+        eng = self.engine
+        if input_file.lower().endswith(".vrt"):
+            v = read_vrt(input_file)
+            nod = -9999.0 if v.nodata is None else v.nodata
+            tiles, xo, yo = load_tiles(v)
+            src = eng.dem_mosaic(tiles, xo, yo, v.width, v.height, fill=nod)
+            gt, w, h = v.geotransform, v.width, v.height
+        else:
+            data, gt, nod = read_geotiff(input_file)
+            nod = -9999.0 if nod is None else nod
+            import torch
+
+            src = eng.tensor(data, torch.float32)
+            h, w = data.shape
+        lon0, dlon, rx, lat_top, ry, ndlat = gt
+        if rx != 0 or ry != 0 or not (dlon > 0 and ndlat < 0):
+            raise ValueError("expected a north-up geographic grid")
+        grid = GeoGridDesc(int(w), int(h), float(lon0), float(lat_top), float(dlon),
+                           float(-ndlat), float(nod), 0)
+        dem = eng.reproject_dem(src, grid, dst_geo, unit_m, resample, zone)
+        return dem, dst_geo
 
     def build_cost_raster(self, input_file, geometry, params, dem_threshold=0.0):
         eng = self.engine
