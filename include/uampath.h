@@ -259,6 +259,24 @@ int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* tm, const float* src_de
                       const uam_geo_grid_desc* src, const uam_raster_desc* dst, double unit_m,
                       int32_t resample, float* dst_dev, uam_stream stream);
 
+/* ---- Land / populated-area polygons --------------------------------
+ * DataProcessor(min_area, large_area, divisions, min_approx_polygon_area) of
+ * map_generation/data_processor.py:9-13 (defaults 750000 m^2, 32000000 m^2, 5, 780000 m^2). */
+typedef struct {
+    double min_area, large_area, min_approx_area;
+    int32_t divisions, pad;
+} uam_polyproc_params;
+/* DataProcessor.process_polygons (data_processor.py:15-75) on polygons in plane metres (host):
+ * unary_union (inputs must have disjoint interiors; shared boundaries merge), area filter,
+ * divisions^2 split of large polygons, cv2.minAreaRect + boxPoints + np.intp per polygon /
+ * piece, final area filter.  Rings: ring r = xy[ring_start[r] .. ring_start[r+1]) (open or
+ * closed), ring_hole[r] != 0 for holes.  Output: *n_rects rectangles, rect_xy[r][4][2]
+ * integer metres in cv2.boxPoints order (at most max_rects written; more -> UAM_E_INVALID
+ * with *n_rects set).  Definition: oracle/uam_oracle.c orc_process_polygons. */
+int uam_process_polygons(const double* xy, const int64_t* ring_start, int32_t n_rings,
+                         const int32_t* ring_hole, const uam_polyproc_params* params,
+                         int64_t* rect_xy, int32_t max_rects, int32_t* n_rects);
+
 /* Kernel variant for the raster/volume evaluations (0 = automatic).  1 = one wave per
  * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
  * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,

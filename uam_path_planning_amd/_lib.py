@@ -82,6 +82,12 @@ class GeoGridDesc(ctypes.Structure):
                 ("dlat", ctypes.c_double), ("nodata", ctypes.c_float), ("pad", ctypes.c_int32)]
 
 
+class PolyprocParams(ctypes.Structure):
+    _fields_ = [("min_area", ctypes.c_double), ("large_area", ctypes.c_double),
+                ("min_approx_area", ctypes.c_double), ("divisions", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes); the full exported surface of include/uampath.h
 SIGNATURES = {
     "uam_abi_version": (ctypes.c_int, []),
@@ -119,6 +125,9 @@ SIGNATURES = {
     "uam_reproject_dem": (ctypes.c_int, [_vp, ctypes.POINTER(TmParams), _vp,
                                          ctypes.POINTER(GeoGridDesc), ctypes.POINTER(RasterDesc),
                                          ctypes.c_double, ctypes.c_int32, _vp, _vp]),
+    "uam_process_polygons": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, _vp,
+                                            ctypes.POINTER(PolyprocParams), _vp, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int32)]),
     "uam_refine_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64,
                                                     ctypes.POINTER(RefineParams)]),
     "uam_refine": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(RefineParams), _vp,

@@ -7,6 +7,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "uampath.hip")
+SRCS = [SRC, os.path.join(HERE, "csrc", "polyproc.cpp")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", "polyproc.h")]
 HEADER = os.path.join(ROOT, "include", "uampath.h")
 OUT = os.path.join(HERE, "lib", "libuampath.so")
 ARCH = os.environ.get("UAM_OFFLOAD_ARCH", "gfx950")
@@ -28,7 +30,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HEADER, __file__))
+    return any(os.path.getmtime(p) > t for p in (*DEPS, HEADER, __file__))
 
 
 def build_library(force=False, verbose=False):
@@ -36,7 +38,7 @@ def build_library(force=False, verbose=False):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-o", tmp, SRC]
+    cmd = [hipcc(), *HIPCC_FLAGS, "-o", tmp, *SRCS]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -1827,6 +1827,17 @@ KOut make_kout(const uam_path_outputs* o) {
 
 }  // namespace
 
+// error reporting for the host-only translation units (polyproc.cpp)
+int uam_fail_(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
 extern "C" {
 
 int uam_abi_version(void) { return UAM_ABI_VERSION; }
