@@ -277,6 +277,18 @@ int uam_process_polygons(const double* xy, const int64_t* ring_start, int32_t n_
                          const int32_t* ring_hole, const uam_polyproc_params* params,
                          int64_t* rect_xy, int32_t max_rects, int32_t* n_rects);
 
+/* The DEM route (DataManager.load_dem_polygons_from_geotiff + process_polygons,
+ * map_generation/main.py:27-35): mask (dem == -9999 if threshold == -9999 else
+ * dem > threshold, data_manager.py:14-17) -> 4-connected regions (rasterio.features.shapes)
+ * labelled on the GPU -> the same approximation as uam_process_polygons, with pixel corners
+ * at x0 + i dx, y_top - j dy (times unit_m metres).  Large regions are split into their box
+ * pieces by a second labelling on the grid refined at the box edges.  Output as
+ * uam_process_polygons (regions in raster order of their first cell).  Definition:
+ * oracle/uam_oracle.c orc_dem_polygons. */
+int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* desc,
+                     float threshold, double unit_m, const uam_polyproc_params* params,
+                     int64_t* rect_xy, int32_t max_rects, int32_t* n_rects, uam_stream stream);
+
 /* Kernel variant for the raster/volume evaluations (0 = automatic).  1 = one wave per
  * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
  * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,

@@ -125,6 +125,40 @@ def reproject(src, ggrid, rdesc, unit=1000.0, resample=0, tm=None):
     return out
 
 
+class _Polyproc(ctypes.Structure):
+    _fields_ = [("min_area", ctypes.c_double), ("large_area", ctypes.c_double),
+                ("min_approx_area", ctypes.c_double), ("divisions", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+def polyproc(min_area=750000, large_area=32000000, divisions=5, min_approx_polygon_area=780000):
+    return _Polyproc(float(min_area), float(large_area), float(min_approx_polygon_area),
+                     int(divisions), 0)
+
+
+def min_area_rect(points):
+    """cv2.boxPoints(cv2.minAreaRect(float32 points)) -> np.intp  (restatement)."""
+    p = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+    box = np.zeros(8, np.int64)
+    lib().orc_min_area_rect(_ptr(p, _f64p), ctypes.c_int64(len(p)),
+                            box.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    return box.reshape(4, 2)
+
+
+def dem_polygons(dem, rdesc, threshold=0.0, unit=1000.0, pp=None):
+    """load_dem_polygons_from_geotiff + process_polygons -> [n, 4, 2] int64 rectangles."""
+    d = np.ascontiguousarray(dem, dtype=np.float32)
+    pp = pp or polyproc()
+    cap = 4096
+    out = np.zeros((cap, 4, 2), np.int64)
+    n = lib().orc_dem_polygons(_ptr(d, _f32p), ctypes.byref(rdesc), ctypes.c_float(threshold),
+                               ctypes.c_double(unit), ctypes.byref(pp),
+                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                               ctypes.c_int64(cap))
+    assert n <= cap
+    return out[:n]
+
+
 def build():
     """Compile liboracle.so (gcc) if it is missing or older than its source."""
     src = os.path.join(HERE, "uam_oracle.c")
@@ -146,6 +180,7 @@ def lib():
                      "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d",
                      "orc_refine"):
             getattr(_lib, name).restype = ctypes.c_int
+        _lib.orc_dem_polygons.restype = ctypes.c_int64
     return _lib
 
 

@@ -26,6 +26,7 @@
  *
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math).
  */
+#include <float.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1151,4 +1152,343 @@ void orc_reproject(const orc_tm* t, const float* src, const orc_geo_grid* g,
             out[iy * dst->nx + ix] = val;
         }
     }
+}
+
+/* ======================================================================================
+ * Land polygons from the DEM: load_dem_polygons_from_geotiff
+ * (data_manager.py:11-19: mask, rasterio.features.shapes, 4-connectivity) followed by
+ * DataProcessor.process_polygons (data_processor.py:15-75).  cv2.minAreaRect + boxPoints are
+ * restated in float32 after OpenCV's convexHull / rotatingCalipers / RotatedRect::points;
+ * the restatement is pinned on the reference's populated_area output (tests). */
+typedef struct {
+    double min_area, large_area, min_approx_area;
+    int32_t divisions, pad;
+} orc_polyproc;
+
+typedef struct {
+    float x, y;
+} orc_p2f;
+
+static int p2f_cmp(const void* a, const void* b) {
+    const orc_p2f *p = (const orc_p2f*)a, *q = (const orc_p2f*)b;
+    if (p->x != q->x) return p->x < q->x ? -1 : 1;
+    if (p->y != q->y) return p->y < q->y ? -1 : 1;
+    return 0;
+}
+
+static double p2f_cross(orc_p2f o, orc_p2f a, orc_p2f b) {
+    return ((double)a.x - o.x) * ((double)b.y - o.y) - ((double)a.y - o.y) * ((double)b.x - o.x);
+}
+
+/* strictly convex hull, counter-clockwise, first vertex = largest (x, y); returns size */
+static int orc_hull(orc_p2f* p, int n, orc_p2f* h) {
+    qsort(p, n, sizeof(orc_p2f), p2f_cmp);
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if (m == 0 || p[i].x != p[m - 1].x || p[i].y != p[m - 1].y) p[m++] = p[i];
+    if (m < 3) {
+        for (int i = 0; i < m; ++i) h[i] = p[i];
+        return m;
+    }
+    int k = 0;
+    for (int i = 0; i < m; ++i) {
+        while (k >= 2 && p2f_cross(h[k - 2], h[k - 1], p[i]) <= 0) --k;
+        h[k++] = p[i];
+    }
+    for (int i = m - 2, t = k + 1; i >= 0; --i) {
+        while (k >= t && p2f_cross(h[k - 2], h[k - 1], p[i]) <= 0) --k;
+        h[k++] = p[i];
+    }
+    --k;
+    int top = 0;
+    for (int i = 1; i < k; ++i)
+        if (h[i].x > h[top].x || (h[i].x == h[top].x && h[i].y > h[top].y)) top = i;
+    orc_p2f* tmp = (orc_p2f*)malloc(sizeof(orc_p2f) * k);
+    for (int i = 0; i < k; ++i) tmp[i] = h[(top + i) % k];
+    for (int i = 0; i < k; ++i) h[i] = tmp[i];
+    free(tmp);
+    return k;
+}
+
+/* cv2.boxPoints(cv2.minAreaRect(pts)) -> np.intp; pts as doubles (cast to float32) */
+void orc_min_area_rect(const double* xy, int64_t n, int64_t* box) {
+    orc_p2f* p = (orc_p2f*)malloc(sizeof(orc_p2f) * (n > 0 ? n : 1));
+    orc_p2f* h = (orc_p2f*)malloc(sizeof(orc_p2f) * (2 * n + 2));
+    for (int64_t i = 0; i < n; ++i) p[i].x = (float)xy[2 * i], p[i].y = (float)xy[2 * i + 1];
+    const int m = n > 0 ? orc_hull(p, (int)n, h) : 0;
+    float cx, cy, w, hh, ang;
+    if (m > 2) {
+        float* vx = (float*)malloc(sizeof(float) * m);
+        float* vy = (float*)malloc(sizeof(float) * m);
+        float* iv = (float*)malloc(sizeof(float) * m);
+        int left = 0, bottom = 0, right = 0, top = 0;
+        float left_x = h[0].x, right_x = h[0].x, top_y = h[0].y, bottom_y = h[0].y;
+        orc_p2f pt0 = h[0];
+        for (int i = 0; i < m; ++i) {
+            if (pt0.x < left_x) left_x = pt0.x, left = i;
+            if (pt0.x > right_x) right_x = pt0.x, right = i;
+            if (pt0.y > top_y) top_y = pt0.y, top = i;
+            if (pt0.y < bottom_y) bottom_y = pt0.y, bottom = i;
+            orc_p2f pt = h[(i + 1) < m ? i + 1 : 0];
+            double dx = pt.x - pt0.x, dy = pt.y - pt0.y;
+            vx[i] = (float)dx, vy[i] = (float)dy;
+            iv[i] = (float)(1. / sqrt(dx * dx + dy * dy));
+            pt0 = pt;
+        }
+        float orientation = 0;
+        {
+            double ax = vx[m - 1], ay = vy[m - 1];
+            for (int i = 0; i < m; ++i) {
+                double bx = vx[i], by = vy[i], cv = ax * by - ay * bx;
+                if (cv != 0) {
+                    orientation = cv > 0 ? 1.f : -1.f;
+                    break;
+                }
+                ax = bx, ay = by;
+            }
+        }
+        float ba = orientation, bb = 0, minarea = FLT_MAX, sa = 0, sw = 0, sb = 0, sh = 0;
+        int seq[4] = {bottom, right, top, left}, sl = 0, sbot = 0;
+        for (int k = 0; k < m; ++k) {
+            float dp[4];
+            dp[0] = +ba * vx[seq[0]] + bb * vy[seq[0]];
+            dp[1] = -bb * vx[seq[1]] + ba * vy[seq[1]];
+            dp[2] = -ba * vx[seq[2]] - bb * vy[seq[2]];
+            dp[3] = +bb * vx[seq[3]] - ba * vy[seq[3]];
+            float maxcos = dp[0] * iv[seq[0]];
+            int me = 0;
+            for (int i = 1; i < 4; ++i) {
+                float ca = dp[i] * iv[seq[i]];
+                if (ca > maxcos) me = i, maxcos = ca;
+            }
+            const int pi = seq[me];
+            const float lx = vx[pi] * iv[pi], ly = vy[pi] * iv[pi];
+            if (me == 0) ba = lx, bb = ly;
+            else if (me == 1) ba = ly, bb = -lx;
+            else if (me == 2) ba = -lx, bb = -ly;
+            else ba = -ly, bb = lx;
+            seq[me] = (seq[me] + 1 == m) ? 0 : seq[me] + 1;
+            float dx = h[seq[1]].x - h[seq[3]].x, dy = h[seq[1]].y - h[seq[3]].y;
+            const float width = dx * ba + dy * bb;
+            dx = h[seq[2]].x - h[seq[0]].x, dy = h[seq[2]].y - h[seq[0]].y;
+            const float height = -dx * bb + dy * ba;
+            const float area = width * height;
+            if (area <= minarea) {
+                minarea = area, sl = seq[3], sa = ba, sw = width, sb = bb, sh = height;
+                sbot = seq[0];
+            }
+        }
+        const float A1 = sa, B1 = sb, A2 = -sb, B2 = sa;
+        const float C1 = A1 * h[sl].x + h[sl].y * B1, C2 = A2 * h[sbot].x + h[sbot].y * B2;
+        const float idet = 1.f / (A1 * B2 - A2 * B1);
+        const float px = (C1 * B2 - C2 * B1) * idet, py = (A1 * C2 - A2 * C1) * idet;
+        const float o1x = A1 * sw, o1y = B1 * sw, o2x = A2 * sh, o2y = B2 * sh;
+        cx = px + (o1x + o2x) * 0.5f;
+        cy = py + (o1y + o2y) * 0.5f;
+        w = (float)sqrt((double)o1x * o1x + (double)o1y * o1y);
+        hh = (float)sqrt((double)o2x * o2x + (double)o2y * o2y);
+        ang = (float)atan2((double)o1y, (double)o1x);
+        free(vx), free(vy), free(iv);
+    } else if (m == 2) {
+        cx = (h[0].x + h[1].x) * 0.5f, cy = (h[0].y + h[1].y) * 0.5f;
+        double dx = h[1].x - h[0].x, dy = h[1].y - h[0].y;
+        w = (float)sqrt(dx * dx + dy * dy), hh = 0;
+        ang = (float)atan2(dy, dx);
+    } else {
+        cx = m ? h[0].x : 0, cy = m ? h[0].y : 0, w = hh = 0, ang = 0;
+    }
+    ang = (float)(ang * 180 / M_PI);
+    const double a_ = ang * M_PI / 180.;
+    const float b = (float)cos(a_) * 0.5f, a = (float)sin(a_) * 0.5f;
+    float q[8];
+    q[0] = cx - a * hh - b * w;
+    q[1] = cy + b * hh - a * w;
+    q[2] = cx + a * hh - b * w;
+    q[3] = cy - b * hh - a * w;
+    q[4] = 2 * cx - q[0];
+    q[5] = 2 * cy - q[1];
+    q[6] = 2 * cx - q[2];
+    q[7] = 2 * cy - q[3];
+    for (int i = 0; i < 8; ++i) box[i] = (int64_t)q[i];
+    free(p), free(h);
+}
+
+static double box_area8(const int64_t* b) {
+    double s = 0.0;
+    for (int i = 0; i < 4; ++i) {
+        const int j = (i + 1) & 3;
+        s += (double)b[2 * i] * (double)b[2 * j + 1] - (double)b[2 * j] * (double)b[2 * i + 1];
+    }
+    return fabs(0.5 * s);
+}
+
+/* sequential union-find labelling, root = smallest index; cut arrays as uam_dem_polygons */
+static int32_t uf_find(int32_t* L, int32_t x) {
+    while (L[x] != x) {
+        L[x] = L[L[x]];
+        x = L[x];
+    }
+    return x;
+}
+
+static void label4(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* rowbox,
+                   int32_t* L) {
+    for (int32_t y = 0; y < ny; ++y)
+        for (int32_t x = 0; x < nx; ++x) {
+            const int64_t i = (int64_t)y * nx + x;
+            if (L[i] < 0) continue;
+            if (x + 1 < nx && L[i + 1] >= 0 && (!colbox || colbox[x] == colbox[x + 1])) {
+                int32_t a = uf_find(L, (int32_t)i), b = uf_find(L, (int32_t)(i + 1));
+                if (a != b) L[a > b ? a : b] = a < b ? a : b;
+            }
+            if (y + 1 < ny && L[i + nx] >= 0 && (!rowbox || rowbox[y] == rowbox[y + 1])) {
+                int32_t a = uf_find(L, (int32_t)i), b = uf_find(L, (int32_t)(i + nx));
+                if (a != b) L[a > b ? a : b] = a < b ? a : b;
+            }
+        }
+    for (int64_t i = 0; i < (int64_t)nx * ny; ++i)
+        if (L[i] >= 0) L[i] = uf_find(L, (int32_t)i);
+}
+
+typedef struct {
+    int32_t n, cnt, x0, y0, x1, y1, root;
+} orc_comp;
+
+/* components of a labelled grid in raster order of their roots, with per-row extents */
+static orc_comp* comps_of(int32_t nx, int32_t ny, const int32_t* L, int32_t* ncomp,
+                          int32_t** rxmin, int32_t** rxmax, int64_t** roff) {
+    const int64_t n = (int64_t)nx * ny;
+    int32_t* id = (int32_t*)malloc(sizeof(int32_t) * (n > 0 ? n : 1));
+    int32_t nc = 0;
+    for (int64_t i = 0; i < n; ++i) id[i] = (L[i] == (int32_t)i) ? nc++ : -1;
+    orc_comp* c = (orc_comp*)calloc(nc > 0 ? nc : 1, sizeof(orc_comp));
+    for (int32_t k = 0; k < nc; ++k) c[k].x0 = c[k].y0 = INT32_MAX, c[k].x1 = c[k].y1 = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        if (L[i] < 0) continue;
+        orc_comp* q = &c[id[L[i]]];
+        const int32_t y = (int32_t)(i / nx), x = (int32_t)(i % nx);
+        q->cnt++;
+        if (x < q->x0) q->x0 = x;
+        if (x > q->x1) q->x1 = x;
+        if (y < q->y0) q->y0 = y;
+        if (y > q->y1) q->y1 = y;
+        q->root = L[i];
+    }
+    int64_t rows = 0;
+    *roff = (int64_t*)malloc(sizeof(int64_t) * (nc > 0 ? nc : 1));
+    for (int32_t k = 0; k < nc; ++k) (*roff)[k] = rows, rows += c[k].y1 - c[k].y0 + 1;
+    *rxmin = (int32_t*)malloc(sizeof(int32_t) * (rows > 0 ? rows : 1));
+    *rxmax = (int32_t*)malloc(sizeof(int32_t) * (rows > 0 ? rows : 1));
+    for (int64_t r = 0; r < rows; ++r) (*rxmin)[r] = INT32_MAX, (*rxmax)[r] = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        if (L[i] < 0) continue;
+        const int32_t k = id[L[i]], y = (int32_t)(i / nx), x = (int32_t)(i % nx);
+        const int64_t s = (*roff)[k] + (y - c[k].y0);
+        if (x < (*rxmin)[s]) (*rxmin)[s] = x;
+        if (x > (*rxmax)[s]) (*rxmax)[s] = x;
+    }
+    free(id);
+    *ncomp = nc;
+    return c;
+}
+
+static int64_t emit_region(const orc_comp* q, const int32_t* mn, const int32_t* mx,
+                           const double* xlo, const double* xhi, const double* ylo,
+                           const double* yhi, double min_approx, int64_t* out, int64_t nout,
+                           int64_t cap) {
+    const int32_t rows = q->y1 - q->y0 + 1;
+    double* pts = (double*)malloc(sizeof(double) * 8 * rows);
+    int64_t np = 0;
+    for (int32_t r = 0; r < rows; ++r) {
+        if (mn[r] > mx[r]) continue;
+        const int32_t row = q->y0 + r;
+        const double xs[2] = {xlo[mn[r]], xhi[mx[r]]};
+        for (int e = 0; e < 2; ++e) {
+            pts[2 * np] = xs[e], pts[2 * np + 1] = yhi[row], ++np;
+            pts[2 * np] = xs[e], pts[2 * np + 1] = ylo[row], ++np;
+        }
+    }
+    int64_t box[8];
+    orc_min_area_rect(pts, np, box);
+    free(pts);
+    if (np == 0 || !(box_area8(box) > min_approx)) return nout;
+    if (nout < cap)
+        for (int i = 0; i < 8; ++i) out[8 * nout + i] = box[i];
+    return nout + 1;
+}
+
+/* -> number of rectangles (rects written up to cap) */
+int64_t orc_dem_polygons(const float* dem, const orc_raster* rd, float thr, double unit,
+                         const orc_polyproc* pp, int64_t* rects, int64_t cap) {
+    const int32_t nx = rd->nx, ny = rd->ny;
+    const int64_t n = (int64_t)nx * ny;
+    const double X0 = rd->x0 * unit, DX = rd->dx * unit, Y0 = rd->y_top * unit, DY = rd->dy * unit;
+    int32_t* L = (int32_t*)malloc(sizeof(int32_t) * n);
+    for (int64_t i = 0; i < n; ++i) {
+        const float v = dem[i];
+        const int m = (thr == -9999.0f) ? (v == -9999.0f) : (v > thr);
+        L[i] = m ? (int32_t)i : -1;
+    }
+    label4(nx, ny, NULL, NULL, L);
+    int32_t nc, *mn, *mx;
+    int64_t* roff;
+    orc_comp* c = comps_of(nx, ny, L, &nc, &mn, &mx, &roff);
+    double *xlo = (double*)malloc(sizeof(double) * nx), *xhi = (double*)malloc(sizeof(double) * nx);
+    double *ylo = (double*)malloc(sizeof(double) * ny), *yhi = (double*)malloc(sizeof(double) * ny);
+    for (int32_t i = 0; i < nx; ++i) xlo[i] = X0 + i * DX, xhi[i] = X0 + (i + 1) * DX;
+    for (int32_t j = 0; j < ny; ++j) yhi[j] = Y0 - j * DY, ylo[j] = Y0 - (j + 1) * DY;
+    const double cell = fabs(DX * DY);
+    const int D = pp->divisions;
+    int64_t nout = 0;
+    for (int32_t k = 0; k < nc; ++k) {
+        const double area = c[k].cnt * cell;
+        if (!(area > pp->min_area)) continue;
+        if (!(area > pp->large_area)) {
+            nout = emit_region(&c[k], mn + roff[k], mx + roff[k], xlo, xhi, ylo, yhi,
+                               pp->min_approx_area, rects, nout, cap);
+            continue;
+        }
+        const double minx = X0 + c[k].x0 * DX, maxx = X0 + (c[k].x1 + 1) * DX;
+        const double maxy = Y0 - c[k].y0 * DY, miny = Y0 - (c[k].y1 + 1) * DY;
+        const double ddx = (maxx - minx) / D, ddy = (maxy - miny) / D;
+        const int32_t W0 = c[k].x1 - c[k].x0 + 1, H0 = c[k].y1 - c[k].y0 + 1;
+        int32_t *co = (int32_t*)malloc(sizeof(int32_t) * W0 * D),
+                *cb = (int32_t*)malloc(sizeof(int32_t) * W0 * D);
+        int32_t *ro = (int32_t*)malloc(sizeof(int32_t) * H0 * D),
+                *rb = (int32_t*)malloc(sizeof(int32_t) * H0 * D);
+        double *sxl = (double*)malloc(sizeof(double) * W0 * D), *sxh = (double*)malloc(sizeof(double) * W0 * D);
+        double *syl = (double*)malloc(sizeof(double) * H0 * D), *syh = (double*)malloc(sizeof(double) * H0 * D);
+        int32_t ws = 0, hs = 0;
+        for (int32_t col = c[k].x0; col <= c[k].x1; ++col)
+            for (int j = 0; j < D; ++j) {
+                const double lo = fmax(xlo[col], minx + j * ddx), hi = fmin(xhi[col], minx + (j + 1) * ddx);
+                if (hi > lo) co[ws] = col, cb[ws] = j, sxl[ws] = lo, sxh[ws] = hi, ++ws;
+            }
+        for (int32_t row = c[k].y0; row <= c[k].y1; ++row)
+            for (int kk = D - 1; kk >= 0; --kk) {
+                const double lo = fmax(ylo[row], miny + kk * ddy), hi = fmin(yhi[row], miny + (kk + 1) * ddy);
+                if (hi > lo) ro[hs] = row, rb[hs] = kk, syl[hs] = lo, syh[hs] = hi, ++hs;
+            }
+        int32_t* L2 = (int32_t*)malloc(sizeof(int32_t) * ws * hs);
+        for (int32_t t = 0; t < hs; ++t)
+            for (int32_t s2 = 0; s2 < ws; ++s2) {
+                const int64_t i = (int64_t)t * ws + s2;
+                L2[i] = (L[(int64_t)ro[t] * nx + co[s2]] == c[k].root) ? (int32_t)i : -1;
+            }
+        label4(ws, hs, cb, rb, L2);
+        int32_t np2, *pmn, *pmx;
+        int64_t* poff;
+        orc_comp* pc = comps_of(ws, hs, L2, &np2, &pmn, &pmx, &poff);
+        /* boxes j outer, k inner; within a box, raster order of the piece's first cell */
+        for (int j = 0; j < D; ++j)
+            for (int kk = 0; kk < D; ++kk)
+                for (int32_t q = 0; q < np2; ++q)
+                    if (cb[pc[q].x0] == j && rb[pc[q].y0] == kk)
+                        nout = emit_region(&pc[q], pmn + poff[q], pmx + poff[q], sxl, sxh, syl,
+                                           syh, pp->min_approx_area, rects, nout, cap);
+        free(pc), free(pmn), free(pmx), free(poff), free(L2);
+        free(co), free(cb), free(ro), free(rb), free(sxl), free(sxh), free(syl), free(syh);
+    }
+    free(c), free(mn), free(mx), free(roff), free(L), free(xlo), free(xhi), free(ylo), free(yhi);
+    return nout;
 }

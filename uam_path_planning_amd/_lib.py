@@ -128,6 +128,9 @@ SIGNATURES = {
     "uam_process_polygons": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, _vp,
                                             ctypes.POINTER(PolyprocParams), _vp, ctypes.c_int32,
                                             ctypes.POINTER(ctypes.c_int32)]),
+    "uam_dem_polygons": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(RasterDesc), ctypes.c_float,
+                                        ctypes.c_double, ctypes.POINTER(PolyprocParams), _vp,
+                                        ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), _vp]),
     "uam_refine_workspace_bytes": (ctypes.c_int64, [_vp, ctypes.c_int64,
                                                     ctypes.POINTER(RefineParams)]),
     "uam_refine": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(RefineParams), _vp,

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/uampath.h"
+#include "polyproc.h"
 
 #define UAM_TUNING_MAX 10
 #define UAM_TUNING_WAVE 9       // force the wave-per-path kernel (K2w)
@@ -1591,6 +1592,206 @@ __global__ __launch_bounds__(256) void k_reproject(KTm k, KGeoGrid g, KRaster r,
     dst[i] = val;
 }
 
+// ----------------------------------------------------------------------------------------
+// K8: DEM polygonisation: the connected regions rasterio.features.shapes
+// returns for the DEM mask (data_manager.py:11-19, 4-connectivity), as union-find labels.
+// L[i] = smallest linear index of i's component (the root), -1 off the mask.  Merging hooks
+// the larger root under the smaller with atomicMin (L[x] <= x always holds, so every find
+// terminates); labels are flattened afterwards.  A labelling grid may carry "cuts": cells s and
+// s+1 of a row (t and t+1 of a column) connect only when colbox[s] == colbox[s+1]
+// (rowbox[t] == rowbox[t+1]) -- the split of a large polygon into its box pieces
+// (data_processor.py:34-51) as labelling on a grid refined at the box edges.
+__device__ __forceinline__ int32_t ccl_find(const int32_t* L, int32_t x) {
+    while (true) {
+        const int32_t p = __hip_atomic_load(&L[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p == x) return x;
+        x = p;
+    }
+}
+
+__device__ __forceinline__ void ccl_union(int32_t* L, int32_t a, int32_t b) {
+    while (true) {
+        a = ccl_find(L, a);
+        b = ccl_find(L, b);
+        if (a == b) return;
+        if (a > b) {
+            const int32_t t = a;
+            a = b;
+            b = t;
+        }
+        const int32_t old = atomicMin(&L[b], a);
+        if (old == b) return;  // b was a root: now under a
+        b = old;               // somebody re-hooked b meanwhile: retry from its new parent
+    }
+}
+
+// mask of data_manager.py:14-17: dem == -9999 when threshold == -9999, else dem > threshold
+__global__ __launch_bounds__(256) void k_ccl_init_dem(const float* __restrict__ dem, int64_t n,
+                                                      float thr, int32_t* __restrict__ L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = dem[i];
+    const bool m = (thr == -9999.0f) ? (v == -9999.0f) : (v > thr);
+    L[i] = m ? (int32_t)i : -1;
+}
+
+// refined sub-grid of one component: cell (s, t) <-> source pixel (col_of[s], row_of[t])
+__global__ __launch_bounds__(256) void k_ccl_init_sub(const int32_t* __restrict__ Lsrc,
+                                                      int32_t src_nx, int32_t root,
+                                                      const int32_t* __restrict__ col_of,
+                                                      const int32_t* __restrict__ row_of,
+                                                      int32_t ws, int32_t hs,
+                                                      int32_t* __restrict__ L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)ws * hs) return;
+    const int32_t t = (int32_t)(i / ws), s = (int32_t)(i - (int64_t)t * ws);
+    const int64_t src = (int64_t)row_of[t] * src_nx + col_of[s];
+    L[i] = (Lsrc[src] == root) ? (int32_t)i : -1;
+}
+
+__global__ __launch_bounds__(256) void k_ccl_merge(int32_t nx, int32_t ny,
+                                                   const int32_t* __restrict__ colbox,
+                                                   const int32_t* __restrict__ rowbox,
+                                                   int32_t* __restrict__ L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nx * ny) return;
+    if (L[i] < 0) return;
+    const int32_t y = (int32_t)(i / nx), x = (int32_t)(i - (int64_t)y * nx);
+    if (x + 1 < nx && L[i + 1] >= 0 && (!colbox || colbox[x] == colbox[x + 1]))
+        ccl_union(L, (int32_t)i, (int32_t)(i + 1));
+    if (y + 1 < ny && L[i + nx] >= 0 && (!rowbox || rowbox[y] == rowbox[y + 1]))
+        ccl_union(L, (int32_t)i, (int32_t)(i + nx));
+}
+
+__global__ __launch_bounds__(256) void k_ccl_flatten(int64_t n, int32_t* __restrict__ L) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || L[i] < 0) return;
+    L[i] = ccl_find(L, (int32_t)i);
+}
+
+constexpr int CCL_ITEMS = 16;  // cells per thread in the root scan (block = 256 x 16 cells)
+
+__global__ __launch_bounds__(256) void k_ccl_count_roots(const int32_t* __restrict__ L,
+                                                         int64_t n, int32_t* __restrict__ cnt) {
+    const int64_t base = (int64_t)blockIdx.x * 256 * CCL_ITEMS;
+    int c = 0;
+    for (int it = 0; it < CCL_ITEMS; ++it) {
+        const int64_t i = base + (int64_t)it * 256 + threadIdx.x;
+        if (i < n && L[i] == (int32_t)i) ++c;
+    }
+    c = wave_isum(c);
+    __shared__ int part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// component id of every root = rank of the root in raster order (deterministic)
+__global__ __launch_bounds__(256) void k_ccl_assign(const int32_t* __restrict__ L, int64_t n,
+                                                    const int32_t* __restrict__ off,
+                                                    int32_t* __restrict__ cid) {
+    const int64_t base = (int64_t)blockIdx.x * 256 * CCL_ITEMS;
+    __shared__ int wsum[4];
+    int running = off[blockIdx.x];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int it = 0; it < CCL_ITEMS; ++it) {
+        const int64_t i = base + (int64_t)it * 256 + threadIdx.x;
+        const bool r = i < n && L[i] == (int32_t)i;
+        const uint64_t bal = __ballot(r);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wv] = __popcll(bal);
+        __syncthreads();
+        int woff = 0;
+        for (int k = 0; k < wv; ++k) woff += wsum[k];
+        if (r) cid[i] = running + woff + before;
+        running += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
+// per component: cell count and bounding box (wave-aggregated when a wave's cells share one)
+__global__ __launch_bounds__(256) void k_ccl_stats(const int32_t* __restrict__ L,
+                                                   const int32_t* __restrict__ cid, int32_t nx,
+                                                   int64_t n, int32_t* __restrict__ cnt,
+                                                   int32_t* __restrict__ bx0,
+                                                   int32_t* __restrict__ by0,
+                                                   int32_t* __restrict__ bx1,
+                                                   int32_t* __restrict__ by1,
+                                                   int32_t* __restrict__ croot) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < n && L[i] >= 0;
+    const int32_t c = in ? cid[L[i]] : -1;
+    if (in && L[i] == (int32_t)i) croot[c] = (int32_t)i;
+    const int32_t y = in ? (int32_t)(i / nx) : 0, x = in ? (int32_t)(i - (int64_t)y * nx) : 0;
+    const int32_t c0 = __shfl(c, 0, 64);
+    if (__ballot(c != c0) == 0) {  // wave-uniform component (or all background)
+        if (c0 < 0) return;
+        const int k = wave_isum(1);
+        int xmn = x, xmx = x, ymn = y, ymx = y;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            xmn = min(xmn, __shfl_xor(xmn, o, 64));
+            xmx = max(xmx, __shfl_xor(xmx, o, 64));
+            ymn = min(ymn, __shfl_xor(ymn, o, 64));
+            ymx = max(ymx, __shfl_xor(ymx, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&cnt[c0], k);
+            atomicMin(&bx0[c0], xmn);
+            atomicMax(&bx1[c0], xmx);
+            atomicMin(&by0[c0], ymn);
+            atomicMax(&by1[c0], ymx);
+        }
+        return;
+    }
+    if (c < 0) return;
+    atomicAdd(&cnt[c], 1);
+    atomicMin(&bx0[c], x);
+    atomicMax(&bx1[c], x);
+    atomicMin(&by0[c], y);
+    atomicMax(&by1[c], y);
+}
+
+// per kept component and row: leftmost / rightmost cell (hull input)
+__global__ __launch_bounds__(256) void k_ccl_extents(const int32_t* __restrict__ L,
+                                                     const int32_t* __restrict__ cid,
+                                                     int32_t nx, int64_t n,
+                                                     const int64_t* __restrict__ row_off,
+                                                     const int32_t* __restrict__ by0,
+                                                     int32_t* __restrict__ xmin,
+                                                     int32_t* __restrict__ xmax) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < n && L[i] >= 0;
+    const int32_t c = in ? cid[L[i]] : -1;
+    const int64_t ro = c >= 0 ? row_off[c] : -1;
+    const int32_t y = in ? (int32_t)(i / nx) : 0, x = in ? (int32_t)(i - (int64_t)y * nx) : 0;
+    const int64_t slot = ro >= 0 ? ro + (y - by0[c]) : -1;
+    const int64_t s0 = __shfl(slot, 0, 64);
+    if (__ballot(slot != s0) == 0) {
+        if (s0 < 0) return;
+        int xmn = x, xmx = x;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            xmn = min(xmn, __shfl_xor(xmn, o, 64));
+            xmx = max(xmx, __shfl_xor(xmx, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&xmin[s0], xmn);
+            atomicMax(&xmax[s0], xmx);
+        }
+        return;
+    }
+    if (slot < 0) return;
+    atomicMin(&xmin[slot], x);
+    atomicMax(&xmax[slot], x);
+}
+
+__global__ __launch_bounds__(256) void k_fill_i32(int32_t* __restrict__ p, int64_t n,
+                                                  int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -2431,6 +2632,272 @@ int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* t, const float* src,
     hipLaunchKernelGGL(k_reproject, dim3(grid_for(cells, 256, INT32_MAX)), dim3(256), 0,
                        (hipStream_t)stream, k, g, kr, unit_m, resample, src, out);
     HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+// ---- DEM polygons (K8) -------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    int64_t n = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(int64_t count) {
+        n = count;
+        return hipMalloc(&p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
+    }
+};
+
+#define HIP_TRY2(expr)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(UAM_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+    } while (0)
+
+struct CompStats {
+    std::vector<int32_t> cnt, x0, y0, x1, y1, root;
+};
+
+// label a grid (optionally with cuts) and return per-component stats; L is initialised
+int label_grid(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* rowbox,
+               int32_t* L, DevBuf<int32_t>& cid, CompStats& st, hipStream_t s) {
+    const int64_t n = (int64_t)nx * ny;
+    const dim3 g(grid_for(n, 256, INT32_MAX)), b(256);
+    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, nx, ny, colbox, rowbox, L);
+    hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, n, L);
+    const int64_t nblk = (n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
+    DevBuf<int32_t> cnt, off;
+    HIP_TRY2(cnt.alloc(nblk));
+    HIP_TRY2(off.alloc(nblk));
+    hipLaunchKernelGGL(k_ccl_count_roots, dim3((unsigned)nblk), b, 0, s, L, n, cnt.p);
+    std::vector<int32_t> h(nblk);
+    HIP_TRY2(hipMemcpyAsync(h.data(), cnt.p, nblk * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY2(hipStreamSynchronize(s));
+    int64_t acc = 0;
+    for (int64_t i = 0; i < nblk; ++i) {
+        const int32_t c = h[i];
+        h[i] = (int32_t)acc;
+        acc += c;
+    }
+    const int32_t ncomp = (int32_t)acc;
+    HIP_TRY2(hipMemcpyAsync(off.p, h.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY2(cid.alloc(n));
+    hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)nblk), b, 0, s, L, n, off.p, cid.p);
+    DevBuf<int32_t> a;
+    HIP_TRY2(a.alloc(6 * (int64_t)std::max(ncomp, 1)));
+    const dim3 gc(grid_for(std::max(ncomp, 1), 256, INT32_MAX));
+    int32_t* cntp = a.p;
+    int32_t *bx0 = a.p + ncomp, *by0 = a.p + 2 * (int64_t)ncomp, *bx1 = a.p + 3 * (int64_t)ncomp,
+            *by1 = a.p + 4 * (int64_t)ncomp, *rt = a.p + 5 * (int64_t)ncomp;
+    if (ncomp > 0) {
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, cntp, (int64_t)ncomp, 0);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, bx0, (int64_t)ncomp, INT32_MAX);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by0, (int64_t)ncomp, INT32_MAX);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, bx1, (int64_t)ncomp, -1);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by1, (int64_t)ncomp, -1);
+        hipLaunchKernelGGL(k_ccl_stats, g, b, 0, s, L, cid.p, nx, n, cntp, bx0, by0, bx1, by1,
+                           rt);
+    }
+    HIP_TRY2(hipGetLastError());
+    std::vector<int32_t> all(6 * (int64_t)ncomp);
+    if (ncomp > 0)
+        HIP_TRY2(hipMemcpyAsync(all.data(), a.p, all.size() * sizeof(int32_t),
+                                hipMemcpyDeviceToHost, s));
+    HIP_TRY2(hipStreamSynchronize(s));
+    auto col = [&](int k) {
+        return std::vector<int32_t>(all.begin() + (int64_t)k * ncomp,
+                                    all.begin() + (int64_t)(k + 1) * ncomp);
+    };
+    st.cnt = col(0), st.x0 = col(1), st.y0 = col(2), st.x1 = col(3), st.y1 = col(4);
+    st.root = col(5);
+    return UAM_OK;
+}
+
+// per-row [xmin, xmax] of the selected components (sel[c] true), row tables concatenated
+int row_extents(int32_t nx, int32_t ny, const int32_t* L, const int32_t* cid,
+                const CompStats& st, const std::vector<char>& sel, std::vector<int64_t>& off,
+                std::vector<int32_t>& xmin, std::vector<int32_t>& xmax, hipStream_t s) {
+    const int32_t ncomp = (int32_t)st.cnt.size();
+    off.assign(ncomp, -1);
+    int64_t rows = 0;
+    for (int32_t c = 0; c < ncomp; ++c)
+        if (sel[c]) {
+            off[c] = rows;
+            rows += st.y1[c] - st.y0[c] + 1;
+        }
+    xmin.assign(rows, INT32_MAX);
+    xmax.assign(rows, -1);
+    if (rows == 0) return UAM_OK;
+    DevBuf<int64_t> doff;
+    DevBuf<int32_t> dy0, dmn, dmx;
+    HIP_TRY2(doff.alloc(ncomp));
+    HIP_TRY2(dy0.alloc(ncomp));
+    HIP_TRY2(dmn.alloc(rows));
+    HIP_TRY2(dmx.alloc(rows));
+    HIP_TRY2(hipMemcpyAsync(doff.p, off.data(), ncomp * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY2(hipMemcpyAsync(dy0.p, st.y0.data(), ncomp * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY2(hipMemcpyAsync(dmn.p, xmin.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY2(hipMemcpyAsync(dmx.p, xmax.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const int64_t n = (int64_t)nx * ny;
+    hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, L, cid,
+                       nx, n, doff.p, dy0.p, dmn.p, dmx.p);
+    HIP_TRY2(hipGetLastError());
+    HIP_TRY2(hipMemcpyAsync(xmin.data(), dmn.p, rows * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY2(hipMemcpyAsync(xmax.data(), dmx.p, rows * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY2(hipStreamSynchronize(s));
+    return UAM_OK;
+}
+
+// hull input of one labelled region: the four corners of each row's [xmin, xmax] run;
+// column c spans [xlo[c], xhi[c]], row r spans [ylo[r], yhi[r]]
+void region_corners(int32_t ry0, int32_t ry1, const int32_t* xmin, const int32_t* xmax,
+                    const std::vector<double>& xlo, const std::vector<double>& xhi,
+                    const std::vector<double>& ylo, const std::vector<double>& yhi,
+                    std::vector<uampoly::Pt>& pts) {
+    pts.clear();
+    for (int32_t r = ry0; r <= ry1; ++r) {
+        const int32_t a = xmin[r - ry0], b = xmax[r - ry0];
+        if (a > b) continue;
+        pts.push_back({xlo[a], yhi[r]});
+        pts.push_back({xlo[a], ylo[r]});
+        pts.push_back({xhi[b], yhi[r]});
+        pts.push_back({xhi[b], ylo[r]});
+    }
+}
+
+void emit_rect(const std::vector<uampoly::Pt>& pts, double min_approx,
+               std::vector<int64_t>& out) {
+    int64_t box[8];
+    if (!uampoly::min_area_rect_box(pts, box)) return;
+    if (!(uampoly::box_area(box) > min_approx)) return;
+    out.insert(out.end(), box, box + 8);
+}
+
+}  // namespace
+
+extern "C" {
+
+int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, float threshold,
+                     double unit_m, const uam_polyproc_params* prm, int64_t* rect_xy,
+                     int32_t max_rects, int32_t* n_rects, uam_stream stream) {
+    if (!ctx || !dem || !rd || !prm || !n_rects) return fail(UAM_E_INVALID, "NULL argument");
+    if (rd->nx <= 0 || rd->ny <= 0) return fail(UAM_E_INVALID, "raster size %dx%d", rd->nx, rd->ny);
+    if (!(unit_m > 0.0) || prm->divisions < 1) return fail(UAM_E_INVALID, "bad unit / divisions");
+    const int32_t nx = rd->nx, ny = rd->ny;
+    const int64_t n = (int64_t)nx * ny;
+    if (n >= INT32_MAX) return fail(UAM_E_INVALID, "raster too large for int32 labels");
+    // plane metres of pixel corners, as an affine geotransform in metres gives them
+    const double X0 = rd->x0 * unit_m, DX = rd->dx * unit_m, Y0 = rd->y_top * unit_m,
+                 DY = rd->dy * unit_m;
+    DeviceGuard dg(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    DevBuf<int32_t> L, cid;
+    HIP_TRY2(L.alloc(n));
+    hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, dem,
+                       n, threshold, L.p);
+    CompStats st;
+    int rc = label_grid(nx, ny, nullptr, nullptr, L.p, cid, st, s);
+    if (rc) return rc;
+    const int32_t ncomp = (int32_t)st.cnt.size();
+    const double cell = std::fabs(DX * DY);
+    std::vector<char> small(ncomp, 0), large(ncomp, 0);
+    for (int32_t c = 0; c < ncomp; ++c) {
+        const double area = st.cnt[c] * cell;
+        if (!(area > prm->min_area)) continue;
+        (area > prm->large_area ? large : small)[c] = 1;
+    }
+    std::vector<int64_t> off;
+    std::vector<int32_t> xmin, xmax;
+    rc = row_extents(nx, ny, L.p, cid.p, st, small, off, xmin, xmax, s);
+    if (rc) return rc;
+    std::vector<double> xlo(nx), xhi(nx), ylo(ny), yhi(ny);
+    for (int32_t i = 0; i < nx; ++i) xlo[i] = X0 + i * DX, xhi[i] = X0 + (i + 1) * DX;
+    for (int32_t j = 0; j < ny; ++j) yhi[j] = Y0 - j * DY, ylo[j] = Y0 - (j + 1) * DY;
+    std::vector<int64_t> out;
+    std::vector<uampoly::Pt> pts;
+    const int D = prm->divisions;
+    for (int32_t c = 0; c < ncomp; ++c) {
+        if (small[c]) {
+            region_corners(st.y0[c], st.y1[c], &xmin[off[c]], &xmax[off[c]], xlo, xhi, ylo, yhi,
+                           pts);
+            emit_rect(pts, prm->min_approx_area, out);
+            continue;
+        }
+        if (!large[c]) continue;
+        // data_processor.py:34-51: D x D boxes over polygon.bounds; a piece = connected part
+        // of polygon n box = component of the grid refined at the box edges, cut there
+        const double minx = X0 + st.x0[c] * DX, maxx = X0 + (st.x1[c] + 1) * DX;
+        const double maxy = Y0 - st.y0[c] * DY, miny = Y0 - (st.y1[c] + 1) * DY;
+        const double ddx = (maxx - minx) / D, ddy = (maxy - miny) / D;
+        std::vector<int32_t> col_of, colbox, row_of, rowbox;
+        std::vector<double> sxlo, sxhi, sylo, syhi;
+        for (int32_t col = st.x0[c]; col <= st.x1[c]; ++col)
+            for (int j = 0; j < D; ++j) {
+                const double lo = std::max(xlo[col], minx + j * ddx);
+                const double hi = std::min(xhi[col], minx + (j + 1) * ddx);
+                if (hi > lo) {
+                    col_of.push_back(col), colbox.push_back(j);
+                    sxlo.push_back(lo), sxhi.push_back(hi);
+                }
+            }
+        for (int32_t row = st.y0[c]; row <= st.y1[c]; ++row)
+            for (int k = D - 1; k >= 0; --k) {
+                const double lo = std::max(ylo[row], miny + k * ddy);
+                const double hi = std::min(yhi[row], miny + (k + 1) * ddy);
+                if (hi > lo) {
+                    row_of.push_back(row), rowbox.push_back(k);
+                    sylo.push_back(lo), syhi.push_back(hi);
+                }
+            }
+        const int32_t ws = (int32_t)col_of.size(), hs = (int32_t)row_of.size();
+        const int64_t sn = (int64_t)ws * hs;
+        DevBuf<int32_t> dco, dcb, dro, drb, L2, cid2;
+        HIP_TRY2(dco.alloc(ws));
+        HIP_TRY2(dcb.alloc(ws));
+        HIP_TRY2(dro.alloc(hs));
+        HIP_TRY2(drb.alloc(hs));
+        HIP_TRY2(L2.alloc(sn));
+        HIP_TRY2(hipMemcpyAsync(dco.p, col_of.data(), ws * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(dcb.p, colbox.data(), ws * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(dro.p, row_of.data(), hs * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(drb.p, rowbox.data(), hs * 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0, s,
+                           L.p, nx, st.root[c], dco.p, dro.p, ws, hs, L2.p);
+        CompStats ps;
+        rc = label_grid(ws, hs, dcb.p, drb.p, L2.p, cid2, ps, s);
+        if (rc) return rc;
+        const int32_t np = (int32_t)ps.cnt.size();
+        std::vector<char> all(np, 1);
+        std::vector<int64_t> poff;
+        std::vector<int32_t> pmn, pmx;
+        rc = row_extents(ws, hs, L2.p, cid2.p, ps, all, poff, pmn, pmx, s);
+        if (rc) return rc;
+        // reference order: boxes j (x) outer, k (y) inner
+        std::vector<int32_t> order(np);
+        for (int32_t i = 0; i < np; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+            const int ja = colbox[ps.x0[a]], jb = colbox[ps.x0[b]];
+            if (ja != jb) return ja < jb;
+            return rowbox[ps.y0[a]] < rowbox[ps.y0[b]];
+        });
+        for (int32_t i : order) {
+            region_corners(ps.y0[i], ps.y1[i], &pmn[poff[i]], &pmx[poff[i]], sxlo, sxhi, sylo,
+                           syhi, pts);
+            emit_rect(pts, prm->min_approx_area, out);
+        }
+    }
+    const int64_t nr = (int64_t)out.size() / 8;
+    *n_rects = (int32_t)nr;
+    if (rect_xy)
+        for (int64_t i = 0; i < std::min<int64_t>(nr, max_rects) * 8; ++i) rect_xy[i] = out[i];
+    if (nr > max_rects)
+        return fail(UAM_E_INVALID, "%lld rectangles > max_rects %d", (long long)nr, max_rects);
     return UAM_OK;
 }
 

@@ -431,6 +431,31 @@ class Engine:
             self.stream), "uam_reproject_dem")
         return out
 
+    # -- land polygons from the DEM (K8) -------------------------------
+    def dem_polygons(self, dem, geo, threshold=0.0, unit_m=1000.0, params=None):
+        """DEM mask -> 4-connected regions (GPU labelling) -> DataProcessor approximation.
+        dem [ny, nx] float32 on RasterGeo geo (units of unit_m metres).  -> list of int64
+        [4, 2] rectangles in metres (cv2.boxPoints order)."""
+        torch = _torch()
+        d = self.tensor(dem, torch.float32).contiguous()
+        if tuple(d.shape) != (geo.ny, geo.nx):
+            raise ValueError(f"dem must be [{geo.ny}, {geo.nx}]")
+        prm = params if params is not None else _lib.PolyprocParams(750000.0, 32000000.0,
+                                                                    780000.0, 5, 0)
+        n = ctypes.c_int32(0)
+        cap = 256
+        while True:
+            out = np.zeros((cap, 4, 2), np.int64)
+            st = self.lib.uam_dem_polygons(self._ctx, _ptr(d), ctypes.byref(geo.as_struct()),
+                                           float(threshold), float(unit_m), ctypes.byref(prm),
+                                           out.ctypes.data, cap, ctypes.byref(n), self.stream)
+            if st == _lib.UAM_OK:
+                return [out[i] for i in range(n.value)]
+            if n.value > cap:
+                cap = n.value
+                continue
+            _lib.check(st, "uam_dem_polygons")
+
     def synchronize(self):
         _lib.check(self.lib.uam_synchronize(self._ctx, self.stream), "uam_synchronize")
 

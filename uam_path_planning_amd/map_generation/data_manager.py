@@ -31,6 +31,17 @@ def geo_from_geotransform(width, height, gt, nodata=-9999.0, dem_threshold=0.0):
                      dem_threshold=float(dem_threshold))
 
 
+class DemRegions:
+    """The DEM mask regions of load_dem_polygons_from_geotiff, kept on the device: the
+    4-connected regions of (dem == -9999 if threshold == -9999 else dem > threshold)
+    (data_manager.py:11-19).  DataProcessor.process_polygons labels and approximates them on
+    the GPU (uam_dem_polygons)."""
+
+    def __init__(self, engine, dem, geo, threshold, unit_m=1000.0):
+        self.engine, self.dem, self.geo = engine, dem, geo
+        self.threshold, self.unit_m = float(threshold), float(unit_m)
+
+
 class DataManager:
     def __init__(self, engine=None):
         self._engine = engine
@@ -91,6 +102,40 @@ class DataManager:
         eng.set_params(params)
         return eng.raster_build(geo, dem)
 
+    def load_polygons_from_shapefile(self, input_file, src_epsg=4612, dst_epsg=2443):
+        """data_manager.py:21-27: polygons of a shapefile in EPSG:4612 -> EPSG:2443 metres
+        (GPU transform, K7).  -> list of (shell [n, 2], [holes]) with the ESRI ring roles
+        (clockwise = shell, counter-clockwise = hole)."""
+        import numpy as np
+
+        from ..geo.crs import to_crs
+        from ..geo.shapefile import POLYGON, read_shapefile
+
+        kind, geoms = read_shapefile(input_file)
+        if kind != POLYGON:
+            raise ValueError(f"{input_file}: shape type {kind} is not Polygon")
+        rings = [r for g in geoms if g for r in g]
+        if not rings:
+            return []
+        flat = to_crs(np.vstack(rings), src_epsg, dst_epsg, self.engine)
+        out, o = [], 0
+        for g in geoms:
+            if not g:
+                continue
+            for r in g:
+                xy = flat[o:o + len(r)]
+                o += len(r)
+                x, y = r[:, 0], r[:, 1]
+                if 0.5 * np.sum(x[:-1] * y[1:] - x[1:] * y[:-1]) > 0 and out:   # hole
+                    out[-1][1].append(xy)
+                else:
+                    out.append((xy, []))
+        return out
+
+    def load_dem_polygons(self, dem, geo, threshold_dem=0, unit_m=1000.0):
+        """Regions of an already-loaded DEM (device or host array on RasterGeo geo)."""
+        return DemRegions(self.engine, dem, geo, threshold_dem, unit_m)
+
     def load_dem_mask(self, input_file, threshold_dem=0):
         """Boolean mask [rows][cols] of data_manager.py:14-17, evaluated on the GPU (K1)."""
         from ..engine import Engine, PathParams
@@ -104,9 +149,10 @@ class DataManager:
         return ((rec[..., 3] & 2) != 0).cpu().numpy()
 
     def load_dem_polygons_from_geotiff(self, input_file, threshold_dem=0):
-        raise NotImplementedError("polygonising the DEM mask (rasterio.features.shapes + "
-                                  "shapely) is outside the device hot path; use "
-                                  "load_dem_mask() for the mask itself")
+        """data_manager.py:11-19: the mask regions of the DEM (plane raster, metres via the
+        file's geotransform scale) as DemRegions for DataProcessor.process_polygons."""
+        dem, geo = self.load_dem(input_file)
+        return DemRegions(self.engine, dem, geo, threshold_dem, unit_m=1.0)
 
     @staticmethod
     def save_polygons(polygons, output_file):

@@ -35,7 +35,14 @@ class DataProcessor:
                                    float(self.min_approx_polygon_area), int(self.divisions), 0)
 
     def process_polygons(self, polygons):
-        """-> list of int64 [4, 2] rectangles (cv2.boxPoints order, metres)."""
+        """-> list of int64 [4, 2] rectangles (cv2.boxPoints order, metres).  ``polygons``:
+        vector polygons (plane metres), or the DemRegions that
+        DataManager.load_dem_polygons_from_geotiff returns (GPU route, uam_dem_polygons)."""
+        from .data_manager import DemRegions
+
+        if isinstance(polygons, DemRegions):
+            return polygons.engine.dem_polygons(polygons.dem, polygons.geo, polygons.threshold,
+                                                polygons.unit_m, self.params())
         rings, holes = [], []
         for p in polygons:
             shell, hs = _as_polygon(p)
