@@ -1604,7 +1604,7 @@ __global__ __launch_bounds__(256) void k_reproject(KTm k, KGeoGrid g, KRaster r,
 __device__ __forceinline__ int32_t ccl_find(const int32_t* L, int32_t x) {
     while (true) {
         const int32_t p = __hip_atomic_load(&L[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p == x) return x;
+        if (p == x || p < 0 || p > x) return x;  // L[x] <= x always; never walk out of range
         x = p;
     }
 }
@@ -1625,14 +1625,30 @@ __device__ __forceinline__ void ccl_union(int32_t* L, int32_t a, int32_t b) {
     }
 }
 
-// mask of data_manager.py:14-17: dem == -9999 when threshold == -9999, else dem > threshold
+// mask of data_manager.py:14-17: dem == -9999 when threshold == -9999, else dem > threshold.
+// Each cell starts labelled with the first cell of its horizontal run inside its wave (ballot
+// of run breaks), so k_ccl_merge only has to join runs across waves and rows.
+__device__ __forceinline__ int32_t run_start_label(bool m, int64_t i, int32_t nx,
+                                                   bool cut_before = false) {
+    const int lane = threadIdx.x & 63;
+    const int prev = __shfl_up((int)m, 1, 64);  // every lane takes part (no divergence)
+    const bool brk = m && (lane == 0 || (i % nx) == 0 || !prev || cut_before);
+    const uint64_t b = __ballot(brk) & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
+    const int start = 63 - __clzll(b);  // highest break at or below this lane
+    return m ? (int32_t)(i - (lane - start)) : -1;
+}
+
 __global__ __launch_bounds__(256) void k_ccl_init_dem(const float* __restrict__ dem, int64_t n,
-                                                      float thr, int32_t* __restrict__ L) {
+                                                      int32_t nx, float thr,
+                                                      int32_t* __restrict__ L) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float v = dem[i];
-    const bool m = (thr == -9999.0f) ? (v == -9999.0f) : (v > thr);
-    L[i] = m ? (int32_t)i : -1;
+    bool m = false;
+    if (i < n) {
+        const float v = dem[i];
+        m = (thr == -9999.0f) ? (v == -9999.0f) : (v > thr);
+    }
+    const int32_t l = run_start_label(m, i, nx);
+    if (i < n) L[i] = l;
 }
 
 // refined sub-grid of one component: cell (s, t) <-> source pixel (col_of[s], row_of[t])
@@ -1640,23 +1656,37 @@ __global__ __launch_bounds__(256) void k_ccl_init_sub(const int32_t* __restrict_
                                                       int32_t src_nx, int32_t root,
                                                       const int32_t* __restrict__ col_of,
                                                       const int32_t* __restrict__ row_of,
+                                                      const int32_t* __restrict__ colbox,
                                                       int32_t ws, int32_t hs,
                                                       int32_t* __restrict__ L) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)ws * hs) return;
-    const int32_t t = (int32_t)(i / ws), s = (int32_t)(i - (int64_t)t * ws);
-    const int64_t src = (int64_t)row_of[t] * src_nx + col_of[s];
-    L[i] = (Lsrc[src] == root) ? (int32_t)i : -1;
+    const bool valid = i < (int64_t)ws * hs;
+    const int32_t t = valid ? (int32_t)(i / ws) : 0, s = valid ? (int32_t)(i - (int64_t)t * ws) : 0;
+    const bool m = valid && Lsrc[(int64_t)row_of[t] * src_nx + col_of[s]] == root;
+    const bool cut = valid && s > 0 && colbox[s] != colbox[s - 1];
+    const int32_t l = run_start_label(m, i, ws, cut);
+    if (valid) L[i] = l;
 }
 
+// Joins 4-neighbours.  With runs pre-labelled (runs = true) only two kinds of join remain:
+// the left neighbour across a wave boundary, and the cell above when the left neighbour does
+// not already connect the same two rows (left and above-left both on the mask).
 __global__ __launch_bounds__(256) void k_ccl_merge(int32_t nx, int32_t ny,
                                                    const int32_t* __restrict__ colbox,
-                                                   const int32_t* __restrict__ rowbox,
+                                                   const int32_t* __restrict__ rowbox, int runs,
                                                    int32_t* __restrict__ L) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)nx * ny) return;
     if (L[i] < 0) return;
     const int32_t y = (int32_t)(i / nx), x = (int32_t)(i - (int64_t)y * nx);
+    if (runs) {
+        const bool left = x > 0 && L[i - 1] >= 0 && (!colbox || colbox[x] == colbox[x - 1]);
+        if (left && (threadIdx.x & 63) == 0) ccl_union(L, (int32_t)i, (int32_t)(i - 1));
+        if (y > 0 && L[i - nx] >= 0 && (!rowbox || rowbox[y] == rowbox[y - 1]) &&
+            !(left && L[i - nx - 1] >= 0))
+            ccl_union(L, (int32_t)i, (int32_t)(i - nx));
+        return;
+    }
     if (x + 1 < nx && L[i + 1] >= 0 && (!colbox || colbox[x] == colbox[x + 1]))
         ccl_union(L, (int32_t)i, (int32_t)(i + 1));
     if (y + 1 < ny && L[i + nx] >= 0 && (!rowbox || rowbox[y] == rowbox[y + 1]))
@@ -1709,7 +1739,12 @@ __global__ __launch_bounds__(256) void k_ccl_assign(const int32_t* __restrict__ 
     }
 }
 
-// per component: cell count and bounding box (wave-aggregated when a wave's cells share one)
+// per component: cell count, bounding box and root.  Each block folds its 256 x CCL_ITEMS
+// cells into a small LDS table (open addressing on the component id), then flushes one set
+// of global atomics per distinct component: a large region costs O(blocks) global atomics
+// instead of O(cells).  Table overflow falls back to direct global atomics.
+constexpr int STAT_SLOTS = 32;
+
 __global__ __launch_bounds__(256) void k_ccl_stats(const int32_t* __restrict__ L,
                                                    const int32_t* __restrict__ cid, int32_t nx,
                                                    int64_t n, int32_t* __restrict__ cnt,
@@ -1718,38 +1753,73 @@ __global__ __launch_bounds__(256) void k_ccl_stats(const int32_t* __restrict__ L
                                                    int32_t* __restrict__ bx1,
                                                    int32_t* __restrict__ by1,
                                                    int32_t* __restrict__ croot) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool in = i < n && L[i] >= 0;
-    const int32_t c = in ? cid[L[i]] : -1;
-    if (in && L[i] == (int32_t)i) croot[c] = (int32_t)i;
-    const int32_t y = in ? (int32_t)(i / nx) : 0, x = in ? (int32_t)(i - (int64_t)y * nx) : 0;
-    const int32_t c0 = __shfl(c, 0, 64);
-    if (__ballot(c != c0) == 0) {  // wave-uniform component (or all background)
-        if (c0 < 0) return;
-        const int k = wave_isum(1);
-        int xmn = x, xmx = x, ymn = y, ymx = y;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            xmn = min(xmn, __shfl_xor(xmn, o, 64));
-            xmx = max(xmx, __shfl_xor(xmx, o, 64));
-            ymn = min(ymn, __shfl_xor(ymn, o, 64));
-            ymx = max(ymx, __shfl_xor(ymx, o, 64));
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&cnt[c0], k);
-            atomicMin(&bx0[c0], xmn);
-            atomicMax(&bx1[c0], xmx);
-            atomicMin(&by0[c0], ymn);
-            atomicMax(&by1[c0], ymx);
-        }
-        return;
+    __shared__ int32_t key[STAT_SLOTS], sc[STAT_SLOTS], sx0[STAT_SLOTS], sy0[STAT_SLOTS],
+        sx1[STAT_SLOTS], sy1[STAT_SLOTS];
+    if (threadIdx.x < STAT_SLOTS) {
+        key[threadIdx.x] = -1;
+        sc[threadIdx.x] = 0;
+        sx0[threadIdx.x] = sy0[threadIdx.x] = INT32_MAX;
+        sx1[threadIdx.x] = sy1[threadIdx.x] = -1;
     }
-    if (c < 0) return;
-    atomicAdd(&cnt[c], 1);
-    atomicMin(&bx0[c], x);
-    atomicMax(&bx1[c], x);
-    atomicMin(&by0[c], y);
-    atomicMax(&by1[c], y);
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 256 * CCL_ITEMS;
+    for (int it = 0; it < CCL_ITEMS; ++it) {
+        const int64_t i = base + (int64_t)it * 256 + threadIdx.x;
+        const bool in = i < n && L[i] >= 0;
+        const int32_t c = in ? cid[L[i]] : -1;
+        if (in && L[i] == (int32_t)i) croot[c] = (int32_t)i;
+        const int32_t y = in ? (int32_t)(i / nx) : 0, x = in ? (int32_t)(i - (int64_t)y * nx) : 0;
+        // wave-uniform component: reduce in registers first
+        const int32_t c0 = __shfl(c, 0, 64);
+        const bool uni = __ballot(c != c0) == 0;
+        int32_t cc = c, k = 1, xmn = x, xmx = x, ymn = y, ymx = y;
+        bool lead = true;
+        if (uni) {
+            k = wave_isum(1);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                xmn = min(xmn, __shfl_xor(xmn, o, 64));
+                xmx = max(xmx, __shfl_xor(xmx, o, 64));
+                ymn = min(ymn, __shfl_xor(ymn, o, 64));
+                ymx = max(ymx, __shfl_xor(ymx, o, 64));
+            }
+            lead = (threadIdx.x & 63) == 0;
+        }
+        if (cc < 0 || !lead) continue;
+        int slot = -1;
+        for (int p = 0; p < STAT_SLOTS; ++p) {
+            const int h = (int)(((uint32_t)cc * 2654435761u + p) % STAT_SLOTS);
+            const int32_t old = atomicCAS(&key[h], -1, cc);
+            if (old == -1 || old == cc) {
+                slot = h;
+                break;
+            }
+        }
+        if (slot >= 0) {
+            atomicAdd(&sc[slot], k);
+            atomicMin(&sx0[slot], xmn);
+            atomicMax(&sx1[slot], xmx);
+            atomicMin(&sy0[slot], ymn);
+            atomicMax(&sy1[slot], ymx);
+        } else {
+            atomicAdd(&cnt[cc], k);
+            atomicMin(&bx0[cc], xmn);
+            atomicMax(&bx1[cc], xmx);
+            atomicMin(&by0[cc], ymn);
+            atomicMax(&by1[cc], ymx);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < STAT_SLOTS) {
+        const int32_t cc = key[threadIdx.x];
+        if (cc >= 0) {
+            atomicAdd(&cnt[cc], sc[threadIdx.x]);
+            atomicMin(&bx0[cc], sx0[threadIdx.x]);
+            atomicMax(&bx1[cc], sx1[threadIdx.x]);
+            atomicMin(&by0[cc], sy0[threadIdx.x]);
+            atomicMax(&by1[cc], sy1[threadIdx.x]);
+        }
+    }
 }
 
 // per kept component and row: leftmost / rightmost cell (hull input)
@@ -2665,11 +2735,11 @@ struct CompStats {
 };
 
 // label a grid (optionally with cuts) and return per-component stats; L is initialised
-int label_grid(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* rowbox,
+int label_grid(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* rowbox, bool runs,
                int32_t* L, DevBuf<int32_t>& cid, CompStats& st, hipStream_t s) {
     const int64_t n = (int64_t)nx * ny;
     const dim3 g(grid_for(n, 256, INT32_MAX)), b(256);
-    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, nx, ny, colbox, rowbox, L);
+    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, nx, ny, colbox, rowbox, runs ? 1 : 0, L);
     hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, n, L);
     const int64_t nblk = (n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
     DevBuf<int32_t> cnt, off;
@@ -2701,8 +2771,8 @@ int label_grid(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* row
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by0, (int64_t)ncomp, INT32_MAX);
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, bx1, (int64_t)ncomp, -1);
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by1, (int64_t)ncomp, -1);
-        hipLaunchKernelGGL(k_ccl_stats, g, b, 0, s, L, cid.p, nx, n, cntp, bx0, by0, bx1, by1,
-                           rt);
+        hipLaunchKernelGGL(k_ccl_stats, dim3((unsigned)nblk), b, 0, s, L, cid.p, nx, n, cntp,
+                           bx0, by0, bx1, by1, rt);
     }
     HIP_TRY2(hipGetLastError());
     std::vector<int32_t> all(6 * (int64_t)ncomp);
@@ -2800,9 +2870,9 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     DevBuf<int32_t> L, cid;
     HIP_TRY2(L.alloc(n));
     hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, dem,
-                       n, threshold, L.p);
+                       n, nx, threshold, L.p);
     CompStats st;
-    int rc = label_grid(nx, ny, nullptr, nullptr, L.p, cid, st, s);
+    int rc = label_grid(nx, ny, nullptr, nullptr, true, L.p, cid, st, s);
     if (rc) return rc;
     const int32_t ncomp = (int32_t)st.cnt.size();
     const double cell = std::fabs(DX * DY);
@@ -2868,9 +2938,9 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         HIP_TRY2(hipMemcpyAsync(dro.p, row_of.data(), hs * 4, hipMemcpyHostToDevice, s));
         HIP_TRY2(hipMemcpyAsync(drb.p, rowbox.data(), hs * 4, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0, s,
-                           L.p, nx, st.root[c], dco.p, dro.p, ws, hs, L2.p);
+                           L.p, nx, st.root[c], dco.p, dro.p, dcb.p, ws, hs, L2.p);
         CompStats ps;
-        rc = label_grid(ws, hs, dcb.p, drb.p, L2.p, cid2, ps, s);
+        rc = label_grid(ws, hs, dcb.p, drb.p, true, L2.p, cid2, ps, s);
         if (rc) return rc;
         const int32_t np = (int32_t)ps.cnt.size();
         std::vector<char> all(np, 1);
