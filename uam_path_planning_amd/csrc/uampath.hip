@@ -66,12 +66,25 @@ struct alignas(16) DevShape {  // 128 B
     double cx, cy;
     double box_pen[4];  // xmin, xmax, ymin, ymax
     double box_obs[4];
-    double pad[2];
+    int32_t region;     // region of a region shape, -1 for obstacles
+    int32_t pad0;
+    double pad1;
 };
 
 __host__ __device__ __forceinline__ bool outside(const double* b, double x0, double x1) {
     return x0 < b[0] || x0 > b[1] || x1 < b[2] || x1 > b[3];  // NaN -> false (evaluate)
 }
+
+// Uniform-grid shape index (built by uam_set_params): for every cell the shapes whose culling
+// box meets it, in ascending shape order, CSR-encoded; slot gx*gy lists the shapes that are
+// never culled (what a point off the grid must evaluate).  Exact: a shape missing from a
+// point's list has a box that does not contain the point, so box culling would skip it.
+struct KShapeGrid {
+    double x0, y0, x1, y1, inv_dx, inv_dy;
+    int32_t gx, gy;
+    const int32_t* start[3];  // 0 = region penalty (box_pen), 1 = psi, 2 = hit
+    const int32_t* items[3];
+};
 
 struct KGeom {
     const DevIneq* __restrict__ ineq;
@@ -79,7 +92,17 @@ struct KGeom {
     int32_t n_obstacles;
     int32_t n_regions;
     int32_t region_first[UAM_MAX_REGIONS + 1];
+    KShapeGrid grid;  // grid.gx == 0: no index
 };
+
+// list slot of a point: its grid cell, gx*gy off the grid, -1 for NaN (no index: evaluate all)
+__device__ __forceinline__ int grid_slot(const KShapeGrid& gr, double x, double y) {
+    if (!(x == x) || !(y == y)) return -1;
+    if (x < gr.x0 || x > gr.x1 || y < gr.y0 || y > gr.y1) return gr.gx * gr.gy;
+    const int cx = min((int)floor((x - gr.x0) * gr.inv_dx), gr.gx - 1);
+    const int cy = min((int)floor((y - gr.y0) * gr.inv_dy), gr.gy - 1);
+    return cy * gr.gx + cx;
+}
 
 struct KParams {
     int32_t N;
@@ -181,19 +204,52 @@ __device__ __forceinline__ double region_penalty(const KGeom& g, const KParams& 
     return p.weights[r] * t;
 }
 
-// problem.py:49-56
+// problem.py:49-56.  With the grid index: the region shapes of the point's list, in ascending
+// order; a region with no listed shape adds w_r * (+0), an exact no-op, so it is skipped.
 __device__ __forceinline__ double total_penalty(const KGeom& g, const KParams& p, double x0,
                                                 double x1) {
-    double pen = 0.0;
-    for (int r = 0; r < g.n_regions; ++r) pen = pen + region_penalty(g, p, r, x0, x1);
+    const int slot = g.grid.gx ? grid_slot(g.grid, x0, x1) : -1;
+    if (slot < 0) {
+        double pen = 0.0;
+        for (int r = 0; r < g.n_regions; ++r) pen = pen + region_penalty(g, p, r, x0, x1);
+        return pen;
+    }
+    double pen = 0.0, t = 0.0;
+    int rc = -1;
+    const int k1 = g.grid.start[0][slot + 1];
+    for (int k = g.grid.start[0][slot]; k < k1; ++k) {
+        const DevShape& sh = g.shape[g.grid.items[0][k]];
+        if (sh.region != rc) {
+            if (rc >= 0) pen = pen + p.weights[rc] * t;
+            rc = sh.region;
+            t = 0.0;
+        }
+        if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;
+        const double v = psi(g, sh, x0, x1, p.penalty_smooth != 0, p.enlargement);
+        t = sh.has_center ? t + v / sh.norm_pen : t + v;
+    }
+    if (rc >= 0) pen = pen + p.weights[rc] * t;
     return pen;
 }
 
 __device__ __forceinline__ bool collides(const KGeom& g, double x0, double x1) {
     bool hit = false;
+    const int slot = g.grid.gx ? grid_slot(g.grid, x0, x1) : -1;
+    if (slot >= 0) {
+        const int k1 = g.grid.start[2][slot + 1];
+        for (int k = g.grid.start[2][slot]; k < k1; ++k) {
+            const DevShape& sh = g.shape[g.grid.items[2][k]];
+            if ((sh.flags & SHAPE_CULL_HIT) && outside(sh.box_obs, x0, x1)) continue;
+            hit = hit || contains(g, sh, x0, x1);
+        }
+        return hit;
+    }
+    // a NaN coordinate makes every h(x) > 1e-14 test false (contains() is true) unless a finite
+    // axis inequality decides: never cull such a point (slot -1 comes here)
+    const bool nan = !(x0 == x0) || !(x1 == x1);
     for (int s = 0; s < g.n_obstacles; ++s) {
         const DevShape& sh = g.shape[s];
-        if ((sh.flags & SHAPE_CULL_HIT) && outside(sh.box_obs, x0, x1)) continue;
+        if (!nan && (sh.flags & SHAPE_CULL_HIT) && outside(sh.box_obs, x0, x1)) continue;
         hit = hit || contains(g, sh, x0, x1);
     }
     return hit;
@@ -203,6 +259,16 @@ __device__ __forceinline__ bool collides(const KGeom& g, double x0, double x1) {
 __device__ __forceinline__ double obstacle_psi_sum(const KGeom& g, const KParams& p, double x0,
                                                    double x1) {
     double acc = 0.0;
+    const int slot = g.grid.gx ? grid_slot(g.grid, x0, x1) : -1;
+    if (slot >= 0) {
+        const int k1 = g.grid.start[1][slot + 1];
+        for (int k = g.grid.start[1][slot]; k < k1; ++k) {
+            const DevShape& sh = g.shape[g.grid.items[1][k]];
+            if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) continue;
+            acc = acc + psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+        }
+        return acc;
+    }
     for (int s = 0; s < g.n_obstacles; ++s) {
         const DevShape& sh = g.shape[s];
         if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) continue;
@@ -564,10 +630,20 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
             double x0, x1;
             src.at(j, x0, x1);
             a.cost = a.cost + total_penalty(g, p, x0, x1) / dN;
-            for (int s = 0; s < g.n_obstacles; ++s) {
-                const double v = obstacle_psi(g, p, s, x0, x1);
-                a.nsum = a.nsum + v;
-                if (grow) grow[3 * N + s * W + j] = v;
+            const int slot = (g.grid.gx && !grow) ? grid_slot(g.grid, x0, x1) : -1;
+            if (slot >= 0) {  // listed obstacles only: the others add +0 (exact no-op)
+                const int k1 = g.grid.start[1][slot + 1];
+                for (int k = g.grid.start[1][slot]; k < k1; ++k) {
+                    const DevShape& sh = g.shape[g.grid.items[1][k]];
+                    if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) continue;
+                    a.nsum = a.nsum + psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+                }
+            } else {
+                for (int s = 0; s < g.n_obstacles; ++s) {
+                    const double v = obstacle_psi(g, p, s, x0, x1);
+                    a.nsum = a.nsum + v;
+                    if (grow) grow[3 * N + s * W + j] = v;
+                }
             }
             a.nh += collides(g, x0, x1) ? 1 : 0;
         }
@@ -823,6 +899,48 @@ __device__ __forceinline__ double psi_vg(const KGeom& g, const DevShape& sh, dou
 __device__ double phi_vg(const KGeom& g, const KParams& p, double x0, double x1, bool want,
                          double& dx, double& dy) {
     double pen = 0.0, gx = 0.0, gy = 0.0;
+    const int slot = g.grid.gx ? grid_slot(g.grid, x0, x1) : -1;
+    if (slot >= 0) {  // grid-listed region shapes, regions in order (see total_penalty)
+        double t = 0.0, tx = 0.0, ty = 0.0;
+        int rc = -1;
+        const int k1 = g.grid.start[0][slot + 1];
+        for (int k = g.grid.start[0][slot]; k < k1; ++k) {
+            const DevShape& sh = g.shape[g.grid.items[0][k]];
+            if (sh.region != rc) {
+                if (rc >= 0) {
+                    pen = pen + p.weights[rc] * t;
+                    gx = gx + p.weights[rc] * tx;
+                    gy = gy + p.weights[rc] * ty;
+                }
+                rc = sh.region;
+                t = tx = ty = 0.0;
+            }
+            if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1)) continue;
+            double ex, ey;
+            const double v = psi_vg(g, sh, x0, x1, p.enlargement, want, ex, ey);
+            if (sh.has_center) {
+                t = t + v / sh.norm_pen;
+                if (want && v != 0.0) {
+                    tx = tx + ex / sh.norm_pen;
+                    ty = ty + ey / sh.norm_pen;
+                }
+            } else {
+                t = t + v;
+                if (want && v != 0.0) {
+                    tx = tx + ex;
+                    ty = ty + ey;
+                }
+            }
+        }
+        if (rc >= 0) {
+            pen = pen + p.weights[rc] * t;
+            gx = gx + p.weights[rc] * tx;
+            gy = gy + p.weights[rc] * ty;
+        }
+        dx = gx;
+        dy = gy;
+        return pen;
+    }
     for (int r = 0; r < g.n_regions; ++r) {
         double t = 0.0, tx = 0.0, ty = 0.0;
         const int s1 = g.region_first[r + 1];
@@ -2050,6 +2168,7 @@ struct uam_ctx {
     int variant = 0;  // uam_set_tuning; 0 = default
     std::vector<DevIneq> h_ineq;
     std::vector<DevShape> h_shape;
+    int32_t* d_grid = nullptr;  // shape-grid index (KShapeGrid), rebuilt by uam_set_params
 };
 
 namespace {
@@ -2140,6 +2259,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     DeviceGuard dg(ctx->device);
     if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
+    if (ctx->d_grid) (void)hipFree(ctx->d_grid);
     delete ctx;
 }
 
@@ -2188,12 +2308,18 @@ int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
         ts[s].count = geom->shape_count[s];
         ts[s].cx = geom->shape_center[2 * s];
         ts[s].cy = geom->shape_center[2 * s + 1];
+        ts[s].region = -1;
     }
+    for (int r = 0; r < nr; ++r)
+        for (int s = geom->region_first[r]; s < geom->region_first[r + 1]; ++s) ts[s].region = r;
     if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     ctx->d_ineq = nullptr;
     ctx->d_shape = nullptr;
     ctx->have_geom = ctx->have_params = false;
+    if (ctx->d_grid) (void)hipFree(ctx->d_grid);
+    ctx->d_grid = nullptr;
+    ctx->kg.grid = KShapeGrid{};
     HIP_TRY(hipMalloc(&ctx->d_ineq, hi.size()));
     HIP_TRY(hipMalloc(&ctx->d_shape, hs.size()));
     HIP_TRY(hipMemcpy(ctx->d_ineq, hi.data(), hi.size(), hipMemcpyHostToDevice));
@@ -2210,6 +2336,88 @@ int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
     for (int r = 0; r <= UAM_MAX_REGIONS; ++r)
         kg.region_first[r] = r <= nr ? geom->region_first[r] : ns;
     ctx->have_geom = true;
+    return UAM_OK;
+}
+
+// Shape-grid index (KShapeGrid).  Lists: 0 = region shapes by box_pen (SHAPE_CULL_PEN),
+// 1 = obstacles by box_obs for psi (SHAPE_CULL_PSI), 2 = obstacles by box_obs for contains
+// (SHAPE_CULL_HIT); a shape without its cull flag is listed in every cell and in the off-grid
+// slot.  The grid spans the union of the flagged boxes.
+static constexpr int kShapeGridN = 64;
+
+static int build_shape_grid(uam_ctx* ctx) {
+    if (ctx->d_grid) (void)hipFree(ctx->d_grid);
+    ctx->d_grid = nullptr;
+    ctx->kg.grid = KShapeGrid{};
+    const int ns = ctx->n_shapes, nobs = ctx->kg.n_obstacles;
+    const int first_reg = ctx->kg.region_first[0], last_reg = ctx->kg.region_first[ctx->kg.n_regions];
+    struct Src {
+        int lo, hi, flag;
+        bool pen;
+    } src[3] = {{first_reg, last_reg, SHAPE_CULL_PEN, true},
+                {0, nobs, SHAPE_CULL_PSI, false},
+                {0, nobs, SHAPE_CULL_HIT, false}};
+    double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+    int flagged = 0;
+    for (int l = 0; l < 3; ++l)
+        for (int sh = src[l].lo; sh < src[l].hi; ++sh) {
+            const DevShape& d = ctx->h_shape[sh];
+            if (!(d.flags & src[l].flag)) continue;
+            const double* b = src[l].pen ? d.box_pen : d.box_obs;
+            if (!(std::isfinite(b[0]) && std::isfinite(b[1]) && std::isfinite(b[2]) &&
+                  std::isfinite(b[3])))
+                continue;
+            x0 = std::min(x0, b[0]), x1 = std::max(x1, b[1]);
+            y0 = std::min(y0, b[2]), y1 = std::max(y1, b[3]);
+            ++flagged;
+        }
+    if (flagged == 0 || ns == 0 || !(x1 > x0) || !(y1 > y0)) return UAM_OK;  // no index
+    const int G = kShapeGridN, cells = G * G;
+    KShapeGrid gr{};
+    gr.x0 = x0, gr.x1 = x1, gr.y0 = y0, gr.y1 = y1;
+    gr.inv_dx = G / (x1 - x0), gr.inv_dy = G / (y1 - y0);
+    gr.gx = gr.gy = G;
+    auto cell_of = [&](double v, double o, double inv) {
+        const double f = std::floor((v - o) * inv);
+        return (int)std::max(0.0, std::min((double)(G - 1), f));
+    };
+    std::vector<int32_t> all;
+    size_t offs[3][2];
+    for (int l = 0; l < 3; ++l) {
+        std::vector<std::vector<int32_t>> lists(cells + 1);
+        for (int sh = src[l].lo; sh < src[l].hi; ++sh) {
+            const DevShape& d = ctx->h_shape[sh];
+            const double* b = src[l].pen ? d.box_pen : d.box_obs;
+            const bool finite = std::isfinite(b[0]) && std::isfinite(b[1]) &&
+                                std::isfinite(b[2]) && std::isfinite(b[3]);
+            if (!(d.flags & src[l].flag) || !finite) {  // never culled: everywhere
+                for (int c = 0; c <= cells; ++c) lists[c].push_back(sh);
+                continue;
+            }
+            if (b[1] < x0 || b[0] > x1 || b[3] < y0 || b[2] > y1) continue;
+            const int cx0 = cell_of(b[0], x0, gr.inv_dx), cx1 = cell_of(b[1], x0, gr.inv_dx);
+            const int cy0 = cell_of(b[2], y0, gr.inv_dy), cy1 = cell_of(b[3], y0, gr.inv_dy);
+            for (int cy = cy0; cy <= cy1; ++cy)
+                for (int cx = cx0; cx <= cx1; ++cx) lists[cy * G + cx].push_back(sh);
+        }
+        offs[l][0] = all.size();
+        int32_t run = 0;
+        all.push_back(0);
+        for (int c = 0; c <= cells; ++c) {
+            run += (int32_t)lists[c].size();
+            all.push_back(run);
+        }
+        offs[l][1] = all.size();
+        for (int c = 0; c <= cells; ++c) all.insert(all.end(), lists[c].begin(), lists[c].end());
+    }
+    HIP_TRY(hipMalloc(&ctx->d_grid, all.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(ctx->d_grid, all.data(), all.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    for (int l = 0; l < 3; ++l) {
+        gr.start[l] = ctx->d_grid + offs[l][0];
+        gr.items[l] = ctx->d_grid + offs[l][1];
+    }
+    ctx->kg.grid = gr;
     return UAM_OK;
 }
 
@@ -2250,7 +2458,12 @@ int uam_set_params(uam_ctx* ctx, const uam_params* prm, uam_stream stream) {
         hipLaunchKernelGGL(k_prepare, dim3(grid_for(ctx->n_shapes, 64)), dim3(64), 0,
                            (hipStream_t)stream, ctx->kg, k, ctx->d_shape, ctx->n_shapes);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        HIP_TRY(hipMemcpy(ctx->h_shape.data(), ctx->d_shape, sizeof(DevShape) * ctx->n_shapes,
+                          hipMemcpyDeviceToHost));
     }
+    st = build_shape_grid(ctx);
+    if (st) return st;
     ctx->have_params = true;
     return UAM_OK;
 }
