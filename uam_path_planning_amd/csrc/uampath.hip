@@ -1034,6 +1034,7 @@ struct RfPath {
     const double* dr;  // LDS [W][2] search direction
     const double* yk;  // LDS [3N]
     const double* yo;  // global [S][W]
+    const uint64_t* act;  // LDS [W][RF_MASKW]: rows with a nonzero multiplier (null: no masks)
     int N, W;
     __device__ __forceinline__ void pt(int j, double a, double& x, double& y) const {
         x = z[2 * j];
@@ -1054,6 +1055,39 @@ __device__ __forceinline__ double wdot(const double* u, const double* v, int N, 
         s = s + t;
     }
     return wave_sum(s);
+}
+
+// Candidate no-fly rows of a waypoint: the obstacles the grid index lists at its position
+// (psi may be nonzero there) or whose multiplier is nonzero (act); every other row adds
+// (c/2)(0 + 0/c)^2 = +0 to L and nothing to the gradient, so skipping it is exact.  Rows are
+// visited in ascending order.  No index / NaN point: all rows.
+constexpr int RF_MASKW = 4;  // bitmask words per waypoint: S <= 256 uses the masks
+
+__device__ __forceinline__ uint64_t pick_word(const uint64_t (&cw)[RF_MASKW], int w) {
+    return w == 0 ? cw[0] : (w == 1 ? cw[1] : (w == 2 ? cw[2] : cw[3]));  // no dynamic index
+}
+
+__device__ __forceinline__ void rf_candidates(const KGeom& g, double x, double y,
+                                              const uint64_t* act, uint64_t (&cw)[RF_MASKW]) {
+    const int S = g.n_obstacles;
+    const int slot = g.grid.gx ? grid_slot(g.grid, x, y) : -1;
+#pragma unroll
+    for (int w = 0; w < RF_MASKW; ++w) cw[w] = act ? act[w] : 0ull;
+    if (slot < 0) {
+#pragma unroll
+        for (int w = 0; w < RF_MASKW; ++w) {
+            const int lo = 64 * w;
+            cw[w] = S >= lo + 64 ? ~0ull : (S > lo ? ((1ull << (S - lo)) - 1ull) : 0ull);
+        }
+        return;
+    }
+    const int k1 = g.grid.start[1][slot + 1];
+    for (int k = g.grid.start[1][slot]; k < k1; ++k) {
+        const int sh = g.grid.items[1][k];
+#pragma unroll
+        for (int w = 0; w < RF_MASKW; ++w)
+            if ((sh >> 6) == w) cw[w] |= 1ull << (sh & 63);
+    }
 }
 
 __device__ __forceinline__ double seg_term(double px, double py, double qx, double qy, bool ls,
@@ -1141,7 +1175,7 @@ __device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int l
                 }
             }
         }
-        for (int s = 0; s < g.n_obstacles; ++s) {
+        auto obstacle_row = [&](int s) {
             const DevShape& sh = g.shape[s];
             double v = 0.0, ox = 0.0, oy = 0.0;
             if (!((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)))
@@ -1153,6 +1187,17 @@ __device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int l
                 gx = gx + coef * ox;
                 gy = gy + coef * oy;
             }
+        };
+        if (rp.act) {
+            uint64_t cw[RF_MASKW];
+            rf_candidates(g, xj, yj, rp.act + (int64_t)j * RF_MASKW, cw);
+            const int nw = (g.n_obstacles + 63) >> 6;
+#pragma unroll 1
+            for (int w = 0; w < nw; ++w)
+                for (uint64_t b = pick_word(cw, w); b; b &= b - 1)
+                    obstacle_row(64 * w + __builtin_ctzll(b));
+        } else {
+            for (int s = 0; s < g.n_obstacles; ++s) obstacle_row(s);
         }
         saug = saug + aj;
         double tg = 0.0;
@@ -1237,11 +1282,13 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
     if (path >= P) return;  // whole wave
     const int N = p.N, W = N + 2, S = g.n_obstacles;
     const int m = rf.memory < 0 ? 0 : (rf.memory > RF_MAXM ? RF_MAXM : rf.memory);
-    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM);
+    const bool use_mask = S <= 64 * RF_MASKW;
+    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM + RF_MASKW * W);
     double* gr = z + 2 * W;
     double* dr = gr + 2 * W;
     double* yk = dr + 2 * W;
     double* rho = yk + 3 * N;
+    uint64_t* act = use_mask ? reinterpret_cast<uint64_t*>(rho + RF_MAXM) : nullptr;
     double* zg = wp + path * (int64_t)W * 2;
     double* yo = ws + path * ((int64_t)S * W + (int64_t)m * 4 * W);
     double* hs = yo + (int64_t)S * W;
@@ -1252,10 +1299,12 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
         dr[k] = 0.0;
     }
     for (int k = lane; k < 3 * N; k += 64) yk[k] = 0.0;
+    if (act)
+        for (int k = lane; k < RF_MASKW * W; k += 64) act[k] = 0ull;
     for (int s = 0; s < S; ++s)
         for (int j = lane; j < W; j += 64) yo[(int64_t)s * W + j] = 0.0;
     wave_sync();
-    RfPath rp{z, gr, dr, yk, yo, N, W};
+    RfPath rp{z, gr, dr, yk, yo, act, N, W};
     const bool ms = p.maxratio_smooth != 0;
     double c = rf.c0, alpha = rf.alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
     int32_t used = 0;
@@ -1357,13 +1406,25 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
                     sj = sj + cv[t] * cv[t];
                 }
             }
-            for (int s = 0; s < S; ++s) {
+            auto update_row = [&](int s) {
                 const DevShape& sh = g.shape[s];
-                if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)) continue;  // +0
+                if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)) return;  // +0
                 const double v = psi(g, sh, xj, yj, true, 0.0);
                 double* yi = yo + (int64_t)s * W + j;
                 *yi = *yi + c * v;
                 sj = sj + v * v;
+                if (act && v != 0.0) act[(int64_t)j * RF_MASKW + (s >> 6)] |= 1ull << (s & 63);
+            };
+            if (act) {  // rows with psi = 0 leave y and the sum unchanged
+                uint64_t cw[RF_MASKW];
+                rf_candidates(g, xj, yj, nullptr, cw);
+                const int nw = (S + 63) >> 6;
+#pragma unroll 1
+                for (int w = 0; w < nw; ++w)
+                    for (uint64_t b = pick_word(cw, w); b; b &= b - 1)
+                        update_row(64 * w + __builtin_ctzll(b));
+            } else {
+                for (int s = 0; s < S; ++s) update_row(s);
             }
             si = si + sj;
         }
@@ -2790,7 +2851,7 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
         !(rp->max_step > 0.0) || rp->memory < 0 || rp->memory > RF_MAXM)
         return fail(UAM_E_INVALID, "bad refine params (memory must be 0..%d)", RF_MAXM);
     const int64_t N = ctx->kp.N, W = N + 2;
-    const int64_t per_wave = (6 * W + 3 * N + RF_MAXM) * (int64_t)sizeof(double);
+    const int64_t per_wave = (6 * W + 3 * N + RF_MAXM + RF_MASKW * W) * (int64_t)sizeof(double);
     if (per_wave > 65536)
         return fail(UAM_E_INVALID, "N = %lld too large for refinement (LDS)", (long long)N);
     if (n_paths == 0) return UAM_OK;
