@@ -147,3 +147,24 @@ def test_dropin_solve_candidates_selection(eng):
     one = solver.solve(solver.create_x_init(res["displacements"][2]), params)
     np.testing.assert_array_equal(np.asarray(one["x"]), res["x"][2])   # batch == single
     assert _select([3.0, 1.0, 1.0, 2.0]) == 1 and _select([0.0, 2.0]) == 1
+
+
+def test_refine_large_paths_and_many_obstacles(eng, oracle_mod):
+    """N = 254 (W = 256: 4 waypoints per lane, two waves per workgroup) and a map with more
+    obstacles than the active-row masks hold (S > 256: the full-row fallback)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    opts = {"length_smooth": True, "penalty_smooth": True, "obstacle_smooth": True,
+            "maxratio_smooth": False}
+    spec = canonical_spec(nfz_polygons=64)
+    orc = _setup(eng, oracle_mod, spec, 254, opts, spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"], tuple(spec["x_start"]))
+    wp = oracle_mod.gen_paths(random_pairs(3, seed=11), arc_table(254, displacements(5)))
+    _check(eng, orc, oracle_mod, wp, n_outer=2, n_inner=5)
+    many = canonical_spec(nfz_polygons=300, seed=4)          # 306 obstacles
+    orc = _setup(eng, oracle_mod, many, 30, opts, many["maxratio"], many["maxalpha"],
+                 many["enlargement"], many["weights"], tuple(many["x_start"]))
+    wp = oracle_mod.gen_paths(random_pairs(8, seed=12), arc_table(30, displacements(5)))
+    _check(eng, orc, oracle_mod, wp, n_outer=2, n_inner=6)
