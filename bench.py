@@ -203,6 +203,8 @@ def main():
     # at most 16384 paths in raster / volume mode; 10 = never)
     wave = args.mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
     kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
+                   "k_bin_count/k_bin_scatter/k_bin_gather + k_eval_pairs<records> (variant 11,"
+                   " binned)" if (args.variant == 11 and raster_mode) else
                    f"k_eval_pairs<{mode}>" + (f" (variant {args.variant or 2})"
                                               if raster_mode else ""))
     result = {

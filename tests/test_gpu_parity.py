@@ -334,7 +334,7 @@ def test_kernel_variants_bit_identical(eng, oracle_mod, D):
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 333, 80, nfz=4, D=D)
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
     try:
-        for v in range(0, 11):
+        for v in range(0, 12):
             eng.set_tuning(v)
             gpu = eng.eval_generated(pairs, ut, raster=raster)
             _assert_paths_equal(gpu, ref, raster=True)

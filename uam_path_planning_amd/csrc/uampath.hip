@@ -31,7 +31,8 @@
 #include "../../include/uampath.h"
 #include "polyproc.h"
 
-#define UAM_TUNING_MAX 10
+#define UAM_TUNING_MAX 11
+#define UAM_TUNING_BINNED 11    // binned raster evaluation (K2b)
 #define UAM_TUNING_WAVE 9       // force the wave-per-path kernel (K2w)
 #define UAM_TUNING_LANE 10      // never pick K2w automatically
 #define UAM_WAVE_AUTO_PATHS 16384  // auto: K2w up to here (tools/probe_wave.py crossover)
@@ -492,6 +493,28 @@ __device__ __forceinline__ void consume_chunk(const Chunk<C>& ch, int j0, int W,
     }
 }
 
+// Records mode (internal, binned raster evaluation K2b): the waypoint's record was already
+// gathered into recs[path * W + j] (bit 31 of .w set = off the raster); the pass-2 sums are
+// eval_path's, so outputs are bit-identical to the gathering kernels.
+constexpr int MODE_RECORDS = 3;
+constexpr uint32_t REC_OFF = 0x80000000u;
+
+template <int C>
+__device__ __forceinline__ void issue_chunk_rec(const uint4* __restrict__ recs, int64_t base,
+                                                int j0, int W, Chunk<C>& ch) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        const int j = j0 + t;
+        ch.in[t] = false;
+        ch.r[t] = make_uint4(0, 0, 0, 0);
+        if (j < W) {
+            const uint4 r = recs[base + j];
+            ch.in[t] = !(r.w & REC_OFF);
+            ch.r[t] = r;
+        }
+    }
+}
+
 // Volume mode (BASELINE config 5, no reference counterpart): the waypoint's voxel
 // (ix, iy as in raster mode, iz = floor((z - z0) / dz)) holds {risk f32, psi_nfz f32,
 // terrain f32, flags}; risk already carries the altitude-layer weight.
@@ -647,6 +670,12 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
             }
             a.nh += collides(g, x0, x1) ? 1 : 0;
         }
+    } else if (MODE == MODE_RECORDS) {
+        for (int j0 = 0; j0 < W; j0 += C) {
+            Chunk<C> ch;
+            issue_chunk_rec<C>(rec, path * (int64_t)W, j0, W, ch);
+            consume_chunk<C>(ch, j0, W, dN, a);
+        }
     } else {
         int32_t* cells = out.cells ? out.cells + path * W : nullptr;
         if (!PIPE) {
@@ -675,7 +704,7 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
 // raster: cruise altitude - highest terrain under the waypoints; volume: min over waypoints of
 // (waypoint altitude - terrain of its column); analytic: NaN (no DEM)
 __device__ __forceinline__ double clearance(const KParams& p, int mode, const PathAcc& a) {
-    return mode == UAM_MODE_RASTER ? p.altitude - a.hmax
+    return (mode == UAM_MODE_RASTER || mode == MODE_RECORDS) ? p.altitude - a.hmax
                                    : (mode == UAM_MODE_VOLUME ? a.cmin : (double)NAN);
 }
 
@@ -2041,6 +2070,197 @@ __global__ __launch_bounds__(256) void k_fill_i32(int32_t* __restrict__ p, int64
     if (i < n) p[i] = v;
 }
 
+// ----------------------------------------------------------------------------------------
+// K2b: binned raster evaluation (tuning 11).  Every waypoint gather of K2 misses L2 and moves
+// a 128-B line for a 16-B record.  Here the waypoints are first binned by
+// raster tile (BIN_TS x BIN_TS cells = 1 MiB of records), each tile's gathers then run on one
+// XCD while the tile sits in that XCD's 4-MiB L2, and the per-path reduction reads the
+// gathered records contiguously.  Record values and summation order are K2's.
+constexpr int BIN_TS = 256;     // tile side (cells)
+constexpr int BIN_ITEMS = 16;   // waypoints per thread in the binning kernels (4096 per block)
+
+struct KBin {
+    const double* pairs;
+    const double* utab;
+    int32_t D, W;
+    int64_t n_wp;      // P * W
+    int32_t tiles_x, n_tiles;  // n_tiles real tiles; bucket n_tiles = off the raster
+    int32_t n_blocks;  // binning blocks
+};
+
+__device__ __forceinline__ void bin_point(const KBin& kb, const KRaster& rs, int64_t g,
+                                          int32_t& tile, int32_t& cell) {
+    const int64_t path = g / kb.W;
+    const int j = (int)(g - path * kb.W);
+    const int64_t q = path / kb.D;
+    const int d = (int)(path - q * kb.D);
+    const double4 pr = reinterpret_cast<const double4*>(kb.pairs)[q];
+    double x, y;
+    if (j == 0) {
+        x = pr.x, y = pr.y;
+    } else if (j == kb.W - 1) {
+        x = pr.z, y = pr.w;
+    } else {
+        const double* u = kb.utab + ((int64_t)d * (kb.W - 2) + (j - 1)) * 2;
+        arc_point(pr.x, pr.y, pr.z, pr.w, u[0], u[1], x, y);
+    }
+    const double fx = floor((x - rs.x0) * rs.inv_dx);
+    const double fy = floor((rs.y_top - y) * rs.inv_dy);
+    const bool in = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny);
+    if (!in) {
+        tile = kb.n_tiles;
+        cell = -1;
+        return;
+    }
+    const int ix = (int)fx, iy = (int)fy;
+    tile = (iy / BIN_TS) * kb.tiles_x + ix / BIN_TS;
+    cell = iy * rs.nx + ix;
+}
+
+__global__ __launch_bounds__(256) void k_bin_count(KBin kb, KRaster rs,
+                                                   int32_t* __restrict__ counts) {
+    extern __shared__ int32_t hist[];
+    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256) hist[t] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 256 * BIN_ITEMS;
+    for (int it = 0; it < BIN_ITEMS; ++it) {
+        const int64_t g = base + (int64_t)it * 256 + threadIdx.x;
+        if (g >= kb.n_wp) break;
+        int32_t tile, cell;
+        bin_point(kb, rs, g, tile, cell);
+        atomicAdd(&hist[tile], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256)
+        counts[(int64_t)t * kb.n_blocks + blockIdx.x] = hist[t];  // tile-major
+}
+
+__global__ __launch_bounds__(256) void k_bin_scatter(KBin kb, KRaster rs,
+                                                     const int32_t* __restrict__ offs,
+                                                     uint2* __restrict__ bucket) {
+    extern __shared__ int32_t cur[];
+    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256)
+        cur[t] = offs[(int64_t)t * kb.n_blocks + blockIdx.x];
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 256 * BIN_ITEMS;
+    for (int it = 0; it < BIN_ITEMS; ++it) {
+        const int64_t g = base + (int64_t)it * 256 + threadIdx.x;
+        if (g >= kb.n_wp) break;
+        int32_t tile, cell;
+        bin_point(kb, rs, g, tile, cell);
+        const int32_t pos = atomicAdd(&cur[tile], 1);
+        bucket[pos] = make_uint2((uint32_t)g, (uint32_t)cell);
+    }
+}
+
+// exclusive scan of n int32 (n < 2^31): per-block scan, block-total scan, add
+constexpr int SCAN_ITEMS = 16;
+__global__ __launch_bounds__(256) void k_scan_local(const int32_t* __restrict__ in, int64_t n,
+                                                    int32_t* __restrict__ out,
+                                                    int32_t* __restrict__ totals) {
+    __shared__ int32_t wsum[4];
+    const int64_t base = (int64_t)blockIdx.x * 256 * SCAN_ITEMS + (int64_t)threadIdx.x * SCAN_ITEMS;
+    int32_t v[SCAN_ITEMS], run = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const int64_t i = base + k;
+        v[k] = i < n ? in[i] : 0;
+        const int32_t t = v[k];
+        v[k] = run;
+        run += t;
+    }
+    // inclusive scan of the thread totals across the block
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int32_t woff = 0;
+    for (int k = 0; k < wv; ++k) woff += wsum[k];
+    const int32_t excl = woff + x - run;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const int64_t i = base + k;
+        if (i < n) out[i] = v[k] + excl;
+    }
+    if (threadIdx.x == 255) totals[blockIdx.x] = woff + x;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_totals(int32_t* __restrict__ totals, int n) {
+    __shared__ int32_t buf[4096];
+    __shared__ int32_t part[1024];
+    int32_t run = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x * 4 + k;
+        buf[i] = i < n ? totals[i] : 0;
+    }
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x * 4 + k;
+        const int32_t t = buf[i];
+        buf[i] = run;
+        run += t;
+    }
+    part[threadIdx.x] = run;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of 1024 totals
+        const int32_t y = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    const int32_t excl = part[threadIdx.x] - run;
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x * 4 + k;
+        if (i < n) totals[i] = buf[i] + excl;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(int32_t* __restrict__ out, int64_t n,
+                                                  const int32_t* __restrict__ totals) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] += totals[i / (256 * SCAN_ITEMS)];
+}
+
+// XCD-pinned gather: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch);
+// group x = b % 8 walks the tiles t == x (mod 8), its K blocks splitting each tile's bucket,
+// so a tile's 1 MiB of records is fetched into one XCD's L2 and served from there.
+constexpr int GATHER_CH = 2048;  // entries per block step (8 per thread)
+__global__ __launch_bounds__(256) void k_bin_gather(const uint2* __restrict__ bucket,
+                                                    const int32_t* __restrict__ offs,
+                                                    int32_t n_tiles, int32_t n_blocks_bin,
+                                                    int64_t n_wp,
+                                                    const uint4* __restrict__ rec,
+                                                    uint4* __restrict__ recs, int K) {
+    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
+    for (int t = x; t <= n_tiles; t += 8) {
+        const int64_t b0 = offs[(int64_t)t * n_blocks_bin];
+        const int64_t b1 = t < n_tiles ? offs[(int64_t)(t + 1) * n_blocks_bin] : n_wp;
+        for (int64_t c0 = b0 + (int64_t)r * GATHER_CH; c0 < b1; c0 += (int64_t)K * GATHER_CH) {
+            uint2 e[GATHER_CH / 256];
+            uint4 v[GATHER_CH / 256];
+#pragma unroll
+            for (int k = 0; k < GATHER_CH / 256; ++k) {
+                const int64_t i = c0 + (int64_t)k * 256 + threadIdx.x;
+                e[k] = i < b1 ? bucket[i] : make_uint2(0xffffffffu, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < GATHER_CH / 256; ++k) {
+                if (e[k].x == 0xffffffffu) continue;
+                v[k] = (t < n_tiles) ? rec[e[k].y] : make_uint4(0, 0, 0, REC_OFF);
+            }
+#pragma unroll
+            for (int k = 0; k < GATHER_CH / 256; ++k)
+                if (e[k].x != 0xffffffffu) recs[e[k].x] = v[k];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -2230,6 +2450,8 @@ struct uam_ctx {
     std::vector<DevIneq> h_ineq;
     std::vector<DevShape> h_shape;
     int32_t* d_grid = nullptr;  // shape-grid index (KShapeGrid), rebuilt by uam_set_params
+    void* d_ws = nullptr;       // grow-only scratch of the binned evaluation (K2b)
+    size_t ws_bytes = 0;
 };
 
 namespace {
@@ -2321,6 +2543,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
+    if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     delete ctx;
 }
 
@@ -2679,6 +2902,59 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
     return UAM_OK;
 }
 
+// K2b launch; returns 1 if launched, 0 if the batch does not fit (caller falls back)
+static int launch_binned(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
+                         int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
+                         int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    if (ko.cells || D > 16) return 0;
+    const int64_t W = ctx->kp.N + 2, P = n_pairs * D, n_wp = P * W;
+    if (n_wp >= INT32_MAX) return 0;
+    const int tiles_x = (kr.nx + BIN_TS - 1) / BIN_TS, tiles_y = (kr.ny + BIN_TS - 1) / BIN_TS;
+    const int64_t NT = (int64_t)tiles_x * tiles_y;
+    const int64_t NB = (n_wp + 256 * BIN_ITEMS - 1) / (256 * BIN_ITEMS);
+    const int64_t ncount = (NT + 1) * NB;
+    const int64_t nsb = (ncount + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    if (NT + 1 > 8192 || nsb > 4096) return 0;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_counts = al(ncount * 4), b_offs = al(ncount * 4), b_tot = al(4096 * 4),
+                 b_bucket = al((size_t)n_wp * 8), b_recs = al((size_t)n_wp * 16);
+    const size_t need = b_counts + b_offs + b_tot + b_bucket + b_recs;
+    if (need > ctx->ws_bytes) {
+        if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+        ctx->d_ws = nullptr;
+        ctx->ws_bytes = 0;
+        if (hipMalloc(&ctx->d_ws, need) != hipSuccess) return fail(UAM_E_NOMEM, "binned scratch");
+        ctx->ws_bytes = need;
+    }
+    char* w = (char*)ctx->d_ws;
+    int32_t* counts = (int32_t*)w;
+    int32_t* offs = (int32_t*)(w + b_counts);
+    int32_t* tot = (int32_t*)(w + b_counts + b_offs);
+    uint2* bucket = (uint2*)(w + b_counts + b_offs + b_tot);
+    uint4* recs = (uint4*)(w + b_counts + b_offs + b_tot + b_bucket);
+    KBin kb{pairs, utab, D, (int32_t)W, n_wp, tiles_x, (int32_t)NT, (int32_t)NB};
+    const size_t hist = (size_t)(NT + 1) * sizeof(int32_t);
+    hipLaunchKernelGGL(k_bin_count, dim3((unsigned)NB), dim3(256), hist, s, kb, kr, counts);
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, counts, ncount, offs,
+                       tot);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, tot, (int)nsb);
+    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(ncount, 256, INT32_MAX)), dim3(256), 0, s, offs,
+                       ncount, tot);
+    hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)NB), dim3(256), hist, s, kb, kr, offs,
+                       bucket);
+    const int K = 128;  // blocks per XCD group
+    hipLaunchKernelGGL(k_bin_gather, dim3(8 * K), dim3(256), 0, s, bucket, offs, (int32_t)NT,
+                       (int32_t)NB, n_wp, (const uint4*)rec, recs, K);
+    const int64_t blocks = (n_pairs + 63) / 64;
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    const KVolume kv{};
+    hipLaunchKernelGGL((k_eval_pairs<MODE_RECORDS, 8, false, 1>), dim3((unsigned)blocks),
+                       dim3(64 * D), lds, s, ctx->kg, ctx->kp, kr, kv, (const uint4*)recs, pairs,
+                       n_pairs, utab, D, ko, best_f, best_l);
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "binned evaluation launch");
+    return 1;
+}
+
 int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec, const double* pairs, int64_t n_pairs,
                        const double* utab, int32_t D, const uam_path_outputs* out,
@@ -2705,6 +2981,11 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
         const KVolume kv{};
         st = launch_wave(ctx, mode, true, kr, kv, rec, nullptr, pairs, utab, D, n_pairs * D, ko,
                          best_f, best_l, s);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
+    if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_BINNED) {
+        st = launch_binned(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
         if (st == 1) return UAM_OK;
     }
