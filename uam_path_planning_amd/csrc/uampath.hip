@@ -3265,16 +3265,22 @@ int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* t, const float* src,
 
 namespace {
 
+// stream-ordered scratch (the runtime's memory pool serves repeated calls without a device
+// synchronisation per allocation)
+thread_local hipStream_t g_devbuf_stream = nullptr;
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     int64_t n = 0;
+    hipStream_t s = nullptr;
     ~DevBuf() {
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, s);
     }
     hipError_t alloc(int64_t count) {
         n = count;
-        return hipMalloc(&p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
+        s = g_devbuf_stream;
+        return hipMallocAsync((void**)&p, (size_t)std::max<int64_t>(count, 1) * sizeof(T), s);
     }
 };
 
@@ -3379,21 +3385,55 @@ int row_extents(int32_t nx, int32_t ny, const int32_t* L, const int32_t* cid,
     return UAM_OK;
 }
 
-// hull input of one labelled region: the four corners of each row's [xmin, xmax] run;
-// column c spans [xlo[c], xhi[c]], row r spans [ylo[r], yhi[r]]
+// hull input of one labelled region: each row's [xmin, xmax] run contributes its four pixel
+// corners (column c spans [xlo[c], xhi[c]], row r spans [ylo[r], yhi[r]]).  Of the corners at
+// one float32 y only the smallest and largest x can be hull vertices, and of those only the
+// convex left / right chains; the hull's orientation test is exact on these float32
+// coordinates, so this O(rows) filter leaves the hull -- and cv2.minAreaRect -- unchanged
+// while the sort inside it sees a few dozen points instead of 4 per row
 void region_corners(int32_t ry0, int32_t ry1, const int32_t* xmin, const int32_t* xmax,
                     const std::vector<double>& xlo, const std::vector<double>& xhi,
                     const std::vector<double>& ylo, const std::vector<double>& yhi,
                     std::vector<uampoly::Pt>& pts) {
-    pts.clear();
+    struct Lvl {
+        float y, lo, hi;
+    };
+    thread_local std::vector<Lvl> lv;
+    thread_local std::vector<uampoly::Pt> ch;
+    lv.clear();
+    auto add = [&](double y, double lo, double hi) {
+        const float fy = (float)y, fl = (float)lo, fh = (float)hi;
+        if (!lv.empty() && lv.back().y == fy) {
+            lv.back().lo = std::min(lv.back().lo, fl);
+            lv.back().hi = std::max(lv.back().hi, fh);
+        } else {
+            lv.push_back({fy, fl, fh});
+        }
+    };
     for (int32_t r = ry0; r <= ry1; ++r) {
         const int32_t a = xmin[r - ry0], b = xmax[r - ry0];
         if (a > b) continue;
-        pts.push_back({xlo[a], yhi[r]});
-        pts.push_back({xlo[a], ylo[r]});
-        pts.push_back({xhi[b], yhi[r]});
-        pts.push_back({xhi[b], ylo[r]});
+        add(yhi[r], xlo[a], xhi[b]);
+        add(ylo[r], xlo[a], xhi[b]);
     }
+    // same predicate as the hull's: double arithmetic on float32 inputs
+    auto cross = [](const uampoly::Pt& o, const uampoly::Pt& a, const uampoly::Pt& b) {
+        return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x);
+    };
+    auto chain = [&](bool left) {
+        ch.clear();
+        const int64_t m = (int64_t)lv.size();
+        for (int64_t i = 0; i < m; ++i) {
+            const Lvl& e = lv[left ? i : m - 1 - i];  // left: top -> bottom, right: bottom -> top
+            const uampoly::Pt p{(double)(left ? e.lo : e.hi), (double)e.y};
+            while (ch.size() >= 2 && cross(ch[ch.size() - 2], ch.back(), p) <= 0) ch.pop_back();
+            ch.push_back(p);
+        }
+        pts.insert(pts.end(), ch.begin(), ch.end());
+    };
+    pts.clear();
+    chain(true);
+    chain(false);
 }
 
 void emit_rect(const std::vector<uampoly::Pt>& pts, double min_approx,
@@ -3422,6 +3462,7 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
                  DY = rd->dy * unit_m;
     DeviceGuard dg(ctx->device);
     hipStream_t s = (hipStream_t)stream;
+    g_devbuf_stream = s;
     DevBuf<int32_t> L, cid;
     HIP_TRY2(L.alloc(n));
     hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, dem,
