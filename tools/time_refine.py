@@ -1,5 +1,6 @@
 """Time batched refinement (uam_refine) on generated candidates of the canonical map.
-usage: python tools/time_refine.py [--pairs Q] [--N N] [--outer O] [--inner I] [--nfz K]"""
+usage: python tools/time_refine.py [--pairs Q] [--N N] [--outer O] [--inner I] [--nfz K]
+       [--memory M]"""
 import argparse
 import json
 import os
@@ -15,6 +16,9 @@ def main():
     ap.add_argument("--outer", type=int, default=10)
     ap.add_argument("--inner", type=int, default=20)
     ap.add_argument("--nfz", type=int, default=0)
+    ap.add_argument("--memory", type=int, default=8)
+    ap.add_argument("--empty", action="store_true",
+                    help="same regions and weights, no shapes (isolates the geometry cost)")
     a = ap.parse_args()
     import torch
     from uam_path_planning_amd.arcs import arc_table
@@ -25,12 +29,16 @@ def main():
     from uam_path_planning_amd.synthetic import random_pairs
 
     spec = canonical_spec(nfz_polygons=a.nfz)
+    if a.empty:
+        spec["obstacles"] = []
+        for r in spec["regions"]:
+            r["shapes"] = []
     eng = Engine(0)
     eng.set_geometry(compile_map(build_region_map(spec)))
     eng.set_params(canonical_params(spec, N=a.N, anchor=tuple(spec["x_start"])))
     wp = eng.gen_paths(torch.tensor(random_pairs(a.pairs, seed=3), device="cuda"),
                        arc_table(a.N, displacements(5)))
-    rp = {"n_outer": a.outer, "n_inner": a.inner}
+    rp = {"n_outer": a.outer, "n_inner": a.inner, "memory": a.memory}
     eng.refine(wp[:64], rp)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,9 +50,10 @@ def main():
     ms = e0.elapsed_time(e1)
     c1 = out["cost"]
     P = wp.shape[0]
-    print(json.dumps({"paths": P, "N": a.N, "outer": a.outer, "inner": a.inner, "nfz": a.nfz,
+    print(json.dumps({"paths": P, "N": a.N, "outer": a.outer, "inner": a.inner, "nfz": a.nfz, "empty": a.empty,
                       "ms": ms, "paths_per_s": P / (ms / 1e3),
-                      "steps_mean": float(out["iters"].double().mean()),
+                      "memory": a.memory, "steps_mean": float(out["iters"].double().mean()),
+                      "steps_per_s": float(out["iters"].double().sum()) / (ms / 1e3),
                       "cost_before_mean": float(c0.mean()), "cost_after_mean": float(c1.mean()),
                       "improved_frac": float((c1 < c0).double().mean()),
                       "infeas_median": float(out["infeas"].median())}))

@@ -1051,9 +1051,38 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// v of lane l ^ OFF (whole wave active).  32 / 16: gfx950's permlane swaps; 8: DPP row_ror:8
+// (= xor 8 inside a 16-lane row); 4: row_ror:4 reads lane l^4 or l^4^8, which hold the same
+// value once the xor-8 stage has run (wave_sum only); 2 / 1: DPP quad_perm.  All VALU, no
+// LDS round trip (ds_bpermute) per stage.
+template <int OFF>
+__device__ __forceinline__ double lane_xor(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    if constexpr (OFF == 32 || OFF == 16) {
+        const auto a = OFF == 32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                                 : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = OFF == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                                 : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        const bool upper = (threadIdx.x & OFF) != 0;  // lanes whose partner is below them
+        lo = upper ? a[0] : a[1];
+        hi = upper ? b[0] : b[1];
+    } else {
+        constexpr int ctrl = OFF == 8 ? 0x128 : (OFF == 4 ? 0x124 : (OFF == 2 ? 0x4E : 0xB1));
+        lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, ctrl, 0xf, 0xf, false);
+        hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, ctrl, 0xf, 0xf, false);
+    }
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// xor butterfly 32..1 (the oracle's wsum tree); every lane ends with the same value
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    v = v + lane_xor<32>(v);
+    v = v + lane_xor<16>(v);
+    v = v + lane_xor<8>(v);
+    v = v + lane_xor<4>(v);
+    v = v + lane_xor<2>(v);
+    v = v + lane_xor<1>(v);
     return v;
 }
 
@@ -1063,8 +1092,8 @@ struct RfPath {
     const double* dr;  // LDS [W][2] search direction
     const double* yk;  // LDS [3N]
     const double* yo;  // global [S][W]
-    const uint64_t* act;  // LDS [W][RF_MASKW]: rows with a nonzero multiplier (null: no masks)
-    int N, W;
+    const uint64_t* act;  // LDS [W][nmw]: rows with a nonzero multiplier (null: no masks)
+    int N, W, nmw;
     __device__ __forceinline__ void pt(int j, double a, double& x, double& y) const {
         x = z[2 * j];
         y = z[2 * j + 1];
@@ -1092,16 +1121,23 @@ __device__ __forceinline__ double wdot(const double* u, const double* v, int N, 
 // visited in ascending order.  No index / NaN point: all rows.
 constexpr int RF_MASKW = 4;  // bitmask words per waypoint: S <= 256 uses the masks
 
+// mask words per waypoint for S obstacles (0: no masks); sizes the wave's LDS slice, so maps
+// with <= 64 obstacles keep 6 waves per SIMD resident
+__host__ __device__ __forceinline__ int rf_mask_words(int S) {
+    return (S > 0 && S <= 64 * RF_MASKW) ? (S + 63) >> 6 : 0;
+}
+
 __device__ __forceinline__ uint64_t pick_word(const uint64_t (&cw)[RF_MASKW], int w) {
     return w == 0 ? cw[0] : (w == 1 ? cw[1] : (w == 2 ? cw[2] : cw[3]));  // no dynamic index
 }
 
 __device__ __forceinline__ void rf_candidates(const KGeom& g, double x, double y,
-                                              const uint64_t* act, uint64_t (&cw)[RF_MASKW]) {
+                                              const uint64_t* act, int nmw,
+                                              uint64_t (&cw)[RF_MASKW]) {
     const int S = g.n_obstacles;
     const int slot = g.grid.gx ? grid_slot(g.grid, x, y) : -1;
 #pragma unroll
-    for (int w = 0; w < RF_MASKW; ++w) cw[w] = act ? act[w] : 0ull;
+    for (int w = 0; w < RF_MASKW; ++w) cw[w] = (act && w < nmw) ? act[w] : 0ull;
     if (slot < 0) {
 #pragma unroll
         for (int w = 0; w < RF_MASKW; ++w) {
@@ -1135,8 +1171,9 @@ __device__ __forceinline__ double seg_term(double px, double py, double qx, doub
 
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
 // gradient accumulation order as oracle refine_L.
-__device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int lane, double a,
-                       double c, bool want, double* fout, double* gn2) {
+__device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp,
+                                       int lane, double a, double c, bool want, double* fout,
+                                       double* gn2) {
     const int N = rp.N, W = rp.W;
     const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     const double hc = 0.5 * c, dN = (double)N, sc = (double)(N + 1);
@@ -1219,7 +1256,7 @@ __device__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp, int l
         };
         if (rp.act) {
             uint64_t cw[RF_MASKW];
-            rf_candidates(g, xj, yj, rp.act + (int64_t)j * RF_MASKW, cw);
+            rf_candidates(g, xj, yj, rp.act + (int64_t)j * rp.nmw, rp.nmw, cw);
             const int nw = (g.n_obstacles + 63) >> 6;
 #pragma unroll 1
             for (int w = 0; w < nw; ++w)
@@ -1299,25 +1336,27 @@ __device__ void lbfgs_dir(const double* gr, double* dr, const double* hs, const 
     }
 }
 
-__global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
-                                                double* __restrict__ wp, int64_t P,
-                                                double* __restrict__ ws,
-                                                double* __restrict__ cost,
-                                                double* __restrict__ infeas,
-                                                int32_t* __restrict__ iters) {
+// register budget: <= 128 VGPRs keeps 4 waves per SIMD (rf_L inlined at every call site; an
+// out-of-line call spills around s_swappc)
+#ifndef UAM_RF_WAVES
+#define UAM_RF_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVES))) void k_refine(
+    KGeom g, KParams p, KRefine rf, double* __restrict__ wp, int64_t P, double* __restrict__ ws,
+    double* __restrict__ cost, double* __restrict__ infeas, int32_t* __restrict__ iters) {
     extern __shared__ double rf_lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int64_t path = (int64_t)blockIdx.x * wpb + wave;
     if (path >= P) return;  // whole wave
     const int N = p.N, W = N + 2, S = g.n_obstacles;
     const int m = rf.memory < 0 ? 0 : (rf.memory > RF_MAXM ? RF_MAXM : rf.memory);
-    const bool use_mask = S <= 64 * RF_MASKW;
-    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM + RF_MASKW * W);
+    const int nmw = rf_mask_words(S);
+    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM + nmw * W);
     double* gr = z + 2 * W;
     double* dr = gr + 2 * W;
     double* yk = dr + 2 * W;
     double* rho = yk + 3 * N;
-    uint64_t* act = use_mask ? reinterpret_cast<uint64_t*>(rho + RF_MAXM) : nullptr;
+    uint64_t* act = nmw ? reinterpret_cast<uint64_t*>(rho + RF_MAXM) : nullptr;
     double* zg = wp + path * (int64_t)W * 2;
     double* yo = ws + path * ((int64_t)S * W + (int64_t)m * 4 * W);
     double* hs = yo + (int64_t)S * W;
@@ -1329,11 +1368,11 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
     }
     for (int k = lane; k < 3 * N; k += 64) yk[k] = 0.0;
     if (act)
-        for (int k = lane; k < RF_MASKW * W; k += 64) act[k] = 0ull;
+        for (int k = lane; k < nmw * W; k += 64) act[k] = 0ull;
     for (int s = 0; s < S; ++s)
         for (int j = lane; j < W; j += 64) yo[(int64_t)s * W + j] = 0.0;
     wave_sync();
-    RfPath rp{z, gr, dr, yk, yo, act, N, W};
+    RfPath rp{z, gr, dr, yk, yo, act, N, W, nmw};
     const bool ms = p.maxratio_smooth != 0;
     double c = rf.c0, alpha = rf.alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
     int32_t used = 0;
@@ -1442,11 +1481,11 @@ __global__ __launch_bounds__(256) void k_refine(KGeom g, KParams p, KRefine rf,
                 double* yi = yo + (int64_t)s * W + j;
                 *yi = *yi + c * v;
                 sj = sj + v * v;
-                if (act && v != 0.0) act[(int64_t)j * RF_MASKW + (s >> 6)] |= 1ull << (s & 63);
+                if (act && v != 0.0) act[(int64_t)j * nmw + (s >> 6)] |= 1ull << (s & 63);
             };
             if (act) {  // rows with psi = 0 leave y and the sum unchanged
                 uint64_t cw[RF_MASKW];
-                rf_candidates(g, xj, yj, nullptr, cw);
+                rf_candidates(g, xj, yj, nullptr, 0, cw);
                 const int nw = (S + 63) >> 6;
 #pragma unroll 1
                 for (int w = 0; w < nw; ++w)
@@ -3132,7 +3171,8 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
         !(rp->max_step > 0.0) || rp->memory < 0 || rp->memory > RF_MAXM)
         return fail(UAM_E_INVALID, "bad refine params (memory must be 0..%d)", RF_MAXM);
     const int64_t N = ctx->kp.N, W = N + 2;
-    const int64_t per_wave = (6 * W + 3 * N + RF_MAXM + RF_MASKW * W) * (int64_t)sizeof(double);
+    const int64_t per_wave =
+        (6 * W + 3 * N + RF_MAXM + rf_mask_words(ctx->kg.n_obstacles) * W) * (int64_t)sizeof(double);
     if (per_wave > 65536)
         return fail(UAM_E_INVALID, "N = %lld too large for refinement (LDS)", (long long)N);
     if (n_paths == 0) return UAM_OK;
