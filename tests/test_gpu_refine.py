@@ -168,3 +168,28 @@ def test_refine_large_paths_and_many_obstacles(eng, oracle_mod):
                  many["enlargement"], many["weights"], tuple(many["x_start"]))
     wp = oracle_mod.gen_paths(random_pairs(8, seed=12), arc_table(30, displacements(5)))
     _check(eng, orc, oracle_mod, wp, n_outer=2, n_inner=6)
+
+
+def test_refine_mask_widths_and_region_list_walk(eng, oracle_mod):
+    """The wave-cooperative geometry walk in each of its forms: 106 obstacles (two active-row
+    mask words per waypoint) and a region table of more than 256 shapes (no per-cell bitmask:
+    the lanes' lists are merged by their minimum head)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements
+    from uam_path_planning_amd.synthetic import random_convex_polygons, random_pairs
+
+    opts = {"length_smooth": True, "penalty_smooth": True, "obstacle_smooth": True,
+            "maxratio_smooth": False}
+    two = canonical_spec(nfz_polygons=100, seed=5)           # 106 obstacles
+    orc = _setup(eng, oracle_mod, two, 40, opts, two["maxratio"], two["maxalpha"],
+                 two["enlargement"], two["weights"], tuple(two["x_start"]))
+    wp = oracle_mod.gen_paths(random_pairs(8, seed=13), arc_table(40, displacements(5)))
+    _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=8)
+    big = canonical_spec()
+    big["regions"][1]["shapes"] = big["regions"][1]["shapes"] + [
+        {"kind": "polygon", "vertices": v} for v in random_convex_polygons(260, seed=6)]
+    assert sum(len(r["shapes"]) for r in big["regions"]) > 256
+    orc = _setup(eng, oracle_mod, big, 40, opts, big["maxratio"], big["maxalpha"],
+                 big["enlargement"], big["weights"], tuple(big["x_start"]))
+    wp = oracle_mod.gen_paths(random_pairs(8, seed=14), arc_table(40, displacements(5)))
+    _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=8)

@@ -85,6 +85,10 @@ struct KShapeGrid {
     int32_t gx, gy;
     const int32_t* start[3];  // 0 = region penalty (box_pen), 1 = psi, 2 = hit
     const int32_t* items[3];
+    // lists 0 and 1 as per-slot bitmasks (bit i of word w: shape mbase + 64 w + i), mw words
+    // per slot; null when the table spans more than 256 shapes
+    const uint64_t* mask[2];
+    int32_t mbase[2], mw[2];
 };
 
 struct KGeom {
@@ -1056,23 +1060,46 @@ __device__ __forceinline__ void wave_sync() {
 // value once the xor-8 stage has run (wave_sum only); 2 / 1: DPP quad_perm.  All VALU, no
 // LDS round trip (ds_bpermute) per stage.
 template <int OFF>
-__device__ __forceinline__ double lane_xor(double v) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v) {
     if constexpr (OFF == 32 || OFF == 16) {
-        const auto a = OFF == 32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
-                                 : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-        const auto b = OFF == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
-                                 : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-        const bool upper = (threadIdx.x & OFF) != 0;  // lanes whose partner is below them
-        lo = upper ? a[0] : a[1];
-        hi = upper ? b[0] : b[1];
+        const auto a = OFF == 32 ? __builtin_amdgcn_permlane32_swap(v, v, false, false)
+                                 : __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & OFF) != 0 ? a[0] : a[1];  // a[0]: partner below, a[1]: above
     } else {
         constexpr int ctrl = OFF == 8 ? 0x128 : (OFF == 4 ? 0x124 : (OFF == 2 ? 0x4E : 0xB1));
-        lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, ctrl, 0xf, 0xf, false);
-        hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, ctrl, 0xf, 0xf, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xf, 0xf, false);
     }
+}
+
+template <int OFF>
+__device__ __forceinline__ double lane_xor(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = lane_xor_u32<OFF>((uint32_t)u), hi = lane_xor_u32<OFF>((uint32_t)(u >> 32));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// wave-wide min / or (whole wave active; order-free, so the xor-4 stage may read l^4^8)
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+    v = min(v, (int32_t)lane_xor_u32<32>((uint32_t)v));
+    v = min(v, (int32_t)lane_xor_u32<16>((uint32_t)v));
+    v = min(v, (int32_t)lane_xor_u32<8>((uint32_t)v));
+    v = min(v, (int32_t)lane_xor_u32<4>((uint32_t)v));
+    v = min(v, (int32_t)lane_xor_u32<2>((uint32_t)v));
+    v = min(v, (int32_t)lane_xor_u32<1>((uint32_t)v));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo |= lane_xor_u32<32>(lo), hi |= lane_xor_u32<32>(hi);
+    lo |= lane_xor_u32<16>(lo), hi |= lane_xor_u32<16>(hi);
+    lo |= lane_xor_u32<8>(lo), hi |= lane_xor_u32<8>(hi);
+    lo |= lane_xor_u32<4>(lo), hi |= lane_xor_u32<4>(hi);
+    lo |= lane_xor_u32<2>(lo), hi |= lane_xor_u32<2>(hi);
+    lo |= lane_xor_u32<1>(lo), hi |= lane_xor_u32<1>(hi);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // xor butterfly 32..1 (the oracle's wsum tree); every lane ends with the same value
@@ -1146,6 +1173,13 @@ __device__ __forceinline__ void rf_candidates(const KGeom& g, double x, double y
         }
         return;
     }
+    if (g.grid.mask[1]) {  // mbase[1] == 0: bit s is obstacle s
+        const uint64_t* m = g.grid.mask[1] + (int64_t)slot * g.grid.mw[1];
+#pragma unroll
+        for (int w = 0; w < RF_MASKW; ++w)
+            if (w < g.grid.mw[1]) cw[w] |= m[w];
+        return;
+    }
     const int k1 = g.grid.start[1][slot + 1];
     for (int k = g.grid.start[1][slot]; k < k1; ++k) {
         const int sh = g.grid.items[1][k];
@@ -1169,8 +1203,141 @@ __device__ __forceinline__ double seg_term(double px, double py, double qx, doub
     return ls ? n * n : n;
 }
 
+// Read-only table entry at a wave-uniform index through the constant address space: the
+// geometry tables do not change during a launch, and this lets the compiler use scalar loads
+// (s_load) even though the kernel stores to global memory (which rules out its noclobber
+// proof for plain global loads).
+template <typename T>
+__device__ __forceinline__ T uload(const T* base, int i) {
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    using CW = const __attribute__((address_space(4))) uint32_t;
+    CW* src = (CW*)(base + i);
+    T out;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) dst[k] = src[k];
+    return out;
+}
+
+// psi_vg for a wave-uniform shape (records through uload); same operations as psi_vg
+__device__ __forceinline__ double psi_vg_u(const KGeom& g, const DevShape& sh, double x0,
+                                           double x1, double e, bool want, double& dx,
+                                           double& dy) {
+    double v = 1.0;
+    const int end = sh.first + sh.count;
+    for (int i = sh.first; i < end; ++i) {
+        const DevIneq q = uload(g.ineq, i);
+        const double m = fmin(ineq_h(&q, x0, x1) - e, 0.0);
+        v = v * (m * m);
+    }
+    dx = 0.0;
+    dy = 0.0;
+    if (want && v != 0.0) {
+        double ox = 0.0, oy = 0.0;
+        for (int i = sh.first; i < end; ++i) {
+            const DevIneq q = uload(g.ineq, i);
+            const double m = fmin(ineq_h(&q, x0, x1) - e, 0.0);
+            const double coef = (2.0 * v) / m;
+            double hx, hy;
+            ineq_grad(&q, x0, x1, hx, hy);
+            ox = ox + coef * hx;
+            oy = oy + coef * hy;
+        }
+        dx = ox;
+        dy = oy;
+    }
+    return v;
+}
+
+// Phi and grad Phi at every lane's point, computed by the wave together (uniform control flow,
+// whole wave active; lanes with !valid contribute nothing).  Each lane walks its own grid list
+// in ascending order exactly as phi_vg does, so its sums are bit-identical to phi_vg; the wave
+// visits the union of the lanes' lists in ascending order (the minimum of the lane heads), so
+// the shape index is wave-uniform and the shape and inequality records come through scalar
+// loads instead of per-lane dependent gathers.  No index or a NaN point: phi_vg itself.
+__device__ __forceinline__ double phi_vg_wave(const KGeom& g, const KParams& p, double x0,
+                                              double x1, bool valid, bool want, double& dx,
+                                              double& dy) {
+    const int slot = valid ? (g.grid.gx ? grid_slot(g.grid, x0, x1) : -1) : -2;
+    double pen = 0.0, gx = 0.0, gy = 0.0;
+    int k = 0, k1 = 0;
+    if (slot >= 0) {
+        k = g.grid.start[0][slot];
+        k1 = g.grid.start[0][slot + 1];
+    }
+    double t = 0.0, tx = 0.0, ty = 0.0;
+    int rc = -1;
+    // the lane's list as bitmask words (ascending bits = ascending shapes), or -- tables over
+    // 256 shapes -- a cursor into the list
+    const int mw = g.grid.mask[0] ? g.grid.mw[0] : 0;
+    uint64_t lm[RF_MASKW] = {0ull, 0ull, 0ull, 0ull};
+    if (mw && slot >= 0) {
+        const uint64_t* m = g.grid.mask[0] + (int64_t)slot * mw;
+#pragma unroll
+        for (int w = 0; w < RF_MASKW; ++w)
+            if (w < mw) lm[w] = m[w];
+    }
+    int w = 0;
+    uint64_t ub = mw ? wave_or_u64(lm[0]) : 0ull;
+    for (;;) {
+        int s, cand;
+        if (mw) {  // next set bit of the union, wave-uniform
+            while (!ub && ++w < mw) ub = wave_or_u64(pick_word(lm, w));
+            if (!ub) break;
+            const int bit = __builtin_ctzll(ub);
+            ub &= ub - 1;
+            s = g.grid.mbase[0] + 64 * w + bit;
+            cand = ((pick_word(lm, w) >> bit) & 1ull) ? s : INT32_MAX;
+        } else {
+            cand = k < k1 ? g.grid.items[0][k] : INT32_MAX;
+            s = wave_min_i32(cand);  // wave-uniform
+            if (s == INT32_MAX) break;
+        }
+        if (cand == s) {
+            ++k;
+            const DevShape sh = uload(g.shape, s);
+            if (sh.region != rc) {
+                if (rc >= 0) {
+                    pen = pen + p.weights[rc] * t;
+                    gx = gx + p.weights[rc] * tx;
+                    gy = gy + p.weights[rc] * ty;
+                }
+                rc = sh.region;
+                t = tx = ty = 0.0;
+            }
+            if (!((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x0, x1))) {
+                double ex, ey;
+                const double v = psi_vg_u(g, sh, x0, x1, p.enlargement, want, ex, ey);
+                if (sh.has_center) {
+                    t = t + v / sh.norm_pen;
+                    if (want && v != 0.0) {
+                        tx = tx + ex / sh.norm_pen;
+                        ty = ty + ey / sh.norm_pen;
+                    }
+                } else {
+                    t = t + v;
+                    if (want && v != 0.0) {
+                        tx = tx + ex;
+                        ty = ty + ey;
+                    }
+                }
+            }
+        }
+    }
+    if (rc >= 0) {
+        pen = pen + p.weights[rc] * t;
+        gx = gx + p.weights[rc] * tx;
+        gy = gy + p.weights[rc] * ty;
+    }
+    if (slot == -1) pen = phi_vg(g, p, x0, x1, want, gx, gy);
+    dx = gx;
+    dy = gy;
+    return pen;
+}
+
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
-// gradient accumulation order as oracle refine_L.
+// gradient accumulation order as oracle refine_L.  The waypoint loop runs a wave-uniform trip
+// count (lane j = jb + lane, valid = j < W) so the geometry can be walked by the whole wave.
 __device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const RfPath& rp,
                                        int lane, double a, double c, bool want, double* fout,
                                        double* gn2) {
@@ -1179,73 +1346,78 @@ __device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const R
     const double hc = 0.5 * c, dN = (double)N, sc = (double)(N + 1);
     const int kend = p.quirk_length ? N : N + 1;
     double sl = 0.0, sphi = 0.0, saug = 0.0, sg = 0.0;
-    for (int j = lane; j < W; j += 64) {
-        const bool inner = want && j >= 1 && j <= N;
-        double xj, yj;
-        rp.pt(j, a, xj, yj);
-        double lj = 0.0, vx0 = 0.0, vy0 = 0.0;
-        if (j == 0) {
-            if (p.quirk_length) {
-                const double ax = p.anchor_mode ? p.anchor_x : xj;
-                const double ay = p.anchor_mode ? p.anchor_y : yj;
-                lj = seg_term(ax, ay, xj, yj, ls, sc, false, vx0, vy0);
-            }
-        } else if (j <= kend) {
-            double px, py;
-            rp.pt(j - 1, a, px, py);
-            lj = seg_term(px, py, xj, yj, ls, sc, inner, vx0, vy0);
-        }
-        sl = sl + lj;
+    for (int jb = 0; jb < W; jb += 64) {
+        const int j = jb + lane;
+        const bool valid = j < W;
+        const bool inner = want && valid && j >= 1 && j <= N;
+        double xj = 0.0, yj = 0.0;
+        if (valid) rp.pt(j, a, xj, yj);
         double ex, ey;
-        sphi = sphi + phi_vg(g, p, xj, yj, inner, ex, ey) / dN;
+        const double ph = phi_vg_wave(g, p, xj, yj, valid, inner, ex, ey);
         double aj = 0.0, gx = 0.0, gy = 0.0;
-        if (j < N) {
-            double q1x, q1y, q2x, q2y, cv[3], dq[3][2];
-            rp.pt(j + 1, a, q1x, q1y);
-            rp.pt(j + 2, a, q2x, q2y);
-            kin_col(xj, yj, q1x, q1y, q2x, q2y, p.r_eff, p.mincos, ms, -1, cv, dq);
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const double tt = cv[t] + rp.yk[3 * j + t] / c;
-                aj = aj + hc * (tt * tt);
+        if (valid) {
+            double lj = 0.0, vx0 = 0.0, vy0 = 0.0;
+            if (j == 0) {
+                if (p.quirk_length) {
+                    const double ax = p.anchor_mode ? p.anchor_x : xj;
+                    const double ay = p.anchor_mode ? p.anchor_y : yj;
+                    lj = seg_term(ax, ay, xj, yj, ls, sc, false, vx0, vy0);
+                }
+            } else if (j <= kend) {
+                double px, py;
+                rp.pt(j - 1, a, px, py);
+                lj = seg_term(px, py, xj, yj, ls, sc, inner, vx0, vy0);
             }
-        }
-        if (inner) {
-            if (j <= kend) {
-                gx = gx + vx0;
-                gy = gy + vy0;
-            }
-            if (j + 1 <= kend) {
-                double qx, qy, vx, vy;
-                rp.pt(j + 1, a, qx, qy);
-                seg_term(xj, yj, qx, qy, ls, sc, true, vx, vy);
-                gx = gx - vx;
-                gy = gy - vy;
-            }
-            gx = gx + ex / dN;
-            gy = gy + ey / dN;
-            for (int q = 2; q >= 0; --q) {  // k = j - q ascending
-                const int k = j - q;
-                if (k < 0 || k >= N) continue;
-                double k0x, k0y, k1x, k1y, k2x, k2y, cv[3], dq[3][2];
-                rp.pt(k, a, k0x, k0y);
-                rp.pt(k + 1, a, k1x, k1y);
-                rp.pt(k + 2, a, k2x, k2y);
-                kin_col(k0x, k0y, k1x, k1y, k2x, k2y, p.r_eff, p.mincos, ms, q, cv, dq);
+            sl = sl + lj;
+            sphi = sphi + ph / dN;
+            if (j < N) {
+                double q1x, q1y, q2x, q2y, cv[3], dq[3][2];
+                rp.pt(j + 1, a, q1x, q1y);
+                rp.pt(j + 2, a, q2x, q2y);
+                kin_col(xj, yj, q1x, q1y, q2x, q2y, p.r_eff, p.mincos, ms, -1, cv, dq);
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
-                    if (!(cv[t] > 0.0)) continue;
-                    const double coef = c * (cv[t] + rp.yk[3 * k + t] / c);
-                    gx = gx + coef * dq[t][0];
-                    gy = gy + coef * dq[t][1];
+                    const double tt = cv[t] + rp.yk[3 * j + t] / c;
+                    aj = aj + hc * (tt * tt);
+                }
+            }
+            if (inner) {
+                if (j <= kend) {
+                    gx = gx + vx0;
+                    gy = gy + vy0;
+                }
+                if (j + 1 <= kend) {
+                    double qx, qy, vx, vy;
+                    rp.pt(j + 1, a, qx, qy);
+                    seg_term(xj, yj, qx, qy, ls, sc, true, vx, vy);
+                    gx = gx - vx;
+                    gy = gy - vy;
+                }
+                gx = gx + ex / dN;
+                gy = gy + ey / dN;
+                for (int q = 2; q >= 0; --q) {  // k = j - q ascending
+                    const int k = j - q;
+                    if (k < 0 || k >= N) continue;
+                    double k0x, k0y, k1x, k1y, k2x, k2y, cv[3], dq[3][2];
+                    rp.pt(k, a, k0x, k0y);
+                    rp.pt(k + 1, a, k1x, k1y);
+                    rp.pt(k + 2, a, k2x, k2y);
+                    kin_col(k0x, k0y, k1x, k1y, k2x, k2y, p.r_eff, p.mincos, ms, q, cv, dq);
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) {
+                        if (!(cv[t] > 0.0)) continue;
+                        const double coef = c * (cv[t] + rp.yk[3 * k + t] / c);
+                        gx = gx + coef * dq[t][0];
+                        gy = gy + coef * dq[t][1];
+                    }
                 }
             }
         }
-        auto obstacle_row = [&](int s) {
-            const DevShape& sh = g.shape[s];
+        auto obstacle_row = [&](int s) {  // s wave-uniform
+            const DevShape sh = uload(g.shape, s);
             double v = 0.0, ox = 0.0, oy = 0.0;
             if (!((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xj, yj)))
-                v = psi_vg(g, sh, xj, yj, 0.0, inner, ox, oy);
+                v = psi_vg_u(g, sh, xj, yj, 0.0, inner, ox, oy);
             const double tt = v + rp.yo[(int64_t)s * W + j] / c;
             aj = aj + hc * (tt * tt);
             if (inner && v != 0.0) {
@@ -1255,24 +1427,32 @@ __device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const R
             }
         };
         if (rp.act) {
-            uint64_t cw[RF_MASKW];
-            rf_candidates(g, xj, yj, rp.act + (int64_t)j * rp.nmw, rp.nmw, cw);
+            // each lane's candidate rows in ascending order; the wave walks their union so
+            // the row index (and the shape's records) is wave-uniform
+            uint64_t cw[RF_MASKW] = {0ull, 0ull, 0ull, 0ull};
+            if (valid) rf_candidates(g, xj, yj, rp.act + (int64_t)j * rp.nmw, rp.nmw, cw);
             const int nw = (g.n_obstacles + 63) >> 6;
 #pragma unroll 1
-            for (int w = 0; w < nw; ++w)
-                for (uint64_t b = pick_word(cw, w); b; b &= b - 1)
-                    obstacle_row(64 * w + __builtin_ctzll(b));
-        } else {
+            for (int w = 0; w < nw; ++w) {
+                const uint64_t mine = pick_word(cw, w);
+                for (uint64_t b = wave_or_u64(mine); b; b &= b - 1) {
+                    const int bit = __builtin_ctzll(b);
+                    if ((mine >> bit) & 1ull) obstacle_row(64 * w + bit);
+                }
+            }
+        } else if (valid) {
             for (int s = 0; s < g.n_obstacles; ++s) obstacle_row(s);
         }
-        saug = saug + aj;
-        double tg = 0.0;
-        if (inner) {
-            rp.gr[2 * j] = gx;
-            rp.gr[2 * j + 1] = gy;
-            tg = gx * gx + gy * gy;
+        if (valid) {
+            saug = saug + aj;
+            double tg = 0.0;
+            if (inner) {
+                rp.gr[2 * j] = gx;
+                rp.gr[2 * j + 1] = gy;
+                tg = gx * gx + gy * gy;
+            }
+            sg = sg + tg;
         }
-        sg = sg + tg;
     }
     sl = wave_sum(sl);
     sphi = wave_sum(sphi);
@@ -1284,9 +1464,9 @@ __device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const R
 }
 
 // L-BFGS two-loop recursion: dr = -H gr over the cnt newest (s, y) pairs of the ring
-__device__ void lbfgs_dir(const double* gr, double* dr, const double* hs, const double* hy,
-                          const double* rho, double gamma, int m, int cnt, int head, int N,
-                          int W, int lane) {
+__device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const double* hs,
+                                          const double* hy, const double* rho, double gamma,
+                                          int m, int cnt, int head, int N, int W, int lane) {
     double ai[RF_MAXM];
     for (int j = lane; j < W; j += 64) {
         if (j >= 1 && j <= N) {
@@ -2733,6 +2913,26 @@ static int build_shape_grid(uam_ctx* ctx) {
         offs[l][1] = all.size();
         for (int c = 0; c <= cells; ++c) all.insert(all.end(), lists[c].begin(), lists[c].end());
     }
+    // bitmask form of lists 0 and 1 (<= 256 shapes), appended as int32 pairs after the lists
+    size_t moff[2] = {0, 0};
+    for (int l = 0; l < 2; ++l) {
+        const int span = src[l].hi - src[l].lo;
+        gr.mbase[l] = src[l].lo;
+        gr.mw[l] = (span > 0 && span <= 256) ? (span + 63) >> 6 : 0;
+        if (!gr.mw[l]) continue;
+        while (all.size() % 2) all.push_back(0);  // 8-B alignment of the words
+        moff[l] = all.size();
+        std::vector<uint64_t> words((size_t)(cells + 1) * gr.mw[l], 0ull);
+        const int32_t* st0 = all.data() + offs[l][0];
+        const int32_t* it0 = all.data() + offs[l][1];
+        for (int c = 0; c <= cells; ++c)
+            for (int32_t k = st0[c]; k < st0[c + 1]; ++k) {
+                const int b = it0[k] - src[l].lo;
+                words[(size_t)c * gr.mw[l] + (b >> 6)] |= 1ull << (b & 63);
+            }
+        const int32_t* w32 = reinterpret_cast<const int32_t*>(words.data());
+        all.insert(all.end(), w32, w32 + 2 * words.size());
+    }
     HIP_TRY(hipMalloc(&ctx->d_grid, all.size() * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(ctx->d_grid, all.data(), all.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
@@ -2740,6 +2940,8 @@ static int build_shape_grid(uam_ctx* ctx) {
         gr.start[l] = ctx->d_grid + offs[l][0];
         gr.items[l] = ctx->d_grid + offs[l][1];
     }
+    for (int l = 0; l < 2; ++l)
+        gr.mask[l] = gr.mw[l] ? reinterpret_cast<const uint64_t*>(ctx->d_grid + moff[l]) : nullptr;
     ctx->kg.grid = gr;
     return UAM_OK;
 }
