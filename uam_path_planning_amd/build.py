@@ -38,7 +38,9 @@ def build_library(force=False, verbose=False):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-o", tmp, *SRCS]
+    # UAM_HIPCC_EXTRA: extra flags for tuning experiments (e.g. "-DUAM_RF_WAVES=3")
+    extra = os.environ.get("UAM_HIPCC_EXTRA", "").split()
+    cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", tmp, *SRCS]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -1464,9 +1464,10 @@ __device__ __forceinline__ double rf_L(const KGeom& g, const KParams& p, const R
 }
 
 // L-BFGS two-loop recursion: dr = -H gr over the cnt newest (s, y) pairs of the ring
-__device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const double* hs,
-                                          const double* hy, const double* rho, double gamma,
-                                          int m, int cnt, int head, int N, int W, int lane) {
+__device__ __forceinline__ void lbfgs_dir_loops(const double* gr, double* dr, const double* hs,
+                                                const double* hy, const double* rho,
+                                                double gamma, int m, int cnt, int head, int N,
+                                                int W, int lane) {
     double ai[RF_MAXM];
     for (int j = lane; j < W; j += 64) {
         if (j >= 1 && j <= N) {
@@ -1516,6 +1517,94 @@ __device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const do
     }
 }
 
+// Two waypoint slots per lane (W <= 128): a lane's entries j = lane, lane + 64 of the ring
+// vector at ring slot sl
+struct RingPair {
+    double a0, a1, b0, b1;  // (x, y) of slot 0, (x, y) of slot 1
+};
+
+__device__ __forceinline__ RingPair ring_load(const double* base, int sl, int W, int lane) {
+    const double* v = base + (int64_t)sl * 2 * W;
+    RingPair r{0.0, 0.0, 0.0, 0.0};
+    const int j0 = lane, j1 = lane + 64;
+    if (j0 < W) r.a0 = v[2 * j0], r.a1 = v[2 * j0 + 1];
+    if (j1 < W) r.b0 = v[2 * j1], r.b1 = v[2 * j1 + 1];
+    return r;
+}
+
+// The same recursion with the direction held in registers and each stage's ring vectors
+// loaded one stage ahead (the loads do not depend on the recursion, its dot products do):
+// every operation and its order are those of lbfgs_dir_loops, so dr is bit-identical.
+__device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const double* hs,
+                                          const double* hy, const double* rho, double* ai,
+                                          double gamma, int m, int cnt, int head, int N, int W,
+                                          int lane) {
+#ifndef UAM_RF_PREFETCH
+#define UAM_RF_PREFETCH 1
+#endif
+    if (W > 128 || !UAM_RF_PREFETCH) {
+        lbfgs_dir_loops(gr, dr, hs, hy, rho, gamma, m, cnt, head, N, W, lane);
+        return;
+    }
+    const int j0 = lane, j1 = lane + 64;
+    const bool v0 = j0 < W, v1 = j1 < W;  // the lane's slots on the path (wdot's loop range)
+    const bool in0 = j0 >= 1 && j0 <= N, in1 = j1 >= 1 && j1 <= N;
+    double q0x = 0.0, q0y = 0.0, q1x = 0.0, q1y = 0.0;
+    if (in0) q0x = gr[2 * j0], q0y = gr[2 * j0 + 1];
+    if (in1) q1x = gr[2 * j1], q1y = gr[2 * j1 + 1];
+    // lane-sequential dot over the lane's slots, then the xor tree (== wdot)
+    auto dot = [&](const RingPair& u) {
+        double s = 0.0;
+        if (v0) s = s + (in0 ? u.a0 * q0x + u.a1 * q0y : 0.0);
+        if (v1) s = s + (in1 ? u.b0 * q1x + u.b1 * q1y : 0.0);
+        return wave_sum(s);
+    };
+    RingPair S{}, Y{};  // ai: the wave's LDS (uniform values, no registers held across loops)
+    if (cnt > 0) {
+        const int sl = (head - 1 + m) % m;
+        S = ring_load(hs, sl, W, lane);
+        Y = ring_load(hy, sl, W, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < RF_MAXM; ++i) {
+        if (i >= cnt) break;
+        const int sl = (head - 1 - i + m) % m;
+        RingPair nS{}, nY{};
+        if (i + 1 < cnt) {  // next stage's vectors, in flight during this stage's reduction
+            const int nsl = (head - 2 - i + 2 * m) % m;
+            nS = ring_load(hs, nsl, W, lane);
+            nY = ring_load(hy, nsl, W, lane);
+        }
+        const double a = rho[sl] * dot(S);
+        ai[i] = a;  // every lane writes the same value
+        if (in0) q0x = q0x - a * Y.a0, q0y = q0y - a * Y.a1;
+        if (in1) q1x = q1x - a * Y.b0, q1y = q1y - a * Y.b1;
+        if (i + 1 < cnt) S = nS, Y = nY;
+    }
+    if (in0) q0x = gamma * q0x, q0y = gamma * q0y;
+    if (in1) q1x = gamma * q1x, q1y = gamma * q1y;
+    // second loop, oldest first: its first stage (i = cnt - 1) reuses the vectors the first
+    // loop ended with
+#pragma unroll
+    for (int i = RF_MAXM - 1; i >= 0; --i) {
+        if (i >= cnt) continue;
+        const int sl = (head - 1 - i + m) % m;
+        RingPair nS{}, nY{};
+        if (i > 0) {
+            const int nsl = (head - i + m) % m;
+            nS = ring_load(hs, nsl, W, lane);
+            nY = ring_load(hy, nsl, W, lane);
+        }
+        const double b = rho[sl] * dot(Y);
+        const double d = ai[i] - b;
+        if (in0) q0x = q0x + S.a0 * d, q0y = q0y + S.a1 * d;
+        if (in1) q1x = q1x + S.b0 * d, q1y = q1y + S.b1 * d;
+        if (i > 0) S = nS, Y = nY;
+    }
+    if (in0) dr[2 * j0] = -q0x, dr[2 * j0 + 1] = -q0y;
+    if (in1) dr[2 * j1] = -q1x, dr[2 * j1 + 1] = -q1y;
+}
+
 // register budget: <= 128 VGPRs keeps 4 waves per SIMD (rf_L inlined at every call site; an
 // out-of-line call spills around s_swappc)
 #ifndef UAM_RF_WAVES
@@ -1531,12 +1620,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVE
     const int N = p.N, W = N + 2, S = g.n_obstacles;
     const int m = rf.memory < 0 ? 0 : (rf.memory > RF_MAXM ? RF_MAXM : rf.memory);
     const int nmw = rf_mask_words(S);
-    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + RF_MAXM + nmw * W);
+    double* z = rf_lds + (int64_t)wave * (6 * W + 3 * N + 2 * RF_MAXM + nmw * W);
     double* gr = z + 2 * W;
     double* dr = gr + 2 * W;
     double* yk = dr + 2 * W;
     double* rho = yk + 3 * N;
-    uint64_t* act = nmw ? reinterpret_cast<uint64_t*>(rho + RF_MAXM) : nullptr;
+    double* aiv = rho + RF_MAXM;
+    uint64_t* act = nmw ? reinterpret_cast<uint64_t*>(aiv + RF_MAXM) : nullptr;
     double* zg = wp + path * (int64_t)W * 2;
     double* yo = ws + path * ((int64_t)S * W + (int64_t)m * 4 * W);
     double* hs = yo + (int64_t)S * W;
@@ -1566,7 +1656,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVE
             if (sqrt(gn2) <= rf.inner_tol) break;
             double gd = 0.0, dn2 = gn2;
             if (cnt > 0) {
-                lbfgs_dir(gr, dr, hs, hy, rho, gamma, m, cnt, head, N, W, lane);
+                lbfgs_dir(gr, dr, hs, hy, rho, aiv, gamma, m, cnt, head, N, W, lane);
                 gd = wdot(gr, dr, N, lane);
                 if (!(gd < 0.0))
                     cnt = 0;
@@ -3374,7 +3464,8 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
         return fail(UAM_E_INVALID, "bad refine params (memory must be 0..%d)", RF_MAXM);
     const int64_t N = ctx->kp.N, W = N + 2;
     const int64_t per_wave =
-        (6 * W + 3 * N + RF_MAXM + rf_mask_words(ctx->kg.n_obstacles) * W) * (int64_t)sizeof(double);
+        (6 * W + 3 * N + 2 * RF_MAXM + rf_mask_words(ctx->kg.n_obstacles) * W) *
+        (int64_t)sizeof(double);
     if (per_wave > 65536)
         return fail(UAM_E_INVALID, "N = %lld too large for refinement (LDS)", (long long)N);
     if (n_paths == 0) return UAM_OK;
