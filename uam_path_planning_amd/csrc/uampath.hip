@@ -1809,6 +1809,20 @@ __device__ __forceinline__ int wave_isum(int v) {
     return v;
 }
 
+// UAM_EW_PROF builds (tuning experiments only): lane 0 of each of the first 1024 paths stamps
+// s_memtime at the phase boundaries of k_eval_wave; uam_debug_ew_prof copies the stamps out.
+#ifdef UAM_EW_PROF
+__device__ uint64_t g_ew_prof[1024 * 8];
+#define EW_STAMP(k)                                                                      \
+    do {                                                                                 \
+        if (lane == 0 && path < 1024) g_ew_prof[path * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define EW_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 template <int MODE, bool GEN>
 __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster rs, KVolume vs,
                                                    const uint4* __restrict__ rec,
@@ -1820,6 +1834,7 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int64_t path = (int64_t)blockIdx.x * wpb + wave;
     if (path >= n_paths) return;  // whole wave
+    EW_STAMP(0);
     const int N = p.N, W = N + 2;
     const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     double* px = ew_lds + (int64_t)wave * ewave_doubles(N);
@@ -1857,6 +1872,7 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
         py[j] = y;
     }
     wave_sync();
+    EW_STAMP(1);
     // geometry terms: lq = get_cost length term of the segment ending at j (anchor segment
     // for j = 0; +0.0 where eval_path adds nothing), sg = true segment norm, kinematic rows
     for (int j = lane; j < W; j += 64) {
@@ -1899,6 +1915,7 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             }
         }
     }
+    EW_STAMP(2);
     // record gathers, up to 4 per lane in flight; ph / ps = +0.0 for off-grid waypoints
     double hmax = -INFINITY, cmin = INFINITY;
     int nh = 0, off = 0, below = 0;
@@ -1963,26 +1980,37 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             }
         }
     }
+    EW_STAMP(3);
     hmax = wave_fmax(hmax);
     cmin = wave_fmin(cmin);
     nh = wave_isum(nh);
     off = wave_isum(off);
     below = wave_isum(below);
     wave_sync();
-    // eval_path's sequential sums, same order, four chains on four lanes at once (L, length,
-    // no-fly sum, kinematic sum), then the cost chain seeded with (N+1) L.  Every accumulator
-    // starts at +0.0, so the +0.0 entries are exact no-ops.
+    EW_STAMP(4);
+    // eval_path's sequential sums, same order, on four lanes at once: phase A runs the W-term
+    // chains (lane 0 L, lane 1 length, lane 2 no-fly sum) and the first W kinematic rows
+    // (lane 3); lane 0 then seeds the cost chain with (N+1) L and phase B runs it beside the
+    // rest of the kinematic chain (lane 3), so the serial length is max(2W, 3N) adds, not
+    // 3N + W.  Every accumulator starts at +0.0, so the +0.0 entries are exact no-ops.
     const double* arr = lane == 0 ? lq : (lane == 1 ? sg : (lane == 2 ? ps : kn));
-    const int cnt = lane < 3 ? W : (lane == 3 ? 3 * N : 0);
+    const int na = lane < 3 ? W : (lane == 3 ? min(W, 3 * N) : 0);
     double acc = 0.0;
 #pragma unroll 8
-    for (int i = 0; i < cnt; ++i) acc = acc + arr[i];
-    const double L = __shfl(acc, 0, 64), len = __shfl(acc, 1, 64);
-    const double nsum = __shfl(acc, 2, 64), ksum = __shfl(acc, 3, 64);
-    if (lane == 0) {
-        double cost = (double)(N + 1) * L;
+    for (int i = 0; i < na; ++i) acc = acc + arr[i];
+    double L = acc;
+    if (lane == 0) acc = (double)(N + 1) * L;
+    const double* brr = lane == 0 ? ph : kn + W;
+    const int nb = lane == 0 ? W : (lane == 3 ? 3 * N - na : 0);
 #pragma unroll 8
-        for (int j = 0; j < W; ++j) cost = cost + ph[j];
+    for (int i = 0; i < nb; ++i) acc = acc + brr[i];
+    L = __shfl(L, 0, 64);
+    const double len = __shfl(acc, 1, 64), nsum = __shfl(acc, 2, 64);
+    const double ksum = __shfl(acc, 3, 64);
+    EW_STAMP(5);
+    if (lane == 0) {
+        const double cost = acc;
+        EW_STAMP(6);
         if (out.cost) out.cost[path] = cost;
         if (out.length_q) out.length_q[path] = L;
         if (out.length) out.length[path] = len;
@@ -3926,6 +3954,15 @@ int uam_path_length(uam_ctx* ctx, const double* pts, int64_t n_paths, int32_t n_
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
+
+#ifdef UAM_EW_PROF
+int uam_debug_ew_prof(uint64_t* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ew_prof), (size_t)std::min(n, 1024 * 8) * 8) ==
+                   hipSuccess
+               ? UAM_OK
+               : UAM_E_HIP;
+}
+#endif
 
 int uam_synchronize(uam_ctx* ctx, uam_stream stream) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
