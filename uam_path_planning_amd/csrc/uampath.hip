@@ -2028,13 +2028,34 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
 // K7: coordinate reference systems.  Transverse Mercator between
 // geographic JGD2000/JGD2011 (lon, lat degrees) and the Japan Plane Rectangular CS (metres),
 // the transform pyproj applies at data_manager.py:24-26 / 84-85 and main.py:106-115.  Krueger
-// series to n^6, geodetic latitude from conformal latitude by 5 Newton steps; definition and
+// series to n^6, geodetic latitude from conformal latitude by 2 Newton steps; definition and
 // coefficient formulas as oracle/uam_oracle.c (tm_prepare / tm_fwd1 / tm_inv1); the host
 // computes the coefficients once (KTm) so device and oracle share them.
 struct KTm {
     double k0, A, e, e2, xi0, lon0, fe, fn;
     double alpha[6], beta[6];
 };
+
+// Krueger series by complex Clenshaw summation: oracle/uam_oracle.c kr_sum, same operations
+__device__ __forceinline__ void kr_sum(const double (&c)[6], double xi, double eta, double& sr,
+                                       double& si) {
+    const double s2 = sin(2.0 * xi), c2 = cos(2.0 * xi);
+    const double sh = sinh(2.0 * eta), ch = cosh(2.0 * eta);
+    const double ar = 2.0 * (c2 * ch), ai = -2.0 * (s2 * sh);
+    double y0r = 0.0, y0i = 0.0, y1r = 0.0, y1i = 0.0;
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        const double tr = (ar * y0r - ai * y0i) - y1r + c[j];
+        const double ti = (ar * y0i + ai * y0r) - y1i;
+        y1r = y0r;
+        y1i = y0i;
+        y0r = tr;
+        y0i = ti;
+    }
+    const double zr = s2 * ch, zi = c2 * sh;
+    sr = y0r * zr - y0i * zi;
+    si = y0r * zi + y0i * zr;
+}
 
 __device__ __forceinline__ void tm_fwd(const KTm& k, double lon, double lat, double& x,
                                        double& y) {
@@ -2043,13 +2064,9 @@ __device__ __forceinline__ void tm_fwd(const KTm& k, double lon, double lat, dou
     const double tt = sinh(atanh(s) - k.e * atanh(k.e * s));
     const double xp = atan2(tt, cos(dl));
     const double ep = atanh(sin(dl) / sqrt(1.0 + tt * tt));
-    double xi = xp, eta = ep;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const double c = 2.0 * (j + 1);
-        xi = xi + k.alpha[j] * (sin(c * xp) * cosh(c * ep));
-        eta = eta + k.alpha[j] * (cos(c * xp) * sinh(c * ep));
-    }
+    double sr, si;
+    kr_sum(k.alpha, xp, ep, sr, si);
+    const double xi = xp + sr, eta = ep + si;
     x = k.k0 * k.A * eta + k.fe;
     y = k.k0 * k.A * (xi - k.xi0) + k.fn;
 }
@@ -2058,20 +2075,16 @@ __device__ __forceinline__ void tm_inv(const KTm& k, double x, double y, double&
                                        double& lat) {
     const double kA = k.k0 * k.A;
     const double xi = (y - k.fn) / kA + k.xi0, eta = (x - k.fe) / kA;
-    double xp = xi, ep = eta;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const double c = 2.0 * (j + 1);
-        xp = xp - k.beta[j] * (sin(c * xi) * cosh(c * eta));
-        ep = ep - k.beta[j] * (cos(c * xi) * sinh(c * eta));
-    }
+    double sr, si;
+    kr_sum(k.beta, xi, eta, sr, si);
+    const double xp = xi - sr, ep = eta - si;
     const double se = sinh(ep), cx = cos(xp);
     const double taup = sin(xp) / sqrt(se * se + cx * cx);
     const double lam = atan2(se, cx);
     const double e = k.e, e2m = 1.0 - k.e2;
-    double tau = taup;
+    double tau = taup / e2m;  // oracle tm_inv1: GeographicLib's start, 2 Newton steps
 #pragma unroll
-    for (int it = 0; it < 5; ++it) {
+    for (int it = 0; it < 2; ++it) {
         const double r = sqrt(1.0 + tau * tau);
         const double sg = sinh(e * atanh(e * tau / r));
         const double tp = tau * sqrt(1.0 + sg * sg) - sg * r;
