@@ -169,6 +169,28 @@ def test_raster_build_vs_oracle(eng, oracle_mod, thr):
     np.testing.assert_array_equal(rec, ref.view(np.int32))
 
 
+def test_raster_build_list_walk_and_partial_waves(eng, oracle_mod):
+    """K1's wave walk without per-cell bitmasks (306 obstacles and a region table of more than
+    256 shapes: the lists merged by their minimum head) on a 250^2 raster (waves span row ends;
+    the last wave is partial)."""
+    from uam_path_planning_amd.scenario import canonical_spec, raster_geo
+    from uam_path_planning_amd.synthetic import random_convex_polygons, synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=300, seed=4)
+    spec["regions"][1]["shapes"] = spec["regions"][1]["shapes"] + [
+        {"kind": "polygon", "vertices": v} for v in random_convex_polygons(260, seed=6)]
+    orc = _setup(eng, oracle_mod, spec, 80, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"])
+    geo = raster_geo(250)
+    dem = synthetic_dem(250)
+    rec = _np(eng.raster_build(geo, dem).rec)
+    ref = orc.raster_build(oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top,
+                                                         geo.dx, geo.dy, geo.nodata,
+                                                         geo.dem_threshold), dem)
+    np.testing.assert_array_equal(rec, ref.view(np.int32))
+    assert (rec[..., 3] & 1).any()
+
+
 # ---- raster eval (K2) ---------------------------------------------------------------------
 def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5):
     from uam_path_planning_amd.arcs import arc_table

@@ -85,10 +85,10 @@ struct KShapeGrid {
     int32_t gx, gy;
     const int32_t* start[3];  // 0 = region penalty (box_pen), 1 = psi, 2 = hit
     const int32_t* items[3];
-    // lists 0 and 1 as per-slot bitmasks (bit i of word w: shape mbase + 64 w + i), mw words
-    // per slot; null when the table spans more than 256 shapes
-    const uint64_t* mask[2];
-    int32_t mbase[2], mw[2];
+    // the lists as per-slot bitmasks (bit i of word w: shape mbase + 64 w + i), mw words per
+    // slot; null when the table spans more than 256 shapes
+    const uint64_t* mask[3];
+    int32_t mbase[3], mw[3];
 };
 
 struct KGeom {
@@ -337,27 +337,6 @@ __global__ __launch_bounds__(256) void k_eval_points(KGeom g, KParams p,
 
 // K1: record per cell.  One lane per cell, rows contiguous -> coalesced DEM reads and
 // 16-B record stores (one global_store_dwordx4 per lane).
-__global__ __launch_bounds__(256) void k_raster_build(KGeom g, KParams p, KRaster rs,
-                                                      const float* __restrict__ dem,
-                                                      float nodata, float thr,
-                                                      uint4* __restrict__ rec) {
-    const int64_t total = (int64_t)rs.nx * rs.ny;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
-         c += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t iy = c / rs.nx, ix = c - iy * rs.nx;
-        const double xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
-        const double yc = rs.y_top - ((double)iy + 0.5) * rs.dy;
-        const float z = dem ? dem[c] : 0.0f;
-        uint32_t fl = 0;
-        if (collides(g, xc, yc)) fl |= UAM_FLAG_NFZ;
-        if (thr == -9999.0f ? (z == -9999.0f) : (z > thr)) fl |= UAM_FLAG_MASK;
-        if (z == nodata) fl |= UAM_FLAG_NODATA;
-        const float phi = (float)total_penalty(g, p, xc, yc);
-        const float ps = (float)obstacle_psi_sum(g, p, xc, yc);
-        rec[c] = make_uint4(__float_as_uint(phi), __float_as_uint(ps), __float_as_uint(z), fl);
-    }
-}
-
 __global__ __launch_bounds__(256) void k_dem_mosaic(const float* __restrict__ tiles, int n_tiles,
                                                     int th, int tw,
                                                     const int32_t* __restrict__ xoff,
@@ -1333,6 +1312,149 @@ __device__ __forceinline__ double phi_vg_wave(const KGeom& g, const KParams& p, 
     dx = gx;
     dy = gy;
     return pen;
+}
+
+// Walk the union of the lanes' grid lists of table L (0 penalty, 1 psi, 2 hit) in ascending
+// shape order, wave-uniformly (uniform control flow, whole wave active): body(s, mine) with s
+// wave-uniform and mine = s is in this lane's list (slot < 0: empty list).  Each lane thus
+// sees exactly its own list, in its order; the wave's shape index is uniform, so the records
+// come through scalar loads.  Per-cell bitmasks when the table has them, else the lists
+// merged by their minimum head.
+template <int L, class F>
+__device__ __forceinline__ void wave_walk(const KGeom& g, int slot, F&& body) {
+    const int mw = g.grid.mask[L] ? g.grid.mw[L] : 0;
+    if (mw) {
+        uint64_t lm[RF_MASKW] = {0ull, 0ull, 0ull, 0ull};
+        if (slot >= 0) {
+            const uint64_t* m = g.grid.mask[L] + (int64_t)slot * mw;
+#pragma unroll
+            for (int w = 0; w < RF_MASKW; ++w)
+                if (w < mw) lm[w] = m[w];
+        }
+#pragma unroll 1
+        for (int w = 0; w < mw; ++w) {
+            const uint64_t mine = pick_word(lm, w);
+            for (uint64_t b = wave_or_u64(mine); b; b &= b - 1) {
+                const int bit = __builtin_ctzll(b);
+                body(g.grid.mbase[L] + 64 * w + bit, ((mine >> bit) & 1ull) != 0);
+            }
+        }
+        return;
+    }
+    int k = 0, k1 = 0;
+    if (slot >= 0) {
+        k = g.grid.start[L][slot];
+        k1 = g.grid.start[L][slot + 1];
+    }
+    for (;;) {
+        const int cand = k < k1 ? g.grid.items[L][k] : INT32_MAX;
+        const int s = wave_min_i32(cand);
+        if (s == INT32_MAX) break;
+        const bool mine = cand == s;
+        if (mine) ++k;
+        body(s, mine);
+    }
+}
+
+// psi / contains of a wave-uniform shape (records through uload); same operations as psi /
+// contains
+__device__ __forceinline__ double psi_u(const KGeom& g, const DevShape& sh, double x0, double x1,
+                                        bool smooth, double e) {
+    double r = 1.0;
+    const int end = sh.first + sh.count;
+    for (int i = sh.first; i < end; ++i) {
+        const DevIneq q = uload(g.ineq, i);
+        const double h = ineq_h(&q, x0, x1);
+        if (smooth) {
+            const double m = fmin(h - e, 0.0);
+            r = r * (m * m);
+        } else {
+            r = r * fmin(e - h, 0.0);
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool contains_u(const KGeom& g, const DevShape& sh, double x0,
+                                           double x1) {
+    const int end = sh.first + sh.count;
+    bool in = true;
+    for (int i = sh.first; i < end; ++i) {
+        const DevIneq q = uload(g.ineq, i);
+        in = in && !(ineq_h(&q, x0, x1) > 1e-14);
+    }
+    return in;
+}
+
+// K1: one 16-B record per DEM cell {Phi, sum psi_nfz, dem, flags} (data_manager.py:14-17 mask,
+// problem.py:49-56 Phi, the no-fly g rows' psi, Map.collides).  A wave covers 64 consecutive
+// cells of a row, which nearly always share one grid cell: the three shape tables are walked
+// by the whole wave (wave_walk), each lane adding exactly what total_penalty /
+// obstacle_psi_sum / collides add, in their order -- records bit-identical to those
+// functions.  Cells with no index slot (no grid, NaN) use the per-lane functions.
+__global__ __launch_bounds__(256) void k_raster_build(KGeom g, KParams p, KRaster rs,
+                                                      const float* __restrict__ dem,
+                                                      float nodata, float thr,
+                                                      uint4* __restrict__ rec) {
+    const int64_t total = (int64_t)rs.nx * rs.ny;
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < total;
+         base += stride) {  // wave-uniform trip count
+        const int64_t c = base + lane;
+        const bool valid = c < total;
+        double xc = 0.0, yc = 0.0;
+        float z = 0.0f;
+        if (valid) {
+            const int64_t iy = c / rs.nx, ix = c - iy * rs.nx;
+            xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
+            yc = rs.y_top - ((double)iy + 0.5) * rs.dy;
+            z = dem ? dem[c] : 0.0f;
+        }
+        const int slot = valid ? (g.grid.gx ? grid_slot(g.grid, xc, yc) : -1) : -2;
+        double pen = 0.0, t = 0.0;
+        int rc = -1;
+        wave_walk<0>(g, slot, [&](int s, bool mine) {
+            if (!mine) return;
+            const DevShape sh = uload(g.shape, s);
+            if (sh.region != rc) {
+                if (rc >= 0) pen = pen + p.weights[rc] * t;
+                rc = sh.region;
+                t = 0.0;
+            }
+            if ((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, xc, yc)) return;
+            const double v = psi_u(g, sh, xc, yc, p.penalty_smooth != 0, p.enlargement);
+            t = sh.has_center ? t + v / sh.norm_pen : t + v;
+        });
+        if (rc >= 0) pen = pen + p.weights[rc] * t;
+        double acc = 0.0;
+        wave_walk<1>(g, slot, [&](int s, bool mine) {
+            if (!mine) return;
+            const DevShape sh = uload(g.shape, s);
+            if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, xc, yc)) return;
+            acc = acc + psi_u(g, sh, xc, yc, p.obstacle_smooth != 0, 0.0);
+        });
+        bool hit = false;
+        wave_walk<2>(g, slot, [&](int s, bool mine) {
+            if (!mine) return;
+            const DevShape sh = uload(g.shape, s);
+            if ((sh.flags & SHAPE_CULL_HIT) && outside(sh.box_obs, xc, yc)) return;
+            hit = hit || contains_u(g, sh, xc, yc);
+        });
+        if (slot == -1) {
+            pen = total_penalty(g, p, xc, yc);
+            acc = obstacle_psi_sum(g, p, xc, yc);
+            hit = collides(g, xc, yc);
+        }
+        if (valid) {
+            uint32_t fl = 0;
+            if (hit) fl |= UAM_FLAG_NFZ;
+            if (thr == -9999.0f ? (z == -9999.0f) : (z > thr)) fl |= UAM_FLAG_MASK;
+            if (z == nodata) fl |= UAM_FLAG_NODATA;
+            rec[c] = make_uint4(__float_as_uint((float)pen), __float_as_uint((float)acc),
+                                __float_as_uint(z), fl);
+        }
+    }
 }
 
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
@@ -3044,9 +3166,9 @@ static int build_shape_grid(uam_ctx* ctx) {
         offs[l][1] = all.size();
         for (int c = 0; c <= cells; ++c) all.insert(all.end(), lists[c].begin(), lists[c].end());
     }
-    // bitmask form of lists 0 and 1 (<= 256 shapes), appended as int32 pairs after the lists
-    size_t moff[2] = {0, 0};
-    for (int l = 0; l < 2; ++l) {
+    // bitmask form of the lists (<= 256 shapes), appended as int32 pairs after the lists
+    size_t moff[3] = {0, 0, 0};
+    for (int l = 0; l < 3; ++l) {
         const int span = src[l].hi - src[l].lo;
         gr.mbase[l] = src[l].lo;
         gr.mw[l] = (span > 0 && span <= 256) ? (span + 63) >> 6 : 0;
@@ -3071,7 +3193,7 @@ static int build_shape_grid(uam_ctx* ctx) {
         gr.start[l] = ctx->d_grid + offs[l][0];
         gr.items[l] = ctx->d_grid + offs[l][1];
     }
-    for (int l = 0; l < 2; ++l)
+    for (int l = 0; l < 3; ++l)
         gr.mask[l] = gr.mw[l] ? reinterpret_cast<const uint64_t*>(ctx->d_grid + moff[l]) : nullptr;
     ctx->kg.grid = gr;
     return UAM_OK;
