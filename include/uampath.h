@@ -293,9 +293,11 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
  * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,
  * differing in gathers per chunk / software pipelining / occupancy; 9 = one wave per path
- * (lanes over waypoints; small batches); 10 = never one wave per path.  0 picks the wave
- * per path kernel for batches up to 16384 paths and variant 2 above.  All variants return
- * bit-identical results. */
+ * (lanes over waypoints; small batches); 10 = never one wave per path; 11 = binned raster
+ * evaluation (K2b); 12 = tile-sorted raster evaluation (K2t: waypoints binned by raster
+ * tile, XCD-pinned gathers from L2, per-block LDS reduction; pass 1 on a side stream).
+ * 0 picks the wave per path kernel for batches up to 16384 paths and variant 2 above.  All
+ * variants return bit-identical results. */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */

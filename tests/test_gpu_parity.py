@@ -192,7 +192,7 @@ def test_raster_build_list_walk_and_partial_waves(eng, oracle_mod):
 
 
 # ---- raster eval (K2) ---------------------------------------------------------------------
-def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5):
+def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5, geo=None):
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
     from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
@@ -200,8 +200,9 @@ def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5):
     spec = canonical_spec(nfz_polygons=nfz)
     orc = _setup(eng, oracle_mod, spec, N, spec["options"], spec["maxratio"], spec["maxalpha"],
                  spec["enlargement"], spec["weights"], altitude=320.0)
-    geo = raster_geo(R)
-    dem = synthetic_dem(R)
+    geo = geo or raster_geo(R)
+    dem = synthetic_dem(geo.nx) if geo.nx == geo.ny else synthetic_dem(max(geo.nx, geo.ny))[
+        :geo.ny, :geo.nx].copy()
     raster = eng.raster_build(geo, dem)
     rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
                                        geo.nodata, geo.dem_threshold)
@@ -356,7 +357,7 @@ def test_kernel_variants_bit_identical(eng, oracle_mod, D):
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 333, 80, nfz=4, D=D)
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
     try:
-        for v in range(0, 12):
+        for v in range(0, 13):
             eng.set_tuning(v)
             gpu = eng.eval_generated(pairs, ut, raster=raster)
             _assert_paths_equal(gpu, ref, raster=True)
@@ -371,6 +372,37 @@ def test_kernel_variants_bit_identical(eng, oracle_mod, D):
         eng.set_tuning(0)
     with pytest.raises(ValueError):
         eng.set_tuning(99)
+
+
+@pytest.mark.parametrize("R,Q,N,D,crop", [(512, 1003, 80, 5, False), (700, 257, 80, 3, True),
+                                            (2048, 333, 254, 5, False), (300, 77, 1, 16, True),
+                                            (8192, 2000, 80, 5, False)])
+def test_tiled_eval_vs_oracle(eng, oracle_mod, R, Q, N, D, crop):
+    """K2t (tuning 12: tile-binned, LDS-sorted, XCD-pinned gathers, block reduction) against
+    the oracle: partial edge tiles, rasters that do not cover the paths (off-raster bin),
+    ragged last path-blocks, W = 3 and W = 256 (smaller path-blocks), D = 16, 8192^2."""
+    from uam_path_planning_amd.engine import RasterGeo
+
+    geo = None
+    if crop:   # R x R/2 cells over part of the map: many waypoints fall off the raster
+        geo = RasterGeo(nx=R, ny=R // 2, x0=8.0, y_top=5.0, dx=40.0 / R, dy=40.0 / R,
+                        nodata=-9999.0, dem_threshold=0.0)
+    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, R, Q, N, nfz=4, D=D,
+                                                   geo=geo)
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
+    if crop:
+        assert (ref["offmap"] > 0).any() and (ref["offmap"] < N + 2).any()
+    try:
+        eng.set_tuning(12)
+        for _ in range(2):   # second launch reuses the grown scratch
+            gpu = eng.eval_generated(pairs, ut, raster=raster)
+            _assert_paths_equal(gpu, ref, raster=True)
+            np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                          oracle_mod.argmin(ref["cost"], D, True))
+            np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
+                                          oracle_mod.argmin(ref["length"], D, False))
+    finally:
+        eng.set_tuning(0)
 
 
 @pytest.mark.parametrize("enl", [-0.5, -1e-3, 0.0, 1e-3, 0.3, 2.0])

@@ -78,7 +78,7 @@ def main():
         eng.set_tuning(0)
         del raster
         torch.cuda.empty_cache()
-    for R in [int(x) for x in args.sizes.split(",")]:
+    for R in [int(x) for x in args.sizes.split(",") if x]:
         geo = raster_geo(R)
         dem = eng.tensor(synthetic_dem(R), torch.float32)
         t_build, _ = timed(lambda: eng.raster_build(geo, dem), reps=3, warm=1)
@@ -94,6 +94,8 @@ def main():
         del raster, dem
         torch.cuda.empty_cache()
     Qa = args.analytic_pairs
+    if not Qa:
+        return
     pa = pairs[:Qa]
     oa = eng.outputs(Qa * 5, 82)
     med, best = timed(lambda: eng.eval_generated(pa, ut, raster=None, outputs=oa), reps=5)

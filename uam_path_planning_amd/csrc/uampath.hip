@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -31,8 +32,9 @@
 #include "../../include/uampath.h"
 #include "polyproc.h"
 
-#define UAM_TUNING_MAX 11
+#define UAM_TUNING_MAX 12
 #define UAM_TUNING_BINNED 11    // binned raster evaluation (K2b)
+#define UAM_TUNING_TILED 12     // tile-sorted raster evaluation (K2t)
 #define UAM_TUNING_WAVE 9       // force the wave-per-path kernel (K2w)
 #define UAM_TUNING_LANE 10      // never pick K2w automatically
 #define UAM_WAVE_AUTO_PATHS 16384  // auto: K2w up to here (tools/probe_wave.py crossover)
@@ -547,22 +549,14 @@ __device__ __forceinline__ void consume_chunk_vol(const Chunk<C>& ch, const Path
     }
 }
 
-// One path: pass 1 = geometry-only terms (length_of, true length, kinematic rows), pass 2 =
-// per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk,
-// PIPE = issue chunk k+1's gathers before consuming chunk k (two chunks in flight).
-template <int MODE, bool GEN, int C, bool PIPE>
-__device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
-                                             const KVolume& vs, const uint4* __restrict__ rec,
-                                             const PathSrc<GEN>& src, int64_t path,
-                                             const KOut& out) {
+// Pass 1 of a path: get_cost's length term L (problem.py:130-146 with the quirk), the true
+// length (length_of, solver.py:49) and the sum of the 3N kinematic rows (problem.py:100-107),
+// optionally storing the rows.  Shared by every path kernel, so their bits agree.
+template <bool GEN>
+__device__ __forceinline__ void path_pass1(const KParams& p, const PathSrc<GEN>& src,
+                                           double* grow, PathAcc& a) {
     const int N = p.N, W = N + 2;
     const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
-    const int n_rows = 3 * N + g.n_obstacles * W;
-    double* grow =
-        (MODE == UAM_MODE_ANALYTIC && out.g_rows) ? out.g_rows + path * n_rows : nullptr;
-    PathAcc a;
-
-    // ---- pass 1 ---------------------------------------------------------------------------
     double px, py;
     src.at(0, px, py);
     double L = 0.0;
@@ -614,9 +608,25 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
     a.L = L;
     a.len = len;
     a.ksum = ksum;
+}
+
+// One path: pass 1 = geometry-only terms (length_of, true length, kinematic rows), pass 2 =
+// per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk,
+// PIPE = issue chunk k+1's gathers before consuming chunk k (two chunks in flight).
+template <int MODE, bool GEN, int C, bool PIPE>
+__device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
+                                             const KVolume& vs, const uint4* __restrict__ rec,
+                                             const PathSrc<GEN>& src, int64_t path,
+                                             const KOut& out) {
+    const int N = p.N, W = N + 2;
+    const int n_rows = 3 * N + g.n_obstacles * W;
+    double* grow =
+        (MODE == UAM_MODE_ANALYTIC && out.g_rows) ? out.g_rows + path * n_rows : nullptr;
+    PathAcc a;
+    path_pass1<GEN>(p, src, grow, a);
 
     // ---- pass 2: cost = (N+1) L + sum_j phi(p_j)/N  (problem.py:41-43) ------------------
-    a.cost = (double)(N + 1) * L;
+    a.cost = (double)(N + 1) * a.L;
     a.nsum = 0.0;
     a.nh = 0;
     a.off = 0;
@@ -2733,6 +2743,386 @@ __global__ __launch_bounds__(256) void k_bin_gather(const uint2* __restrict__ bu
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// K2t: tile-sorted raster evaluation (tuning 12).  K2's waypoint gathers are random 16-B
+// reads, each moving a 128-B line out of HBM, so K2 sits at the fabric's
+// random-line rate.  K2t moves every waypoint through on-chip caches instead, in four
+// launches that only stream:
+//   A1 k_tb_count    K2's pass 1 (L, length, kinematic sum) per path, plus a histogram of
+//                    each path-block's waypoints over 256x256-cell raster tiles (1 MiB).
+//   S1 k_tb_rowscan  per-tile exclusive scan over the blocks (bin offsets).
+//   A2 k_tb_scatter  one workgroup per path-block: regenerate the waypoints, sort them by
+//                    tile in LDS, write them as contiguous runs into the tile-major bins.
+//   B  k_tb_gather   XCD-pinned: tiles t == x (mod 8) on XCD x, so a tile's records are
+//                    fetched into one L2 once and served from there; each gathered record
+//                    goes back, tagged with its slot, into its path-block's region as a
+//                    contiguous run (one run per (tile, block)).
+//   C  k_tb_reduce   one workgroup per path-block: the region is read contiguously and
+//                    placed in LDS by slot, then each lane sums its path in waypoint order.
+// Every order-dependent float64 sum runs in eval_path's order over the same values, and the
+// terms eval_path skips (off the raster) are stored as +0, an exact no-op on accumulators
+// that start at +0 (cost = (N+1)L >= +0), so K2t is bit-identical to K2.
+constexpr int TB_TS = 256;            // tile side in cells (256^2 x 16 B = 1 MiB of records)
+constexpr int TB_MAX_NTB = 4096;      // tiles + 1 (off-raster bin)
+constexpr uint32_t TB_OFF = 0x8000u;  // record flag: waypoint off the raster
+constexpr int TB_CH = 2048;           // entries per gather step of one workgroup
+
+// nontemporal (streaming) 8-/16-B loads and stores: the builtins take clang vector types
+typedef uint32_t tb_u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t tb_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint2 tb_ldnt(const uint2* p) {
+    const tb_u2 v = __builtin_nontemporal_load(reinterpret_cast<const tb_u2*>(p));
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 tb_ldnt(const uint4* p) {
+    const tb_u4 v = __builtin_nontemporal_load(reinterpret_cast<const tb_u4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void tb_stnt(uint4 v, uint4* p) {
+    tb_u4 w;
+    w.x = v.x, w.y = v.y, w.z = v.z, w.w = v.w;
+    __builtin_nontemporal_store(w, reinterpret_cast<tb_u4*>(p));
+}
+
+struct KTile {
+    const double* pairs;
+    const double* utab;
+    int64_t n_pairs, P;
+    int32_t D, W, PB, NB, SB;       // pairs per block, blocks, slot capacity per block
+    int32_t tiles_x, NT, NTB;       // NTB = NT + 1; bin NT = off the raster
+    int32_t* cnt;                   // [NTB][NB]: counts, then per-row exclusive prefix
+    int32_t* rowtot;                // [NTB] row totals
+    int32_t* tstart;                // [NTB + 1] start of each tile's bin (k_tb_tstart)
+    int32_t dbg;                    // diagnostics (UAM_TB_DBG): 1 = B skips gathers, 2 = B
+                                    // skips stores
+    int32_t* boff;                  // [NB][NTB] block-local exclusive prefix over tiles
+    uint2* ent;                     // tile-major bins {slot<<16 | tile cell, dest}
+    uint4* recb;                    // [NB][SB] gathered records, slot in w's high half
+    double* kin;                    // [3][P] L, length, kinematic sum
+};
+
+// raster cell of a point (uampath.h convention, exactly issue_chunk's arithmetic)
+__device__ __forceinline__ bool raster_cell(const KRaster& rs, double x0, double x1, int& ix,
+                                            int& iy) {
+    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+    const bool in = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny);
+    ix = in ? (int)fx : 0;
+    iy = in ? (int)fy : 0;
+    return in;
+}
+
+// exclusive scan of n <= TB_MAX_NTB ints into s[0..n] (s[n] = total), by wave 0 of the block
+__device__ __forceinline__ void tb_scan_small(const int32_t* __restrict__ v, int n,
+                                              int32_t* s) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int32_t carry = 0;
+        for (int t0 = 0; t0 < n; t0 += 64) {
+            const int t = t0 + lane;
+            const int32_t x0 = t < n ? v[t] : 0;
+            int32_t x = x0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (t < n) s[t] = carry + x - x0;
+            carry += __shfl(x, 63, 64);
+        }
+        if (lane == 0) s[n] = carry;
+    }
+    __syncthreads();
+}
+
+// K2 pass 1 for every path (L, length, kinematic sum -> kin), one lane per path in K2's layout
+// (wave = displacement, lane = pair).  ALU-bound; it runs on a second stream beside A1..B.
+__global__ __launch_bounds__(1024) void k_tb_kin(KParams p, KTile kt) {
+    const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t q = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    if (q >= kt.n_pairs) return;
+    const double4 pr = reinterpret_cast<const double4*>(kt.pairs)[q];
+    PathSrc<true> src;
+    src.W = kt.W;
+    src.wp = nullptr;
+    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    src.za = src.zb = 0.0;
+    src.u = kt.utab + (int64_t)d * p.N * 2;
+    PathAcc a;
+    path_pass1<true>(p, src, nullptr, a);
+    const int64_t path = q * kt.D + d;
+    kt.kin[path] = a.L;
+    kt.kin[kt.P + path] = a.len;
+    kt.kin[2 * kt.P + path] = a.ksum;
+}
+
+// waypoint i (slot = path_local * W + j) of path-block b, exactly PathSrc<true>::at
+__device__ __forceinline__ void tb_point(const KParams& p, const KTile& kt, int64_t b, int i,
+                                         double& x, double& y) {
+    const int W = kt.W, D = kt.D;
+    const int pl = i / W, j = i - pl * W;
+    const int ql = pl / D, d = pl - ql * D;
+    const double4 pr = reinterpret_cast<const double4*>(kt.pairs)[b * kt.PB + ql];
+    if (j == 0) {
+        x = pr.x, y = pr.y;
+    } else if (j == W - 1) {
+        x = pr.z, y = pr.w;
+    } else {
+        const double* u = kt.utab + ((int64_t)d * p.N + (j - 1)) * 2;
+        arc_point(pr.x, pr.y, pr.z, pr.w, u[0], u[1], x, y);
+    }
+}
+
+// A1: histogram of one path-block's waypoints over the tiles (one workgroup per block):
+// cnt[t][b] (tile-major, for S1) and the block-local exclusive prefix boff[b][t].
+__global__ __launch_bounds__(256) void k_tb_count(KParams p, KRaster rs, KTile kt) {
+    extern __shared__ int32_t tb_hist[];  // [NTB]
+    const int NTB = kt.NTB;
+    for (int i = threadIdx.x; i < NTB; i += blockDim.x) tb_hist[i] = 0;
+    __syncthreads();
+    const int64_t b = blockIdx.x;
+    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
+    const int nwp = npair * kt.D * kt.W;
+    for (int i = threadIdx.x; i < nwp; i += blockDim.x) {
+        double x, y;
+        tb_point(p, kt, b, i, x, y);
+        int ix, iy;
+        const int t = raster_cell(rs, x, y, ix, iy) ? (iy / TB_TS) * kt.tiles_x + ix / TB_TS
+                                                    : kt.NT;
+        atomicAdd(&tb_hist[t], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < NTB; t += blockDim.x)
+        kt.cnt[(int64_t)t * kt.NB + b] = tb_hist[t];
+    if (threadIdx.x < 64) {  // block-local exclusive prefix over tiles
+        const int lane = threadIdx.x;
+        int32_t carry = 0;
+        for (int t0 = 0; t0 < NTB; t0 += 64) {
+            const int t = t0 + lane;
+            const int32_t v = t < NTB ? tb_hist[t] : 0;
+            int32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (t < NTB) kt.boff[b * NTB + t] = carry + x - v;
+            carry += __shfl(x, 63, 64);
+        }
+    }
+}
+
+// S1: exclusive scan of each tile row cnt[t][0..NB) in place; rowtot[t] = the row's total.
+__global__ __launch_bounds__(1024) void k_tb_rowscan(KTile kt) {
+    __shared__ int32_t wsum[16];
+    int32_t* row = kt.cnt + (int64_t)blockIdx.x * kt.NB;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t carry = 0;
+    for (int i0 = 0; i0 < kt.NB; i0 += 4096) {
+        int32_t v[4], run = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + threadIdx.x * 4 + k;
+            v[k] = i < kt.NB ? row[i] : 0;
+            const int32_t t = v[k];
+            v[k] = run;
+            run += t;
+        }
+        int32_t x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        int32_t woff = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            const int32_t w = k < (int)(blockDim.x >> 6) ? wsum[k] : 0;
+            woff += k < wv ? w : 0;
+            tot += w;
+        }
+        const int32_t excl = carry + woff + x - run;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + threadIdx.x * 4 + k;
+            if (i < kt.NB) row[i] = v[k] + excl;
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) kt.rowtot[blockIdx.x] = carry;
+}
+
+// S2: tile bin starts = exclusive scan of the row totals (one wave).
+__global__ __launch_bounds__(64) void k_tb_tstart(KTile kt) {
+    tb_scan_small(kt.rowtot, kt.NTB, kt.tstart);
+}
+
+// A2: one workgroup per path-block.  Slot i = path_local * W + j (path_local = pair_local * D
+// + d, the global path order).
+__global__ __launch_bounds__(256) void k_tb_scatter(KParams p, KRaster rs, KTile kt) {
+    extern __shared__ __attribute__((aligned(16))) int32_t tb_s[];
+    const int NTB = kt.NTB;
+    int32_t* base = tb_s;                     // [NTB + 1] tile starts, then run bases
+    int32_t* cur = base + NTB + 1;            // [NTB] LDS cursors
+    uint2* el = reinterpret_cast<uint2*>(tb_s + ((2 * NTB + 2) & ~1));  // [SB]
+    uint16_t* tl = reinterpret_cast<uint16_t*>(el + kt.SB);               // [SB]
+    const int64_t b = blockIdx.x;
+    for (int t = threadIdx.x; t < NTB; t += blockDim.x) {
+        const int32_t bo = kt.boff[b * NTB + t];
+        base[t] = kt.tstart[t] + kt.cnt[(int64_t)t * kt.NB + b] - bo;
+        cur[t] = bo;
+    }
+    __syncthreads();
+    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
+    const int nwp = npair * kt.D * kt.W;
+    for (int i = threadIdx.x; i < nwp; i += blockDim.x) {
+        double x, y;
+        tb_point(p, kt, b, i, x, y);
+        int ix, iy, t;
+        uint32_t tc = 0;
+        if (raster_cell(rs, x, y, ix, iy)) {
+            t = (iy / TB_TS) * kt.tiles_x + ix / TB_TS;
+            tc = (uint32_t)((iy % TB_TS) * TB_TS + ix % TB_TS);
+        } else {
+            t = kt.NT;
+        }
+        const int pos = atomicAdd(&cur[t], 1);
+        // entry: slot and tile cell; destination of the gathered record = block region + the
+        // entry's rank in the block's tile-sorted order (the order B writes the runs in)
+        el[pos] = make_uint2(((uint32_t)i << 16) | tc, (uint32_t)(b * kt.SB + pos));
+        tl[pos] = (uint16_t)t;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nwp; i += blockDim.x) kt.ent[base[tl[i]] + i] = el[i];
+}
+
+// B: XCD-pinned gather (blocks b and b + 8 share an XCD).  Group x = blockIdx % 8 walks the
+// tiles t == x (mod 8); its K workgroups split each tile's bin in TB_CH-entry steps.
+__global__ __launch_bounds__(256) void k_tb_gather(KRaster rs, KTile kt,
+                                                   const uint4* __restrict__ rec, int K) {
+    __shared__ int32_t tst[TB_MAX_NTB + 1];
+    const int NTB = kt.NTB;
+    for (int t = threadIdx.x; t <= NTB; t += blockDim.x) tst[t] = kt.tstart[t];
+    __syncthreads();
+    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
+    constexpr int E = TB_CH / 256;
+    for (int t = x; t < NTB; t += 8) {
+        const int64_t s0 = tst[t], s1 = tst[t + 1];
+        const bool on = t < kt.NT;
+        const int64_t tbase = on ? (int64_t)(t / kt.tiles_x) * TB_TS * rs.nx +
+                                       (int64_t)(t % kt.tiles_x) * TB_TS
+                                 : 0;
+        for (int64_t c0 = s0 + (int64_t)r * TB_CH; c0 < s1; c0 += (int64_t)K * TB_CH) {
+            uint2 e[E];
+            uint4 v[E];
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                const int64_t i = c0 + k * 256 + threadIdx.x;
+                e[k] = i < s1 ? tb_ldnt(kt.ent + i) : make_uint2(0u, 0xffffffffu);
+            }
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                const uint32_t tc = e[k].x & 0xffffu;
+                v[k] = (on && e[k].y != 0xffffffffu && !(kt.dbg & 1))
+                           ? rec[tbase + (int64_t)(tc / TB_TS) * rs.nx + tc % TB_TS]
+                           : make_uint4(0u, 0u, 0u, TB_OFF);
+            }
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                if (e[k].y == 0xffffffffu || (kt.dbg & 2)) continue;
+                const uint32_t slot = e[k].x >> 16;
+                tb_stnt(make_uint4(v[k].x, v[k].y, v[k].z, (v[k].w & 0xffffu) | (slot << 16)),
+                        kt.recb + e[k].y);
+            }
+        }
+    }
+}
+
+// C: one workgroup per path-block.  LDS holds Φ, Σψ and the terrain term per slot (row
+// stride Ws = W | 1, odd, so the lanes' column walk is bank-conflict free).
+__global__ __launch_bounds__(256) void k_tb_reduce(KParams p, KTile kt, KOut out,
+                                                   int32_t* __restrict__ best_f,
+                                                   int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double tb_d[];
+    const int W = kt.W, D = kt.D, Ws = W | 1, PBD = kt.PB * D;
+    double* s_cost = tb_d;                  // [PBD]
+    double* s_len = s_cost + PBD;           // [PBD]
+    float* phi = reinterpret_cast<float*>(s_len + PBD);
+    float* psi = phi + PBD * Ws;
+    float* ter = psi + PBD * Ws;
+    int32_t* nh = reinterpret_cast<int32_t*>(ter + PBD * Ws);
+    int32_t* off = nh + PBD;
+    for (int i = threadIdx.x; i < PBD; i += blockDim.x) nh[i] = off[i] = 0;
+    __syncthreads();
+    const int64_t b = blockIdx.x;
+    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
+    const int npath = npair * D, nwp = npath * W;
+    const uint4* __restrict__ src = kt.recb + b * kt.SB;
+    constexpr int E = 8;  // records in flight per thread
+    for (int i0 = 0; i0 < nwp; i0 += E * 256) {
+        uint4 r[E];
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            const int i = i0 + k * 256 + (int)threadIdx.x;
+            r[k] = i < nwp ? tb_ldnt(src + i) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            if (i0 + k * 256 + (int)threadIdx.x >= nwp) break;
+            const int slot = (int)(r[k].w >> 16);
+            const int pl = slot / W, j = slot - pl * W;
+            const int s = pl * Ws + j;
+            if (r[k].w & TB_OFF) {
+                phi[s] = 0.0f;
+                psi[s] = 0.0f;
+                ter[s] = 0.0f;  // off the raster counts as sea level (consume_chunk)
+                atomicAdd(&off[pl], 1);
+            } else {
+                phi[s] = __uint_as_float(r[k].x);
+                psi[s] = __uint_as_float(r[k].y);
+                ter[s] = (r[k].w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r[k].z);
+                if (r[k].w & UAM_FLAG_NFZ) atomicAdd(&nh[pl], 1);
+            }
+        }
+    }
+    __syncthreads();
+    const int l = threadIdx.x;
+    if (l < npath) {
+        const int64_t path = b * PBD + l;
+        const double L = kt.kin[path], len = kt.kin[kt.P + path],
+                     ks = kt.kin[2 * kt.P + path];
+        const double dN = (double)p.N;
+        double cost = (double)(p.N + 1) * L, nsum = 0.0, hmax = -INFINITY;
+        const float* fp = phi + l * Ws;
+        const float* fs = psi + l * Ws;
+        const float* ft = ter + l * Ws;
+        for (int j = 0; j < W; ++j) {
+            cost = cost + (double)fp[j] / dN;
+            nsum = nsum + (double)fs[j];
+            hmax = fmax(hmax, (double)ft[j]);
+        }
+        if (out.cost) out.cost[path] = cost;
+        if (out.length_q) out.length_q[path] = L;
+        if (out.length) out.length[path] = len;
+        if (out.kin_sum) out.kin_sum[path] = ks;
+        if (out.nfz_sum) out.nfz_sum[path] = nsum;
+        if (out.nfz_hits) out.nfz_hits[path] = nh[l];
+        if (out.offmap) out.offmap[path] = off[l];
+        if (out.min_clearance) out.min_clearance[path] = p.altitude - hmax;
+        if (out.below_terrain) out.below_terrain[path] = 0;
+        s_cost[l] = cost;
+        s_len[l] = len;
+    }
+    __syncthreads();
+    if (l < npair) {
+        const int64_t q = b * kt.PB + l;
+        if (best_f) best_f[q] = select_best(s_cost + l * D, 1, D, true);
+        if (best_l) best_l[q] = select_best(s_len + l * D, 1, D, false);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
                                                    int64_t n_pairs,
                                                    const double* __restrict__ utab, int D,
@@ -2924,6 +3314,11 @@ struct uam_ctx {
     int32_t* d_grid = nullptr;  // shape-grid index (KShapeGrid), rebuilt by uam_set_params
     void* d_ws = nullptr;       // grow-only scratch of the binned evaluation (K2b)
     size_t ws_bytes = 0;
+    int tb_k = 0;               // K2t gather workgroups per XCD (0 = default; UAM_TB_K env)
+    int tb_pb = 0;              // K2t pairs per path-block (0 = default; UAM_TB_PB env)
+    int tb_dbg = 0;             // K2t diagnostics (UAM_TB_DBG env, KTile::dbg)
+    hipStream_t s2 = nullptr;   // K2t side stream (pass 1 beside the streaming launches)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -3005,6 +3400,9 @@ int uam_ctx_create(int device, uam_ctx** out) {
     uam_ctx* c = new (std::nothrow) uam_ctx();
     if (!c) return fail(UAM_E_NOMEM, "ctx allocation failed");
     c->device = device;
+    if (const char* e = std::getenv("UAM_TB_K")) c->tb_k = std::atoi(e);  // tuning experiments
+    if (const char* e = std::getenv("UAM_TB_PB")) c->tb_pb = std::atoi(e);
+    if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
     *out = c;
     return UAM_OK;
 }
@@ -3016,6 +3414,9 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
     delete ctx;
 }
 
@@ -3449,6 +3850,97 @@ static int launch_binned(uam_ctx* ctx, const KRaster& kr, const void* rec, const
     return 1;
 }
 
+// K2t launch (tuning 12); returns 1 if launched, 0 if the batch does not fit (caller falls
+// back to K2).  Path-block size PB: the largest of 16, 8, 4, 2, 1 pairs whose LDS image
+// (12 B per slot in C, 10 B per slot in A2) fits kTbLds.
+static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
+                        int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
+                        int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    if (ko.cells || ko.g_rows || D > 16) return 0;
+    const int64_t W = ctx->kp.N + 2, P = n_pairs * D, n_wp = P * W;
+    if (n_wp >= INT32_MAX) return 0;
+    const int tiles_x = (kr.nx + TB_TS - 1) / TB_TS, tiles_y = (kr.ny + TB_TS - 1) / TB_TS;
+    const int64_t NT = (int64_t)tiles_x * tiles_y, NTB = NT + 1;
+    if (NTB > TB_MAX_NTB) return 0;
+    constexpr size_t kTbLds = 96 * 1024;
+    const int64_t Ws = W | 1;
+    int PB = ctx->tb_pb > 0 ? ctx->tb_pb : 8;
+    auto lds_c = [&](int pb) { return (size_t)pb * D * (16 + 8 + 12 * Ws); };
+    auto lds_a2 = [&](int pb) { return (size_t)(2 * NTB + 2) * 4 + (size_t)pb * D * W * 10; };
+    while (PB > 1 && (lds_c(PB) > kTbLds || lds_a2(PB) > kTbLds || PB * D * W >= 65536))
+        PB /= 2;
+    if (lds_c(PB) > kTbLds || lds_a2(PB) > kTbLds || PB * D * W >= 65536) return 0;
+    const int64_t NB = (n_pairs + PB - 1) / PB, SB = (int64_t)PB * D * W;
+    if (NB >= INT32_MAX / NTB) return 0;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_cnt = al(NTB * NB * 4), b_tot = al((2 * NTB + 1) * 4), b_boff = al(NB * NTB * 4),
+                 b_ent = al((size_t)n_wp * 8), b_recb = al((size_t)NB * SB * 16),
+                 b_kin = al((size_t)P * 24);
+    const size_t need = b_cnt + b_tot + b_boff + b_ent + b_recb + b_kin;
+    if (need > ctx->ws_bytes) {
+        if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+        ctx->d_ws = nullptr;
+        ctx->ws_bytes = 0;
+        if (hipMalloc(&ctx->d_ws, need) != hipSuccess) return fail(UAM_E_NOMEM, "tiled scratch");
+        ctx->ws_bytes = need;
+    }
+    char* w = (char*)ctx->d_ws;
+    KTile kt{};
+    kt.pairs = pairs;
+    kt.utab = utab;
+    kt.n_pairs = n_pairs;
+    kt.P = P;
+    kt.D = D;
+    kt.W = (int32_t)W;
+    kt.PB = PB;
+    kt.NB = (int32_t)NB;
+    kt.SB = (int32_t)SB;
+    kt.tiles_x = tiles_x;
+    kt.NT = (int32_t)NT;
+    kt.NTB = (int32_t)NTB;
+    kt.cnt = (int32_t*)w;
+    kt.rowtot = (int32_t*)(w + b_cnt);
+    kt.tstart = kt.rowtot + NTB;
+    kt.dbg = ctx->tb_dbg;
+    kt.boff = (int32_t*)(w + b_cnt + b_tot);
+    kt.ent = (uint2*)(w + b_cnt + b_tot + b_boff);
+    kt.recb = (uint4*)(w + b_cnt + b_tot + b_boff + b_ent);
+    kt.kin = (double*)(w + b_cnt + b_tot + b_boff + b_ent + b_recb);
+    static bool attrs = false;
+    if (!attrs) {
+        (void)hipFuncSetAttribute((const void*)k_tb_scatter,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds);
+        (void)hipFuncSetAttribute((const void*)k_tb_reduce,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds);
+        attrs = true;
+    }
+    // pass 1 (ALU-bound) on a second stream, beside the streaming launches A1..B
+    if (!ctx->s2) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+    if (!(kt.dbg & 4))
+        hipLaunchKernelGGL(k_tb_kin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D), 0,
+                           ctx->s2, ctx->kp, kt);
+    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+    hipLaunchKernelGGL(k_tb_count, dim3((unsigned)NB), dim3(256), (size_t)NTB * 4, s, ctx->kp, kr,
+                       kt);
+    hipLaunchKernelGGL(k_tb_rowscan, dim3((unsigned)NTB), dim3(1024), 0, s, kt);
+    hipLaunchKernelGGL(k_tb_tstart, dim3(1), dim3(64), 0, s, kt);
+    hipLaunchKernelGGL(k_tb_scatter, dim3((unsigned)NB), dim3(256), lds_a2(PB), s, ctx->kp, kr,
+                       kt);
+    const int K = ctx->tb_k > 0 ? ctx->tb_k : 128;  // workgroups per XCD group
+    hipLaunchKernelGGL(k_tb_gather, dim3(8 * K), dim3(256), 0, s, kr, kt, (const uint4*)rec, K);
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    hipLaunchKernelGGL(k_tb_reduce, dim3((unsigned)NB), dim3(256), lds_c(PB), s, ctx->kp, kt, ko,
+                       best_f, best_l);
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "tiled evaluation launch");
+    return 1;
+}
+
 int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec, const double* pairs, int64_t n_pairs,
                        const double* utab, int32_t D, const uam_path_outputs* out,
@@ -3480,6 +3972,11 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     }
     if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_BINNED) {
         st = launch_binned(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
+    if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_TILED) {
+        st = launch_tiled(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
         if (st == 1) return UAM_OK;
     }
