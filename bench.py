@@ -68,10 +68,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one GPU per rank; UAM_BENCH_RANKS_PER_GPU > 1 packs ranks onto fewer GPUs (rehearsal of
+    # the N-rank path on a 1-GPU box, with UAM_DIST_BACKEND=gloo since RCCL needs a GPU per
+    # rank)
+    per_gpu = max(1, int(os.environ.get("UAM_BENCH_RANKS_PER_GPU", "1")))
+    backend = None
+    local = local // per_gpu
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("UAM_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -108,6 +118,9 @@ def main():
 
     # ---- cost raster / volume: rank 0 builds (K1), one RCCL broadcast --------------------
     setup = {}
+    if world > 1:
+        setup["dist_backend"] = backend
+        setup["ranks_per_gpu"] = per_gpu
     geo = raster_geo(R)
     raster = volume = None
     if raster_mode or volume_mode:
@@ -226,7 +239,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (DEM seed 1 with the Nagasaki DEM's statistics, pairs seed 0, "
                 "NFZ polygons seed 2; canonical map geometry from the reference data files)",
-        "config": {"workload": f"{args.workload}: {cfg['name']}",
+        "config": {"workload": f"{args.workload}: {workload_name(cfg['name'], world)}",
                    "dem": f"{R}x{R}", "pairs_per_gpu": Q, "displacements": D,
                    "waypoints_per_path": W, "paths_per_gpu": P, "mode": args.mode,
                    "no_fly_shapes": geom.n_obstacles, "region_shapes":
@@ -319,6 +332,15 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def workload_name(name, world):
+    """The BASELINE config's name with its GPU count replaced by this run's (weak scaling:
+    the per-GPU workload is the config's, the job spans `world` GPUs)."""
+    import re
+
+    base = re.sub(r",\s*\d+\s*(x|\u00d7)?\s*(MI355X|GPUs?)\s*$", "", name)
+    return f"{base}, {world} GPU" + ("s" if world > 1 else "")
 
 
 def cpu_threads(requested):
