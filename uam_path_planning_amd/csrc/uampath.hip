@@ -1467,6 +1467,238 @@ __global__ __launch_bounds__(256) void k_raster_build(KGeom g, KParams p, KRaste
     }
 }
 
+// ---- K1 with CPL cells (rows) per lane ------------------------------------------------------
+// The single-cell K1 spends most of its issue slots in the scalar walk (measured: 357 SALU,
+// 499 VALU and 53 SMEM instructions per 64-cell wave on the cfg3 map, profiles/r01/k1/): the
+// union walk, the shape and inequality records and the loop control are paid once per wave.
+// Here a wave covers a strip of 64 columns x CPL rows, one column per lane, so each walk step
+// and each scalar record load serves CPL cells; each inequality is evaluated once for all the
+// lane's cells, and the no-fly psi and contains tables are walked together (one h per
+// inequality for both).  Every cell still adds exactly its own list's terms in its own order.
+
+// table-L walk over CPL cells per lane: body(s, mine), mine = bit k set iff s is in cell k's
+// list; s ascending and wave-uniform (see wave_walk)
+template <int L, int CPL, class F>
+__device__ __forceinline__ void wave_walk_cells(const KGeom& g, const int (&slot)[CPL],
+                                                F&& body) {
+    const int mw = g.grid.mask[L] ? g.grid.mw[L] : 0;
+    if (mw) {
+#pragma unroll 1
+        for (int w = 0; w < mw; ++w) {
+            uint64_t mk[CPL], any = 0ull;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                mk[k] = slot[k] >= 0 ? g.grid.mask[L][(int64_t)slot[k] * mw + w] : 0ull;
+                any |= mk[k];
+            }
+            for (uint64_t b = wave_or_u64(any); b; b &= b - 1) {
+                const int bit = __builtin_ctzll(b);
+                uint32_t mine = 0;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) mine |= (uint32_t)((mk[k] >> bit) & 1ull) << k;
+                body(g.grid.mbase[L] + 64 * w + bit, mine);
+            }
+        }
+        return;
+    }
+    int kk[CPL], k1[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        kk[k] = k1[k] = 0;
+        if (slot[k] >= 0) {
+            kk[k] = g.grid.start[L][slot[k]];
+            k1[k] = g.grid.start[L][slot[k] + 1];
+        }
+    }
+    for (;;) {
+        int cand[CPL], lmin = INT32_MAX;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            cand[k] = kk[k] < k1[k] ? g.grid.items[L][kk[k]] : INT32_MAX;
+            lmin = min(lmin, cand[k]);
+        }
+        const int s = wave_min_i32(lmin);
+        if (s == INT32_MAX) break;
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (cand[k] == s) {
+                mine |= 1u << k;
+                ++kk[k];
+            }
+        body(s, mine);
+    }
+}
+
+// the two obstacle tables (1: psi, 2: contains) in one ascending walk when both have masks:
+// body(s, mine_psi, mine_hit)
+template <int CPL, class F>
+__device__ __forceinline__ void wave_walk_obs_cells(const KGeom& g, const int (&slot)[CPL],
+                                                    F&& body) {
+    const int mw = g.grid.mask[1] ? g.grid.mw[1] : 0;
+    if (mw && g.grid.mask[2] && g.grid.mw[2] == mw && g.grid.mbase[2] == g.grid.mbase[1]) {
+#pragma unroll 1
+        for (int w = 0; w < mw; ++w) {
+            uint64_t m1[CPL], m2[CPL], any = 0ull;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const bool on = slot[k] >= 0;
+                m1[k] = on ? g.grid.mask[1][(int64_t)slot[k] * mw + w] : 0ull;
+                m2[k] = on ? g.grid.mask[2][(int64_t)slot[k] * mw + w] : 0ull;
+                any |= m1[k] | m2[k];
+            }
+            for (uint64_t b = wave_or_u64(any); b; b &= b - 1) {
+                const int bit = __builtin_ctzll(b);
+                uint32_t a1 = 0, a2 = 0;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    a1 |= (uint32_t)((m1[k] >> bit) & 1ull) << k;
+                    a2 |= (uint32_t)((m2[k] >> bit) & 1ull) << k;
+                }
+                body(g.grid.mbase[1] + 64 * w + bit, a1, a2);
+            }
+        }
+        return;
+    }
+    wave_walk_cells<1, CPL>(g, slot, [&](int s, uint32_t m) { body(s, m, 0u); });
+    wave_walk_cells<2, CPL>(g, slot, [&](int s, uint32_t m) { body(s, 0u, m); });
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
+                                                            const float* __restrict__ dem,
+                                                            float nodata, float thr,
+                                                            uint4* __restrict__ rec) {
+    const int sxn = (rs.nx + 63) / 64;
+    const int64_t n_strips = (int64_t)sxn * ((rs.ny + CPL - 1) / CPL);
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const bool pen_smooth = p.penalty_smooth != 0, obs_smooth = p.obstacle_smooth != 0;
+    for (int64_t st = w0; st < n_strips; st += nw) {  // wave-uniform strip index
+        const int sy = (int)(st / sxn), sx = (int)(st - (int64_t)sy * sxn);
+        const int ix = sx * 64 + lane;
+        const double xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
+        double yc[CPL];
+        int slot[CPL];
+        bool valid[CPL];
+        float z[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int iy = sy * CPL + k;
+            valid[k] = ix < rs.nx && iy < rs.ny;
+            yc[k] = rs.y_top - ((double)iy + 0.5) * rs.dy;
+            z[k] = (valid[k] && dem) ? dem[(int64_t)iy * rs.nx + ix] : 0.0f;
+            slot[k] = valid[k] ? (g.grid.gx ? grid_slot(g.grid, xc, yc[k]) : -1) : -2;
+        }
+        // Φ: total_penalty's region loop, per cell
+        double pen[CPL], t[CPL];
+        int rc[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) pen[k] = t[k] = 0.0, rc[k] = -1;
+        wave_walk_cells<0, CPL>(g, slot, [&](int s, uint32_t mine) {
+            if (!mine) return;
+            const DevShape sh = uload(g.shape, s);
+            uint32_t need = 0;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (!((mine >> k) & 1u)) continue;
+                if (sh.region != rc[k]) {
+                    if (rc[k] >= 0) pen[k] = pen[k] + p.weights[rc[k]] * t[k];
+                    rc[k] = sh.region;
+                    t[k] = 0.0;
+                }
+                if (!((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, xc, yc[k])))
+                    need |= 1u << k;
+            }
+            if (!need) return;
+            double r[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) r[k] = 1.0;
+            const int end = sh.first + sh.count;
+            for (int i = sh.first; i < end; ++i) {  // psi_u, one record load for all cells
+                const DevIneq q = uload(g.ineq, i);
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const double h = ineq_h(&q, xc, yc[k]);
+                    if (pen_smooth) {
+                        const double m = fmin(h - p.enlargement, 0.0);
+                        r[k] = r[k] * (m * m);
+                    } else {
+                        r[k] = r[k] * fmin(p.enlargement - h, 0.0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+                if ((need >> k) & 1u)
+                    t[k] = sh.has_center ? t[k] + r[k] / sh.norm_pen : t[k] + r[k];
+        });
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (rc[k] >= 0) pen[k] = pen[k] + p.weights[rc[k]] * t[k];
+        // Σψ_nfz (obstacle_psi_sum, e = 0) and Map.collides, one h per inequality for both
+        double acc[CPL];
+        bool hit[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = 0.0, hit[k] = false;
+        wave_walk_obs_cells<CPL>(g, slot, [&](int s, uint32_t m1, uint32_t m2) {
+            if (!(m1 | m2)) return;
+            const DevShape sh = uload(g.shape, s);
+            uint32_t n1 = 0, n2 = 0;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const bool out = outside(sh.box_obs, xc, yc[k]);
+                if (((m1 >> k) & 1u) && !((sh.flags & SHAPE_CULL_PSI) && out)) n1 |= 1u << k;
+                if (((m2 >> k) & 1u) && !((sh.flags & SHAPE_CULL_HIT) && out)) n2 |= 1u << k;
+            }
+            if (!(n1 | n2)) return;
+            double r[CPL];
+            bool in[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) r[k] = 1.0, in[k] = true;
+            const int end = sh.first + sh.count;
+            for (int i = sh.first; i < end; ++i) {
+                const DevIneq q = uload(g.ineq, i);
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const double h = ineq_h(&q, xc, yc[k]);
+                    if (obs_smooth) {
+                        const double m = fmin(h - 0.0, 0.0);
+                        r[k] = r[k] * (m * m);
+                    } else {
+                        r[k] = r[k] * fmin(0.0 - h, 0.0);
+                    }
+                    in[k] = in[k] && !(h > 1e-14);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if ((n1 >> k) & 1u) acc[k] = acc[k] + r[k];
+                if ((n2 >> k) & 1u) hit[k] = hit[k] || in[k];
+            }
+        });
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (slot[k] == -1) {  // no index slot (no grid, NaN): the per-point functions
+                pen[k] = total_penalty(g, p, xc, yc[k]);
+                acc[k] = obstacle_psi_sum(g, p, xc, yc[k]);
+                hit[k] = collides(g, xc, yc[k]);
+            }
+            if (valid[k]) {
+                uint32_t fl = 0;
+                if (hit[k]) fl |= UAM_FLAG_NFZ;
+                if (thr == -9999.0f ? (z[k] == -9999.0f) : (z[k] > thr)) fl |= UAM_FLAG_MASK;
+                if (z[k] == nodata) fl |= UAM_FLAG_NODATA;
+                rec[(int64_t)(sy * CPL + k) * rs.nx + ix] =
+                    make_uint4(__float_as_uint((float)pen[k]), __float_as_uint((float)acc[k]),
+                               __float_as_uint(z[k]), fl);
+            }
+        }
+    }
+}
+
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
 // gradient accumulation order as oracle refine_L.  The waypoint loop runs a wave-uniform trip
 // count (lane j = jb + lane, valid = j < W) so the geometry can be walked by the whole wave.
@@ -3317,6 +3549,8 @@ struct uam_ctx {
     int tb_k = 0;               // K2t gather workgroups per XCD (0 = default; UAM_TB_K env)
     int tb_pb = 0;              // K2t pairs per path-block (0 = default; UAM_TB_PB env)
     int tb_dbg = 0;             // K2t diagnostics (UAM_TB_DBG env, KTile::dbg)
+    int k1_cpl = 0;             // K1 cells per lane: 0 = default (2), 1 = single-cell kernel,
+                                // 2 / 4 / 8 (UAM_K1_CPL env)
     hipStream_t s2 = nullptr;   // K2t side stream (pass 1 beside the streaming launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -3403,6 +3637,7 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_TB_K")) c->tb_k = std::atoi(e);  // tuning experiments
     if (const char* e = std::getenv("UAM_TB_PB")) c->tb_pb = std::atoi(e);
     if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
     *out = c;
     return UAM_OK;
 }
@@ -3672,9 +3907,29 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
     if (!rec) return fail(UAM_E_INVALID, "rec is NULL");
     DeviceGuard dg(ctx->device);
     const int64_t cells = (int64_t)kr.nx * kr.ny;
-    hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0,
-                       (hipStream_t)stream, ctx->kg, ctx->kp, kr, dem, desc->nodata,
-                       desc->dem_threshold, (uint4*)rec);
+    const hipStream_t s = (hipStream_t)stream;
+    const int cpl = ctx->k1_cpl > 0 ? ctx->k1_cpl : 2;  // cells (rows) per lane
+    const int64_t strips = (int64_t)((kr.nx + 63) / 64) * ((kr.ny + cpl - 1) / cpl);
+    const dim3 gs(grid_for(strips * 64, 256));
+    switch (cpl) {
+        case 1:  // the single-cell kernel
+            hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0, s,
+                               ctx->kg, ctx->kp, kr, dem, desc->nodata, desc->dem_threshold,
+                               (uint4*)rec);
+            break;
+        case 2:
+            hipLaunchKernelGGL(k_raster_build_cells<2>, gs, dim3(256), 0, s, ctx->kg, ctx->kp,
+                               kr, dem, desc->nodata, desc->dem_threshold, (uint4*)rec);
+            break;
+        case 8:
+            hipLaunchKernelGGL(k_raster_build_cells<8>, gs, dim3(256), 0, s, ctx->kg, ctx->kp,
+                               kr, dem, desc->nodata, desc->dem_threshold, (uint4*)rec);
+            break;
+        default:
+            hipLaunchKernelGGL(k_raster_build_cells<4>, gs, dim3(256), 0, s, ctx->kg, ctx->kp,
+                               kr, dem, desc->nodata, desc->dem_threshold, (uint4*)rec);
+            break;
+    }
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
