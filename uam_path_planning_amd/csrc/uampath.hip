@@ -3551,6 +3551,7 @@ struct uam_ctx {
     int tb_dbg = 0;             // K2t diagnostics (UAM_TB_DBG env, KTile::dbg)
     int k1_cpl = 0;             // K1 cells per lane: 0 = default (2), 1 = single-cell kernel,
                                 // 2 / 4 / 8 (UAM_K1_CPL env)
+    int k1_grid = 0;            // K1 workgroup cap (0 = one wave per strip; UAM_K1_GRID env)
     hipStream_t s2 = nullptr;   // K2t side stream (pass 1 beside the streaming launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -3638,6 +3639,7 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_TB_PB")) c->tb_pb = std::atoi(e);
     if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
     *out = c;
     return UAM_OK;
 }
@@ -3910,7 +3912,7 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
     const hipStream_t s = (hipStream_t)stream;
     const int cpl = ctx->k1_cpl > 0 ? ctx->k1_cpl : 2;  // cells (rows) per lane
     const int64_t strips = (int64_t)((kr.nx + 63) / 64) * ((kr.ny + cpl - 1) / cpl);
-    const dim3 gs(grid_for(strips * 64, 256));
+    const dim3 gs(grid_for(strips * 64, 256, ctx->k1_grid > 0 ? ctx->k1_grid : (1 << 20)));
     switch (cpl) {
         case 1:  // the single-cell kernel
             hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0, s,
