@@ -2173,6 +2173,26 @@ __device__ __forceinline__ int wave_isum(int v) {
     return v;
 }
 
+// Stable in-place compaction of a[0..n) (the wave's LDS slice) to its entries that are not
+// ±0.0 (NaN is kept); returns their count.  Whole wave active.  Entry i moves to a position
+// <= i, and each chunk is read by every lane before any lane writes, so nothing unread is
+// overwritten.
+__device__ __forceinline__ int wave_compact_nonzero(double* a, int n, int lane) {
+    int cnt = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const double v = i < n ? a[i] : 0.0;
+        const bool nz = i < n && !(v == 0.0);
+        const uint64_t m = __ballot(nz);
+        const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+        wave_sync();
+        if (nz) a[pos] = v;
+        cnt += __popcll(m);
+        wave_sync();
+    }
+    return cnt;
+}
+
 // UAM_EW_PROF builds (tuning experiments only): lane 0 of each of the first 1024 paths stamps
 // s_memtime at the phase boundaries of k_eval_wave; uam_debug_ew_prof copies the stamps out.
 #ifdef UAM_EW_PROF
@@ -2352,22 +2372,26 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     below = wave_isum(below);
     wave_sync();
     EW_STAMP(4);
-    // eval_path's sequential sums, same order, on four lanes at once: phase A runs the W-term
-    // chains (lane 0 L, lane 1 length, lane 2 no-fly sum) and the first W kinematic rows
-    // (lane 3); lane 0 then seeds the cost chain with (N+1) L and phase B runs it beside the
-    // rest of the kinematic chain (lane 3), so the serial length is max(2W, 3N) adds, not
-    // 3N + W.  Every accumulator starts at +0.0, so the +0.0 entries are exact no-ops.
+    // eval_path's sequential sums, same order, on four lanes at once.  Every accumulator
+    // starts at +0.0 and so is never -0.0, which makes a ±0.0 term an exact no-op: the Φ/N,
+    // no-fly and kinematic term lists are first compacted (stable, in place) to their nonzero
+    // entries -- an arc within the turn and ratio limits has no nonzero kinematic row at all.
+    // Phase A: lane 0 L (W terms), lane 1 length (W), lane 2 no-fly sum, lane 3 kinematic
+    // sum; then lane 0 seeds the cost chain with (N+1) L and adds the nonzero Φ/N terms.  The
+    // serial length is max(W + nnz(Φ), nnz(kinematic)) adds instead of max(2W, 3N).
+    const int nps = wave_compact_nonzero(ps, W, lane);
+    const int nph = wave_compact_nonzero(ph, W, lane);
+    const int nkn = wave_compact_nonzero(kn, 3 * N, lane);
     const double* arr = lane == 0 ? lq : (lane == 1 ? sg : (lane == 2 ? ps : kn));
-    const int na = lane < 3 ? W : (lane == 3 ? min(W, 3 * N) : 0);
+    const int na = lane < 2 ? W : (lane == 2 ? nps : (lane == 3 ? nkn : 0));
     double acc = 0.0;
 #pragma unroll 8
     for (int i = 0; i < na; ++i) acc = acc + arr[i];
     double L = acc;
     if (lane == 0) acc = (double)(N + 1) * L;
-    const double* brr = lane == 0 ? ph : kn + W;
-    const int nb = lane == 0 ? W : (lane == 3 ? 3 * N - na : 0);
+    const int nb = lane == 0 ? nph : 0;
 #pragma unroll 8
-    for (int i = 0; i < nb; ++i) acc = acc + brr[i];
+    for (int i = 0; i < nb; ++i) acc = acc + ph[i];
     L = __shfl(L, 0, 64);
     const double len = __shfl(acc, 1, 64), nsum = __shfl(acc, 2, 64);
     const double ksum = __shfl(acc, 3, 64);
