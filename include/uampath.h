@@ -297,7 +297,13 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * evaluation (K2b); 12 = tile-sorted raster evaluation (K2t: waypoints binned by raster
  * tile, XCD-pinned gathers from L2, per-block LDS reduction; pass 1 on a side stream).
  * 0 picks the wave per path kernel for batches up to 16384 paths and variant 2 above.  All
- * variants return bit-identical results. */
+ * variants return bit-identical results.
+ *
+ * Tuning experiments only (read once, by uam_ctx_create; unset = the defaults): UAM_K1_CPL
+ * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
+ * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
+ * UAM_TB_DBG (K2t diagnostics that change results: 1 skips the gathers, 2 the stores,
+ * 4 pass 1).  None of them changes results except UAM_TB_DBG. */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */
