@@ -21,11 +21,13 @@
 // tables are read with wave-uniform addresses (scalar cache) in the analytic mode.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -3556,6 +3558,11 @@ bool shape_box(const DevIneq* q, int n, double e, double box[4]) {
 
 }  // namespace
 
+namespace {
+void pinned_arena_free(void* a);  // K8 host arena (defined with PinnedArena)
+void dev_arena_free(void* a);     // K8 device arena (defined with DevArena)
+}  // namespace
+
 struct uam_ctx {
     int device = 0;
     DevIneq* d_ineq = nullptr;
@@ -3578,6 +3585,8 @@ struct uam_ctx {
     int k1_grid = 0;            // K1 workgroup cap (0 = one wave per strip; UAM_K1_GRID env)
     hipStream_t s2 = nullptr;   // K2t side stream (pass 1 beside the streaming launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
+    void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
 };
 
 namespace {
@@ -3678,6 +3687,8 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
+    if (ctx->pinned) pinned_arena_free(ctx->pinned);
+    if (ctx->devarena) dev_arena_free(ctx->devarena);
     delete ctx;
 }
 
@@ -4539,22 +4550,41 @@ int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* t, const float* src,
 
 namespace {
 
-// stream-ordered scratch (the runtime's memory pool serves repeated calls without a device
-// synchronisation per allocation)
-thread_local hipStream_t g_devbuf_stream = nullptr;
+// Device scratch of uam_dem_polygons, served from a grow-only arena the context keeps and
+// reset at the start of each call (every use is complete before the call returns).  Freeing
+// ~30 stream-ordered buffers per call cost ~2.4 ms at 8192^2; the arena costs nothing.
+struct DevArena {
+    std::vector<std::pair<char*, size_t>> chunks;
+    size_t chunk = 0, used = 0;
+    void reset() { chunk = 0, used = 0; }
+    void* get(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        while (chunk < chunks.size() && used + bytes > chunks[chunk].second) ++chunk, used = 0;
+        if (chunk == chunks.size()) {
+            const size_t sz = std::max(bytes, (size_t)64 << 20);
+            void* p = nullptr;
+            if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
+            chunks.emplace_back((char*)p, sz);
+            used = 0;
+        }
+        void* p = chunks[chunk].first + used;
+        used += bytes;
+        return p;
+    }
+    ~DevArena() {
+        for (auto& c : chunks) (void)hipFree(c.first);
+    }
+};
+thread_local DevArena* g_devarena = nullptr;  // the calling context's arena
 
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     int64_t n = 0;
-    hipStream_t s = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFreeAsync(p, s);
-    }
     hipError_t alloc(int64_t count) {
         n = count;
-        s = g_devbuf_stream;
-        return hipMallocAsync((void**)&p, (size_t)std::max<int64_t>(count, 1) * sizeof(T), s);
+        p = (T*)g_devarena->get((size_t)std::max<int64_t>(count, 1) * sizeof(T));
+        return p ? hipSuccess : hipErrorOutOfMemory;
     }
 };
 
@@ -4569,94 +4599,178 @@ struct CompStats {
     std::vector<int32_t> cnt, x0, y0, x1, y1, root;
 };
 
-// label a grid (optionally with cuts) and return per-component stats; L is initialised
-int label_grid(int32_t nx, int32_t ny, const int32_t* colbox, const int32_t* rowbox, bool runs,
-               int32_t* L, DevBuf<int32_t>& cid, CompStats& st, hipStream_t s) {
-    const int64_t n = (int64_t)nx * ny;
-    const dim3 g(grid_for(n, 256, INT32_MAX)), b(256);
-    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, nx, ny, colbox, rowbox, runs ? 1 : 0, L);
-    hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, n, L);
-    const int64_t nblk = (n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
-    DevBuf<int32_t> cnt, off;
-    HIP_TRY2(cnt.alloc(nblk));
-    HIP_TRY2(off.alloc(nblk));
-    hipLaunchKernelGGL(k_ccl_count_roots, dim3((unsigned)nblk), b, 0, s, L, n, cnt.p);
-    std::vector<int32_t> h(nblk);
-    HIP_TRY2(hipMemcpyAsync(h.data(), cnt.p, nblk * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY2(hipStreamSynchronize(s));
-    int64_t acc = 0;
-    for (int64_t i = 0; i < nblk; ++i) {
-        const int32_t c = h[i];
-        h[i] = (int32_t)acc;
-        acc += c;
+// Page-locked host memory for the device -> host copies (so they stay asynchronous), served
+// from a grow-only arena the context keeps: pinning and unpinning pages costs milliseconds, so
+// chunks are allocated once and reused by later calls.
+struct PinnedArena {
+    std::vector<std::pair<char*, size_t>> chunks;
+    size_t chunk = 0, used = 0;
+    void reset() { chunk = 0, used = 0; }
+    void* get(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        while (chunk < chunks.size() && used + bytes > chunks[chunk].second) ++chunk, used = 0;
+        if (chunk == chunks.size()) {
+            const size_t sz = std::max(bytes, (size_t)8 << 20);
+            void* p = nullptr;
+            if (hipHostMalloc(&p, sz) != hipSuccess) return nullptr;
+            chunks.emplace_back((char*)p, sz);
+            used = 0;
+        }
+        void* p = chunks[chunk].first + used;
+        used += bytes;
+        return p;
     }
-    const int32_t ncomp = (int32_t)acc;
-    HIP_TRY2(hipMemcpyAsync(off.p, h.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    HIP_TRY2(cid.alloc(n));
-    hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)nblk), b, 0, s, L, n, off.p, cid.p);
-    DevBuf<int32_t> a;
-    HIP_TRY2(a.alloc(6 * (int64_t)std::max(ncomp, 1)));
-    const dim3 gc(grid_for(std::max(ncomp, 1), 256, INT32_MAX));
-    int32_t* cntp = a.p;
-    int32_t *bx0 = a.p + ncomp, *by0 = a.p + 2 * (int64_t)ncomp, *bx1 = a.p + 3 * (int64_t)ncomp,
-            *by1 = a.p + 4 * (int64_t)ncomp, *rt = a.p + 5 * (int64_t)ncomp;
-    if (ncomp > 0) {
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, cntp, (int64_t)ncomp, 0);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, bx0, (int64_t)ncomp, INT32_MAX);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by0, (int64_t)ncomp, INT32_MAX);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, bx1, (int64_t)ncomp, -1);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, by1, (int64_t)ncomp, -1);
-        hipLaunchKernelGGL(k_ccl_stats, dim3((unsigned)nblk), b, 0, s, L, cid.p, nx, n, cntp,
-                           bx0, by0, bx1, by1, rt);
+    ~PinnedArena() {
+        for (auto& c : chunks) (void)hipHostFree(c.first);
     }
+};
+thread_local PinnedArena* g_pinned = nullptr;  // the calling context's arena
+void pinned_arena_free(void* a) { delete static_cast<PinnedArena*>(a); }
+void dev_arena_free(void* a) { delete static_cast<DevArena*>(a); }
+
+template <typename T>
+struct PinnedBuf {
+    T* p = nullptr;
+    hipError_t alloc(int64_t count) {
+        p = (T*)g_pinned->get((size_t)std::max<int64_t>(count, 1) * sizeof(T));
+        return p ? hipSuccess : hipErrorOutOfMemory;
+    }
+};
+
+// Labelling of one grid in three stages, so that several grids can be in flight between two
+// host synchronisations (uam_dem_polygons labels all large regions together).
+//   1: merge, flatten, per-block root counts (copied to the host)     -- then synchronise
+//   2: root ranks from the host prefix, component stats (to the host) -- then synchronise
+//   3: unpack the stats
+struct GridJob {
+    int32_t nx = 0, ny = 0;
+    int64_t n = 0, nblk = 0;
+    int32_t* L = nullptr;
+    int32_t ncomp = 0;
+    DevBuf<int32_t> cnt, off, cid, a;
+    PinnedBuf<int32_t> hcnt, hall;
+    std::vector<int32_t> hoff;
+    CompStats st;
+};
+
+int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool runs,
+              hipStream_t s) {
+    j.n = (int64_t)j.nx * j.ny;
+    const dim3 g(grid_for(j.n, 256, INT32_MAX)), b(256);
+    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, j.nx, j.ny, colbox, rowbox, runs ? 1 : 0, j.L);
+    hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
+    j.nblk = (j.n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
+    HIP_TRY2(j.cnt.alloc(j.nblk));
+    HIP_TRY2(j.off.alloc(j.nblk));
+    HIP_TRY2(j.hcnt.alloc(j.nblk));
+    hipLaunchKernelGGL(k_ccl_count_roots, dim3((unsigned)j.nblk), b, 0, s, j.L, j.n, j.cnt.p);
     HIP_TRY2(hipGetLastError());
-    std::vector<int32_t> all(6 * (int64_t)ncomp);
-    if (ncomp > 0)
-        HIP_TRY2(hipMemcpyAsync(all.data(), a.p, all.size() * sizeof(int32_t),
-                                hipMemcpyDeviceToHost, s));
-    HIP_TRY2(hipStreamSynchronize(s));
-    auto col = [&](int k) {
-        return std::vector<int32_t>(all.begin() + (int64_t)k * ncomp,
-                                    all.begin() + (int64_t)(k + 1) * ncomp);
-    };
-    st.cnt = col(0), st.x0 = col(1), st.y0 = col(2), st.x1 = col(3), st.y1 = col(4);
-    st.root = col(5);
+    HIP_TRY2(hipMemcpyAsync(j.hcnt.p, j.cnt.p, j.nblk * sizeof(int32_t), hipMemcpyDeviceToHost,
+                            s));
     return UAM_OK;
 }
 
-// per-row [xmin, xmax] of the selected components (sel[c] true), row tables concatenated
-int row_extents(int32_t nx, int32_t ny, const int32_t* L, const int32_t* cid,
-                const CompStats& st, const std::vector<char>& sel, std::vector<int64_t>& off,
-                std::vector<int32_t>& xmin, std::vector<int32_t>& xmax, hipStream_t s) {
-    const int32_t ncomp = (int32_t)st.cnt.size();
-    off.assign(ncomp, -1);
+int lg_stage2(GridJob& j, hipStream_t s) {
+    j.hoff.resize(j.nblk);
+    int64_t acc = 0;
+    for (int64_t i = 0; i < j.nblk; ++i) {
+        j.hoff[i] = (int32_t)acc;
+        acc += j.hcnt.p[i];
+    }
+    j.ncomp = (int32_t)acc;
+    const int32_t nc = j.ncomp;
+    const dim3 b(256);
+    HIP_TRY2(hipMemcpyAsync(j.off.p, j.hoff.data(), j.nblk * sizeof(int32_t),
+                            hipMemcpyHostToDevice, s));
+    HIP_TRY2(j.cid.alloc(j.n));
+    hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)j.nblk), b, 0, s, j.L, j.n, j.off.p, j.cid.p);
+    HIP_TRY2(j.a.alloc(6 * (int64_t)std::max(nc, 1)));
+    HIP_TRY2(j.hall.alloc(6 * (int64_t)std::max(nc, 1)));
+    if (nc > 0) {
+        const dim3 gc(grid_for(nc, 256, INT32_MAX));
+        int32_t* p = j.a.p;
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p, (int64_t)nc, 0);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + nc, (int64_t)nc, INT32_MAX);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 2 * (int64_t)nc, (int64_t)nc, INT32_MAX);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 3 * (int64_t)nc, (int64_t)nc, -1);
+        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 4 * (int64_t)nc, (int64_t)nc, -1);
+        hipLaunchKernelGGL(k_ccl_stats, dim3((unsigned)j.nblk), b, 0, s, j.L, j.cid.p, j.nx, j.n,
+                           p, p + nc, p + 2 * (int64_t)nc, p + 3 * (int64_t)nc,
+                           p + 4 * (int64_t)nc, p + 5 * (int64_t)nc);
+        HIP_TRY2(hipGetLastError());
+        HIP_TRY2(hipMemcpyAsync(j.hall.p, j.a.p, 6 * (int64_t)nc * sizeof(int32_t),
+                                hipMemcpyDeviceToHost, s));
+    }
+    return UAM_OK;
+}
+
+void lg_stage3(GridJob& j) {
+    const int64_t nc = j.ncomp;
+    auto col = [&](int k) {
+        return std::vector<int32_t>(j.hall.p + k * nc, j.hall.p + (k + 1) * nc);
+    };
+    j.st.cnt = col(0), j.st.x0 = col(1), j.st.y0 = col(2), j.st.x1 = col(3), j.st.y1 = col(4);
+    j.st.root = col(5);
+}
+
+// label a grid and return its component stats (synchronises twice)
+int label_grid(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool runs,
+               hipStream_t s) {
+    int rc = lg_stage1(j, colbox, rowbox, runs, s);
+    if (rc) return rc;
+    HIP_TRY2(hipStreamSynchronize(s));
+    rc = lg_stage2(j, s);
+    if (rc) return rc;
+    HIP_TRY2(hipStreamSynchronize(s));
+    lg_stage3(j);
+    return UAM_OK;
+}
+
+// per-row [xmin, xmax] of the selected components (sel[c] true), row tables concatenated:
+// stage 1 launches and queues the copy back, stage 2 (after a synchronisation) unpacks
+struct ExtJob {
+    std::vector<int64_t> off;
     int64_t rows = 0;
+    DevBuf<int64_t> doff;
+    DevBuf<int32_t> dy0, dmn;
+    PinnedBuf<int32_t> hmn;
+    std::vector<int32_t> xmin, xmax;
+};
+
+int ext_stage1(ExtJob& e, int32_t nx, int32_t ny, const int32_t* L, const int32_t* cid,
+               const CompStats& st, const std::vector<char>& sel, hipStream_t s) {
+    const int32_t ncomp = (int32_t)st.cnt.size();
+    e.off.assign(ncomp, -1);
+    e.rows = 0;
     for (int32_t c = 0; c < ncomp; ++c)
         if (sel[c]) {
-            off[c] = rows;
-            rows += st.y1[c] - st.y0[c] + 1;
+            e.off[c] = e.rows;
+            e.rows += st.y1[c] - st.y0[c] + 1;
         }
-    xmin.assign(rows, INT32_MAX);
-    xmax.assign(rows, -1);
-    if (rows == 0) return UAM_OK;
-    DevBuf<int64_t> doff;
-    DevBuf<int32_t> dy0, dmn, dmx;
-    HIP_TRY2(doff.alloc(ncomp));
-    HIP_TRY2(dy0.alloc(ncomp));
-    HIP_TRY2(dmn.alloc(rows));
-    HIP_TRY2(dmx.alloc(rows));
-    HIP_TRY2(hipMemcpyAsync(doff.p, off.data(), ncomp * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIP_TRY2(hipMemcpyAsync(dy0.p, st.y0.data(), ncomp * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    HIP_TRY2(hipMemcpyAsync(dmn.p, xmin.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    HIP_TRY2(hipMemcpyAsync(dmx.p, xmax.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (e.rows == 0) return UAM_OK;
+    HIP_TRY2(e.doff.alloc(ncomp));
+    HIP_TRY2(e.dy0.alloc(ncomp));
+    HIP_TRY2(e.dmn.alloc(2 * e.rows));
+    HIP_TRY2(e.hmn.alloc(2 * e.rows));
+    HIP_TRY2(hipMemcpyAsync(e.doff.p, e.off.data(), ncomp * sizeof(int64_t),
+                            hipMemcpyHostToDevice, s));
+    HIP_TRY2(hipMemcpyAsync(e.dy0.p, st.y0.data(), ncomp * sizeof(int32_t),
+                            hipMemcpyHostToDevice, s));
+    const dim3 gr(grid_for(e.rows, 256, INT32_MAX)), b(256);
+    hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p, e.rows, INT32_MAX);
+    hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p + e.rows, e.rows, -1);
     const int64_t n = (int64_t)nx * ny;
-    hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, L, cid,
-                       nx, n, doff.p, dy0.p, dmn.p, dmx.p);
+    hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), b, 0, s, L, cid, nx, n,
+                       e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
     HIP_TRY2(hipGetLastError());
-    HIP_TRY2(hipMemcpyAsync(xmin.data(), dmn.p, rows * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY2(hipMemcpyAsync(xmax.data(), dmx.p, rows * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY2(hipStreamSynchronize(s));
+    HIP_TRY2(hipMemcpyAsync(e.hmn.p, e.dmn.p, 2 * e.rows * sizeof(int32_t),
+                            hipMemcpyDeviceToHost, s));
     return UAM_OK;
+}
+
+void ext_stage2(ExtJob& e) {
+    e.xmin.assign(e.hmn.p, e.hmn.p + e.rows);
+    e.xmax.assign(e.hmn.p + e.rows, e.hmn.p + 2 * e.rows);
 }
 
 // hull input of one labelled region: each row's [xmin, xmax] run contributes its four pixel
@@ -4736,14 +4850,36 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
                  DY = rd->dy * unit_m;
     DeviceGuard dg(ctx->device);
     hipStream_t s = (hipStream_t)stream;
-    g_devbuf_stream = s;
-    DevBuf<int32_t> L, cid;
+    if (!ctx->pinned) ctx->pinned = new (std::nothrow) PinnedArena();
+    if (!ctx->devarena) ctx->devarena = new (std::nothrow) DevArena();
+    if (!ctx->pinned || !ctx->devarena) return fail(UAM_E_NOMEM, "K8 arenas");
+    g_pinned = (PinnedArena*)ctx->pinned;
+    g_pinned->reset();
+    g_devarena = (DevArena*)ctx->devarena;
+    g_devarena->reset();
+    // UAM_K8_PROF=1: host timestamps of the phases (at the existing synchronisation points)
+    static const bool prof = std::getenv("UAM_K8_PROF") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what) {
+        if (prof)
+            std::fprintf(stderr, "[k8] %-28s %9.3f ms\n", what,
+                         std::chrono::duration<double, std::milli>(
+                             std::chrono::steady_clock::now() - t_start).count());
+    };
+    struct AtExit {  // stamps after every scratch buffer below has been released
+        std::function<void()> f;
+        ~AtExit() { f(); }
+    } at_exit{[&] { stamp("returned (scratch released)"); }};
+    DevBuf<int32_t> L;
     HIP_TRY2(L.alloc(n));
     hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, dem,
                        n, nx, threshold, L.p);
-    CompStats st;
-    int rc = label_grid(nx, ny, nullptr, nullptr, true, L.p, cid, st, s);
+    GridJob mj;
+    mj.nx = nx, mj.ny = ny, mj.L = L.p;
+    int rc = label_grid(mj, nullptr, nullptr, true, s);
     if (rc) return rc;
+    stamp("labelled + stats");
+    const CompStats& st = mj.st;
     const int32_t ncomp = (int32_t)st.cnt.size();
     const double cell = std::fabs(DX * DY);
     std::vector<char> small(ncomp, 0), large(ncomp, 0);
@@ -4752,38 +4888,43 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         if (!(area > prm->min_area)) continue;
         (area > prm->large_area ? large : small)[c] = 1;
     }
-    std::vector<int64_t> off;
-    std::vector<int32_t> xmin, xmax;
-    rc = row_extents(nx, ny, L.p, cid.p, st, small, off, xmin, xmax, s);
+    ExtJob me;
+    rc = ext_stage1(me, nx, ny, L.p, mj.cid.p, st, small, s);
     if (rc) return rc;
     std::vector<double> xlo(nx), xhi(nx), ylo(ny), yhi(ny);
     for (int32_t i = 0; i < nx; ++i) xlo[i] = X0 + i * DX, xhi[i] = X0 + (i + 1) * DX;
     for (int32_t j = 0; j < ny; ++j) yhi[j] = Y0 - j * DY, ylo[j] = Y0 - (j + 1) * DY;
-    std::vector<int64_t> out;
-    std::vector<uampoly::Pt> pts;
-    const int D = prm->divisions;
-    for (int32_t c = 0; c < ncomp; ++c) {
-        if (small[c]) {
-            region_corners(st.y0[c], st.y1[c], &xmin[off[c]], &xmax[off[c]], xlo, xhi, ylo, yhi,
-                           pts);
-            emit_rect(pts, prm->min_approx_area, out);
-            continue;
+    // Large regions (data_processor.py:34-51: D x D boxes over polygon.bounds; a piece =
+    // connected part of polygon n box = component of the region's grid refined at the box
+    // edges, cut there).  All of them are labelled together, three synchronisations in all.
+    struct Region {
+        int32_t c = 0, ws = 0, hs = 0;
+        std::vector<int32_t> col_of, colbox, row_of, rowbox;
+        std::vector<double> sxlo, sxhi, sylo, syhi;
+        DevBuf<int32_t> dco, dcb, dro, drb, L2;
+        GridJob job;
+        ExtJob ext;
+    };
+    std::vector<Region> regs;  // reserved: a Region's buffers must never be copied
+    regs.reserve(std::count(large.begin(), large.end(), (char)1));
+    for (int32_t c = 0; c < ncomp; ++c)
+        if (large[c]) {
+            regs.emplace_back();
+            regs.back().c = c;
         }
-        if (!large[c]) continue;
-        // data_processor.py:34-51: D x D boxes over polygon.bounds; a piece = connected part
-        // of polygon n box = component of the grid refined at the box edges, cut there
+    const int D = prm->divisions;
+    for (Region& r : regs) {
+        const int32_t c = r.c;
         const double minx = X0 + st.x0[c] * DX, maxx = X0 + (st.x1[c] + 1) * DX;
         const double maxy = Y0 - st.y0[c] * DY, miny = Y0 - (st.y1[c] + 1) * DY;
         const double ddx = (maxx - minx) / D, ddy = (maxy - miny) / D;
-        std::vector<int32_t> col_of, colbox, row_of, rowbox;
-        std::vector<double> sxlo, sxhi, sylo, syhi;
         for (int32_t col = st.x0[c]; col <= st.x1[c]; ++col)
             for (int j = 0; j < D; ++j) {
                 const double lo = std::max(xlo[col], minx + j * ddx);
                 const double hi = std::min(xhi[col], minx + (j + 1) * ddx);
                 if (hi > lo) {
-                    col_of.push_back(col), colbox.push_back(j);
-                    sxlo.push_back(lo), sxhi.push_back(hi);
+                    r.col_of.push_back(col), r.colbox.push_back(j);
+                    r.sxlo.push_back(lo), r.sxhi.push_back(hi);
                 }
             }
         for (int32_t row = st.y0[c]; row <= st.y1[c]; ++row)
@@ -4791,47 +4932,74 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
                 const double lo = std::max(ylo[row], miny + k * ddy);
                 const double hi = std::min(yhi[row], miny + (k + 1) * ddy);
                 if (hi > lo) {
-                    row_of.push_back(row), rowbox.push_back(k);
-                    sylo.push_back(lo), syhi.push_back(hi);
+                    r.row_of.push_back(row), r.rowbox.push_back(k);
+                    r.sylo.push_back(lo), r.syhi.push_back(hi);
                 }
             }
-        const int32_t ws = (int32_t)col_of.size(), hs = (int32_t)row_of.size();
-        const int64_t sn = (int64_t)ws * hs;
-        DevBuf<int32_t> dco, dcb, dro, drb, L2, cid2;
-        HIP_TRY2(dco.alloc(ws));
-        HIP_TRY2(dcb.alloc(ws));
-        HIP_TRY2(dro.alloc(hs));
-        HIP_TRY2(drb.alloc(hs));
-        HIP_TRY2(L2.alloc(sn));
-        HIP_TRY2(hipMemcpyAsync(dco.p, col_of.data(), ws * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(dcb.p, colbox.data(), ws * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(dro.p, row_of.data(), hs * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(drb.p, rowbox.data(), hs * 4, hipMemcpyHostToDevice, s));
+        r.ws = (int32_t)r.col_of.size(), r.hs = (int32_t)r.row_of.size();
+        const int64_t sn = (int64_t)r.ws * r.hs;
+        HIP_TRY2(r.dco.alloc(r.ws));
+        HIP_TRY2(r.dcb.alloc(r.ws));
+        HIP_TRY2(r.dro.alloc(r.hs));
+        HIP_TRY2(r.drb.alloc(r.hs));
+        HIP_TRY2(r.L2.alloc(sn));
+        HIP_TRY2(hipMemcpyAsync(r.dco.p, r.col_of.data(), r.ws * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(r.dcb.p, r.colbox.data(), r.ws * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(r.dro.p, r.row_of.data(), r.hs * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(r.drb.p, r.rowbox.data(), r.hs * 4, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0, s,
-                           L.p, nx, st.root[c], dco.p, dro.p, dcb.p, ws, hs, L2.p);
-        CompStats ps;
-        rc = label_grid(ws, hs, dcb.p, drb.p, true, L2.p, cid2, ps, s);
+                           L.p, nx, st.root[c], r.dco.p, r.dro.p, r.dcb.p, r.ws, r.hs, r.L2.p);
+        r.job.nx = r.ws, r.job.ny = r.hs, r.job.L = r.L2.p;
+        rc = lg_stage1(r.job, r.dcb.p, r.drb.p, true, s);
         if (rc) return rc;
+    }
+    HIP_TRY2(hipStreamSynchronize(s));  // main extents, every region's root counts
+    ext_stage2(me);
+    for (Region& r : regs) {
+        rc = lg_stage2(r.job, s);
+        if (rc) return rc;
+    }
+    HIP_TRY2(hipStreamSynchronize(s));  // every region's component stats
+    for (Region& r : regs) {
+        lg_stage3(r.job);
+        const std::vector<char> all(r.job.st.cnt.size(), 1);
+        rc = ext_stage1(r.ext, r.ws, r.hs, r.L2.p, r.job.cid.p, r.job.st, all, s);
+        if (rc) return rc;
+    }
+    HIP_TRY2(hipStreamSynchronize(s));  // every region's row extents
+    stamp("large regions labelled");
+    // rectangles in component order (small: the region; large: its pieces, boxes j (x) outer,
+    // k (y) inner -- the reference's order)
+    std::vector<int64_t> out;
+    std::vector<uampoly::Pt> pts;
+    size_t ri = 0;
+    for (int32_t c = 0; c < ncomp; ++c) {
+        if (small[c]) {
+            region_corners(st.y0[c], st.y1[c], &me.xmin[me.off[c]], &me.xmax[me.off[c]], xlo,
+                           xhi, ylo, yhi, pts);
+            emit_rect(pts, prm->min_approx_area, out);
+            continue;
+        }
+        if (!large[c]) continue;
+        Region& r = regs[ri++];
+        ext_stage2(r.ext);
+        const CompStats& ps = r.job.st;
         const int32_t np = (int32_t)ps.cnt.size();
-        std::vector<char> all(np, 1);
-        std::vector<int64_t> poff;
-        std::vector<int32_t> pmn, pmx;
-        rc = row_extents(ws, hs, L2.p, cid2.p, ps, all, poff, pmn, pmx, s);
-        if (rc) return rc;
-        // reference order: boxes j (x) outer, k (y) inner
         std::vector<int32_t> order(np);
         for (int32_t i = 0; i < np; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-            const int ja = colbox[ps.x0[a]], jb = colbox[ps.x0[b]];
+            const int ja = r.colbox[ps.x0[a]], jb = r.colbox[ps.x0[b]];
             if (ja != jb) return ja < jb;
-            return rowbox[ps.y0[a]] < rowbox[ps.y0[b]];
+            return r.rowbox[ps.y0[a]] < r.rowbox[ps.y0[b]];
         });
         for (int32_t i : order) {
-            region_corners(ps.y0[i], ps.y1[i], &pmn[poff[i]], &pmx[poff[i]], sxlo, sxhi, sylo,
-                           syhi, pts);
+            region_corners(ps.y0[i], ps.y1[i], &r.ext.xmin[r.ext.off[i]], &r.ext.xmax[r.ext.off[i]],
+                           r.sxlo, r.sxhi, r.sylo, r.syhi, pts);
             emit_rect(pts, prm->min_approx_area, out);
         }
     }
+    stamp("all rectangles");
+    if (prof) std::fprintf(stderr, "[k8] components %d, large regions %zu\n", ncomp, regs.size());
     const int64_t nr = (int64_t)out.size() / 8;
     *n_rects = (int32_t)nr;
     if (rect_xy)
