@@ -106,3 +106,26 @@ def test_population_pipeline_reproduces_reference(eng, tmp_path):
     got = DataProcessor().process_polygons(polys)
     sets = lambda rs: sorted(sorted(map(tuple, np.asarray(r).tolist())) for r in rs)
     assert sets(got) == sets(z["rects"])
+
+
+@pytest.mark.parametrize("tiled", ["1", "0"])
+@pytest.mark.parametrize("nx,ny,thr", [(700, 450, 0.0), (129, 1000, 150.0), (1000, 63, 0.0)])
+def test_dem_polygons_tile_edges(oracle_mod, monkeypatch, tiled, nx, ny, thr):
+    """Tile labelling (UAM_K8_TILE=1, the default: 64 x 64 LDS tiles + edge joins) and the
+    cell-parallel merge (0) on rasters that are not multiples of the tile: partial tiles on
+    both edges, a single tile row, components crossing many tile edges, large regions split
+    into box pieces (cuts inside and across tiles)."""
+    from uam_path_planning_amd.engine import Engine, RasterGeo
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    monkeypatch.setenv("UAM_K8_TILE", tiled)
+    e2 = Engine(0)
+    dx = 60.0 / max(nx, ny)
+    geo = RasterGeo(nx=nx, ny=ny, x0=0.0, y_top=20.0, dx=dx, dy=dx, nodata=-9999.0,
+                    dem_threshold=thr)
+    dem = synthetic_dem(max(nx, ny), seed=3)[:ny, :nx].copy()
+    got = _arr(e2.dem_polygons(dem, geo, thr))
+    rd = oracle_mod.Oracle.raster_desc(nx, ny, geo.x0, geo.y_top, dx, dx)
+    ref = oracle_mod.dem_polygons(dem, rd, thr, 1000.0)
+    assert len(ref) > 0
+    np.testing.assert_array_equal(got, ref)

@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "uampath.hip")
 SRCS = [SRC, os.path.join(HERE, "csrc", "polyproc.cpp")]
-DEPS = SRCS + [os.path.join(HERE, "csrc", "polyproc.h")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", "polyproc.h"), os.path.join(HERE, "csrc", "ccl_tile.inc")]
 HEADER = os.path.join(ROOT, "include", "uampath.h")
 OUT = os.path.join(HERE, "lib", "libuampath.so")
 ARCH = os.environ.get("UAM_OFFLOAD_ARCH", "gfx950")

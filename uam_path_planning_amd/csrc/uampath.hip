@@ -2647,6 +2647,8 @@ __global__ __launch_bounds__(256) void k_ccl_flatten(int64_t n, int32_t* __restr
     L[i] = ccl_find(L, (int32_t)i);
 }
 
+#include "ccl_tile.inc"
+
 constexpr int CCL_ITEMS = 16;  // cells per thread in the root scan (block = 256 x 16 cells)
 
 __global__ __launch_bounds__(256) void k_ccl_count_roots(const int32_t* __restrict__ L,
@@ -3587,6 +3589,7 @@ struct uam_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
+    bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
 };
 
 namespace {
@@ -3673,6 +3676,7 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
     *out = c;
     return UAM_OK;
 }
@@ -4647,17 +4651,29 @@ struct GridJob {
     int64_t n = 0, nblk = 0;
     int32_t* L = nullptr;
     int32_t ncomp = 0;
+    bool tiled = false;  // tile labelling and the row-segment stats
     DevBuf<int32_t> cnt, off, cid, a;
     PinnedBuf<int32_t> hcnt, hall;
     std::vector<int32_t> hoff;
     CompStats st;
 };
 
+// tiled: L holds k_ccl_tile's output (tile-local roots), so only the tile edges are joined
 int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool runs,
-              hipStream_t s) {
+              hipStream_t s, bool tiled = false) {
     j.n = (int64_t)j.nx * j.ny;
+    j.tiled = tiled;
     const dim3 g(grid_for(j.n, 256, INT32_MAX)), b(256);
-    hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, j.nx, j.ny, colbox, rowbox, runs ? 1 : 0, j.L);
+    if (tiled) {
+        const int32_t tx = (j.nx + CT_W - 1) / CT_W, ty = (j.ny + CT_H - 1) / CT_H;
+        const int64_t nb = (int64_t)(ty - 1) * j.nx + (int64_t)(tx - 1) * j.ny;
+        if (nb > 0)
+            hipLaunchKernelGGL(k_ccl_bmerge, dim3(grid_for(nb, 256, INT32_MAX)), b, 0, s, j.nx,
+                               j.ny, tx, ty, colbox, rowbox, j.L);
+    } else {
+        hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, j.nx, j.ny, colbox, rowbox, runs ? 1 : 0,
+                           j.L);
+    }
     hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
     j.nblk = (j.n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
     HIP_TRY2(j.cnt.alloc(j.nblk));
@@ -4694,9 +4710,16 @@ int lg_stage2(GridJob& j, hipStream_t s) {
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 2 * (int64_t)nc, (int64_t)nc, INT32_MAX);
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 3 * (int64_t)nc, (int64_t)nc, -1);
         hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 4 * (int64_t)nc, (int64_t)nc, -1);
-        hipLaunchKernelGGL(k_ccl_stats, dim3((unsigned)j.nblk), b, 0, s, j.L, j.cid.p, j.nx, j.n,
-                           p, p + nc, p + 2 * (int64_t)nc, p + 3 * (int64_t)nc,
-                           p + 4 * (int64_t)nc, p + 5 * (int64_t)nc);
+        if (j.tiled)
+            hipLaunchKernelGGL(k_ccl_stats_rows,
+                               dim3((unsigned)((j.nx + CS_SEG - 1) / CS_SEG),
+                                    (unsigned)((j.ny + CS_ROWS - 1) / CS_ROWS)),
+                               b, 0, s, j.L, j.cid.p, j.nx, j.ny, p, p + nc, p + 2 * (int64_t)nc,
+                               p + 3 * (int64_t)nc, p + 4 * (int64_t)nc, p + 5 * (int64_t)nc);
+        else
+            hipLaunchKernelGGL(k_ccl_stats, dim3((unsigned)j.nblk), b, 0, s, j.L, j.cid.p, j.nx,
+                               j.n, p, p + nc, p + 2 * (int64_t)nc, p + 3 * (int64_t)nc,
+                               p + 4 * (int64_t)nc, p + 5 * (int64_t)nc);
         HIP_TRY2(hipGetLastError());
         HIP_TRY2(hipMemcpyAsync(j.hall.p, j.a.p, 6 * (int64_t)nc * sizeof(int32_t),
                                 hipMemcpyDeviceToHost, s));
@@ -4715,8 +4738,8 @@ void lg_stage3(GridJob& j) {
 
 // label a grid and return its component stats (synchronises twice)
 int label_grid(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool runs,
-               hipStream_t s) {
-    int rc = lg_stage1(j, colbox, rowbox, runs, s);
+               hipStream_t s, bool tiled = false) {
+    int rc = lg_stage1(j, colbox, rowbox, runs, s, tiled);
     if (rc) return rc;
     HIP_TRY2(hipStreamSynchronize(s));
     rc = lg_stage2(j, s);
@@ -4738,7 +4761,8 @@ struct ExtJob {
 };
 
 int ext_stage1(ExtJob& e, int32_t nx, int32_t ny, const int32_t* L, const int32_t* cid,
-               const CompStats& st, const std::vector<char>& sel, hipStream_t s) {
+               const CompStats& st, const std::vector<char>& sel, hipStream_t s,
+               bool tiled = false) {
     const int32_t ncomp = (int32_t)st.cnt.size();
     e.off.assign(ncomp, -1);
     e.rows = 0;
@@ -4760,8 +4784,13 @@ int ext_stage1(ExtJob& e, int32_t nx, int32_t ny, const int32_t* L, const int32_
     hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p, e.rows, INT32_MAX);
     hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p + e.rows, e.rows, -1);
     const int64_t n = (int64_t)nx * ny;
-    hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), b, 0, s, L, cid, nx, n,
-                       e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
+    if (tiled && ny <= 65535)
+        hipLaunchKernelGGL(k_ccl_extents_rows,
+                           dim3((unsigned)((nx + CS_SEG - 1) / CS_SEG), (unsigned)ny), b, 0, s, L,
+                           cid, nx, e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
+    else
+        hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), b, 0, s, L, cid, nx,
+                           n, e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
     HIP_TRY2(hipGetLastError());
     HIP_TRY2(hipMemcpyAsync(e.hmn.p, e.dmn.p, 2 * e.rows * sizeof(int32_t),
                             hipMemcpyDeviceToHost, s));
@@ -4872,11 +4901,19 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     } at_exit{[&] { stamp("returned (scratch released)"); }};
     DevBuf<int32_t> L;
     HIP_TRY2(L.alloc(n));
-    hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s, dem,
-                       n, nx, threshold, L.p);
+    const bool tiled = ctx->k8_tiled;
+    auto tiles = [](int32_t w, int32_t h) {
+        return dim3((unsigned)((w + CT_W - 1) / CT_W), (unsigned)((h + CT_H - 1) / CT_H));
+    };
+    if (tiled)
+        hipLaunchKernelGGL(k_ccl_tile<CclMaskDem>, tiles(nx, ny), dim3(256), 0, s,
+                           CclMaskDem{dem, threshold, nx}, nx, ny, nullptr, nullptr, L.p);
+    else
+        hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s,
+                           dem, n, nx, threshold, L.p);
     GridJob mj;
     mj.nx = nx, mj.ny = ny, mj.L = L.p;
-    int rc = label_grid(mj, nullptr, nullptr, true, s);
+    int rc = label_grid(mj, nullptr, nullptr, true, s, tiled);
     if (rc) return rc;
     stamp("labelled + stats");
     const CompStats& st = mj.st;
@@ -4889,7 +4926,7 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         (area > prm->large_area ? large : small)[c] = 1;
     }
     ExtJob me;
-    rc = ext_stage1(me, nx, ny, L.p, mj.cid.p, st, small, s);
+    rc = ext_stage1(me, nx, ny, L.p, mj.cid.p, st, small, s, tiled);
     if (rc) return rc;
     std::vector<double> xlo(nx), xhi(nx), ylo(ny), yhi(ny);
     for (int32_t i = 0; i < nx; ++i) xlo[i] = X0 + i * DX, xhi[i] = X0 + (i + 1) * DX;
@@ -4947,10 +4984,16 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         HIP_TRY2(hipMemcpyAsync(r.dcb.p, r.colbox.data(), r.ws * 4, hipMemcpyHostToDevice, s));
         HIP_TRY2(hipMemcpyAsync(r.dro.p, r.row_of.data(), r.hs * 4, hipMemcpyHostToDevice, s));
         HIP_TRY2(hipMemcpyAsync(r.drb.p, r.rowbox.data(), r.hs * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0, s,
-                           L.p, nx, st.root[c], r.dco.p, r.dro.p, r.dcb.p, r.ws, r.hs, r.L2.p);
+        if (tiled)
+            hipLaunchKernelGGL(k_ccl_tile<CclMaskSub>, tiles(r.ws, r.hs), dim3(256), 0, s,
+                               CclMaskSub{L.p, nx, st.root[c], r.dco.p, r.dro.p}, r.ws, r.hs,
+                               r.dcb.p, r.drb.p, r.L2.p);
+        else
+            hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0,
+                               s, L.p, nx, st.root[c], r.dco.p, r.dro.p, r.dcb.p, r.ws, r.hs,
+                               r.L2.p);
         r.job.nx = r.ws, r.job.ny = r.hs, r.job.L = r.L2.p;
-        rc = lg_stage1(r.job, r.dcb.p, r.drb.p, true, s);
+        rc = lg_stage1(r.job, r.dcb.p, r.drb.p, true, s, tiled);
         if (rc) return rc;
     }
     HIP_TRY2(hipStreamSynchronize(s));  // main extents, every region's root counts
@@ -4963,7 +5006,7 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     for (Region& r : regs) {
         lg_stage3(r.job);
         const std::vector<char> all(r.job.st.cnt.size(), 1);
-        rc = ext_stage1(r.ext, r.ws, r.hs, r.L2.p, r.job.cid.p, r.job.st, all, s);
+        rc = ext_stage1(r.ext, r.ws, r.hs, r.L2.p, r.job.cid.p, r.job.st, all, s, tiled);
         if (rc) return rc;
     }
     HIP_TRY2(hipStreamSynchronize(s));  // every region's row extents
