@@ -2302,15 +2302,25 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
         }
     }
     EW_STAMP(2);
-    // record gathers, up to 4 per lane in flight; ph / ps = +0.0 for off-grid waypoints
+    wave_sync();
+    // eval_path's sequential sums, same order, on four lanes at once.  Every accumulator
+    // starts at +0.0 and so is never -0.0, which makes a ±0.0 term an exact no-op: the
+    // kinematic, no-fly and Φ/N term lists are compacted (stable, in place) to their nonzero
+    // entries first -- an arc within the turn and ratio limits has no nonzero kinematic row.
+    // Chains A (lane 0 L over W terms, lane 1 length, lane 3 kinematic sum) need only the
+    // geometry terms, so they run while the first batch of record gathers is in flight;
+    // chains B (lane 0 cost = (N+1) L + the nonzero Φ/N terms, lane 2 no-fly sum) follow.
+    // The serial length is max(gather latency, W) + nnz(Φ) adds instead of max(2W, 3N).
+    const int nkn = wave_compact_nonzero(kn, 3 * N, lane);
     double hmax = -INFINITY, cmin = INFINITY;
     int nh = 0, off = 0, below = 0;
     int32_t* cells = out.cells ? out.cells + path * W : nullptr;
     const double dN = (double)N;
-    for (int jb = lane; jb < W; jb += 256) {
-        uint4 r[4];
-        bool in[4];
-        double zz[4];
+    // record gathers, up to 4 per lane in flight; ph / ps = +0.0 for off-grid waypoints
+    uint4 r[4];
+    bool in[4];
+    double zz[4];
+    auto issue = [&](int jb) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int j = jb + 64 * t;
@@ -2340,6 +2350,8 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             r[t] = rec[cell];
             if (cells) cells[j] = in[t] ? (int32_t)cell : -1;
         }
+    };
+    auto consume = [&](int jb) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int j = jb + 64 * t;
@@ -2365,6 +2377,18 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
                 ++off;
             }
         }
+    };
+    issue(lane);
+    // chains A, beside the gathers
+    const double* arr = lane == 0 ? lq : (lane == 1 ? sg : kn);
+    const int na = lane < 2 ? W : (lane == 3 ? nkn : 0);
+    double acc = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < na; ++i) acc = acc + arr[i];
+    consume(lane);
+    for (int jb = lane + 256; jb < W; jb += 256) {
+        issue(jb);
+        consume(jb);
     }
     EW_STAMP(3);
     hmax = wave_fmax(hmax);
@@ -2374,26 +2398,15 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     below = wave_isum(below);
     wave_sync();
     EW_STAMP(4);
-    // eval_path's sequential sums, same order, on four lanes at once.  Every accumulator
-    // starts at +0.0 and so is never -0.0, which makes a ±0.0 term an exact no-op: the Φ/N,
-    // no-fly and kinematic term lists are first compacted (stable, in place) to their nonzero
-    // entries -- an arc within the turn and ratio limits has no nonzero kinematic row at all.
-    // Phase A: lane 0 L (W terms), lane 1 length (W), lane 2 no-fly sum, lane 3 kinematic
-    // sum; then lane 0 seeds the cost chain with (N+1) L and adds the nonzero Φ/N terms.  The
-    // serial length is max(W + nnz(Φ), nnz(kinematic)) adds instead of max(2W, 3N).
     const int nps = wave_compact_nonzero(ps, W, lane);
     const int nph = wave_compact_nonzero(ph, W, lane);
-    const int nkn = wave_compact_nonzero(kn, 3 * N, lane);
-    const double* arr = lane == 0 ? lq : (lane == 1 ? sg : (lane == 2 ? ps : kn));
-    const int na = lane < 2 ? W : (lane == 2 ? nps : (lane == 3 ? nkn : 0));
-    double acc = 0.0;
-#pragma unroll 8
-    for (int i = 0; i < na; ++i) acc = acc + arr[i];
+    // chains B
     double L = acc;
     if (lane == 0) acc = (double)(N + 1) * L;
-    const int nb = lane == 0 ? nph : 0;
+    const double* brr = lane == 0 ? ph : ps;
+    const int nb = lane == 0 ? nph : (lane == 2 ? nps : 0);
 #pragma unroll 8
-    for (int i = 0; i < nb; ++i) acc = acc + ph[i];
+    for (int i = 0; i < nb; ++i) acc = acc + brr[i];
     L = __shfl(L, 0, 64);
     const double len = __shfl(acc, 1, 64), nsum = __shfl(acc, 2, 64);
     const double ksum = __shfl(acc, 3, 64);
