@@ -2460,6 +2460,25 @@ __device__ __forceinline__ void kr_sum(const double (&c)[6], double xi, double e
     si = y0r * zi + y0i * zr;
 }
 
+// kr_sum with sin/cos(2 xi) and sinh/cosh(2 eta) given (same operations after them)
+__device__ __forceinline__ void kr_sum_pre(const double (&c)[6], double s2, double c2, double sh,
+                                           double ch, double& sr, double& si) {
+    const double ar = 2.0 * (c2 * ch), ai = -2.0 * (s2 * sh);
+    double y0r = 0.0, y0i = 0.0, y1r = 0.0, y1i = 0.0;
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        const double tr = (ar * y0r - ai * y0i) - y1r + c[j];
+        const double ti = (ar * y0i + ai * y0r) - y1i;
+        y1r = y0r;
+        y1i = y0i;
+        y0r = tr;
+        y0i = ti;
+    }
+    const double zr = s2 * ch, zi = c2 * sh;
+    sr = y0r * zr - y0i * zi;
+    si = y0r * zi + y0i * zr;
+}
+
 __device__ __forceinline__ void tm_fwd(const KTm& k, double lon, double lat, double& x,
                                        double& y) {
     const double phi = lat * (M_PI / 180.0), dl = lon * (M_PI / 180.0) - k.lon0;
@@ -2474,12 +2493,21 @@ __device__ __forceinline__ void tm_fwd(const KTm& k, double lon, double lat, dou
     y = k.k0 * k.A * (xi - k.xi0) + k.fn;
 }
 
+// the part of tm_inv after the series' trigonometric inputs (shared by both forms below)
+__device__ __forceinline__ void tm_inv_tail(const KTm& k, double xi, double eta, double sr,
+                                            double si, double& lon, double& lat);
+
 __device__ __forceinline__ void tm_inv(const KTm& k, double x, double y, double& lon,
                                        double& lat) {
     const double kA = k.k0 * k.A;
     const double xi = (y - k.fn) / kA + k.xi0, eta = (x - k.fe) / kA;
     double sr, si;
     kr_sum(k.beta, xi, eta, sr, si);
+    tm_inv_tail(k, xi, eta, sr, si, lon, lat);
+}
+
+__device__ __forceinline__ void tm_inv_tail(const KTm& k, double xi, double eta, double sr,
+                                            double si, double& lon, double& lat) {
     const double xp = xi - sr, ep = eta - si;
     const double se = sinh(ep), cx = cos(xp);
     const double taup = sin(xp) / sqrt(se * se + cx * cx);
@@ -2517,18 +2545,49 @@ struct KGeoGrid {
     float nodata;
 };
 
+// The output grid is axis-aligned in the plane, so the series' inputs separate: xi depends on
+// the row only and eta on the column only.  k_tm_sep tabulates (xi, sin 2xi, cos 2xi) per row
+// and (eta, sinh 2eta, cosh 2eta) per column, with tm_inv's own expressions, so each cell
+// skips four transcendentals and the results are the same bits.
+__global__ __launch_bounds__(256) void k_tm_sep(KTm k, KRaster r, double unit,
+                                                double* __restrict__ rowtab,
+                                                double* __restrict__ coltab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const double kA = k.k0 * k.A;
+    if (i < r.ny) {
+        const double yc = r.y_top - ((double)i + 0.5) * r.dy;
+        const double xi = (yc * unit - k.fn) / kA + k.xi0;
+        rowtab[3 * i] = xi;
+        rowtab[3 * i + 1] = sin(2.0 * xi);
+        rowtab[3 * i + 2] = cos(2.0 * xi);
+    } else if (i < (int64_t)r.ny + r.nx) {
+        const int64_t ix = i - r.ny;
+        const double xc = r.x0 + ((double)ix + 0.5) * r.dx;
+        const double eta = (xc * unit - k.fe) / kA;
+        coltab[3 * ix] = eta;
+        coltab[3 * ix + 1] = sinh(2.0 * eta);
+        coltab[3 * ix + 2] = cosh(2.0 * eta);
+    }
+}
+
 // DEM reprojection (definition: oracle orc_reproject).  One lane per output cell, rows
 // contiguous (coalesced 4-B stores); neighbouring cells read neighbouring source pixels.
 __global__ __launch_bounds__(256) void k_reproject(KTm k, KGeoGrid g, KRaster r, double unit,
                                                    int resample, const float* __restrict__ src,
+                                                   const double* __restrict__ rowtab,
+                                                   const double* __restrict__ coltab,
                                                    float* __restrict__ dst) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)r.nx * r.ny) return;
     const int64_t iy = i / r.nx, ix = i - iy * r.nx;
-    const double xc = r.x0 + ((double)ix + 0.5) * r.dx;
-    const double yc = r.y_top - ((double)iy + 0.5) * r.dy;
     double lon, lat;
-    tm_inv(k, xc * unit, yc * unit, lon, lat);
+    {
+        const double xi = rowtab[3 * iy], eta = coltab[3 * ix];
+        double sr, si;
+        kr_sum_pre(k.beta, rowtab[3 * iy + 1], rowtab[3 * iy + 2], coltab[3 * ix + 1],
+                   coltab[3 * ix + 2], sr, si);
+        tm_inv_tail(k, xi, eta, sr, si, lon, lat);
+    }
     const double u = (lon - g.lon0) / g.dlon, v = (g.lat_top - lat) / g.dlat;
     float val = g.nodata;
     const double fu = floor(u), fv = floor(v);
@@ -3602,6 +3661,8 @@ struct uam_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
+    double* d_tmtab = nullptr;  // K7 reprojection row / column tables (grow-only)
+    size_t tmtab_n = 0;
     bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
 };
 
@@ -3706,6 +3767,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
     if (ctx->pinned) pinned_arena_free(ctx->pinned);
     if (ctx->devarena) dev_arena_free(ctx->devarena);
+    if (ctx->d_tmtab) (void)hipFree(ctx->d_tmtab);
     delete ctx;
 }
 
@@ -4556,8 +4618,21 @@ int uam_reproject_dem(uam_ctx* ctx, const uam_tm_params* t, const float* src,
     const KGeoGrid g{sg->nx, sg->ny, sg->lon0, sg->lat_top, sg->dlon, sg->dlat, sg->nodata};
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     DeviceGuard dg(ctx->device);
+    const size_t tab = (size_t)3 * ((size_t)kr.nx + kr.ny);
+    if (tab > ctx->tmtab_n) {  // grow-only row / column tables (k_tm_sep)
+        if (ctx->d_tmtab) (void)hipFree(ctx->d_tmtab);
+        ctx->d_tmtab = nullptr;
+        ctx->tmtab_n = 0;
+        HIP_TRY(hipMalloc(&ctx->d_tmtab, tab * sizeof(double)));
+        ctx->tmtab_n = tab;
+    }
+    double* rowtab = ctx->d_tmtab;
+    double* coltab = rowtab + 3 * (size_t)kr.ny;
+    hipLaunchKernelGGL(k_tm_sep, dim3(grid_for((int64_t)kr.nx + kr.ny, 256, INT32_MAX)),
+                       dim3(256), 0, (hipStream_t)stream, k, kr, unit_m, rowtab, coltab);
     hipLaunchKernelGGL(k_reproject, dim3(grid_for(cells, 256, INT32_MAX)), dim3(256), 0,
-                       (hipStream_t)stream, k, g, kr, unit_m, resample, src, out);
+                       (hipStream_t)stream, k, g, kr, unit_m, resample, src,
+                       (const double*)rowtab, (const double*)coltab, out);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
