@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libuampath.so")
+# UAM_LIB_PATH: load another build of the same ABI (tuning experiments, e.g. tools/ builds
+# with different compile-time knobs); the default is the in-tree build
+LIB_PATH = os.environ.get("UAM_LIB_PATH") or os.path.join(HERE, "lib", "libuampath.so")
 
 ABI_VERSION = 1
 MAX_REGIONS = 16
