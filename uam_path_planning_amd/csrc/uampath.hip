@@ -4740,6 +4740,7 @@ struct GridJob {
     int32_t* L = nullptr;
     int32_t ncomp = 0;
     bool tiled = false;  // tile labelling and the row-segment stats
+    uint32_t* rootbits = nullptr;  // tiled: tile-local root bits written by k_ccl_tile
     DevBuf<int32_t> cnt, off, cid, a;
     PinnedBuf<int32_t> hcnt, hall;
     std::vector<int32_t> hoff;
@@ -4758,11 +4759,19 @@ int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool run
         if (nb > 0)
             hipLaunchKernelGGL(k_ccl_bmerge, dim3(grid_for(nb, 256, INT32_MAX)), b, 0, s, j.nx,
                                j.ny, tx, ty, colbox, rowbox, j.L);
+        if (j.rootbits) {
+            const int64_t nw = (j.n + 31) / 32;
+            hipLaunchKernelGGL(k_ccl_flatten_roots, dim3(grid_for(nw, 256, INT32_MAX)), b, 0, s,
+                               (const uint32_t*)j.rootbits, nw, j.L);
+            hipLaunchKernelGGL(k_ccl_flatten_cells, g, b, 0, s, j.n, j.L);
+        } else {
+            hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
+        }
     } else {
         hipLaunchKernelGGL(k_ccl_merge, g, b, 0, s, j.nx, j.ny, colbox, rowbox, runs ? 1 : 0,
                            j.L);
+        hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
     }
-    hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
     j.nblk = (j.n + 256 * CCL_ITEMS - 1) / (256 * CCL_ITEMS);
     HIP_TRY2(j.cnt.alloc(j.nblk));
     HIP_TRY2(j.off.alloc(j.nblk));
@@ -4993,13 +5002,18 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     auto tiles = [](int32_t w, int32_t h) {
         return dim3((unsigned)((w + CT_W - 1) / CT_W), (unsigned)((h + CT_H - 1) / CT_H));
     };
-    if (tiled)
+    GridJob mj;
+    DevBuf<uint32_t> mbits;
+    if (tiled) {
+        HIP_TRY2(mbits.alloc((n + 31) / 32));
+        HIP_TRY2(hipMemsetAsync(mbits.p, 0, ((n + 31) / 32) * sizeof(uint32_t), s));
+        mj.rootbits = mbits.p;
         hipLaunchKernelGGL(k_ccl_tile<CclMaskDem>, tiles(nx, ny), dim3(256), 0, s,
-                           CclMaskDem{dem, threshold, nx}, nx, ny, nullptr, nullptr, L.p);
-    else
+                           CclMaskDem{dem, threshold, nx}, nx, ny, nullptr, nullptr, L.p,
+                           mbits.p);
+    } else
         hipLaunchKernelGGL(k_ccl_init_dem, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, s,
                            dem, n, nx, threshold, L.p);
-    GridJob mj;
     mj.nx = nx, mj.ny = ny, mj.L = L.p;
     int rc = label_grid(mj, nullptr, nullptr, true, s, tiled);
     if (rc) return rc;
@@ -5027,6 +5041,7 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         std::vector<int32_t> col_of, colbox, row_of, rowbox;
         std::vector<double> sxlo, sxhi, sylo, syhi;
         DevBuf<int32_t> dco, dcb, dro, drb, L2;
+        DevBuf<uint32_t> bits;
         GridJob job;
         ExtJob ext;
     };
@@ -5072,11 +5087,14 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         HIP_TRY2(hipMemcpyAsync(r.dcb.p, r.colbox.data(), r.ws * 4, hipMemcpyHostToDevice, s));
         HIP_TRY2(hipMemcpyAsync(r.dro.p, r.row_of.data(), r.hs * 4, hipMemcpyHostToDevice, s));
         HIP_TRY2(hipMemcpyAsync(r.drb.p, r.rowbox.data(), r.hs * 4, hipMemcpyHostToDevice, s));
-        if (tiled)
+        if (tiled) {
+            HIP_TRY2(r.bits.alloc((sn + 31) / 32));
+            HIP_TRY2(hipMemsetAsync(r.bits.p, 0, ((sn + 31) / 32) * sizeof(uint32_t), s));
+            r.job.rootbits = r.bits.p;
             hipLaunchKernelGGL(k_ccl_tile<CclMaskSub>, tiles(r.ws, r.hs), dim3(256), 0, s,
                                CclMaskSub{L.p, nx, st.root[c], r.dco.p, r.dro.p}, r.ws, r.hs,
-                               r.dcb.p, r.drb.p, r.L2.p);
-        else
+                               r.dcb.p, r.drb.p, r.L2.p, r.bits.p);
+        } else
             hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0,
                                s, L.p, nx, st.root[c], r.dco.p, r.dro.p, r.dcb.p, r.ws, r.hs,
                                r.L2.p);
