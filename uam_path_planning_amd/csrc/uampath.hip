@@ -2878,10 +2878,15 @@ __global__ __launch_bounds__(256) void k_ccl_extents(const int32_t* __restrict__
     atomicMax(&xmax[slot], x);
 }
 
-__global__ __launch_bounds__(256) void k_fill_i32(int32_t* __restrict__ p, int64_t n,
-                                                  int32_t v) {
+// nseg consecutive arrays of n values, array k filled with v[k]: one launch instead of nseg
+struct FillSegs {
+    int32_t v[6];
+};
+__global__ __launch_bounds__(256) void k_fill_segs_i32(int32_t* __restrict__ p, int64_t n,
+                                                       int32_t nseg, FillSegs fs) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
+    if (i >= n) return;
+    for (int k = 0; k < nseg; ++k) p[k * n + i] = fs.v[k];
 }
 
 // ----------------------------------------------------------------------------------------
@@ -4742,8 +4747,7 @@ struct GridJob {
     bool tiled = false;  // tile labelling and the row-segment stats
     uint32_t* rootbits = nullptr;  // tiled: tile-local root bits written by k_ccl_tile
     DevBuf<int32_t> cnt, off, cid, a;
-    PinnedBuf<int32_t> hcnt, hall;
-    std::vector<int32_t> hoff;
+    PinnedBuf<int32_t> hcnt, hall, hoff;
     CompStats st;
 };
 
@@ -4760,9 +4764,9 @@ int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool run
             hipLaunchKernelGGL(k_ccl_bmerge, dim3(grid_for(nb, 256, INT32_MAX)), b, 0, s, j.nx,
                                j.ny, tx, ty, colbox, rowbox, j.L);
         if (j.rootbits) {
-            const int64_t nw = (j.n + 31) / 32;
+            const int64_t nw = (int64_t)tx * ty * (CT_W * CT_H / 32);
             hipLaunchKernelGGL(k_ccl_flatten_roots, dim3(grid_for(nw, 256, INT32_MAX)), b, 0, s,
-                               (const uint32_t*)j.rootbits, nw, j.L);
+                               (const uint32_t*)j.rootbits, nw, j.nx, tx, j.L);
             hipLaunchKernelGGL(k_ccl_flatten_cells, g, b, 0, s, j.n, j.L);
         } else {
             hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
@@ -4784,16 +4788,16 @@ int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool run
 }
 
 int lg_stage2(GridJob& j, hipStream_t s) {
-    j.hoff.resize(j.nblk);
+    HIP_TRY2(j.hoff.alloc(j.nblk));
     int64_t acc = 0;
     for (int64_t i = 0; i < j.nblk; ++i) {
-        j.hoff[i] = (int32_t)acc;
+        j.hoff.p[i] = (int32_t)acc;
         acc += j.hcnt.p[i];
     }
     j.ncomp = (int32_t)acc;
     const int32_t nc = j.ncomp;
     const dim3 b(256);
-    HIP_TRY2(hipMemcpyAsync(j.off.p, j.hoff.data(), j.nblk * sizeof(int32_t),
+    HIP_TRY2(hipMemcpyAsync(j.off.p, j.hoff.p, j.nblk * sizeof(int32_t),
                             hipMemcpyHostToDevice, s));
     HIP_TRY2(j.cid.alloc(j.n));
     hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)j.nblk), b, 0, s, j.L, j.n, j.off.p, j.cid.p);
@@ -4802,11 +4806,9 @@ int lg_stage2(GridJob& j, hipStream_t s) {
     if (nc > 0) {
         const dim3 gc(grid_for(nc, 256, INT32_MAX));
         int32_t* p = j.a.p;
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p, (int64_t)nc, 0);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + nc, (int64_t)nc, INT32_MAX);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 2 * (int64_t)nc, (int64_t)nc, INT32_MAX);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 3 * (int64_t)nc, (int64_t)nc, -1);
-        hipLaunchKernelGGL(k_fill_i32, gc, b, 0, s, p + 4 * (int64_t)nc, (int64_t)nc, -1);
+        // count 0, x0 / y0 INT32_MAX, x1 / y1 -1 (the root column is written by the stats)
+        hipLaunchKernelGGL(k_fill_segs_i32, gc, b, 0, s, p, (int64_t)nc, 5,
+                           FillSegs{{0, INT32_MAX, INT32_MAX, -1, -1, 0}});
         if (j.tiled)
             hipLaunchKernelGGL(k_ccl_stats_rows,
                                dim3((unsigned)((j.nx + CS_SEG - 1) / CS_SEG),
@@ -4851,9 +4853,8 @@ int label_grid(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool ru
 struct ExtJob {
     std::vector<int64_t> off;
     int64_t rows = 0;
-    DevBuf<int64_t> doff;
-    DevBuf<int32_t> dy0, dmn;
-    PinnedBuf<int32_t> hmn;
+    DevBuf<int32_t> dtab, dmn;  // dtab: int64 row offsets [ncomp], int32 first rows [ncomp]
+    PinnedBuf<int32_t> htab, hmn;
     std::vector<int32_t> xmin, xmax;
 };
 
@@ -4869,25 +4870,28 @@ int ext_stage1(ExtJob& e, int32_t nx, int32_t ny, const int32_t* L, const int32_
             e.rows += st.y1[c] - st.y0[c] + 1;
         }
     if (e.rows == 0) return UAM_OK;
-    HIP_TRY2(e.doff.alloc(ncomp));
-    HIP_TRY2(e.dy0.alloc(ncomp));
+    // row offsets (int64) then first rows (int32), staged in pinned memory: one upload
+    HIP_TRY2(e.dtab.alloc(3 * (int64_t)ncomp));
+    HIP_TRY2(e.htab.alloc(3 * (int64_t)ncomp));
+    std::memcpy(e.htab.p, e.off.data(), ncomp * sizeof(int64_t));
+    std::memcpy(e.htab.p + 2 * (int64_t)ncomp, st.y0.data(), ncomp * sizeof(int32_t));
     HIP_TRY2(e.dmn.alloc(2 * e.rows));
     HIP_TRY2(e.hmn.alloc(2 * e.rows));
-    HIP_TRY2(hipMemcpyAsync(e.doff.p, e.off.data(), ncomp * sizeof(int64_t),
+    HIP_TRY2(hipMemcpyAsync(e.dtab.p, e.htab.p, 3 * (int64_t)ncomp * sizeof(int32_t),
                             hipMemcpyHostToDevice, s));
-    HIP_TRY2(hipMemcpyAsync(e.dy0.p, st.y0.data(), ncomp * sizeof(int32_t),
-                            hipMemcpyHostToDevice, s));
+    const int64_t* doff = reinterpret_cast<const int64_t*>(e.dtab.p);
+    const int32_t* dy0 = e.dtab.p + 2 * (int64_t)ncomp;
     const dim3 gr(grid_for(e.rows, 256, INT32_MAX)), b(256);
-    hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p, e.rows, INT32_MAX);
-    hipLaunchKernelGGL(k_fill_i32, gr, b, 0, s, e.dmn.p + e.rows, e.rows, -1);
+    hipLaunchKernelGGL(k_fill_segs_i32, gr, b, 0, s, e.dmn.p, e.rows, 2,
+                       FillSegs{{INT32_MAX, -1, 0, 0, 0, 0}});
     const int64_t n = (int64_t)nx * ny;
     if (tiled && ny <= 65535)
         hipLaunchKernelGGL(k_ccl_extents_rows,
                            dim3((unsigned)((nx + CS_SEG - 1) / CS_SEG), (unsigned)ny), b, 0, s, L,
-                           cid, nx, e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
+                           cid, nx, doff, dy0, e.dmn.p, e.dmn.p + e.rows);
     else
         hipLaunchKernelGGL(k_ccl_extents, dim3(grid_for(n, 256, INT32_MAX)), b, 0, s, L, cid, nx,
-                           n, e.doff.p, e.dy0.p, e.dmn.p, e.dmn.p + e.rows);
+                           n, doff, dy0, e.dmn.p, e.dmn.p + e.rows);
     HIP_TRY2(hipGetLastError());
     HIP_TRY2(hipMemcpyAsync(e.hmn.p, e.dmn.p, 2 * e.rows * sizeof(int32_t),
                             hipMemcpyDeviceToHost, s));
@@ -5005,8 +5009,8 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     GridJob mj;
     DevBuf<uint32_t> mbits;
     if (tiled) {
-        HIP_TRY2(mbits.alloc((n + 31) / 32));
-        HIP_TRY2(hipMemsetAsync(mbits.p, 0, ((n + 31) / 32) * sizeof(uint32_t), s));
+        const dim3 tg = tiles(nx, ny);
+        HIP_TRY2(mbits.alloc((int64_t)tg.x * tg.y * (CT_W * CT_H / 32)));
         mj.rootbits = mbits.p;
         hipLaunchKernelGGL(k_ccl_tile<CclMaskDem>, tiles(nx, ny), dim3(256), 0, s,
                            CclMaskDem{dem, threshold, nx}, nx, ny, nullptr, nullptr, L.p,
@@ -5040,7 +5044,9 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         int32_t c = 0, ws = 0, hs = 0;
         std::vector<int32_t> col_of, colbox, row_of, rowbox;
         std::vector<double> sxlo, sxhi, sylo, syhi;
-        DevBuf<int32_t> dco, dcb, dro, drb, L2;
+        DevBuf<int32_t> tab, L2;  // col_of, colbox [ws]; row_of, rowbox [hs]
+        PinnedBuf<int32_t> htab;
+        const int32_t *dco = nullptr, *dcb = nullptr, *dro = nullptr, *drb = nullptr;
         DevBuf<uint32_t> bits;
         GridJob job;
         ExtJob ext;
@@ -5078,28 +5084,31 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
             }
         r.ws = (int32_t)r.col_of.size(), r.hs = (int32_t)r.row_of.size();
         const int64_t sn = (int64_t)r.ws * r.hs;
-        HIP_TRY2(r.dco.alloc(r.ws));
-        HIP_TRY2(r.dcb.alloc(r.ws));
-        HIP_TRY2(r.dro.alloc(r.hs));
-        HIP_TRY2(r.drb.alloc(r.hs));
+        const int64_t nt = 2 * (int64_t)r.ws + 2 * (int64_t)r.hs;
+        HIP_TRY2(r.tab.alloc(nt));
+        HIP_TRY2(r.htab.alloc(nt));
         HIP_TRY2(r.L2.alloc(sn));
-        HIP_TRY2(hipMemcpyAsync(r.dco.p, r.col_of.data(), r.ws * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(r.dcb.p, r.colbox.data(), r.ws * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(r.dro.p, r.row_of.data(), r.hs * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY2(hipMemcpyAsync(r.drb.p, r.rowbox.data(), r.hs * 4, hipMemcpyHostToDevice, s));
+        int32_t* h = r.htab.p;
+        std::copy(r.col_of.begin(), r.col_of.end(), h);
+        std::copy(r.colbox.begin(), r.colbox.end(), h + r.ws);
+        std::copy(r.row_of.begin(), r.row_of.end(), h + 2 * (int64_t)r.ws);
+        std::copy(r.rowbox.begin(), r.rowbox.end(), h + 2 * (int64_t)r.ws + r.hs);
+        HIP_TRY2(hipMemcpyAsync(r.tab.p, h, nt * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        r.dco = r.tab.p, r.dcb = r.tab.p + r.ws, r.dro = r.tab.p + 2 * (int64_t)r.ws;
+        r.drb = r.dro + r.hs;
         if (tiled) {
-            HIP_TRY2(r.bits.alloc((sn + 31) / 32));
-            HIP_TRY2(hipMemsetAsync(r.bits.p, 0, ((sn + 31) / 32) * sizeof(uint32_t), s));
+            const dim3 tg = tiles(r.ws, r.hs);
+            HIP_TRY2(r.bits.alloc((int64_t)tg.x * tg.y * (CT_W * CT_H / 32)));
             r.job.rootbits = r.bits.p;
             hipLaunchKernelGGL(k_ccl_tile<CclMaskSub>, tiles(r.ws, r.hs), dim3(256), 0, s,
-                               CclMaskSub{L.p, nx, st.root[c], r.dco.p, r.dro.p}, r.ws, r.hs,
-                               r.dcb.p, r.drb.p, r.L2.p, r.bits.p);
+                               CclMaskSub{L.p, nx, st.root[c], r.dco, r.dro}, r.ws, r.hs, r.dcb,
+                               r.drb, r.L2.p, r.bits.p);
         } else
             hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0,
-                               s, L.p, nx, st.root[c], r.dco.p, r.dro.p, r.dcb.p, r.ws, r.hs,
+                               s, L.p, nx, st.root[c], r.dco, r.dro, r.dcb, r.ws, r.hs,
                                r.L2.p);
         r.job.nx = r.ws, r.job.ny = r.hs, r.job.L = r.L2.p;
-        rc = lg_stage1(r.job, r.dcb.p, r.drb.p, true, s, tiled);
+        rc = lg_stage1(r.job, r.dcb, r.drb, true, s, tiled);
         if (rc) return rc;
     }
     HIP_TRY2(hipStreamSynchronize(s));  // main extents, every region's root counts
