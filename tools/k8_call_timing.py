@@ -1,3 +1,5 @@
+"""Per-call wall time of uam_dem_polygons (run with UAM_K8_PROF=1 for the phase stamps).
+usage: python tools/k8_call_timing.py [size=8192] [calls=4]"""
 import sys, time, os
 sys.path.insert(0, os.getcwd())
 import torch
@@ -5,9 +7,11 @@ from uam_path_planning_amd.engine import Engine
 from uam_path_planning_amd.scenario import raster_geo
 from uam_path_planning_amd.synthetic import synthetic_dem
 eng = Engine(0)
-geo = raster_geo(8192)
-dem = torch.tensor(synthetic_dem(8192, seed=3), device="cuda")
-for i in range(4):
+R = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+geo = raster_geo(R)
+dem = torch.tensor(synthetic_dem(R, seed=3), device="cuda")
+for i in range(K):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     r = eng.dem_polygons(dem, geo, 0.0)

@@ -21,6 +21,7 @@
 // tables are read with wave-uniform addresses (scalar cache) in the analytic mode.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -29,6 +30,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/uampath.h"
@@ -5117,6 +5119,19 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         rc = lg_stage2(r.job, s);
         if (rc) return rc;
     }
+    // the small regions' rectangles (host) while the GPU labels the large ones
+    std::vector<int64_t> small_out;
+    std::vector<int64_t> small_at(ncomp + 1, 0);  // component c: small_out[small_at[c], [c+1])
+    std::vector<uampoly::Pt> pts;
+    for (int32_t c = 0; c < ncomp; ++c) {
+        if (small[c]) {
+            region_corners(st.y0[c], st.y1[c], &me.xmin[me.off[c]], &me.xmax[me.off[c]], xlo,
+                           xhi, ylo, yhi, pts);
+            emit_rect(pts, prm->min_approx_area, small_out);
+        }
+        small_at[c + 1] = (int64_t)small_out.size();
+    }
+    stamp("small rectangles (host)");
     HIP_TRY2(hipStreamSynchronize(s));  // every region's component stats
     for (Region& r : regs) {
         lg_stage3(r.job);
@@ -5128,32 +5143,47 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     stamp("large regions labelled");
     // rectangles in component order (small: the region; large: its pieces, boxes j (x) outer,
     // k (y) inner -- the reference's order)
+    // a large region's pieces are independent host work: up to 8 worker threads take regions
+    // in turn (the helpers keep their scratch thread_local); joined in component order below
+    std::vector<std::vector<int64_t>> rout(regs.size());
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+        std::vector<uampoly::Pt> rp;
+        for (size_t k; (k = next.fetch_add(1)) < regs.size();) {
+            Region& r = regs[k];
+            ext_stage2(r.ext);
+            const CompStats& ps = r.job.st;
+            const int32_t np = (int32_t)ps.cnt.size();
+            std::vector<int32_t> order(np);
+            for (int32_t i = 0; i < np; ++i) order[i] = i;
+            std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+                const int ja = r.colbox[ps.x0[a]], jb = r.colbox[ps.x0[b]];
+                if (ja != jb) return ja < jb;
+                return r.rowbox[ps.y0[a]] < r.rowbox[ps.y0[b]];
+            });
+            for (int32_t i : order) {
+                region_corners(ps.y0[i], ps.y1[i], &r.ext.xmin[r.ext.off[i]],
+                               &r.ext.xmax[r.ext.off[i]], r.sxlo, r.sxhi, r.sylo, r.syhi, rp);
+                emit_rect(rp, prm->min_approx_area, rout[k]);
+            }
+        }
+    };
+    {
+        std::vector<std::thread> pool;
+        for (size_t k = 1; k < std::min<size_t>(regs.size(), 8); ++k) pool.emplace_back(worker);
+        worker();
+        for (auto& t : pool) t.join();
+    }
     std::vector<int64_t> out;
-    std::vector<uampoly::Pt> pts;
+    out.reserve(small_out.size());
     size_t ri = 0;
     for (int32_t c = 0; c < ncomp; ++c) {
         if (small[c]) {
-            region_corners(st.y0[c], st.y1[c], &me.xmin[me.off[c]], &me.xmax[me.off[c]], xlo,
-                           xhi, ylo, yhi, pts);
-            emit_rect(pts, prm->min_approx_area, out);
-            continue;
-        }
-        if (!large[c]) continue;
-        Region& r = regs[ri++];
-        ext_stage2(r.ext);
-        const CompStats& ps = r.job.st;
-        const int32_t np = (int32_t)ps.cnt.size();
-        std::vector<int32_t> order(np);
-        for (int32_t i = 0; i < np; ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-            const int ja = r.colbox[ps.x0[a]], jb = r.colbox[ps.x0[b]];
-            if (ja != jb) return ja < jb;
-            return r.rowbox[ps.y0[a]] < r.rowbox[ps.y0[b]];
-        });
-        for (int32_t i : order) {
-            region_corners(ps.y0[i], ps.y1[i], &r.ext.xmin[r.ext.off[i]], &r.ext.xmax[r.ext.off[i]],
-                           r.sxlo, r.sxhi, r.sylo, r.syhi, pts);
-            emit_rect(pts, prm->min_approx_area, out);
+            out.insert(out.end(), small_out.begin() + small_at[c],
+                       small_out.begin() + small_at[c + 1]);
+        } else if (large[c]) {
+            out.insert(out.end(), rout[ri].begin(), rout[ri].end());
+            ++ri;
         }
     }
     stamp("all rectangles");
