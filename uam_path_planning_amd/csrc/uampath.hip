@@ -3671,6 +3671,8 @@ struct uam_ctx {
     double* d_tmtab = nullptr;  // K7 reprojection row / column tables (grow-only)
     size_t tmtab_n = 0;
     bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
+    int k8_nstreams = 4;        // K8 large regions: streams they are spread over (UAM_K8_STREAMS)
+    hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
 };
 
 namespace {
@@ -3758,6 +3760,8 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
     if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_K8_STREAMS"))
+        c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
     *out = c;
     return UAM_OK;
 }
@@ -3772,6 +3776,8 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
+    for (hipStream_t k : ctx->k8s)
+        if (k) (void)hipStreamDestroy(k);
     if (ctx->pinned) pinned_arena_free(ctx->pinned);
     if (ctx->devarena) dev_arena_free(ctx->devarena);
     if (ctx->d_tmtab) (void)hipFree(ctx->d_tmtab);
@@ -5061,7 +5067,23 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
             regs.back().c = c;
         }
     const int D = prm->divisions;
-    for (Region& r : regs) {
+    // the regions are independent: region k runs on stream k mod NS (the caller's stream and
+    // NS - 1 side streams), so their small launches and tails overlap.  The main labels they
+    // read are complete (label_grid synchronised s).
+    const int NS = std::max(1, std::min<int>(ctx->k8_nstreams, (int)regs.size()));
+    for (int k = 0; k + 1 < NS; ++k)
+        if (!ctx->k8s[k]) HIP_TRY2(hipStreamCreateWithFlags(&ctx->k8s[k], hipStreamNonBlocking));
+    auto rstream = [&](size_t k) { return k % NS == 0 ? s : ctx->k8s[k % NS - 1]; };
+    auto sync_all = [&]() -> hipError_t {
+        for (int k = 0; k < NS; ++k) {
+            const hipError_t e = hipStreamSynchronize(k == 0 ? s : ctx->k8s[k - 1]);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    for (size_t ri = 0; ri < regs.size(); ++ri) {
+        Region& r = regs[ri];
+        const hipStream_t rs = rstream(ri);
         const int32_t c = r.c;
         const double minx = X0 + st.x0[c] * DX, maxx = X0 + (st.x1[c] + 1) * DX;
         const double maxy = Y0 - st.y0[c] * DY, miny = Y0 - (st.y1[c] + 1) * DY;
@@ -5095,28 +5117,28 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         std::copy(r.colbox.begin(), r.colbox.end(), h + r.ws);
         std::copy(r.row_of.begin(), r.row_of.end(), h + 2 * (int64_t)r.ws);
         std::copy(r.rowbox.begin(), r.rowbox.end(), h + 2 * (int64_t)r.ws + r.hs);
-        HIP_TRY2(hipMemcpyAsync(r.tab.p, h, nt * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIP_TRY2(hipMemcpyAsync(r.tab.p, h, nt * sizeof(int32_t), hipMemcpyHostToDevice, rs));
         r.dco = r.tab.p, r.dcb = r.tab.p + r.ws, r.dro = r.tab.p + 2 * (int64_t)r.ws;
         r.drb = r.dro + r.hs;
         if (tiled) {
             const dim3 tg = tiles(r.ws, r.hs);
             HIP_TRY2(r.bits.alloc((int64_t)tg.x * tg.y * (CT_W * CT_H / 32)));
             r.job.rootbits = r.bits.p;
-            hipLaunchKernelGGL(k_ccl_tile<CclMaskSub>, tiles(r.ws, r.hs), dim3(256), 0, s,
+            hipLaunchKernelGGL(k_ccl_tile<CclMaskSub>, tiles(r.ws, r.hs), dim3(256), 0, rs,
                                CclMaskSub{L.p, nx, st.root[c], r.dco, r.dro}, r.ws, r.hs, r.dcb,
                                r.drb, r.L2.p, r.bits.p);
         } else
             hipLaunchKernelGGL(k_ccl_init_sub, dim3(grid_for(sn, 256, INT32_MAX)), dim3(256), 0,
-                               s, L.p, nx, st.root[c], r.dco, r.dro, r.dcb, r.ws, r.hs,
+                               rs, L.p, nx, st.root[c], r.dco, r.dro, r.dcb, r.ws, r.hs,
                                r.L2.p);
         r.job.nx = r.ws, r.job.ny = r.hs, r.job.L = r.L2.p;
-        rc = lg_stage1(r.job, r.dcb, r.drb, true, s, tiled);
+        rc = lg_stage1(r.job, r.dcb, r.drb, true, rs, tiled);
         if (rc) return rc;
     }
-    HIP_TRY2(hipStreamSynchronize(s));  // main extents, every region's root counts
+    HIP_TRY2(sync_all());  // main extents, every region's root counts
     ext_stage2(me);
-    for (Region& r : regs) {
-        rc = lg_stage2(r.job, s);
+    for (size_t ri = 0; ri < regs.size(); ++ri) {
+        rc = lg_stage2(regs[ri].job, rstream(ri));
         if (rc) return rc;
     }
     // the small regions' rectangles (host) while the GPU labels the large ones
@@ -5132,14 +5154,16 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         small_at[c + 1] = (int64_t)small_out.size();
     }
     stamp("small rectangles (host)");
-    HIP_TRY2(hipStreamSynchronize(s));  // every region's component stats
-    for (Region& r : regs) {
+    HIP_TRY2(sync_all());  // every region's component stats
+    for (size_t ri = 0; ri < regs.size(); ++ri) {
+        Region& r = regs[ri];
         lg_stage3(r.job);
         const std::vector<char> all(r.job.st.cnt.size(), 1);
-        rc = ext_stage1(r.ext, r.ws, r.hs, r.L2.p, r.job.cid.p, r.job.st, all, s, tiled);
+        rc = ext_stage1(r.ext, r.ws, r.hs, r.L2.p, r.job.cid.p, r.job.st, all, rstream(ri),
+                        tiled);
         if (rc) return rc;
     }
-    HIP_TRY2(hipStreamSynchronize(s));  // every region's row extents
+    HIP_TRY2(sync_all());  // every region's row extents
     stamp("large regions labelled");
     // rectangles in component order (small: the region; large: its pieces, boxes j (x) outer,
     // k (y) inner -- the reference's order)
