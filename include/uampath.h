@@ -284,7 +284,9 @@ int uam_process_polygons(const double* xy, const int64_t* ring_start, int32_t n_
  * at x0 + i dx, y_top - j dy (times unit_m metres).  Large regions are split into their box
  * pieces by a second labelling on the grid refined at the box edges.  Output as
  * uam_process_polygons (regions in raster order of their first cell).  Definition:
- * oracle/uam_oracle.c orc_dem_polygons. */
+ * oracle/uam_oracle.c orc_dem_polygons.  Work is enqueued on `stream` and, for the large
+ * regions, on up to 3 side streams the context owns (UAM_K8_STREAMS, 1-8, default 4 in all);
+ * the call synchronises all of them before it returns. */
 int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* desc,
                      float threshold, double unit_m, const uam_polyproc_params* params,
                      int64_t* rect_xy, int32_t max_rects, int32_t* n_rects, uam_stream stream);
