@@ -129,3 +129,22 @@ def test_dem_polygons_tile_edges(oracle_mod, monkeypatch, tiled, nx, ny, thr):
     ref = oracle_mod.dem_polygons(dem, rd, thr, 1000.0)
     assert len(ref) > 0
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("streams", ["1", "2", "8"])
+def test_dem_polygons_region_streams(oracle_mod, monkeypatch, streams):
+    """The large regions spread over 1, 2 or 8 streams (UAM_K8_STREAMS; default 4): same
+    rectangles in the same order as the oracle."""
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.scenario import raster_geo
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    monkeypatch.setenv("UAM_K8_STREAMS", streams)
+    e2 = Engine(0)
+    geo = raster_geo(1024)
+    dem = synthetic_dem(1024, seed=5)
+    got = _arr(e2.dem_polygons(dem, geo, 0.0))
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy)
+    ref = oracle_mod.dem_polygons(dem, rd, 0.0, 1000.0)
+    assert len(ref) > 25  # several large regions
+    np.testing.assert_array_equal(got, ref)

@@ -27,7 +27,8 @@ def main():
     for R in [int(x) for x in a.sizes.split(",")]:
         geo = raster_geo(R)
         dem = torch.tensor(synthetic_dem(R, seed=3), device="cuda")
-        rects = eng.dem_polygons(dem, geo, 0.0)          # warm-up
+        for _ in range(3):                               # warm-up (the arenas grow here)
+            rects = eng.dem_polygons(dem, geo, 0.0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.reps):

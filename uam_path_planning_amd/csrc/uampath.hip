@@ -4754,6 +4754,7 @@ struct GridJob {
     int32_t ncomp = 0;
     bool tiled = false;  // tile labelling and the row-segment stats
     uint32_t* rootbits = nullptr;  // tiled: tile-local root bits written by k_ccl_tile
+    DevBuf<uint32_t> groots;       // with rootbits: raster-order bitmap of component roots
     DevBuf<int32_t> cnt, off, cid, a;
     PinnedBuf<int32_t> hcnt, hall, hoff;
     CompStats st;
@@ -4772,10 +4773,22 @@ int lg_stage1(GridJob& j, const int32_t* colbox, const int32_t* rowbox, bool run
             hipLaunchKernelGGL(k_ccl_bmerge, dim3(grid_for(nb, 256, INT32_MAX)), b, 0, s, j.nx,
                                j.ny, tx, ty, colbox, rowbox, j.L);
         if (j.rootbits) {
-            const int64_t nw = (int64_t)tx * ty * (CT_W * CT_H / 32);
+            const int64_t nw = (int64_t)tx * ty * (CT_W * CT_H / 32), ngw = (j.n + 31) / 32;
+            HIP_TRY2(j.groots.alloc(ngw));
+            HIP_TRY2(hipMemsetAsync(j.groots.p, 0, ngw * sizeof(uint32_t), s));
             hipLaunchKernelGGL(k_ccl_flatten_roots, dim3(grid_for(nw, 256, INT32_MAX)), b, 0, s,
-                               (const uint32_t*)j.rootbits, nw, j.nx, tx, j.L);
+                               (const uint32_t*)j.rootbits, nw, j.nx, tx, j.L, j.groots.p);
             hipLaunchKernelGGL(k_ccl_flatten_cells, g, b, 0, s, j.n, j.L);
+            j.nblk = (ngw + 255) / 256;
+            HIP_TRY2(j.cnt.alloc(j.nblk));
+            HIP_TRY2(j.off.alloc(j.nblk));
+            HIP_TRY2(j.hcnt.alloc(j.nblk));
+            hipLaunchKernelGGL(k_ccl_count_rootbits, dim3((unsigned)j.nblk), b, 0, s,
+                               (const uint32_t*)j.groots.p, ngw, j.cnt.p);
+            HIP_TRY2(hipGetLastError());
+            HIP_TRY2(hipMemcpyAsync(j.hcnt.p, j.cnt.p, j.nblk * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, s));
+            return UAM_OK;
         } else {
             hipLaunchKernelGGL(k_ccl_flatten, g, b, 0, s, j.n, j.L);
         }
@@ -4808,7 +4821,12 @@ int lg_stage2(GridJob& j, hipStream_t s) {
     HIP_TRY2(hipMemcpyAsync(j.off.p, j.hoff.p, j.nblk * sizeof(int32_t),
                             hipMemcpyHostToDevice, s));
     HIP_TRY2(j.cid.alloc(j.n));
-    hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)j.nblk), b, 0, s, j.L, j.n, j.off.p, j.cid.p);
+    if (j.groots.p)
+        hipLaunchKernelGGL(k_ccl_assign_rootbits, dim3((unsigned)j.nblk), b, 0, s,
+                           (const uint32_t*)j.groots.p, (j.n + 31) / 32, j.off.p, j.cid.p);
+    else
+        hipLaunchKernelGGL(k_ccl_assign, dim3((unsigned)j.nblk), b, 0, s, j.L, j.n, j.off.p,
+                           j.cid.p);
     HIP_TRY2(j.a.alloc(6 * (int64_t)std::max(nc, 1)));
     HIP_TRY2(j.hall.alloc(6 * (int64_t)std::max(nc, 1)));
     if (nc > 0) {
