@@ -5099,6 +5099,12 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         }
         return hipSuccess;
     };
+    // an early error return must not leave side-stream work reading the arenas, which the
+    // next call reuses: drain every stream on the way out (idle streams return at once)
+    struct Drain {
+        std::function<hipError_t()> f;
+        ~Drain() { (void)f(); }
+    } drain{sync_all};
     for (size_t ri = 0; ri < regs.size(); ++ri) {
         Region& r = regs[ri];
         const hipStream_t rs = rstream(ri);
