@@ -305,7 +305,8 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
  * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
  * UAM_TB_DBG (K2t diagnostics that change results: 1 skips the gathers, 2 the stores,
- * 4 pass 1).  None of them changes results except UAM_TB_DBG. */
+ * 4 pass 1), UAM_PAIR_ORDER=0 (analytic uam_eval_generated without the spatial pair order it
+ * applies to batches of >= 4096 pairs).  None of them changes results except UAM_TB_DBG. */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */

@@ -794,7 +794,8 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
                                                            const double* __restrict__ utab,
                                                            int D, KOut out,
                                                            int32_t* __restrict__ best_f,
-                                                           int32_t* __restrict__ best_l) {
+                                                           int32_t* __restrict__ best_l,
+                                                           const int32_t* __restrict__ order) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int BP = 64 * D;                     // paths per block
     double* s_cost = smem;
@@ -810,9 +811,12 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
-    const int64_t q = q0 + lane;
+    // order (optional): block slot -> pair, a spatial order of the pairs (pair_order); every
+    // pair is still read and written at its own index, so results do not depend on it
+    const bool in = q0 + lane < n_pairs;
+    const int64_t q = (order && in) ? (int64_t)order[q0 + lane] : q0 + lane;
     const int slot = d * 64 + lane;
-    if (q < n_pairs) {
+    if (in) {
         PathSrc<true> src;
         src.W = p.N + 2;
         src.wp = nullptr;
@@ -839,6 +843,20 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         s_bel[slot] = a.below;
     }
     __syncthreads();
+    if (order) {  // scattered pairs: each lane stores its own path
+        if (in) {
+            const int64_t gp = q * D + d;
+            if (out.cost) out.cost[gp] = s_cost[slot];
+            if (out.length_q) out.length_q[gp] = s_L[slot];
+            if (out.length) out.length[gp] = s_len[slot];
+            if (out.kin_sum) out.kin_sum[gp] = s_k[slot];
+            if (out.nfz_sum) out.nfz_sum[gp] = s_n[slot];
+            if (out.min_clearance) out.min_clearance[gp] = s_clr[slot];
+            if (out.nfz_hits) out.nfz_hits[gp] = s_nh[slot];
+            if (out.offmap) out.offmap[gp] = s_off[slot];
+            if (out.below_terrain) out.below_terrain[gp] = s_bel[slot];
+        }
+    } else {
     // coalesced stores: thread t -> block-local path t = (pair t / D, displacement t % D)
     const int t = threadIdx.x;
     const int qi = t / D, di = t - qi * D;
@@ -855,7 +873,8 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         if (out.offmap) out.offmap[gp] = s_off[s];
         if (out.below_terrain) out.below_terrain[gp] = s_bel[s];
     }
-    if (d == 0 && q < n_pairs) {
+    }
+    if (d == 0 && in) {
         if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
         if (best_l) best_l[q] = select_best(s_len + lane, 64, D, false);
     }
@@ -3637,6 +3656,105 @@ bool shape_box(const DevIneq* q, int n, double e, double box[4]) {
     return true;
 }
 
+
+// ----------------------------------------------------------------------------------------
+// Pair order for K3 (analytic mode).  K3 runs one lane per path, so a wave's 64 lanes walk 64
+// shape-grid lists; pairs in a spatial order (Morton order of (x0, y0, xf, yf), 4 bits per
+// coordinate over the pairs' extent) put similar paths in one wave and cut the
+// divergence (8.6 -> 4.8 ms per cfg3 launch, tools/probe_analytic_sort.py).  A counting sort
+// on the 16-bit key: histogram, one-block scan, scatter.  The order inside a key is whatever
+// the atomics give -- results do not depend on it, since each pair is read and written at its
+// own index.
+// doubles as order-preserving unsigned keys (for atomicMin / atomicMax of the bounds)
+__device__ __forceinline__ unsigned long long dkey(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dkey_inv(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// bounds of the pairs' x and y: bnd[0..1] = min x, min y; bnd[2..3] = max x, max y (keys)
+__global__ __launch_bounds__(256) void k_pair_bounds(const double* __restrict__ pairs, int64_t n,
+                                                     unsigned long long* __restrict__ bnd) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double v[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+    if (i < n) {
+        const double4 pr = reinterpret_cast<const double4*>(pairs)[i];
+        v[0] = fmin(pr.x, pr.z), v[1] = fmin(pr.y, pr.w);
+        v[2] = fmax(pr.x, pr.z), v[3] = fmax(pr.y, pr.w);
+    }
+    for (int o = 32; o; o >>= 1) {
+        v[0] = fmin(v[0], __shfl_xor(v[0], o, 64));
+        v[1] = fmin(v[1], __shfl_xor(v[1], o, 64));
+        v[2] = fmax(v[2], __shfl_xor(v[2], o, 64));
+        v[3] = fmax(v[3], __shfl_xor(v[3], o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&bnd[0], dkey(v[0]));
+        atomicMin(&bnd[1], dkey(v[1]));
+        atomicMax(&bnd[2], dkey(v[2]));
+        atomicMax(&bnd[3], dkey(v[3]));
+    }
+}
+
+__device__ __forceinline__ uint32_t pair_key(const double4 pr, const double* b) {
+    auto q4 = [](double v, double lo, double inv) {
+        const double t = (v - lo) * inv;
+        return (uint32_t)(t > 0.0 ? (t < 15.0 ? t : 15.0) : 0.0);  // NaN -> 0
+    };
+    const double ix = 16.0 / fmax(b[2] - b[0], 1e-300), iy = 16.0 / fmax(b[3] - b[1], 1e-300);
+    const uint32_t c[4] = {q4(pr.x, b[0], ix), q4(pr.y, b[1], iy), q4(pr.z, b[0], ix),
+                           q4(pr.w, b[1], iy)};
+    uint32_t k = 0;
+    for (int b = 3; b >= 0; --b)
+        for (int d = 0; d < 4; ++d) k = (k << 1) | ((c[d] >> b) & 1u);
+    return k;
+}
+
+__global__ __launch_bounds__(256) void k_pair_keys(const double* __restrict__ pairs, int64_t n,
+                                                   const unsigned long long* __restrict__ bnd,
+                                                   uint16_t* __restrict__ key,
+                                                   int32_t* __restrict__ hist) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double b[4] = {dkey_inv(bnd[0]), dkey_inv(bnd[1]), dkey_inv(bnd[2]), dkey_inv(bnd[3])};
+    const uint32_t k = pair_key(reinterpret_cast<const double4*>(pairs)[i], b);
+    key[i] = (uint16_t)k;
+    atomicAdd(&hist[k], 1);
+}
+
+// exclusive scan of the 65536 key counts, one workgroup of 1024 threads x 64 counts
+__global__ __launch_bounds__(1024) void k_pair_scan(int32_t* __restrict__ hist) {
+    __shared__ int32_t part[1024];
+    const int t = threadIdx.x;
+    int32_t* h = hist + t * 64;
+    int32_t sum = 0;
+    for (int i = 0; i < 64; ++i) sum += h[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int32_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int32_t run = part[t] - sum;
+    for (int i = 0; i < 64; ++i) {
+        const int32_t c = h[i];
+        h[i] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pair_scatter(const uint16_t* __restrict__ key, int64_t n,
+                                                      int32_t* __restrict__ next,
+                                                      int32_t* __restrict__ order) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    order[atomicAdd(&next[key[i]], 1)] = (int32_t)i;
+}
+
 }  // namespace
 
 namespace {
@@ -3672,6 +3790,9 @@ struct uam_ctx {
     size_t tmtab_n = 0;
     bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
     int k8_nstreams = 4;        // K8 large regions: streams they are spread over (UAM_K8_STREAMS)
+    bool pair_order = true;     // K3: evaluate pairs in a spatial order (UAM_PAIR_ORDER=0: off)
+    void* d_ord = nullptr;      // pair_order scratch (grow-only)
+    size_t ord_bytes = 0;
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
 };
 
@@ -3760,6 +3881,7 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
     if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_PAIR_ORDER")) c->pair_order = std::atoi(e) != 0;
     if (const char* e = std::getenv("UAM_K8_STREAMS"))
         c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
     *out = c;
@@ -3773,6 +3895,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->d_ord) (void)hipFree(ctx->d_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
@@ -4181,6 +4304,43 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
     return UAM_OK;
 }
 
+// K3 pair order (k_pair_keys / k_pair_scan / k_pair_scatter) into the context's scratch; *order
+// stays null when the geometry has no shape grid (nothing to gain)
+static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t s,
+                      const int32_t** order) {
+    *order = nullptr;
+    const KShapeGrid& g = ctx->kg.grid;
+    if (g.gx == 0 || !(g.x1 > g.x0) || !(g.y1 > g.y0)) return UAM_OK;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    // [hist 65536 | max bounds 2 x u64] zeroed together, then min bounds 2 x u64 (all ones)
+    const size_t b_hist = al(65536 * 4 + 16 + 16), b_key = al((size_t)n * 2),
+                 b_ord = al((size_t)n * 4);
+    const size_t need = b_hist + b_key + b_ord;
+    if (need > ctx->ord_bytes) {
+        if (ctx->d_ord) (void)hipFree(ctx->d_ord);
+        ctx->d_ord = nullptr;
+        ctx->ord_bytes = 0;
+        if (hipMalloc(&ctx->d_ord, need) != hipSuccess) return fail(UAM_E_NOMEM, "pair order");
+        ctx->ord_bytes = need;
+    }
+    char* w = (char*)ctx->d_ord;
+    int32_t* hist = (int32_t*)w;
+    uint16_t* key = (uint16_t*)(w + b_hist);
+    int32_t* ord = (int32_t*)(w + b_hist + b_key);
+    unsigned long long* bnd = (unsigned long long*)(w + 65536 * 4);  // min x, min y, max x, max y
+    HIP_TRY(hipMemsetAsync(hist, 0, 65536 * 4 + 32, s));
+    HIP_TRY(hipMemsetAsync(bnd, 0xff, 16, s));
+    const dim3 gr(grid_for(n, 256, INT32_MAX)), b(256);
+    hipLaunchKernelGGL(k_pair_bounds, gr, b, 0, s, pairs, n, bnd);
+    hipLaunchKernelGGL(k_pair_keys, gr, b, 0, s, pairs, n, (const unsigned long long*)bnd, key,
+                       hist);
+    hipLaunchKernelGGL(k_pair_scan, dim3(1), dim3(1024), 0, s, hist);
+    hipLaunchKernelGGL(k_pair_scatter, gr, b, 0, s, (const uint16_t*)key, n, hist, ord);
+    HIP_TRY(hipGetLastError());
+    *order = ord;
+    return UAM_OK;
+}
+
 // K2b launch; returns 1 if launched, 0 if the batch does not fit (caller falls back)
 static int launch_binned(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
                          int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
@@ -4229,7 +4389,7 @@ static int launch_binned(uam_ctx* ctx, const KRaster& kr, const void* rec, const
     const KVolume kv{};
     hipLaunchKernelGGL((k_eval_pairs<MODE_RECORDS, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, s, ctx->kg, ctx->kp, kr, kv, (const uint4*)recs, pairs,
-                       n_pairs, utab, D, ko, best_f, best_l);
+                       n_pairs, utab, D, ko, best_f, best_l, nullptr);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "binned evaluation launch");
     return 1;
 }
@@ -4396,10 +4556,15 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     const dim3 grid((unsigned)blocks), block(64 * D);
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
     const KVolume kv{};
+    const int32_t* order = nullptr;
+    if (mode == UAM_MODE_ANALYTIC && ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
+        st = pair_order(ctx, pairs, n_pairs, s, &order);
+        if (st) return st;
+    }
 #define UAM_LAUNCH_PAIRS(MODE_, C_, PIPE_, MINW_)                                          \
     hipLaunchKernelGGL((k_eval_pairs<MODE_, C_, PIPE_, MINW_>), grid, block, lds, s, ctx->kg, \
                        ctx->kp, kr, kv, (const uint4*)rec, pairs, n_pairs, utab, D, ko,      \
-                       best_f, best_l)
+                       best_f, best_l, order)
     if (mode == UAM_MODE_ANALYTIC) {
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
@@ -4478,7 +4643,8 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
-                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l);
+                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l,
+                       nullptr);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
