@@ -814,7 +814,8 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     // order (optional): block slot -> pair, a spatial order of the pairs (pair_order); every
     // pair is still read and written at its own index, so results do not depend on it
     const bool in = q0 + lane < n_pairs;
-    const int64_t q = (order && in) ? (int64_t)order[q0 + lane] : q0 + lane;
+    const bool ordered = MODE == UAM_MODE_ANALYTIC && order;  // compiled out elsewhere
+    const int64_t q = (ordered && in) ? (int64_t)order[q0 + lane] : q0 + lane;
     const int slot = d * 64 + lane;
     if (in) {
         PathSrc<true> src;
@@ -843,7 +844,7 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         s_bel[slot] = a.below;
     }
     __syncthreads();
-    if (order) {  // scattered pairs: each lane stores its own path
+    if (ordered) {  // scattered pairs: each lane stores its own path
         if (in) {
             const int64_t gp = q * D + d;
             if (out.cost) out.cost[gp] = s_cost[slot];
