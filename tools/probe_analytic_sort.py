@@ -47,8 +47,15 @@ def main():
     # 4 bits per coordinate, ties in random order (what a 16-bit counting sort gives)
     rp = np.random.default_rng(1).permutation(len(host))
     o16 = rp[np.argsort(morton4(host[rp], bits=4), kind="stable")]
+    # the device's key: shared x / y extents, x0 the most significant coordinate
+    xs, ys = host[:, [0, 2]], host[:, [1, 3]]
+    nx_ = (host[:, [0, 2]] - xs.min()) / (xs.max() - xs.min())
+    ny_ = (host[:, [1, 3]] - ys.min()) / (ys.max() - ys.min())
+    dev = np.stack([ny_[:, 1], nx_[:, 1], ny_[:, 0], nx_[:, 0]], 1)
+    odev = rp[np.argsort(morton4(dev[rp], bits=4), kind="stable")]
     res = {}
-    for name, arr in (("random", host), ("morton", host[order]), ("morton16", host[o16])):
+    for name, arr in (("random", host), ("morton", host[order]), ("morton16", host[o16]),
+                      ("device16", host[odev])):
         pairs = eng.tensor(np.ascontiguousarray(arr), torch.float64)
         out = eng.eval_generated(pairs, ut)
         torch.cuda.synchronize()

@@ -3708,8 +3708,10 @@ __device__ __forceinline__ uint32_t pair_key(const double4 pr, const double* b) 
     const uint32_t c[4] = {q4(pr.x, b[0], ix), q4(pr.y, b[1], iy), q4(pr.z, b[0], ix),
                            q4(pr.w, b[1], iy)};
     uint32_t k = 0;
+    // yf, xf, y0, x0 from the most significant bit of each level: measured ~0.17 ms faster on
+    // cfg3 than x0 first (tools/probe_analytic_sort.py, "morton16" vs "device16")
     for (int b = 3; b >= 0; --b)
-        for (int d = 0; d < 4; ++d) k = (k << 1) | ((c[d] >> b) & 1u);
+        for (int d = 3; d >= 0; --d) k = (k << 1) | ((c[d] >> b) & 1u);
     return k;
 }
 
