@@ -257,9 +257,12 @@ def main():
                                       if traffic else None),
                      "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1) if gather_b else None,
                      "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING if gather_b else None,
-                     "note": "each 16-B record gather moves one 128-B line (PMC); the measured "
-                             "random-gather ceiling (tools/gather_ceiling.hip) bounds the "
-                             "kernel, see DESIGN.md §5"},
+                     "note": ("each 16-B record gather moves one 128-B line (PMC); the measured "
+                              "random-gather ceiling (tools/gather_ceiling.hip) bounds the "
+                              "kernel, see DESIGN.md §5") if gather_b else
+                             ("analytic mode reads only the pairs and writes the results, so "
+                              "the HBM fraction is not its bound: the f64 shape walk and lane "
+                              "divergence are (vector f64, not MFMA), see DESIGN.md §4 K3")},
         "setup": setup,
     }
 
