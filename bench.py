@@ -53,6 +53,8 @@ def parse():
                          "OMP_NUM_THREADS capped by the affinity mask and 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
+    ap.add_argument("--no-skip", action="store_true",
+                    help="K2 without the gather-skip summary (A/B; results are identical)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -153,6 +155,10 @@ def main():
             secs = udist.broadcast_raster(table, src=0)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = table.numel() * 4
+            if raster_mode and rank > 0:
+                eng.raster_summary(raster)   # each rank derives the skip table locally
+        if raster_mode and args.no_skip:
+            raster.summary = None
 
     # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
     if volume_mode:

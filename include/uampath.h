@@ -206,6 +206,26 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const double* utab_dev, int32_t D, const uam_path_outputs* out,
                        uam_stream stream);
 
+/* K2 gather skip (build-defined; no reference counterpart; results unchanged).  A bitmap
+ * summary of a record raster: one bit per block x block cells (blocks row-major, nby x nbx;
+ * bit b in 32-bit word b / 32), set when every cell of the block has phi == +-0,
+ * psi_nfz == +-0, no no-fly flag and a terrain <= 0 (dem, 0 on nodata cells; NaN clears it).
+ * K2 keeps the bitmap in LDS and does not gather the records of waypoints in set blocks (they
+ * add exactly nothing to cost, no-fly sum and hits); when a path skipped some and the terrain
+ * maximum of the rest is < 0, it fetches those too, so every output stays bit-identical to
+ * uam_eval_generated.  block: a power of two in [1, 1024] with at most 65536 blocks, or 0 =
+ * automatic (8, doubled until the blocks fit).  The bitmap holds ceil(nbx * nby / 32) words and
+ * must be rebuilt whenever rec changes. */
+int uam_raster_summary_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
+                             int32_t* nbx, int32_t* nby);
+int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
+                       int32_t block, uint32_t* summary_dev, uam_stream stream);
+/* uam_eval_generated in raster mode with the gather skip (summary_dev NULL = no skip). */
+int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
+                         const uint32_t* summary_dev, int32_t block, const double* pairs_dev,
+                         int64_t n_pairs, const double* utab_dev, int32_t D,
+                         const uam_path_outputs* out, uam_stream stream);
+
 /* K5: per group of G consecutive values, the reference's selection rule (main.py:175-180):
  * compare sqrt(v) when take_sqrt (fval = sqrt(cost), solver.py:48), else v. */
 int uam_argmin(uam_ctx* ctx, const double* values_dev, int64_t groups, int32_t G,
@@ -305,8 +325,8 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
  * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
  * UAM_TB_DBG (K2t diagnostics that change results: 1 skips the gathers, 2 the stores,
- * 4 pass 1), UAM_PAIR_ORDER=0 (analytic uam_eval_generated without the spatial pair order it
- * applies to batches of >= 4096 pairs).  None of them changes results except UAM_TB_DBG. */
+ * 4 pass 1), UAM_PAIR_ORDER=0 (uam_eval_generated without the spatial pair order it
+ * applies to batches of >= 4096 pairs; raster batches then also skip the XCD placement).  None of them changes results except UAM_TB_DBG. */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */

@@ -598,3 +598,96 @@ def test_generated_analytic_pair_order(oracle_mod, monkeypatch, order):
                                   oracle_mod.argmin(ref["cost"], D, True))
     np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
                                   oracle_mod.argmin(ref["length"], D, False))
+
+
+@pytest.mark.parametrize("order", ["1", "0"])
+@pytest.mark.parametrize("weights", ["canonical", "zero"])
+def test_raster_pair_order_and_gather_skip(oracle_mod, monkeypatch, order, weights):
+    """K2 (raster, lane per path) with the spatial pair order + XCD placement on and off
+    (UAM_PAIR_ORDER) and with the gather-skip bitmap at several block sizes and without it:
+    every output, the cells and the selection equal the oracle's bit for bit.  With all region
+    weights 0 and every land cell below sea level, Phi is +0 everywhere and almost every block
+    is skippable, so most paths take their maximum terrain from the fetch of the skipped
+    records (the gathered maximum is < 0)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    monkeypatch.setenv("UAM_PAIR_ORDER", order)
+    e2 = Engine(0)
+    spec = canonical_spec(nfz_polygons=16)
+    w = spec["weights"] if weights == "canonical" else [0.0] * len(spec["weights"])
+    orc = _setup(e2, oracle_mod, spec, 40, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], w, altitude=320.0)
+    R = 1024
+    geo = raster_geo(R)
+    dem = synthetic_dem(R)
+    if weights == "zero":
+        dem = np.where(dem == -9999.0, dem, -np.abs(dem) - 1.0).astype(np.float32)
+        dem[::97, ::89] = np.float32(np.nan)
+    raster = e2.raster_build(geo, dem, summary=False)
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                       geo.nodata, geo.dem_threshold)
+    rec = _np(raster.rec).view(np.float32)
+    D = 5
+    ut = arc_table(40, displacements(D))
+    pairs = random_pairs(4500, seed=12)
+    pairs[::97, 0] += 70.0            # some paths leave the raster
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec,
+                         want_cells=True)
+    skipped = []
+    for block in (None, 0, 4, 32):
+        if block is None:
+            raster.summary = None
+        else:
+            e2.raster_summary(raster, block)
+            nb = (-(-R // raster.block)) ** 2
+            bits = np.unpackbits(_np(raster.summary).view(np.uint8), bitorder="little")[:nb]
+            skipped.append(float(bits.mean()))
+        gpu = e2.eval_generated(pairs, ut, raster=raster, want_cells=True)
+        _assert_paths_equal(gpu, ref, raster=True)
+        np.testing.assert_array_equal(_np(gpu["cells"]), ref["cells"])
+        np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                      oracle_mod.argmin(ref["cost"], D, True))
+        np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
+                                      oracle_mod.argmin(ref["length"], D, False))
+    assert max(skipped) > (0.8 if weights == "zero" else 0.2), skipped
+    if weights == "zero":
+        assert (ref["min_clearance"] > 320.0).any()    # maxima below sea level occur
+
+
+def test_raster_summary_table(eng, oracle_mod):
+    """uam_raster_summary == its definition (numpy on the record raster): bit b set iff every
+    cell of block b has phi == +-0, psi == +-0, no NFZ flag and terrain <= 0 (0 on nodata
+    cells, NaN clears the bit); ragged edge blocks included; block sizes beyond the 65536-bit
+    LDS bitmap are refused."""
+    from uam_path_planning_amd.scenario import canonical_spec, raster_geo
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=8)
+    _setup(eng, oracle_mod, spec, 20, spec["options"], spec["maxratio"], spec["maxalpha"],
+           spec["enlargement"], spec["weights"])
+    geo = raster_geo(300)
+    geo.nx, geo.ny = 300, 260
+    dem = synthetic_dem(300)[:260].copy()
+    dem[5, 7] = np.float32(np.nan)
+    dem[200:204, 10:30] = np.float32(-3.0)
+    raster = eng.raster_build(geo, dem, summary=False)
+    rec = _np(raster.rec)
+    phi, psi = rec[..., 0].view(np.float32), rec[..., 1].view(np.float32)
+    terr = np.where(rec[..., 3] & 4, np.float32(0), rec[..., 2].view(np.float32))
+    ok = (phi == 0) & (psi == 0) & ((rec[..., 3] & 1) == 0) & (terr <= 0)   # NaN -> False
+    for block in (2, 4, 8, 32):
+        eng.raster_summary(raster, block)
+        nby, nbx = -(-260 // block), -(-300 // block)
+        want = np.array([[ok[by * block:(by + 1) * block, bx * block:(bx + 1) * block].all()
+                          for bx in range(nbx)] for by in range(nby)]).reshape(-1)
+        got = np.unpackbits(_np(raster.summary).view(np.uint8), bitorder="little")
+        assert got.size == 32 * (-(-want.size // 32))
+        np.testing.assert_array_equal(got[:want.size].astype(bool), want, err_msg=f"B{block}")
+        assert not got[want.size:].any()
+        assert want.any() and not want.all()
+    big = raster_geo(4096)
+    with pytest.raises(ValueError):
+        eng.raster_summary(type(raster)(big, None), 8)

@@ -130,6 +130,10 @@ struct KParams {
 struct KRaster {
     int32_t nx, ny;
     double x0, y_top, dx, dy, inv_dx, inv_dy;
+    // K2 gather skip (uam_raster_summary): bitmap of 2^sshift x 2^sshift cell blocks, snbx
+    // blocks per row, swords 32-bit words; null = gather every waypoint
+    const uint32_t* __restrict__ sum;
+    int32_t sshift, snbx, swords;
 };
 
 struct KVolume {
@@ -482,10 +486,129 @@ __device__ __forceinline__ void consume_chunk(const Chunk<C>& ch, int j0, int W,
     }
 }
 
+// ---- K2 gather skip (uam_raster_summary; build-defined, no reference counterpart) --------
+// A bitmap with one bit per B x B cell block, set when every cell of the block has phi == +-0,
+// psi == +-0, no no-fly flag and a terrain <= 0 (0 on nodata cells, as consume_chunk reads it;
+// NaN terrain clears the bit).  A waypoint in a set block adds exactly nothing to the cost and
+// no-fly sums (x + (+-0) == x for every accumulator, none of which is ever -0) and nothing to
+// nfz_hits, and its terrain cannot raise a path maximum that is >= 0.  K2 holds the bitmap in
+// LDS (<= 8 KiB), so the test costs no memory request; it gathers only the other waypoints and,
+// when it skipped some and the maximum it gathered is < 0 (or none), fetches the skipped
+// records too.  Every output is bit-identical to gathering every waypoint.
+constexpr int SKIP_MAX_BITS = 65536;  // 8 KiB of LDS
+
+// raster cell of a point (uampath.h convention: float64 floor of the scaled offset; -1 off the
+// raster) and whether its block's bit is set (false off the raster)
+__device__ __forceinline__ int32_t raster_cell_skip(const KRaster& rs, const uint32_t* bits,
+                                                   double x0, double x1, bool& skip) {
+    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+    skip = false;
+    if (!((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny))) return -1;
+    const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
+    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+    skip = (bits[b >> 5] >> (b & 31)) & 1u;
+    return iy * rs.nx + ix;
+}
+
+// Pass 2 of a raster path with the gather skip (bits: the bitmap in LDS); chunks of 8 gathers
+// in flight, consumed in waypoint order exactly as consume_chunk does.  (Compacting each chunk
+// to the lane's next 8 needed waypoints measured 3x slower: the per-slot forward scans
+// diverge.)
+template <bool GEN>
+__device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4* __restrict__ rec,
+                                                  const uint32_t* bits, const PathSrc<GEN>& src,
+                                                  int W, int32_t* cells, double dN, PathAcc& a) {
+    bool anyskip = false;
+    for (int j0 = 0; j0 < W; j0 += 8) {
+        uint4 r[8];
+        uint32_t inb = 0, need = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (j0 + t < W) {
+                double x0, x1;
+                src.at(j0 + t, x0, x1);
+                bool sk;
+                const int32_t cl = raster_cell_skip(rs, bits, x0, x1, sk);
+                if (cells) cells[j0 + t] = cl;
+                if (cl >= 0) {
+                    inb |= 1u << t;
+                    if (!sk) {
+                        need |= 1u << t;
+                        r[t] = rec[cl];
+                    }
+                }
+            }
+        }
+        anyskip = anyskip || (inb & ~need);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (j0 + t >= W) break;
+            if (!((inb >> t) & 1u)) {
+                ++a.off;
+                a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
+                continue;
+            }
+            if (!((need >> t) & 1u)) continue;  // adds +-0: an exact no-op
+            a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
+            a.nsum = a.nsum + (double)__uint_as_float(r[t].y);
+            a.nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+            const double terrain =
+                (r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r[t].z);
+            a.hmax = fmax(a.hmax, terrain);
+        }
+    }
+    if (anyskip && !(a.hmax >= 0.0)) {  // a skipped terrain (<= 0) may be the maximum
+        for (int j = 0; j < W; ++j) {
+            double x0, x1;
+            src.at(j, x0, x1);
+            bool sk;
+            const int32_t cl = raster_cell_skip(rs, bits, x0, x1, sk);
+            if (!sk) continue;
+            const uint4 r = rec[cl];
+            a.hmax = fmax(a.hmax, (r.w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r.z));
+        }
+    }
+}
+
+// one thread per B x B block (B = 2^shift, row-major blocks); bit b of word b / 32
+__global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict__ rec, int32_t nx,
+                                                        int32_t ny, int32_t shift, int32_t nbx,
+                                                        int32_t n_blocks,
+                                                        uint32_t* __restrict__ out) {
+    const int32_t blk = blockIdx.x * blockDim.x + threadIdx.x;
+    bool skip = false;
+    if (blk < n_blocks) {
+        const int B = 1 << shift;
+        const int bx = blk % nbx, by = blk / nbx;
+        const int x0 = bx << shift, y0 = by << shift;
+        const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+        skip = true;
+        for (int iy = y0; iy < y1 && skip; ++iy)
+            for (int ix = x0; ix < x1; ++ix) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                const float t = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+                if ((r.x & 0x7fffffffu) || (r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ) ||
+                    !(t <= 0.0f)) {
+                    skip = false;
+                    break;
+                }
+            }
+    }
+    const uint64_t m = __ballot(skip);
+    const int lane = threadIdx.x & 63;
+    const int32_t w = blk >> 5;  // lanes 0 and 32 write the wave's two words
+    if ((lane & 31) == 0 && blk < n_blocks)
+        out[w] = (uint32_t)(lane ? (m >> 32) : m);
+}
+
 // Records mode (internal, binned raster evaluation K2b): the waypoint's record was already
 // gathered into recs[path * W + j] (bit 31 of .w set = off the raster); the pass-2 sums are
 // eval_path's, so outputs are bit-identical to the gathering kernels.
 constexpr int MODE_RECORDS = 3;
+// Raster mode with the gather skip (internal; KRaster::sum set, raster_pass2_skip): its own
+// kernel instantiation, so the plain raster kernel keeps its register budget.
+constexpr int MODE_RASTER_SKIP = 4;
 constexpr uint32_t REC_OFF = 0x80000000u;
 
 template <int C>
@@ -621,7 +744,7 @@ template <int MODE, bool GEN, int C, bool PIPE>
 __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
                                              const KVolume& vs, const uint4* __restrict__ rec,
                                              const PathSrc<GEN>& src, int64_t path,
-                                             const KOut& out) {
+                                             const KOut& out, const uint32_t* sbits = nullptr) {
     const int N = p.N, W = N + 2;
     const int n_rows = 3 * N + g.n_obstacles * W;
     double* grow =
@@ -673,6 +796,9 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
             issue_chunk_rec<C>(rec, path * (int64_t)W, j0, W, ch);
             consume_chunk<C>(ch, j0, W, dN, a);
         }
+    } else if (MODE == MODE_RASTER_SKIP) {
+        raster_pass2_skip<GEN>(rs, rec, sbits, src, W, out.cells ? out.cells + path * W : nullptr,
+                               dN, a);
     } else {
         int32_t* cells = out.cells ? out.cells + path * W : nullptr;
         if (!PIPE) {
@@ -701,7 +827,8 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
 // raster: cruise altitude - highest terrain under the waypoints; volume: min over waypoints of
 // (waypoint altitude - terrain of its column); analytic: NaN (no DEM)
 __device__ __forceinline__ double clearance(const KParams& p, int mode, const PathAcc& a) {
-    return (mode == UAM_MODE_RASTER || mode == MODE_RECORDS) ? p.altitude - a.hmax
+    return (mode == UAM_MODE_RASTER || mode == MODE_RECORDS || mode == MODE_RASTER_SKIP)
+               ? p.altitude - a.hmax
                                    : (mode == UAM_MODE_VOLUME ? a.cmin : (double)NAN);
 }
 
@@ -781,6 +908,13 @@ __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRas
     write_path(out, p, MODE, q * D + d, a);
 }
 
+// Ordered chunk evaluated by workgroup b of nb: XCD x = b % 8 owns the contiguous chunk range
+// [x * (nb / 8) + min(x, nb % 8), ...) and walks it in dispatch order (a bijection on [0, nb)).
+__device__ __forceinline__ int64_t xcd_chunk(int64_t b, int64_t nb) {
+    const int64_t x = b & 7, k = b >> 3;
+    return x * (nb >> 3) + (x < (nb & 7) ? x : (nb & 7)) + k;
+}
+
 // Variant 2+: one workgroup = one block of 64 pairs x all D displacements (wave = d,
 // lane = pair).  Results are staged in LDS and written with unit-stride (coalesced) stores
 // over the block's contiguous path range [b*64*D, (b+1)*64*D); the candidate selection
@@ -807,14 +941,22 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     int32_t* s_nh = reinterpret_cast<int32_t*>(s_clr + BP);
     int32_t* s_off = s_nh + BP;
     int32_t* s_bel = s_off + BP;
+    uint32_t* s_bits = reinterpret_cast<uint32_t*>(s_bel + BP);  // gather-skip bitmap
+    if (MODE == MODE_RASTER_SKIP) {
+        for (int i = threadIdx.x; i < rs.swords; i += blockDim.x) s_bits[i] = rs.sum[i];
+        __syncthreads();
+    }
 
     const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int64_t q0 = (int64_t)blockIdx.x * 64;
-    // order (optional): block slot -> pair, a spatial order of the pairs (pair_order); every
-    // pair is still read and written at its own index, so results do not depend on it
+    // order (optional): slot -> pair, a spatial order of the pairs (pair_order).  Block b takes
+    // the ordered chunk xcd_chunk(b): workgroups are dispatched round-robin over the 8 XCDs,
+    // so the chunks of XCD b % 8 form one contiguous range of the order and the paths sharing
+    // an XCD's L2 are spatial neighbours.  Every pair is still read and written at its own
+    // index, so results do not depend on the order.
+    const bool ordered = order != nullptr;
+    const int64_t q0 = 64 * (ordered ? xcd_chunk(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
     const bool in = q0 + lane < n_pairs;
-    const bool ordered = MODE == UAM_MODE_ANALYTIC && order;  // compiled out elsewhere
     const int64_t q = (ordered && in) ? (int64_t)order[q0 + lane] : q0 + lane;
     const int slot = d * 64 + lane;
     if (in) {
@@ -832,7 +974,7 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         }
         src.u = utab + (int64_t)d * p.N * 2;
         const PathAcc a =
-            eval_path<MODE, true, C, PIPE>(g, p, rs, vs, rec, src, q * D + d, out);
+            eval_path<MODE, true, C, PIPE>(g, p, rs, vs, rec, src, q * D + d, out, s_bits);
         s_cost[slot] = a.cost;
         s_L[slot] = a.L;
         s_len[slot] = a.len;
@@ -844,25 +986,12 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         s_bel[slot] = a.below;
     }
     __syncthreads();
-    if (ordered) {  // scattered pairs: each lane stores its own path
-        if (in) {
-            const int64_t gp = q * D + d;
-            if (out.cost) out.cost[gp] = s_cost[slot];
-            if (out.length_q) out.length_q[gp] = s_L[slot];
-            if (out.length) out.length[gp] = s_len[slot];
-            if (out.kin_sum) out.kin_sum[gp] = s_k[slot];
-            if (out.nfz_sum) out.nfz_sum[gp] = s_n[slot];
-            if (out.min_clearance) out.min_clearance[gp] = s_clr[slot];
-            if (out.nfz_hits) out.nfz_hits[gp] = s_nh[slot];
-            if (out.offmap) out.offmap[gp] = s_off[slot];
-            if (out.below_terrain) out.below_terrain[gp] = s_bel[slot];
-        }
-    } else {
-    // coalesced stores: thread t -> block-local path t = (pair t / D, displacement t % D)
+    // stores staged through LDS: thread t -> block-local path (pair t / D, displacement t % D),
+    // so the D paths of a pair are D consecutive threads and D consecutive addresses
     const int t = threadIdx.x;
     const int qi = t / D, di = t - qi * D;
-    const int64_t gp = q0 * D + t;
     if (q0 + qi < n_pairs) {
+        const int64_t gp = (ordered ? (int64_t)order[q0 + qi] : q0 + qi) * D + di;
         const int s = di * 64 + qi;
         if (out.cost) out.cost[gp] = s_cost[s];
         if (out.length_q) out.length_q[gp] = s_L[s];
@@ -873,7 +1002,6 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         if (out.nfz_hits) out.nfz_hits[gp] = s_nh[s];
         if (out.offmap) out.offmap[gp] = s_off[s];
         if (out.below_terrain) out.below_terrain[gp] = s_bel[s];
-    }
     }
     if (d == 0 && in) {
         if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
@@ -3780,6 +3908,97 @@ __global__ __launch_bounds__(256) void k_pair_scatter(const uint16_t* __restrict
     order[atomicAdd(&next[key[i]], 1)] = (int32_t)i;
 }
 
+// Raster pair order (K2).  Only which pairs share an XCD's L2 (and the dispatch order within
+// it) matters, so a coarse key suffices: 2 bits of each of (yf, xf, y0, x0) over the raster
+// extent, interleaved from the top bit into an 8-bit key (256 bins).  A counting sort without
+// global atomics in two launches over RORD_NB fixed partitions of the pairs: (1) keys and a
+// per-partition LDS histogram, stored bin-major; (2) every partition scans the 256 x RORD_NB
+// counts (thread t owns bin t across all partitions) and scatters its pairs through LDS cursors.
+// cfg3: the order takes the raster kernel from 0.765 to 0.718 ms (profiles/r02).
+#ifndef UAM_RORD_BITS
+#define UAM_RORD_BITS 2
+#endif
+constexpr int RORD_BITS = UAM_RORD_BITS, RORD_BINS = 1 << (4 * RORD_BITS);
+constexpr int RORD_BPT = RORD_BINS / 256;          // bins per thread of the order kernels
+constexpr int RORD_NB = RORD_BPT > 1 ? 16 : 64;    // partitions of the pairs
+static_assert(RORD_BINS >= 256, "at least one bin per thread");
+
+struct KOrdBox {
+    double x0, y0, ix, iy;  // lower corner, 2^RORD_BITS / extent
+};
+
+__device__ __forceinline__ uint32_t rorder_key(const double4 pr, const KOrdBox& b) {
+    auto q = [](double v, double lo, double inv) {
+        const double t = (v - lo) * inv;
+        constexpr double m = (double)((1 << RORD_BITS) - 1);
+        return (uint32_t)(t > 0.0 ? (t < m ? t : m) : 0.0);  // NaN -> 0
+    };
+    const uint32_t c[4] = {q(pr.x, b.x0, b.ix), q(pr.y, b.y0, b.iy), q(pr.z, b.x0, b.ix),
+                           q(pr.w, b.y0, b.iy)};
+    uint32_t k = 0;
+    for (int l = RORD_BITS - 1; l >= 0; --l)
+        for (int d = 3; d >= 0; --d) k = (k << 1) | ((c[d] >> l) & 1u);
+    return k;
+}
+
+__global__ __launch_bounds__(256) void k_rorder_hist(const double* __restrict__ pairs, int64_t n,
+                                                     KOrdBox box, uint16_t* __restrict__ key,
+                                                     int32_t* __restrict__ H) {
+    __shared__ int32_t h[RORD_BINS];
+    const int t = threadIdx.x, blk = blockIdx.x;
+    for (int b = t; b < RORD_BINS; b += 256) h[b] = 0;
+    __syncthreads();
+    const int64_t lo = n * blk / RORD_NB, hi = n * (blk + 1) / RORD_NB;
+    for (int64_t i = lo + t; i < hi; i += 256) {
+        const uint32_t k = rorder_key(reinterpret_cast<const double4*>(pairs)[i], box);
+        key[i] = (uint16_t)k;
+        atomicAdd(&h[k], 1);
+    }
+    __syncthreads();
+    for (int b = t; b < RORD_BINS; b += 256) H[b * RORD_NB + blk] = h[b];
+}
+
+__global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restrict__ key, int64_t n,
+                                                        const int32_t* __restrict__ H,
+                                                        int32_t* __restrict__ order) {
+    __shared__ int32_t part[256];
+    __shared__ int32_t off[RORD_BINS];
+    const int t = threadIdx.x, blk = blockIdx.x;
+    // thread t owns bins [t * BPT, (t + 1) * BPT), each across all partitions
+    const int4* h4 = reinterpret_cast<const int4*>(H + (int64_t)t * RORD_BPT * RORD_NB);
+    int32_t tot = 0;
+    int32_t pre[RORD_BPT], mine[RORD_BPT];
+#pragma unroll
+    for (int bb = 0; bb < RORD_BPT; ++bb) {
+        int32_t bt = 0, bm = 0;
+#pragma unroll
+        for (int k = 0; k < RORD_NB / 4; ++k) {
+            const int4 v = h4[bb * (RORD_NB / 4) + k];
+            const int b = 4 * k;
+            bm += (b < blk ? v.x : 0) + (b + 1 < blk ? v.y : 0) + (b + 2 < blk ? v.z : 0) +
+                  (b + 3 < blk ? v.w : 0);
+            bt += v.x + v.y + v.z + v.w;
+        }
+        pre[bb] = tot;
+        mine[bb] = bm;
+        tot += bt;
+    }
+    part[t] = tot;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan of the thread totals
+        const int32_t x = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int bb = 0; bb < RORD_BPT; ++bb)
+        off[t * RORD_BPT + bb] = part[t] - tot + pre[bb] + mine[bb];
+    __syncthreads();
+    const int64_t lo = n * blk / RORD_NB, hi = n * (blk + 1) / RORD_NB;
+    for (int64_t i = lo + t; i < hi; i += 256) order[atomicAdd(&off[key[i]], 1)] = (int32_t)i;
+}
+
 }  // namespace
 
 namespace {
@@ -3818,6 +4037,9 @@ struct uam_ctx {
     bool pair_order = true;     // K3: evaluate pairs in a spatial order (UAM_PAIR_ORDER=0: off)
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
+    hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
+                                  // another stream waits for it before rewriting the scratch
+    bool ord_pending = false;
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
 };
 
@@ -3920,7 +4142,9 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->ev_ord) (void)hipEventSynchronize(ctx->ev_ord);
     if (ctx->d_ord) (void)hipFree(ctx->d_ord);
+    if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
@@ -4331,6 +4555,32 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
 
 // K3 pair order (k_pair_keys / k_pair_scan / k_pair_scatter) into the context's scratch; *order
 // stays null when the geometry has no shape grid (nothing to gain)
+// The pair-order scratch (ctx->d_ord, grow-only) on stream s: waits for the last launch that
+// read it (possibly on another stream), so two streams sharing a context cannot overwrite each
+// other's order; the caller records ctx->ev_ord after the launch that reads the order.
+static int order_scratch(uam_ctx* ctx, size_t need, hipStream_t s, char** w) {
+    if (!ctx->ev_ord) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_ord, hipEventDisableTiming));
+    if (ctx->ord_pending) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_ord, 0));
+    if (need > ctx->ord_bytes) {
+        if (ctx->d_ord) {
+            HIP_TRY(hipEventSynchronize(ctx->ev_ord));
+            (void)hipFree(ctx->d_ord);
+        }
+        ctx->d_ord = nullptr;
+        ctx->ord_bytes = 0;
+        if (hipMalloc(&ctx->d_ord, need) != hipSuccess) return fail(UAM_E_NOMEM, "pair order");
+        ctx->ord_bytes = need;
+    }
+    *w = (char*)ctx->d_ord;
+    return UAM_OK;
+}
+
+static int order_done(uam_ctx* ctx, hipStream_t s) {
+    HIP_TRY(hipEventRecord(ctx->ev_ord, s));
+    ctx->ord_pending = true;
+    return UAM_OK;
+}
+
 static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t s,
                       const int32_t** order) {
     *order = nullptr;
@@ -4340,15 +4590,9 @@ static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t 
     // [hist 65536 | max bounds 2 x u64] zeroed together, then min bounds 2 x u64 (all ones)
     const size_t b_hist = al(65536 * 4 + 16 + 16), b_key = al((size_t)n * 2),
                  b_ord = al((size_t)n * 4);
-    const size_t need = b_hist + b_key + b_ord;
-    if (need > ctx->ord_bytes) {
-        if (ctx->d_ord) (void)hipFree(ctx->d_ord);
-        ctx->d_ord = nullptr;
-        ctx->ord_bytes = 0;
-        if (hipMalloc(&ctx->d_ord, need) != hipSuccess) return fail(UAM_E_NOMEM, "pair order");
-        ctx->ord_bytes = need;
-    }
-    char* w = (char*)ctx->d_ord;
+    char* w = nullptr;
+    const int st = order_scratch(ctx, b_hist + b_key + b_ord, s, &w);
+    if (st) return st;
     int32_t* hist = (int32_t*)w;
     uint16_t* key = (uint16_t*)(w + b_hist);
     int32_t* ord = (int32_t*)(w + b_hist + b_key);
@@ -4361,6 +4605,30 @@ static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t 
                        hist);
     hipLaunchKernelGGL(k_pair_scan, dim3(1), dim3(1024), 0, s, hist);
     hipLaunchKernelGGL(k_pair_scatter, gr, b, 0, s, (const uint16_t*)key, n, hist, ord);
+    HIP_TRY(hipGetLastError());
+    *order = ord;
+    return UAM_OK;
+}
+
+// K2 pair order over the raster extent (k_rorder_hist / k_rorder_scatter)
+static int raster_pair_order(uam_ctx* ctx, const KRaster& kr, const double* pairs, int64_t n,
+                             hipStream_t s, const int32_t** order) {
+    *order = nullptr;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_h = al((size_t)RORD_BINS * RORD_NB * 4), b_key = al((size_t)n * 2),
+                 b_ord = al((size_t)n * 4);
+    char* w = nullptr;
+    const int st = order_scratch(ctx, b_h + b_key + b_ord, s, &w);
+    if (st) return st;
+    int32_t* H = (int32_t*)w;
+    uint16_t* key = (uint16_t*)(w + b_h);
+    int32_t* ord = (int32_t*)(w + b_h + b_key);
+    const double ex = kr.nx * kr.dx, ey = kr.ny * kr.dy;
+    const KOrdBox box{kr.x0, kr.y_top - ey, (double)(1 << RORD_BITS) / ex,
+                      (double)(1 << RORD_BITS) / ey};
+    hipLaunchKernelGGL(k_rorder_hist, dim3(RORD_NB), dim3(256), 0, s, pairs, n, box, key, H);
+    hipLaunchKernelGGL(k_rorder_scatter, dim3(RORD_NB), dim3(256), 0, s, (const uint16_t*)key, n,
+                       (const int32_t*)H, ord);
     HIP_TRY(hipGetLastError());
     *order = ord;
     return UAM_OK;
@@ -4510,10 +4778,33 @@ static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const 
     return 1;
 }
 
-int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
-                       const void* rec, const double* pairs, int64_t n_pairs,
-                       const double* utab, int32_t D, const uam_path_outputs* out,
-                       uam_stream stream) {
+} // extern "C"
+
+static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shift,
+                        int32_t* nbx, int32_t* nby) {
+    if (!desc || desc->nx <= 0 || desc->ny <= 0) return fail(UAM_E_INVALID, "bad raster desc");
+    auto nblocks = [&](int64_t b) { return ((desc->nx + b - 1) / b) * ((desc->ny + b - 1) / b); };
+    if (block == 0) {  // automatic: 8, doubled until the bitmap fits its 8 KiB of LDS
+        block = 8;
+        while (nblocks(block) > SKIP_MAX_BITS && block < 1024) block *= 2;
+    }
+    int sh = 0;
+    while ((1 << sh) < block) ++sh;
+    if ((1 << sh) != block || block < 1 || block > 1024)
+        return fail(UAM_E_INVALID, "summary block %d is not a power of two in [1, 1024]", block);
+    if (nblocks(block) > SKIP_MAX_BITS)
+        return fail(UAM_E_INVALID, "summary block %d: %lld blocks exceed the %d-bit LDS bitmap",
+                    block, (long long)nblocks(block), SKIP_MAX_BITS);
+    *shift = sh;
+    *nbx = (desc->nx + block - 1) / block;
+    *nby = (desc->ny + block - 1) / block;
+    return UAM_OK;
+}
+
+static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                          const void* rec, const uint32_t* summary, int32_t sblock,
+                          const double* pairs, int64_t n_pairs, const double* utab, int32_t D,
+                          const uam_path_outputs* out, uam_stream stream) {
     int st = check_ctx(ctx, true);
     if (st) return st;
     if (n_pairs < 0 || D < 1) return fail(UAM_E_INVALID, "n_pairs < 0 or D < 1");
@@ -4524,6 +4815,15 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
         st = make_kraster(desc, &kr);
         if (st) return st;
         if (!rec) return fail(UAM_E_INVALID, "raster mode needs rec");
+        if (summary) {
+            int32_t sh, nbx, nby;
+            st = summary_dims(desc, sblock, &sh, &nbx, &nby);
+            if (st) return st;
+            kr.sum = summary;
+            kr.sshift = sh;
+            kr.snbx = nbx;
+            kr.swords = (nbx * nby + 31) / 32;
+        }
     } else if (mode != UAM_MODE_ANALYTIC) {
         return fail(UAM_E_INVALID, "unknown mode %d", mode);
     }
@@ -4579,11 +4879,13 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const dim3 grid((unsigned)blocks), block(64 * D);
-    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t)) +
+                       (kr.sum ? (size_t)kr.swords * 4 : 0);
     const KVolume kv{};
     const int32_t* order = nullptr;
-    if (mode == UAM_MODE_ANALYTIC && ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
-        st = pair_order(ctx, pairs, n_pairs, s, &order);
+    if (ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
+        st = mode == UAM_MODE_ANALYTIC ? pair_order(ctx, pairs, n_pairs, s, &order)
+                                       : raster_pair_order(ctx, kr, pairs, n_pairs, s, &order);
         if (st) return st;
     }
 #define UAM_LAUNCH_PAIRS(MODE_, C_, PIPE_, MINW_)                                          \
@@ -4593,7 +4895,9 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     if (mode == UAM_MODE_ANALYTIC) {
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
-        switch (v) {
+        if (kr.sum) {
+            UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, 8, false, 5);  // occupancy 5 (6 spilled)
+        } else switch (v) {
             case 2: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 1); break;
             case 3: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 1); break;
             case 4: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, true, 1); break;
@@ -4604,6 +4908,54 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
         }
     }
 #undef UAM_LAUNCH_PAIRS
+    HIP_TRY(hipGetLastError());
+    if (order) return order_done(ctx, s);
+    return UAM_OK;
+}
+
+extern "C" {
+
+int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
+                       const void* rec, const double* pairs, int64_t n_pairs,
+                       const double* utab, int32_t D, const uam_path_outputs* out,
+                       uam_stream stream) {
+    return eval_generated(ctx, mode, desc, rec, nullptr, 0, pairs, n_pairs, utab, D, out, stream);
+}
+
+int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
+                         const uint32_t* summary, int32_t block, const double* pairs,
+                         int64_t n_pairs, const double* utab, int32_t D,
+                         const uam_path_outputs* out, uam_stream stream) {
+    return eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs, n_pairs, utab,
+                          D, out, stream);
+}
+
+int uam_raster_summary_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
+                             int32_t* nbx, int32_t* nby) {
+    int32_t sh, bx, by;
+    const int st = summary_dims(desc, block, &sh, &bx, &by);
+    if (st) return st;
+    if (block_out) *block_out = 1 << sh;
+    if (nbx) *nbx = bx;
+    if (nby) *nby = by;
+    return UAM_OK;
+}
+
+int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
+                       int32_t block, uint32_t* summary, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    KRaster kr{};
+    int st = make_kraster(desc, &kr);
+    if (st) return st;
+    if (!rec || !summary) return fail(UAM_E_INVALID, "rec/summary is NULL");
+    int32_t sh, nbx, nby;
+    st = summary_dims(desc, block, &sh, &nbx, &nby);
+    if (st) return st;
+    DeviceGuard dg(ctx->device);
+    const int32_t nb = nbx * nby;
+    hipLaunchKernelGGL(k_raster_summary, dim3(grid_for(nb, 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint4*)rec, kr.nx, kr.ny, sh, nbx, nb,
+                       summary);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }

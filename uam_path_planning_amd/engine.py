@@ -75,9 +75,14 @@ class RasterGeo:
 
 @dataclass
 class CostRaster:
-    """Device record raster: rec [ny, nx, 4] int32 view of {phi f32, psi f32, dem f32, flags}."""
+    """Device record raster: rec [ny, nx, 4] int32 view of {phi f32, psi f32, dem f32, flags};
+    summary: the K2 gather-skip bitmap of rec (uam_raster_summary, one bit per block x block
+    cells; None = K2 gathers every waypoint).  Rebuild it (Engine.raster_summary) after rec
+    changes."""
     geo: RasterGeo
     rec: object = field(repr=False)
+    summary: object = field(default=None, repr=False)
+    block: int = 0
 
     @property
     def nbytes(self):
@@ -111,6 +116,18 @@ class RiskVolume:
 
 def _ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _check_outputs(o, P, Q, W):
+    """Caller-supplied outputs (Engine.outputs) must hold this batch: the kernels write P paths
+    and Q best indices, so a smaller buffer set would be overrun."""
+    for k, t in o.items():
+        need = P * W if k == "cells" else (Q if k.startswith("best_") else P)
+        if k == "g_rows":
+            continue
+        if t.numel() < need:
+            raise ValueError(f"outputs[{k!r}] holds {t.numel()} entries, this batch needs {need}"
+                             f" ({P} paths, {Q} pairs): allocate with Engine.outputs")
 
 
 # refinement defaults (same as oracle.refine_params)
@@ -205,13 +222,30 @@ class Engine:
         return out
 
     # -- raster ---------------------------------------------------------------------------
-    def raster_build(self, geo, dem=None, out=None):
+    def raster_build(self, geo, dem=None, out=None, summary=True):
+        """K1 record raster (+ its K2 gather-skip summary unless summary=False)."""
         torch = _torch()
         d = None if dem is None else self.tensor(dem, torch.float32).reshape(geo.ny, geo.nx)
         rec = out if out is not None else self.empty((geo.ny, geo.nx, 4), torch.int32)
         _lib.check(self.lib.uam_raster_build(self._ctx, ctypes.byref(geo.as_struct()), _ptr(d),
                                              _ptr(rec), self.stream), "uam_raster_build")
-        return CostRaster(geo, rec)
+        r = CostRaster(geo, rec)
+        return self.raster_summary(r) if summary else r
+
+    def raster_summary(self, raster, block=0):
+        """(Re)build raster.summary from raster.rec (block 0 = automatic); returns raster."""
+        torch = _torch()
+        g = raster.geo.as_struct()
+        b, nbx, nby = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.uam_raster_summary_shape(ctypes.byref(g), int(block), ctypes.byref(b),
+                                                     ctypes.byref(nbx), ctypes.byref(nby)),
+                   "uam_raster_summary_shape")
+        sm = self.empty(((nby.value * nbx.value + 31) // 32,), torch.int32)
+        _lib.check(self.lib.uam_raster_summary(self._ctx, ctypes.byref(g), _ptr(raster.rec),
+                                               b.value, _ptr(sm), self.stream),
+                   "uam_raster_summary")
+        raster.summary, raster.block = sm, b.value
+        return raster
 
     def dem_mosaic(self, tiles, xoff, yoff, nx, ny, fill=-9999.0, dem=None):
         torch = _torch()
@@ -284,7 +318,13 @@ class Engine:
                                  want_cells and raster is not None, False, n_pairs=Q)
         else:
             o, s = outputs
+            _check_outputs(o, Q * D, Q, self.params.N + 2)
         geo = None if raster is None else ctypes.byref(raster.geo.as_struct())
+        if raster is not None and raster.summary is not None:
+            _lib.check(self.lib.uam_eval_generated_s(
+                self._ctx, geo, _ptr(raster.rec), _ptr(raster.summary), int(raster.block),
+                _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated_s")
+            return o
         _lib.check(self.lib.uam_eval_generated(
             self._ctx, self._mode(raster), geo, _ptr(None if raster is None else raster.rec),
             _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated")
@@ -313,8 +353,12 @@ class Engine:
         if ut.shape[1] != self.params.N:
             raise ValueError(f"arc table has N={ut.shape[1]}, params N={self.params.N}")
         Q = pr.shape[0]
-        o, s = outputs if outputs is not None else self._outputs(
-            Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False, n_pairs=Q)
+        if outputs is not None:
+            o, s = outputs
+            _check_outputs(o, Q * D, Q, self.params.N + 2)
+        else:
+            o, s = self._outputs(Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False,
+                                 n_pairs=Q)
         _lib.check(self.lib.uam_eval_generated3d(
             self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.vox), _ptr(pr), Q,
             _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated3d")
