@@ -2,27 +2,41 @@
 """Headline benchmark: candidate-paths/s (+ waypoint-evals/s) of the batched candidate-path
 cost evaluation on an R x R DEM cost raster (BASELINE.json metric), MI355X.
 
-One "step" = one pass of the hot path over the batch resident in HBM: the fused kernel
-(arc generator K4 + raster gather / cost reduction K2) over every pair x displacement, then
-the reference's candidate selection (argmin on fval and on length, K5).  Default workload:
-BASELINE config 3 (4096^2 DEM + 69 no-fly shapes, 100k start/goal pairs x 5 displacements =
-500k paths x 82 waypoints per GPU; weak scaling: every rank gets its own 100k pairs).
+One "step" = one pass of the hot path over the batch resident in HBM: the spatial pair order
+(K2o) and the fused kernel (arc generator K4 + raster gather / cost reduction K2) over every
+pair x displacement, with the reference's candidate selection (argmin on fval and on length,
+K5) fused in.  Workloads (--workload; BASELINE.json configs):
+
+  cfg3 (default)  4096^2 DEM + 70 no-fly shapes, 100k start/goal pairs x 5 displacements =
+                  500k paths x 82 waypoints PER GPU (weak scaling: every rank its own 100k
+                  pairs).  The config the north_star target is quoted on.
+  cfg4            8192^2 DEM written as 225 x 150 GeoTIFF tiles (mergeLL.vrt layout) and
+                  ingested on rank 0, 1M paths TOTAL sharded over the GPUs (strong scaling).
+  cfg5            1024 x 1024 x 64 risk volume, 100k pairs per GPU (weak scaling).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
-per GPU, RCCL; rank 0 builds the cost raster (K1) and broadcasts it once over xGMI (timed
-separately, outside the step); pairs are sharded with no collective in the hot loop.
+per GPU.  Rank 0 builds the cost raster (K1) and broadcasts it once with libuampath's RCCL
+broadcast over xGMI (uam_bcast_raster; timed separately, outside the step); each rank derives
+the gather-skip bitmap locally; pairs are sharded with no collective in the hot loop.  Every
+rank checks the first pairs of its shard bit for bit against the CPU oracle; the mismatch
+counts are summed over ranks into the line's "parity".
 
-Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline (algorithmic bytes
-/ HIP-event kernel time vs 8 TB/s HBM) and a CPU baseline: the C oracle (oracle/, a "port")
-timed on this host on a bounded sample of the same workload -- one thread first (which
-doubles as a bit-exact parity check of the GPU outputs on that sample), then the sample over
-the host's CPU share in contiguous pair shards; `cores` is that thread count.
+Prints ONE JSON line (rank 0).  roofline: algorithmic bytes per launch of the dominant kernel
+(16 B per waypoint gather + 16 B of outputs per path = 16 W + 16 B/path) / its
+HIP-event time vs 8 TB/s; "traffic" = the PMC-measured L2->fabric bytes per launch of the same
+kernel (profiles/traffic.json, written by tools/pmc_traffic.py from the rocprofv3 passes of
+this build; they include Infinity-Cache hits).  cpu_baseline: the C oracle (oracle/, a "port")
+timed on this host on a bounded sample of the same workload -- one thread first (which doubles
+as the bit-exact parity check on that sample), then the sample over the host's CPU share in
+contiguous pair shards; `cores` is that thread count.
 """
 import argparse
 import concurrent.futures
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,6 +49,7 @@ METRIC = "candidate-paths/sec + waypoint-evals/sec on N×N DEM at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # independent random 16-B gathers from a 256 MiB table, one MI355X (profiles/r01/gather_ceiling.log)
 RANDOM_GATHER_CEILING = 55.5e9
+PARITY_PAIRS_PER_RANK = 200   # oracle check of every rank's first pairs at N > 1
 
 
 def parse():
@@ -42,10 +57,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--workload", default="cfg3", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--mode", default=None, choices=["raster", "analytic", "volume"],
                     help="default: the workload's mode (raster; volume for cfg5)")
-    ap.add_argument("--pairs", type=int, default=None, help="override pairs per GPU")
+    ap.add_argument("--pairs", type=int, default=None,
+                    help="override the pair count (per GPU, or in total for cfg4)")
     ap.add_argument("--R", type=int, default=None, help="override raster size")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -54,9 +70,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
     ap.add_argument("--no-skip", action="store_true",
-                    help="K2 without the gather-skip summary (A/B; results are identical)")
+                    help="K2 without the gather-skip bitmap (A/B; results are identical)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+                    help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
@@ -70,10 +86,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # one GPU per rank; UAM_BENCH_RANKS_PER_GPU > 1 packs ranks onto fewer GPUs (rehearsal of
+    # one GPU per rank; UAM_BENCH_RANKS_PER_GPU > 1 packs ranks onto fewer GPUs (a rehearsal of
     # the N-rank path on a 1-GPU box, with UAM_DIST_BACKEND=gloo since RCCL needs a GPU per
-    # rank)
+    # rank).  n_gpus always reports physical GPUs.
     per_gpu = max(1, int(os.environ.get("UAM_BENCH_RANKS_PER_GPU", "1")))
+    n_gpus = max(1, world // per_gpu)
     backend = None
     local = local // per_gpu
     if world > 1:
@@ -103,12 +120,14 @@ def main():
         cfg["pairs"] = args.pairs
     if args.R:
         cfg["R"] = args.R
-    R, Q, D, N = cfg["R"], cfg["pairs"], cfg["D"], cfg["N"]
+    R, D, N = cfg["R"], cfg["D"], cfg["N"]
     W = N + 2
     mode = args.mode or cfg["mode"]
     args.mode = mode
     raster_mode = mode == "raster"
     volume_mode = mode == "volume"
+    strong = args.workload == "cfg4"      # 1M paths in total, sharded over the GPUs
+    Q_total = cfg["pairs"] if strong else cfg["pairs"] * world
 
     spec = canonical_spec(nfz_polygons=cfg["nfz_polygons"])
     geom = compile_map(build_region_map(spec))
@@ -120,9 +139,14 @@ def main():
 
     # ---- cost raster / volume: rank 0 builds (K1), one RCCL broadcast --------------------
     setup = {}
+    rccl = world > 1 and backend == "nccl" and per_gpu == 1
     if world > 1:
         setup["dist_backend"] = backend
         setup["ranks_per_gpu"] = per_gpu
+        setup["raster_broadcast"] = ("uam_bcast_raster (RCCL, libuampath C-ABI)" if rccl else
+                                     "torch.distributed.broadcast (rehearsal: ranks share a GPU)")
+        if rccl:
+            udist.init_raster_comm(eng)
     geo = raster_geo(R)
     raster = volume = None
     if raster_mode or volume_mode:
@@ -130,10 +154,29 @@ def main():
         if rank == 0:
             dem = synthetic_dem(R)
             setup["dem_gen_s"] = round(time.perf_counter() - t0, 3)
-            dem_dev = eng.tensor(dem, torch.float32)
+            if args.workload == "cfg4":
+                # the config's "real GeoTIFF DEM": the DEM as 225 x 150 Float32 GeoTIFF tiles +
+                # VRT in the mergeLL.vrt layout, read back through DataManager (device mosaic)
+                from uam_path_planning_amd.map_generation import DataManager, write_tiled_dem
+                tdir = tempfile.mkdtemp(prefix="uam_tiles_")
+                try:
+                    t1 = time.perf_counter()
+                    vrt = write_tiled_dem(dem, (geo.x0, geo.dx, 0.0, geo.y_top, 0.0, -geo.dy),
+                                          tdir)
+                    setup["tiles_written_s"] = round(time.perf_counter() - t1, 3)
+                    t1 = time.perf_counter()
+                    dem_dev, g2 = DataManager(eng).load_dem(vrt)
+                    torch.cuda.synchronize()
+                    setup["tiles_ingest_s"] = round(time.perf_counter() - t1, 3)
+                    setup["tiles"] = len(os.listdir(tdir)) - 1
+                    geo = g2
+                finally:
+                    shutil.rmtree(tdir, ignore_errors=True)
+            else:
+                dem_dev = eng.tensor(dem, torch.float32)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            raster = eng.raster_build(geo, dem_dev)
+            raster = eng.raster_build(geo, dem_dev, summary=False)
             torch.cuda.synchronize()
             setup["raster_build_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
             if volume_mode:
@@ -152,19 +195,26 @@ def main():
         if world > 1:
             dist.barrier()
             table = volume.vox if volume_mode else raster.rec
-            secs = udist.broadcast_raster(table, src=0)
+            secs = udist.broadcast_raster(table, src=0, engine=eng if rccl else None)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = table.numel() * 4
-            if raster_mode and rank > 0:
-                eng.raster_summary(raster)   # each rank derives the skip table locally
-        if raster_mode and args.no_skip:
-            raster.summary = None
+        if raster_mode and not args.no_skip:
+            t1 = time.perf_counter()
+            eng.raster_summary(raster)         # every rank derives the skip bitmap locally
+            torch.cuda.synchronize()
+            setup["skip_bitmap_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+            setup["skip_block"] = raster.block
 
-    # ---- this rank's shard of pairs (weak scaling) -----------------------------------------
-    if volume_mode:
-        pairs_host = udist.weak_shard(random_pairs3d(Q * world, seed=0), Q, rank, world)
+    # ---- this rank's shard of pairs ------------------------------------------------------
+    gen = random_pairs3d if volume_mode else random_pairs
+    all_pairs = gen(Q_total, seed=0)
+    if strong:
+        lo, hi = udist.shard_range(Q_total, rank, world)
+        pairs_host = all_pairs[lo:hi]
     else:
-        pairs_host = udist.weak_shard(random_pairs(Q * world, seed=0), Q, rank, world)
+        pairs_host = udist.weak_shard(all_pairs, cfg["pairs"], rank, world)
+    del all_pairs
+    Q = len(pairs_host)
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
@@ -174,7 +224,7 @@ def main():
         eng.set_tuning(args.variant)
 
     def step(ev=None):
-        # one launch: arc generation + gather + cost reduction + candidate selection
+        # one launch: pair order + arc generation + gather + cost reduction + selection
         if ev is not None:
             ev[0].record()
         if volume_mode:
@@ -203,74 +253,93 @@ def main():
     if world > 1:
         elapsed, kern_ms = udist.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
 
-    total_paths = P * world * args.steps
+    total_paths = Q_total * D * args.steps
     value = total_paths / elapsed
-    # algorithmic bytes per launch of the dominant kernel
+    # algorithmic bytes: one 16-B record (voxel) gather per waypoint + 16 B of
+    # outputs per path; the pair inputs (32 B / D per path) are below the definition's grain
     gather_b = 16 * W if (raster_mode or volume_mode) else 0
-    pair_b = (48.0 if volume_mode else 32.0) / D
-    # 6 f64 + 3 i32 per path (nfz_hits, offmap, below_terrain), 2 i32 best indices per pair
-    out_b = 6 * 8 + 3 * 4 + 8.0 / D
-    bytes_per_path = gather_b + pair_b + out_b
+    bytes_per_path = gather_b + 16
     launch_bytes = bytes_per_path * P
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = traffic_rec = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            key = f"{args.workload}:{args.mode}:R{R}:Q{Q}"
-            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            key = f"{args.workload}:{mode}:R{R}:Q{Q}" + (":noskip" if args.no_skip else "")
+            traffic_rec = tj.get(key)
+            if traffic_rec:
+                traffic = traffic_rec.get("l2_fabric_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
-    # which kernel the library picks (uampath.hip want_wave: tuning 9, or auto for batches of
-    # at most 16384 paths in raster / volume mode; 10 = never)
-    wave = args.mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
+    wave = mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
+    skip = raster_mode and not args.no_skip and raster.summary is not None
     kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
-                   "k_bin_count/k_bin_scatter/k_bin_gather + k_eval_pairs<records> (variant 11,"
-                   " binned)" if (args.variant == 11 and raster_mode) else
-                   f"k_eval_pairs<{mode}>" + (f" (variant {args.variant or 2})"
-                                              if raster_mode else ""))
+                   f"k_eval_pairs<{'raster+skip' if skip else mode}>" +
+                   (f" (variant {args.variant or 2})" if raster_mode and not skip else ""))
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_label": "L2->fabric bytes per launch from rocprofv3 PMC (2 x FETCH_SIZE"
+                                 " + WRITE_SIZE, MI355X_MICROARCH.md §HBM); includes "
+                                 "Infinity-Cache hits" if traffic else None,
+                "traffic_source": (traffic_rec or {}).get("source"),
+                "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+                "algorithmic_bytes_per_path": bytes_per_path,
+                "algorithmic_bytes_def": "SURVEY.md §8(d): 16 B record gather per waypoint "
+                                         "+ 16 B output per path (16 W + 16)",
+                "algorithmic_bytes_per_launch": launch_bytes}
+    if gather_b:
+        roofline.update({
+            "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if traffic else None),
+            "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
+            "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
+            "note": "each 16-B record gather moves one 128-B line (PMC); the measured random-"
+                    "gather ceiling (tools/gather_ceiling.hip) bounds the kernel, DESIGN.md §5"})
+    else:
+        roofline["note"] = ("analytic mode reads only the pairs and writes the results: its "
+                            "bound is the f64 shape walk (DESIGN.md §4 K3), not HBM")
     result = {
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "candidate-paths/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (DEM seed 1 with the Nagasaki DEM's statistics, pairs seed 0, "
                 "NFZ polygons seed 2; canonical map geometry from the reference data files)",
-        "config": {"workload": f"{args.workload}: {workload_name(cfg['name'], world)}",
-                   "dem": f"{R}x{R}", "pairs_per_gpu": Q, "displacements": D,
-                   "waypoints_per_path": W, "paths_per_gpu": P, "mode": args.mode,
-                   "no_fly_shapes": geom.n_obstacles, "region_shapes":
-                   int(geom.region_first[-1] - geom.region_first[0]),
-                   "parallelism": f"pair-sharded dp{world}, raster broadcast once"},
+        "config": {"workload": f"{args.workload}: {workload_name(cfg, n_gpus, Q_total * D)}",
+                   "dem": f"{R}x{R}", "pairs_total": Q_total, "pairs_this_rank": Q,
+                   "displacements": D, "waypoints_per_path": W, "paths_total": Q_total * D,
+                   "mode": mode, "no_fly_shapes": geom.n_obstacles,
+                   "region_shapes": int(geom.region_first[-1] - geom.region_first[0]),
+                   "parallelism": f"pair-sharded dp{n_gpus}, raster broadcast once"},
         "waypoint_evals_per_s": round(value * W, 1),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": kernel_name,
-                     "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_path": bytes_per_path,
-                     "algorithmic_bytes_per_launch": launch_bytes,
-                     "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                      if traffic else None),
-                     "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1) if gather_b else None,
-                     "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING if gather_b else None,
-                     "note": ("each 16-B record gather moves one 128-B line (PMC); the measured "
-                              "random-gather ceiling (tools/gather_ceiling.hip) bounds the "
-                              "kernel, see DESIGN.md §5") if gather_b else
-                             ("analytic mode reads only the pairs and writes the results, so "
-                              "the HBM fraction is not its bound: the f64 shape walk and lane "
-                              "divergence are (vector f64, not MFMA), see DESIGN.md §4 K3")},
+        "roofline": roofline,
         "setup": setup,
     }
+    if world > 1:
+        result["ranks"] = world
+
+    # ---- parity at N > 1: every rank checks the first pairs of its shard --------------------
+    if world > 1:
+        mism = rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_host, o,
+                           D, N)
+        t = torch.tensor(mism, dtype=torch.float64,
+                         device=eng.torch_device if backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        m = [int(x) for x in t.cpu()]
+        result["parity"] = {"paths_checked": m[0], "cost_mismatches": m[1],
+                            "best_index_mismatches": m[2], "ranks": world,
+                            "rule": f"bit-exact float64 vs CPU oracle, first "
+                                    f"{PARITY_PAIRS_PER_RANK} pairs of every rank's shard"}
 
     # ---- CPU baseline + parity sample (rank 0, N=1 only) ----------------------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -279,15 +348,7 @@ def main():
         orc = O.Oracle(O.compile_spec(spec), N, spec["options"], spec["maxratio"],
                        spec["maxalpha"], spec["enlargement"], spec["weights"],
                        altitude=params.altitude)
-        rd = rec = vd = vox = None
-        if raster_mode:
-            rd = O.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
-                                      geo.nodata, geo.dem_threshold)
-            rec = raster.rec.cpu().numpy().view(np.float32)
-        if volume_mode:
-            g3 = volume.geo
-            vd = O.volume_desc(g3.nx, g3.ny, g3.nz, g3.x0, g3.y_top, g3.dx, g3.dy, g3.z0, g3.dz)
-            vox = volume.vox.cpu().numpy().view(np.float32)
+        rd, rec, vd, vox = oracle_inputs(O, geo, raster, volume, mode)
         gpu_cost = o["cost"].cpu().numpy()
         gpu_best = o["best_fval_idx"].cpu().numpy()
         chunk = 50 if mode == "analytic" else 2000
@@ -295,10 +356,7 @@ def main():
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
-            if volume_mode:
-                r = orc.eval_paths3d(O.gen_paths3d(sl, ut_host), vd, vox)
-            else:
-                r = orc.eval_paths(O.gen_paths(sl, ut_host), mode=mode, rdesc=rd, rec=rec)
+            r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox)
             t_cpu += time.perf_counter() - ts
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
@@ -311,11 +369,8 @@ def main():
 
         def shard(lo, hi):
             for c0 in range(lo, hi, chunk):
-                sl = sample[c0:min(hi, c0 + chunk)]
-                if volume_mode:
-                    orc.eval_paths3d(O.gen_paths3d(sl, ut_host), vd, vox)
-                else:
-                    orc.eval_paths(O.gen_paths(sl, ut_host), mode=mode, rdesc=rd, rec=rec)
+                oracle_eval(O, orc, sample[c0:min(hi, c0 + chunk)], ut_host, mode, rd, rec, vd,
+                            vox)
 
         bounds = np.linspace(0, done, threads + 1).astype(int)
         passes, wall = 0, 0.0
@@ -343,13 +398,51 @@ def main():
         dist.destroy_process_group()
 
 
-def workload_name(name, world):
-    """The BASELINE config's name with its GPU count replaced by this run's (weak scaling:
-    the per-GPU workload is the config's, the job spans `world` GPUs)."""
+def oracle_inputs(O, geo, raster, volume, mode):
+    rd = rec = vd = vox = None
+    if mode == "raster":
+        rd = O.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                  geo.nodata, geo.dem_threshold)
+        rec = raster.rec.cpu().numpy().view(np.float32)
+    if mode == "volume":
+        g3 = volume.geo
+        vd = O.volume_desc(g3.nx, g3.ny, g3.nz, g3.x0, g3.y_top, g3.dx, g3.dy, g3.z0, g3.dz)
+        vox = volume.vox.cpu().numpy().view(np.float32)
+    return rd, rec, vd, vox
+
+
+def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox):
+    if mode == "volume":
+        return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
+    return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec)
+
+
+def rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_host, o, D, N):
+    """[paths checked, cost mismatches, best-index mismatches] of this rank's first pairs
+    against the CPU oracle (the checker; run after the timed region)."""
+    from oracle import oracle as O
+    O.build()
+    orc = O.Oracle(O.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                   spec["maxalpha"], spec["enlargement"], spec["weights"],
+                   altitude=params.altitude)
+    n = min(PARITY_PAIRS_PER_RANK, len(pairs_host))
+    rd, rec, vd, vox = oracle_inputs(O, geo, raster, volume, mode)
+    r = oracle_eval(O, orc, pairs_host[:n], ut_host, mode, rd, rec, vd, vox)
+    cost = o["cost"][:n * D].cpu().numpy()
+    best = o["best_fval_idx"][:n].cpu().numpy()
+    return [float(n * D), float(np.sum(r["cost"] != cost)),
+            float(np.sum(O.argmin(r["cost"], D, True) != best))]
+
+
+def workload_name(cfg, n_gpus, paths_total):
+    """The BASELINE config's name for this run: its GPU count is the run's physical GPUs."""
     import re
 
-    base = re.sub(r",\s*\d+\s*(x|\u00d7)?\s*(MI355X|GPUs?)\s*$", "", name)
-    return f"{base}, {world} GPU" + ("s" if world > 1 else "")
+    base = re.sub(r",\s*\d+\s*(x|×)?\s*(MI355X|GPUs?)\s*$", "", cfg["name"])
+    if cfg.get("R") == 8192:   # strong scaling: the total is fixed
+        return f"{base}: {paths_total / 1e6:g}M paths over {n_gpus} GPU" + \
+            ("s" if n_gpus > 1 else "")
+    return f"{base}, {n_gpus} GPU" + ("s" if n_gpus > 1 else "")
 
 
 def cpu_threads(requested):

@@ -249,6 +249,29 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);
 
+/* ---- Raster broadcast over RCCL / xGMI (the reference has no
+ * collective at all -- its only IPC is the solver's TCP socket, path_generation/solver.py:26-38).
+ * The record raster (or volume) is built once and broadcast once; the candidate loop of
+ * main.py:160-193 then shards by pair with no collective.  RCCL is loaded at run time
+ * (librccl.so.1: the one torch already loaded, else the system's); these calls return
+ * UAM_E_STATE when it is absent.
+ *   multi-process (one process per GPU): rank 0 calls uam_comm_unique_id, the caller ships
+ *   the 128 bytes to every rank (e.g. torch.distributed.broadcast_object_list), each rank calls
+ *   uam_comm_init (collective: returns once all nranks joined), then uam_bcast_raster.
+ *   single process, several GPUs: uam_bcast_raster_group (ncclCommInitAll over the contexts'
+ *   devices + one grouped broadcast; the communicators stay with the contexts for later
+ *   uam_bcast_raster calls).
+ * Asynchronous on the stream(s) given, like every other entry point. */
+#define UAM_COMM_ID_BYTES 128
+int uam_comm_unique_id(uint8_t* id_out /* [UAM_COMM_ID_BYTES] */);
+int uam_comm_init(uam_ctx* ctx, const uint8_t* id /* [UAM_COMM_ID_BYTES] */, int32_t nranks,
+                  int32_t rank);
+int uam_comm_destroy(uam_ctx* ctx);
+int uam_bcast_raster(uam_ctx* ctx, void* buf_dev, int64_t bytes, int32_t root,
+                     uam_stream stream);
+int uam_bcast_raster_group(uam_ctx** ctxs, void** bufs_dev, int32_t n, int64_t bytes,
+                           int32_t root, uam_stream* streams);
+
 /* ---- Coordinate reference systems ------------------------------
  * Transverse Mercator on an ellipsoid (Krueger series to n^6, Karney 2011) between geographic
  * (lon, lat) degrees and plane (x = easting, y = northing) metres -- what pyproj's to_crs does

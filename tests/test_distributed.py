@@ -42,6 +42,19 @@ def _worker(rank, world, port, q):
         res["rec_checksum"] = int(rec.to(torch.int64).sum())
         res["bcast_s"] = secs
         res["max"] = D.max_over_ranks([float(rank), 10.0 - rank])
+
+        # the RCCL communicator setup of uam_comm_init: rank 0 draws the id, every rank joins
+        class _Eng:
+            def comm_unique_id(self):
+                assert rank == 0, "only rank 0 draws the unique id"
+                return bytes(range(128))
+
+            def comm_init(self, uid, nranks, r):
+                self.joined = (uid == bytes(range(128)), nranks, r)
+
+        e = _Eng()
+        D.init_raster_comm(e)
+        res["comm"] = e.joined
         # a cost vector per rank: global best must equal the single-process answer
         costs = torch.tensor(np.random.default_rng(rank + 5).uniform(1, 2, size=50))
         if rank == 1:
@@ -75,6 +88,7 @@ def test_gloo_world2():
     assert out[0]["shard_sum"] + out[1]["shard_sum"] == pytest.approx(float(allp.sum()))
     assert out[0]["rec_checksum"] == out[1]["rec_checksum"] != 0
     assert out[0]["max"] == out[1]["max"] == [1.0, 10.0]
+    assert out[0]["comm"] == (True, 2, 0) and out[1]["comm"] == (True, 2, 1)
     assert out[0]["best"] == out[1]["best"] == (0.5, 57)
 
 

@@ -41,6 +41,17 @@ def test_invalid_calls_fail_loudly(lib):
     assert lib.uam_set_geometry(None, None) == _lib.UAM_E_INVALID
     assert b"NULL" in lib.uam_last_error()
     assert lib.uam_argmin(None, None, 1, 1, 0, None, None) == _lib.UAM_E_INVALID
+    assert lib.uam_bcast_raster(None, None, 16, 0, None) == _lib.UAM_E_INVALID
+    assert lib.uam_comm_init(None, None, 1, 0) == _lib.UAM_E_INVALID
+    assert lib.uam_bcast_raster_group(None, None, 0, 16, 0, None) == _lib.UAM_E_INVALID
+    assert lib.uam_raster_summary(None, None, None, 0, None, None) == _lib.UAM_E_INVALID
+    rd = _lib.RasterDesc(4096, 4096, 0.0, 20.0, 60 / 4096, 60 / 4096, -9999.0, 0.0)
+    b, nbx, nby = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    assert lib.uam_raster_summary_shape(ctypes.byref(rd), 0, ctypes.byref(b), ctypes.byref(nbx),
+                                        ctypes.byref(nby)) == _lib.UAM_OK
+    assert (b.value, nbx.value, nby.value) == (16, 256, 256)    # 65536-bit LDS bitmap
+    assert lib.uam_raster_summary_shape(ctypes.byref(rd), 8, None, None, None) == \
+        _lib.UAM_E_INVALID                                        # 262144 blocks: too many
 
 
 def _specs():

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("UAM_LIB_PATH") or os.path.join(HERE, "lib", "libuampa
 ABI_VERSION = 1
 MAX_REGIONS = 16
 RECORD_BYTES = 16
+COMM_ID_BYTES = 128
 
 UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
@@ -126,6 +127,12 @@ SIGNATURES = {
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,
                                             ctypes.POINTER(PathOutputs), _vp]),
+    "uam_comm_unique_id": (ctypes.c_int, [_vp]),
+    "uam_comm_init": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32]),
+    "uam_comm_destroy": (ctypes.c_int, [_vp]),
+    "uam_bcast_raster": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, _vp]),
+    "uam_bcast_raster_group": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int64,
+                                              ctypes.c_int32, _vp]),
     "uam_tm_jprcs": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(TmParams)]),
     "uam_geo_to_plane": (ctypes.c_int, [_vp, ctypes.POINTER(TmParams), _vp, ctypes.c_int64, _vp,
                                         _vp]),

@@ -29,9 +29,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 
 #include "../../include/uampath.h"
 #include "polyproc.h"
@@ -4041,6 +4045,7 @@ struct uam_ctx {
                                   // another stream waits for it before rewriting the scratch
     bool ord_pending = false;
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
+    void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
 };
 
 namespace {
@@ -4135,9 +4140,12 @@ int uam_ctx_create(int device, uam_ctx** out) {
     return UAM_OK;
 }
 
+static void comm_release(uam_ctx* ctx);
+
 void uam_ctx_destroy(uam_ctx* ctx) {
     if (!ctx) return;
     DeviceGuard dg(ctx->device);
+    comm_release(ctx);
     if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
@@ -5832,3 +5840,148 @@ int uam_synchronize(uam_ctx* ctx, uam_stream stream) {
 }
 
 }  // extern "C"
+
+// ---- raster broadcast over RCCL (one broadcast of the record raster, no
+// collective in the hot loop).  RCCL is bound at run time (dlopen): the soname librccl.so.1 that
+// torch already loaded is reused (one RCCL per process), else the system one; the library loads
+// and runs single-GPU work without it.
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclBroadcast) bcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        r.tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
+        r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+        r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+        r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+        r.bcast = (decltype(r.bcast))dlsym(h, "ncclBroadcast");
+        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+        r.ok = r.get_id && r.init_rank && r.init_all && r.destroy && r.bcast && r.group_start &&
+               r.group_end && r.err;
+    });
+    return r;
+}
+
+#define RCCL_TRY(expr)                                                                     \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess) return fail(UAM_E_HIP, "%s: %s", #expr, rccl().err(r_));    \
+    } while (0)
+
+int need_rccl() {
+    return rccl().ok ? UAM_OK : fail(UAM_E_STATE, "RCCL (librccl.so.1) could not be loaded");
+}
+}  // namespace
+
+static void comm_release(uam_ctx* ctx) {
+    if (ctx->comm && rccl().ok) (void)rccl().destroy((ncclComm_t)ctx->comm);
+    ctx->comm = nullptr;
+}
+
+extern "C" {
+
+int uam_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(UAM_E_INVALID, "id is NULL");
+    int st = need_rccl();
+    if (st) return st;
+    ncclUniqueId u;
+    RCCL_TRY(rccl().get_id(&u));
+    std::memcpy(id, u.internal, UAM_COMM_ID_BYTES);
+    return UAM_OK;
+}
+
+int uam_comm_init(uam_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank) {
+    if (!ctx || !id) return fail(UAM_E_INVALID, "ctx/id is NULL");
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(UAM_E_INVALID, "rank %d of %d", rank, nranks);
+    int st = need_rccl();
+    if (st) return st;
+    DeviceGuard dg(ctx->device);
+    comm_release(ctx);
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, UAM_COMM_ID_BYTES);
+    ncclComm_t c = nullptr;
+    RCCL_TRY(rccl().init_rank(&c, nranks, u, rank));
+    ctx->comm = c;
+    return UAM_OK;
+}
+
+int uam_comm_destroy(uam_ctx* ctx) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    DeviceGuard dg(ctx->device);
+    comm_release(ctx);
+    return UAM_OK;
+}
+
+int uam_bcast_raster(uam_ctx* ctx, void* buf, int64_t bytes, int32_t root, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (!ctx->comm) return fail(UAM_E_STATE, "uam_comm_init has not been called");
+    if (bytes < 0 || (bytes > 0 && !buf)) return fail(UAM_E_INVALID, "bad broadcast buffer");
+    if (bytes == 0) return UAM_OK;
+    DeviceGuard dg(ctx->device);
+    RCCL_TRY(rccl().bcast(buf, buf, (size_t)bytes, ncclChar, root, (ncclComm_t)ctx->comm,
+                          (hipStream_t)stream));
+    return UAM_OK;
+}
+
+int uam_bcast_raster_group(uam_ctx** ctxs, void** bufs, int32_t n, int64_t bytes, int32_t root,
+                           uam_stream* streams) {
+    if (!ctxs || !bufs || n < 1) return fail(UAM_E_INVALID, "bad context list");
+    if (root < 0 || root >= n) return fail(UAM_E_INVALID, "root %d of %d", root, n);
+    if (bytes < 0) return fail(UAM_E_INVALID, "bytes < 0");
+    int st = need_rccl();
+    if (st) return st;
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i] || (bytes > 0 && !bufs[i])) return fail(UAM_E_INVALID, "context %d", i);
+        devs[i] = ctxs[i]->device;
+    }
+    std::vector<ncclComm_t> comms(n, nullptr);
+    {
+        DeviceGuard dg(devs[0]);
+        RCCL_TRY(rccl().init_all(comms.data(), n, devs.data()));
+    }
+    for (int i = 0; i < n; ++i) {
+        comm_release(ctxs[i]);
+        ctxs[i]->comm = comms[i];
+    }
+    if (bytes == 0) return UAM_OK;
+    DeviceGuard dg(devs[0]);
+    RCCL_TRY(rccl().group_start());
+    for (int i = 0; i < n; ++i) {
+        if (hipSetDevice(devs[i]) != hipSuccess) {
+            (void)rccl().group_end();
+            return fail(UAM_E_HIP, "hipSetDevice(%d)", devs[i]);
+        }
+        const ncclResult_t r = rccl().bcast(bufs[i], bufs[i], (size_t)bytes, ncclChar, root,
+                                            comms[i], streams ? (hipStream_t)streams[i] : nullptr);
+        if (r != ncclSuccess) {
+            (void)rccl().group_end();
+            return fail(UAM_E_HIP, "ncclBroadcast: %s", rccl().err(r));
+        }
+    }
+    RCCL_TRY(rccl().group_end());
+    return UAM_OK;
+}
+
+}  // extern "C"
+

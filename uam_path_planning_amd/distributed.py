@@ -36,9 +36,23 @@ def weak_shard(global_pairs, per_rank, rank, world):
     return global_pairs[rank * per_rank:(rank + 1) * per_rank]
 
 
-def broadcast_raster(rec, src=0, group=None):
+def init_raster_comm(engine, group=None):
+    """Join every rank's engine to one RCCL communicator of libuampath (uam_comm_init): rank 0
+    draws the unique id, the process group ships its 128 bytes (an object broadcast, so gloo
+    and nccl groups both work), every rank joins.  Collective."""
+    dist = _dist()
+    obj = [engine.comm_unique_id() if dist.get_rank(group) == 0 else None]
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(obj, src=src, group=group)
+    engine.comm_init(obj[0], dist.get_world_size(group), dist.get_rank(group))
+
+
+def broadcast_raster(rec, src=0, group=None, engine=None):
     """Broadcast the record raster tensor (in place) from src; returns seconds taken
-    (synchronised on the tensor's device before and after)."""
+    (synchronised on the tensor's device before and after).  With an engine whose
+    communicator init_raster_comm set up, the bytes move by libuampath's RCCL broadcast
+    (uam_bcast_raster, xGMI on the GPU node); without one (CPU tensors: the gloo tests, or
+    several ranks sharing one GPU in a rehearsal) by torch.distributed.broadcast."""
     import torch
 
     dist = _dist()
@@ -46,7 +60,10 @@ def broadcast_raster(rec, src=0, group=None):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    dist.broadcast(rec, src=src, group=group)
+    if engine is not None:
+        engine.bcast_raster(rec, root=src)
+    else:
+        dist.broadcast(rec, src=src, group=group)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return time.perf_counter() - t0

@@ -500,6 +500,30 @@ class Engine:
                 continue
             _lib.check(st, "uam_dem_polygons")
 
+    # -- raster broadcast over RCCL (uam_comm_* / uam_bcast_raster) ---------------------------
+    def comm_unique_id(self):
+        """128-byte RCCL unique id (rank 0 creates it, every rank passes it to comm_init)."""
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        _lib.check(self.lib.uam_comm_unique_id(buf), "uam_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, uid, nranks, rank):
+        """Join the RCCL communicator of uid as rank of nranks (collective over the ranks)."""
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {_lib.COMM_ID_BYTES} bytes")
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        _lib.check(self.lib.uam_comm_init(self._ctx, buf, int(nranks), int(rank)),
+                   "uam_comm_init")
+
+    def bcast_raster(self, t, root=0):
+        """Broadcast device tensor t (in place) from root over the context's communicator, on
+        this engine's current stream."""
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("bcast_raster needs a contiguous device tensor")
+        _lib.check(self.lib.uam_bcast_raster(self._ctx, _ptr(t), t.numel() * t.element_size(),
+                                             int(root), self.stream), "uam_bcast_raster")
+        return t
+
     def synchronize(self):
         _lib.check(self.lib.uam_synchronize(self._ctx, self.stream), "uam_synchronize")
 

@@ -82,7 +82,9 @@ CONFIGS = {
                  pairs=200, D=5, N=254, nfz_polygons=0, mode="raster"),
     "cfg3": dict(name="100k start/goal pairs x 5 displacements, 4096^2 DEM + polygon NFZ, 1 GPU",
                  R=4096, pairs=100_000, D=5, N=80, nfz_polygons=64, mode="raster"),
-    "cfg4": dict(name="1M candidate paths, 8192^2 DEM (synthetic GeoTIFF tiles), 8 GPUs",
+    # strong scaling: 200k pairs x 5 = 1M paths IN TOTAL, sharded over the GPUs (shard_range)
+    "cfg4": dict(name="8192^2 DEM from synthetic GeoTIFF tiles + polygon NFZ, RCCL raster "
+                      "broadcast, 8 GPUs",
                  R=8192, pairs=200_000, D=5, N=80, nfz_polygons=64, mode="raster"),
     "cfg5": dict(name="3-D 1024x1024x64 (x,y,alt) altitude-dependent risk volume",
                  R=1024, nz=64, z0=0.0, dz=10.0, pairs=100_000, D=5, N=80, nfz_polygons=64,
