@@ -49,6 +49,7 @@ METRIC = "candidate-paths/sec + waypoint-evals/sec on N×N DEM at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # independent random 16-B gathers from a 256 MiB table, one MI355X (profiles/r01/gather_ceiling.log)
 RANDOM_GATHER_CEILING = 55.5e9
+F64_PEAK_TFLOPS = 78.6  # MI355X f64 vector (FMA) spec; tools/f64_peak.hip measures 74.5
 PARITY_PAIRS_PER_RANK = 200   # oracle check of every rank's first pairs at N > 1
 
 
@@ -242,6 +243,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.kernel_timing(True)    # HIP events around the dominant kernel, on its launch stream
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i])
@@ -249,58 +251,43 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    k_total, k_launches = eng.kernel_time()
+    eng.kernel_timing(False)
+    step_ev_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    # multi-launch variants (K2b / K2t, variant 1) are not bracketed: their step time stands in
+    kern_timed = k_launches == args.steps
+    kern_ms = k_total / k_launches if kern_timed else step_ev_ms
     if world > 1:
-        elapsed, kern_ms = udist.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
+        elapsed, kern_ms, step_ev_ms = udist.max_over_ranks([elapsed, kern_ms, step_ev_ms],
+                                                            device=eng.torch_device)
 
     total_paths = Q_total * D * args.steps
     value = total_paths / elapsed
-    # algorithmic bytes: one 16-B record (voxel) gather per waypoint + 16 B of
-    # outputs per path; the pair inputs (32 B / D per path) are below the definition's grain
-    gather_b = 16 * W if (raster_mode or volume_mode) else 0
-    bytes_per_path = gather_b + 16
-    launch_bytes = bytes_per_path * P
-    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_rec = None
+    wave = mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
+    skip = raster_mode and not args.no_skip and raster.summary is not None
+    ktag = "wave" if wave else ("raster+skip" if skip else mode)
+    if raster_mode and not skip and not wave:
+        ktag += f"-v{args.variant or 2}"
+    kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
+                   f"k_eval_pairs<{ktag}>")
+    pkey = f"{args.workload}:{mode}:R{R}:Q{Q}:{ktag}"
+    prof = {}
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
-                tj = json.load(f)
-            key = f"{args.workload}:{mode}:R{R}:Q{Q}" + (":noskip" if args.no_skip else "")
-            traffic_rec = tj.get(key)
-            if traffic_rec:
-                traffic = traffic_rec.get("l2_fabric_bytes_per_launch")
+                prof = json.load(f).get(pkey) or {}
         except (OSError, ValueError):
-            traffic = None
-
-    wave = mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
-    skip = raster_mode and not args.no_skip and raster.summary is not None
-    kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
-                   f"k_eval_pairs<{'raster+skip' if skip else mode}>" +
-                   (f" (variant {args.variant or 2})" if raster_mode and not skip else ""))
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_label": "L2->fabric bytes per launch from rocprofv3 PMC (2 x FETCH_SIZE"
-                                 " + WRITE_SIZE, MI355X_MICROARCH.md §HBM); includes "
-                                 "Infinity-Cache hits" if traffic else None,
-                "traffic_source": (traffic_rec or {}).get("source"),
-                "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
-                "algorithmic_bytes_per_path": bytes_per_path,
-                "algorithmic_bytes_def": "SURVEY.md §8(d): 16 B record gather per waypoint "
-                                         "+ 16 B output per path (16 W + 16)",
-                "algorithmic_bytes_per_launch": launch_bytes}
-    if gather_b:
-        roofline.update({
-            "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                             if traffic else None),
-            "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
-            "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
-            "note": "each 16-B record gather moves one 128-B line (PMC); the measured random-"
-                    "gather ceiling (tools/gather_ceiling.hip) bounds the kernel, DESIGN.md §5"})
+            prof = {}
+    if mode == "analytic":
+        roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
-        roofline["note"] = ("analytic mode reads only the pairs and writes the results: its "
-                            "bound is the f64 shape walk (DESIGN.md §4 K3), not HBM")
+        roofline = gather_roofline(prof, P, W, kern_ms, kernel_name)
+    roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
+                                    "launch of the kernel, on its launch stream "
+                                    "(uam_kernel_timing)" if kern_timed else
+                                    "torch events around the whole step (multi-launch variant)")
+    roofline["step_event_ms"] = round(step_ev_ms, 4)
+    roofline["profile_key"] = pkey
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -396,6 +383,56 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def gather_roofline(prof, P, W, kern_ms, kernel_name):
+    """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
+    definition used in SURVEY, DESIGN §4 and here): one 16-B record gather per waypoint + 16 B
+    of outputs per path = 16 W + 16 B/path.  `traffic`: L2->fabric bytes per launch of the same
+    kernel from this build's rocprofv3 PMC passes (tools/pmc_traffic.py ->
+    profiles/traffic.json; 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM), which
+    include Infinity-Cache hits: they are not proven DRAM bytes."""
+    bytes_per_path = 16 * W + 16
+    launch_bytes = bytes_per_path * P
+    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = prof.get("l2_fabric_bytes_per_launch")
+    r = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+         "traffic_label": ("L2->fabric bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + "
+                           "WRITE_SIZE; includes Infinity-Cache hits)") if traffic else None,
+         "traffic_source": prof.get("source"),
+         "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+         "algorithmic_bytes_per_path": bytes_per_path,
+         "algorithmic_bytes_def": "SURVEY.md §8(d): 16 B record gather per waypoint + 16 B "
+                                  "output per path (16 W + 16)",
+         "algorithmic_bytes_per_launch": launch_bytes,
+         "traffic_over_algorithmic": round(traffic / launch_bytes, 2) if traffic else None,
+         "l2_hit_rate": prof.get("l2_hit_rate"),
+         "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
+         "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
+         "note": "each 16-B record gather that misses L2 moves one 128-B line (PMC); the "
+                 "measured random-gather ceiling (tools/gather_ceiling.hip) bounds the kernel, "
+                 "DESIGN.md §5"}
+    return r
+
+
+def analytic_roofline(prof, P, kern_ms, kernel_name):
+    """f64 roofline of K3 (analytic mode reads 32 B per pair and writes 16 B per path, so HBM
+    does not bound it): f64 FLOP per launch from this build's rocprofv3 PMC pass
+    (64 lanes x (2 FMA + ADD + MUL + TRANS) per f64 VALU instruction, tools/pmc_traffic.py
+    --flops) / the kernel's HIP-event time vs the f64 vector FMA peak."""
+    flops = prof.get("f64_flop_per_launch")
+    r = {"bound": "f64-valu", "unit": "TFLOP/s", "peak": F64_PEAK_TFLOPS,
+         "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
+         "achieved": round(flops / (kern_ms * 1e-3) / 1e12, 3) if flops else None,
+         "frac": round(flops / (kern_ms * 1e-3) / 1e12 / F64_PEAK_TFLOPS, 4) if flops else None,
+         "f64_flop_per_launch": flops, "f64_flop_per_path": (flops / P) if flops else None,
+         "flop_source": prof.get("source"),
+         "wait_any_frac": prof.get("wait_any_frac"), "valu_busy_frac": prof.get("valu_frac"),
+         "traffic": prof.get("l2_fabric_bytes_per_launch"),
+         "peak_note": "MI355X f64 vector FMA spec 78.6 TFLOP/s; tools/f64_peak.hip measures "
+                      "74.5 (DESIGN.md §5)"}
+    return r
 
 
 def oracle_inputs(O, geo, raster, volume, mode):

@@ -347,10 +347,20 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * Tuning experiments only (read once, by uam_ctx_create; unset = the defaults): UAM_K1_CPL
  * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
  * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
- * UAM_TB_DBG (K2t diagnostics that change results: 1 skips the gathers, 2 the stores,
- * 4 pass 1), UAM_PAIR_ORDER=0 (uam_eval_generated without the spatial pair order it
- * applies to batches of >= 4096 pairs; raster batches then also skip the XCD placement).  None of them changes results except UAM_TB_DBG. */
+ * UAM_PAIR_ORDER=0 (uam_eval_generated without the spatial pair order it applies to
+ * batches of >= 4096 pairs; raster batches then also skip the XCD placement).  None of them
+ * changes results.  (K2t's result-changing diagnostics, UAM_TB_DBG, exist only in a
+ * -DUAM_TB_DIAG build of the library.) */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
+
+/* Measurement (bench.py's roofline; build-defined).  uam_kernel_timing(ctx, 1) resets and
+ * starts timing, 0 stops it: while on, the context records a HIP event pair on the launch
+ * stream around every launch of the dominant path kernel (k_eval_pairs / k_eval_wave of
+ * uam_eval_generated, uam_eval_generated_s and uam_eval_generated3d), excluding the pair order
+ * and selection launches.  uam_kernel_time waits for those events and returns the summed
+ * kernel time and the launch count since the last call (then resets the count). */
+int uam_kernel_timing(uam_ctx* ctx, int32_t enable);
+int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */
 int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,

@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 --pmc CSVs of a bench run into per-launch HBM traffic for the dominant
-kernel, corrected as MI355X_MICROARCH.md §HBM prescribes:
+"""Per-launch PMC figures of one kernel from rocprofv3 --pmc passes of a bench run, written to
+profiles/traffic.json under bench.py's profile key (workload:mode:R:Q:kernel-tag), where
+bench.py's roofline reads them.  Corrections as MI355X_MICROARCH.md §HBM prescribes:
 
-  read bytes  = FETCH_SIZE[KiB] * 1024 * 2   (gfx950 tallies each 128-B line request at 64 B;
-                                              cross-checked against TCC_EA0_RDREQ_128B * 128 when
-                                              that counter pass is present)
-  write bytes = WRITE_SIZE[KiB] * 1024        (exact for full-line stores per the guide)
+  L2->fabric read bytes  = FETCH_SIZE[KiB] * 1024 * 2   (gfx950 tallies each 128-B line
+                                                          request at 64 B; cross-checked with
+                                                          TCC_EA0_RDREQ_128B * 128 when present)
+  L2->fabric write bytes = WRITE_SIZE[KiB] * 1024
+These count requests that leave L2, Infinity-Cache hits included: not proven DRAM bytes.
 
-usage: tools/pmc_traffic.py --key cfg3:raster:R4096:Q100000 --kernel k_eval_pairs \
-          --fetch DIR --write DIR [--ea DIR] [--out profiles/traffic.json]
-Each DIR holds rocprofv3's <prefix>_counter_collection.csv of one counter pass.
+Optional passes: --tcc (TCC_HIT_sum, TCC_MISS_sum, TCC_EA0_RDREQ_128B_sum) -> L2 hit rate;
+--sq (SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_ACTIVE_INST_VALU, ...) -> wave-cycle shares;
+--flops (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64) -> f64 FLOP per launch
+(64 lanes x (2 FMA + ADD + MUL + TRANS) per instruction; an upper bound when lanes are masked).
+
+usage: tools/pmc_traffic.py --key cfg3:raster:R4096:Q100000:raster+skip --kernel k_eval_pairs \
+          [--fetch DIR] [--write DIR] [--tcc DIR] [--sq DIR] [--flops DIR] [--source TEXT]
+Each DIR holds rocprofv3's *counter_collection.csv of one counter pass.
 """
 import argparse
 import csv
@@ -21,7 +28,7 @@ import statistics
 
 def load(d, kernel, counter):
     vals = []
-    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
@@ -34,32 +41,70 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--key", required=True)
     ap.add_argument("--kernel", required=True)
-    ap.add_argument("--fetch", required=True)
-    ap.add_argument("--write", required=True)
-    ap.add_argument("--ea", default=None, help="dir with TCC_EA0_RDREQ_128B_sum pass")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--tcc")
+    ap.add_argument("--sq")
+    ap.add_argument("--flops")
+    ap.add_argument("--source", default=None)
     ap.add_argument("--out", default="profiles/traffic.json")
     a = ap.parse_args()
-    fetch_kib, n1 = load(a.fetch, a.kernel, "FETCH_SIZE")
-    write_kib, n2 = load(a.write, a.kernel, "WRITE_SIZE")
-    read_b = fetch_kib * 1024 * 2
-    write_b = write_kib * 1024
-    rec = {"kernel": a.kernel, "launches_profiled": min(n1, n2),
-           "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
-           "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
-           "hbm_bytes_per_launch": read_b + write_b,
-           "correction": "read = 2 x FETCH_SIZE (gfx950 128-B requests tallied at 64 B)"}
-    if a.ea:
-        req128, _ = load(a.ea, a.kernel, "TCC_EA0_RDREQ_128B_sum")
-        rec["tcc_ea0_rdreq_128b"] = req128
-        rec["read_bytes_from_128b_requests"] = req128 * 128
+    rec = {"kernel": a.kernel, "source": a.source}
+    if a.fetch and a.write:
+        fetch_kib, n1 = load(a.fetch, a.kernel, "FETCH_SIZE")
+        write_kib, n2 = load(a.write, a.kernel, "WRITE_SIZE")
+        read_b, write_b = fetch_kib * 1024 * 2, write_kib * 1024
+        rec.update({"launches_profiled": min(n1, n2), "fetch_size_kib_raw": fetch_kib,
+                    "write_size_kib_raw": write_kib,
+                    "l2_fabric_read_bytes_per_launch": read_b,
+                    "l2_fabric_write_bytes_per_launch": write_b,
+                    "l2_fabric_bytes_per_launch": read_b + write_b,
+                    "correction": "read = 2 x FETCH_SIZE (gfx950 128-B requests tallied at "
+                                  "64 B); includes Infinity-Cache hits"})
+    if a.tcc:
+        hit, _ = load(a.tcc, a.kernel, "TCC_HIT_sum")
+        miss, _ = load(a.tcc, a.kernel, "TCC_MISS_sum")
+        rec.update({"tcc_hit": hit, "tcc_miss": miss,
+                    "l2_hit_rate": round(hit / (hit + miss), 4) if hit + miss else None})
+        try:
+            req128, _ = load(a.tcc, a.kernel, "TCC_EA0_RDREQ_128B_sum")
+            rec.update({"tcc_ea0_rdreq_128b": req128,
+                        "read_bytes_from_128b_requests": req128 * 128})
+        except SystemExit:
+            pass
+    if a.sq:
+        cyc, _ = load(a.sq, a.kernel, "SQ_WAVE_CYCLES")
+        out = {"sq_wave_cycles": cyc}
+        for c, k in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_ACTIVE_INST_VALU", "valu_frac"),
+                     ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
+                     ("SQ_ACTIVE_INST_ANY", "active_inst_any_frac")):
+            try:
+                v, _ = load(a.sq, a.kernel, c)
+                out[k] = round(v / cyc, 4) if cyc else None
+            except SystemExit:
+                pass
+        for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM", "SQ_INSTS_SALU", "SQ_BUSY_CYCLES"):
+            try:
+                out[c.lower()], _ = load(a.sq, a.kernel, c)
+            except SystemExit:
+                pass
+        rec.update(out)
+    if a.flops:
+        n = {}
+        for c in ("FMA", "ADD", "MUL", "TRANS"):
+            n[c], _ = load(a.flops, a.kernel, f"SQ_INSTS_VALU_{c}_F64")
+        rec.update({"f64_insts": n,
+                    "f64_flop_per_launch": 64 * (2 * n["FMA"] + n["ADD"] + n["MUL"] + n["TRANS"]),
+                    "flop_rule": "64 lanes x (2 FMA + ADD + MUL + TRANS) per f64 VALU "
+                                 "instruction (SQ_INSTS_VALU_*_F64)"})
     db = {}
     if os.path.exists(a.out):
         db = json.load(open(a.out))
-    db[a.key] = rec
+    db.setdefault(a.key, {}).update({k: v for k, v in rec.items() if v is not None})
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(db, f, indent=1)
-    print(json.dumps({a.key: rec}))
+    print(json.dumps({a.key: db[a.key]}))
 
 
 if __name__ == "__main__":

@@ -123,6 +123,9 @@ SIGNATURES = {
                                        ctypes.c_int32, _vp, _vp]),
     "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
     "uam_set_tuning": (ctypes.c_int, [_vp, ctypes.c_int32]),
+    "uam_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int32]),
+    "uam_kernel_time": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,

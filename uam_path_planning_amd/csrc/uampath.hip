@@ -4026,7 +4026,13 @@ struct uam_ctx {
     size_t ws_bytes = 0;
     int tb_k = 0;               // K2t gather workgroups per XCD (0 = default; UAM_TB_K env)
     int tb_pb = 0;              // K2t pairs per path-block (0 = default; UAM_TB_PB env)
-    int tb_dbg = 0;             // K2t diagnostics (UAM_TB_DBG env, KTile::dbg)
+    int tb_dbg = 0;             // K2t diagnostics (KTile::dbg): read from UAM_TB_DBG only in a
+                                // -DUAM_TB_DIAG build (they change results)
+    bool tb_attrs = false;      // K2t dynamic-LDS attributes raised on this context's device
+    // kernel timing (uam_kernel_timing): HIP event pairs around the dominant path kernel
+    bool ktime_on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ktime_ev;
+    size_t ktime_n = 0;
     int k1_cpl = 0;             // K1 cells per lane: 0 = default (2), 1 = single-cell kernel,
                                 // 2 / 4 / 8 (UAM_K1_CPL env)
     int k1_grid = 0;            // K1 workgroup cap (0 = one wave per strip; UAM_K1_GRID env)
@@ -4055,6 +4061,30 @@ int check_ctx(uam_ctx* ctx, bool need_params) {
     if (!ctx->have_geom) return fail(UAM_E_STATE, "uam_set_geometry has not been called");
     if (need_params && !ctx->have_params)
         return fail(UAM_E_STATE, "uam_set_params has not been called");
+    return UAM_OK;
+}
+
+// Kernel timing (uam_kernel_timing): an event pair recorded on the launch stream around the
+// dominant path kernel; pairs are pooled and reused after uam_kernel_time / a reset.
+int ktime_begin(uam_ctx* ctx, hipStream_t s) {
+    if (!ctx->ktime_on) return UAM_OK;
+    if (ctx->ktime_n == ctx->ktime_ev.size()) {
+        hipEvent_t a, b;
+        HIP_TRY(hipEventCreate(&a));
+        if (hipEventCreate(&b) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            return fail(UAM_E_HIP, "hipEventCreate failed");
+        }
+        ctx->ktime_ev.emplace_back(a, b);
+    }
+    HIP_TRY(hipEventRecord(ctx->ktime_ev[ctx->ktime_n].first, s));
+    return UAM_OK;
+}
+
+int ktime_end(uam_ctx* ctx, hipStream_t s) {
+    if (!ctx->ktime_on) return UAM_OK;
+    HIP_TRY(hipEventRecord(ctx->ktime_ev[ctx->ktime_n].second, s));
+    ++ctx->ktime_n;
     return UAM_OK;
 }
 
@@ -4129,7 +4159,9 @@ int uam_ctx_create(int device, uam_ctx** out) {
     c->device = device;
     if (const char* e = std::getenv("UAM_TB_K")) c->tb_k = std::atoi(e);  // tuning experiments
     if (const char* e = std::getenv("UAM_TB_PB")) c->tb_pb = std::atoi(e);
+#ifdef UAM_TB_DIAG
     if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
+#endif
     if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
     if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
@@ -4155,6 +4187,11 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    for (auto& e : ctx->ktime_ev) {
+        (void)hipEventSynchronize(e.second);
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
     for (hipStream_t k : ctx->k8s)
         if (k) (void)hipStreamDestroy(k);
@@ -4489,6 +4526,8 @@ static int launch_wave(uam_ctx* ctx, int mode, bool gen, const KRaster& kr, cons
     const dim3 grid((unsigned)blocks), block(64 * wpb);
     const size_t lds = (size_t)(wpb * per_wave);
     const uint4* r = (const uint4*)rec;
+    int st = ktime_begin(ctx, s);
+    if (st) return st;
     if (mode == UAM_MODE_VOLUME)
         hipLaunchKernelGGL((k_eval_wave<UAM_MODE_VOLUME, true>), grid, block, lds, s, ctx->kg,
                            ctx->kp, kr, kv, r, wp, pairs, utab, D, n_paths, ko);
@@ -4499,6 +4538,8 @@ static int launch_wave(uam_ctx* ctx, int mode, bool gen, const KRaster& kr, cons
         hipLaunchKernelGGL((k_eval_wave<UAM_MODE_RASTER, false>), grid, block, lds, s, ctx->kg,
                            ctx->kp, kr, kv, r, wp, pairs, utab, D, n_paths, ko);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "k_eval_wave launch failed");
+    st = ktime_end(ctx, s);
+    if (st) return st;
     if (gen && (best_f || best_l)) {
         const int64_t n_pairs = n_paths / D;
         const dim3 g2(grid_for(n_pairs, 256, INT32_MAX));
@@ -4558,6 +4599,29 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
         return fail(UAM_E_INVALID, "tuning variant %d out of range [0, %d]", variant,
                     UAM_TUNING_MAX);
     ctx->variant = variant;
+    return UAM_OK;
+}
+
+int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    ctx->ktime_on = enable != 0;
+    ctx->ktime_n = 0;
+    return UAM_OK;
+}
+
+int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
+    if (!ctx || !ms_total || !launches) return fail(UAM_E_INVALID, "NULL argument");
+    DeviceGuard dg(ctx->device);
+    double tot = 0.0;
+    for (size_t i = 0; i < ctx->ktime_n; ++i) {
+        HIP_TRY(hipEventSynchronize(ctx->ktime_ev[i].second));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, ctx->ktime_ev[i].first, ctx->ktime_ev[i].second));
+        tot += ms;
+    }
+    *ms_total = tot;
+    *launches = (int64_t)ctx->ktime_n;
+    ctx->ktime_n = 0;
     return UAM_OK;
 }
 
@@ -4751,13 +4815,12 @@ static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const 
     kt.ent = (uint2*)(w + b_cnt + b_tot + b_boff);
     kt.recb = (uint4*)(w + b_cnt + b_tot + b_boff + b_ent);
     kt.kin = (double*)(w + b_cnt + b_tot + b_boff + b_ent + b_recb);
-    static bool attrs = false;
-    if (!attrs) {
-        (void)hipFuncSetAttribute((const void*)k_tb_scatter,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds);
-        (void)hipFuncSetAttribute((const void*)k_tb_reduce,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds);
-        attrs = true;
+    if (!ctx->tb_attrs) {  // per context = per device (the caller's DeviceGuard is active)
+        HIP_TRY(hipFuncSetAttribute((const void*)k_tb_scatter,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_tb_reduce,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds));
+        ctx->tb_attrs = true;
     }
     // pass 1 (ALU-bound) on a second stream, beside the streaming launches A1..B
     if (!ctx->s2) {
@@ -4900,6 +4963,8 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
     hipLaunchKernelGGL((k_eval_pairs<MODE_, C_, PIPE_, MINW_>), grid, block, lds, s, ctx->kg, \
                        ctx->kp, kr, kv, (const uint4*)rec, pairs, n_pairs, utab, D, ko,      \
                        best_f, best_l, order)
+    st = ktime_begin(ctx, s);
+    if (st) return st;
     if (mode == UAM_MODE_ANALYTIC) {
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
@@ -4917,6 +4982,8 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
     }
 #undef UAM_LAUNCH_PAIRS
     HIP_TRY(hipGetLastError());
+    st = ktime_end(ctx, s);
+    if (st) return st;
     if (order) return order_done(ctx, s);
     return UAM_OK;
 }
@@ -5026,12 +5093,14 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    st = ktime_begin(ctx, (hipStream_t)stream);
+    if (st) return st;
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
                        (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l,
                        nullptr);
     HIP_TRY(hipGetLastError());
-    return UAM_OK;
+    return ktime_end(ctx, (hipStream_t)stream);
 }
 
 static int refine_memory(const uam_refine_params* rp) {

@@ -267,6 +267,20 @@ class Engine:
     def set_tuning(self, variant):
         _lib.check(self.lib.uam_set_tuning(self._ctx, int(variant)), "uam_set_tuning")
 
+    def kernel_timing(self, enable=True):
+        """Start (and reset) or stop HIP-event timing of the dominant path kernel: the context
+        records an event pair on the launch stream around every k_eval_pairs / k_eval_wave
+        launch (not around the pair order or selection kernels)."""
+        _lib.check(self.lib.uam_kernel_timing(self._ctx, 1 if enable else 0),
+                   "uam_kernel_timing")
+
+    def kernel_time(self):
+        """(total ms, launches) of the timed kernel launches since the last call / reset."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(self.lib.uam_kernel_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)),
+                   "uam_kernel_time")
+        return ms.value, n.value
+
     def _outputs(self, P, W, mode, want_cells, want_g, n_pairs=None):
         torch = _torch()
         o = {k: self.empty((P,), torch.float64) for k in ("cost", "length_q", "length",
