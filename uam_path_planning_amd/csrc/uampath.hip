@@ -1799,7 +1799,7 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
         bool hit[CPL];
 #pragma unroll
         for (int k = 0; k < CPL; ++k) acc[k] = 0.0, hit[k] = false;
-        wave_walk_obs_cells<CPL>(g, slot, [&](int s, uint32_t m1, uint32_t m2) {
+            wave_walk_obs_cells<CPL>(g, slot, [&](int s, uint32_t m1, uint32_t m2) {
             if (!(m1 | m2)) return;
             const DevShape sh = uload(g.shape, s);
             uint32_t n1 = 0, n2 = 0;
@@ -1853,6 +1853,651 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
             }
         }
     }
+}
+
+// The inequalities of a wave-uniform shape in ascending order, their records through scalar
+// loads two at a time (one wait per pair instead of one per record): f(q) per inequality.
+template <class F>
+__device__ __forceinline__ void for_ineqs_u(const KGeom& g, const DevShape& sh, F&& f) {
+    int i = sh.first;
+    const int end = sh.first + sh.count;
+    for (; i + 1 < end; i += 2) {
+        const DevIneq q0 = uload(g.ineq, i);
+        const DevIneq q1 = uload(g.ineq, i + 1);
+        f(q0);
+        f(q1);
+    }
+    if (i < end) f(uload(g.ineq, i));
+}
+
+// ---- K3b: analytic evaluation with cell-sorted waypoints ----------------------------------
+// k_eval_pairs<ANALYTIC> runs one lane per path, so at each step a wave's 64 lanes evaluate 64
+// points that lie kilometres apart: 64 different shape-grid lists, walked with per-lane
+// dependent loads of the shape and inequality records (profiles/r02: 75% of wave cycles
+// parked on s_waitcnt, 7% VALU).  K3b keeps the block layout (wave = displacement, lane =
+// pair; pass 1 and every ordered sum stay with the path's own lane) but evaluates the
+// waypoints in segments of S steps: the block's 64 D S points of a segment are counting-sorted
+// in LDS by the Morton code of their grid cell, and each wave evaluates 64 CPL consecutive
+// sorted points at a time (CPL per lane) -- the same or adjacent cells -- walking the union of
+// their lists wave-uniformly, with the shape and inequality records through scalar loads as
+// K1 does.  Each point's results go to LDS: Phi (f64), its nonzero no-fly psi terms in list
+// order (appended to a term list), their count and the collision bit.  The path's lane then
+// adds them in waypoint order exactly as eval_path does: Phi / N into the cost chain, the psi
+// terms into the no-fly chain (a +-0 term, which the list omits, is an exact no-op on an
+// accumulator that is never -0), the hit count.  A point with more than K3B_KT terms, or whose
+// terms do not fit the segment's term list, is re-walked by its lane (eval_path's own loop).
+// Outputs are bit-identical to k_eval_pairs.
+#ifdef UAM_K3B_DIAG
+// diagnostics build only (tools/probe_k3b.py): [0] chunks, [1] distinct grid slots per chunk,
+// [2] union walk steps (table 0), [3] lane list entries (table 0), [4] / [5] the same for the
+// obstacle walk, [6] points re-walked by their lane; [8..13] s_memtime cycles of workgroup
+// phases (thread 0): pass 1, zero + keys, scan + scatter, evaluation, ordered sums, output
+__device__ unsigned long long g_k3b_diag[16];
+__device__ unsigned long long g_k3b_ev[8];  // eval-phase sub-stamps (lane 0 of each wave)
+__constant__ int g_k3b_skip;  // bit 0: skip the evaluation phase (timing of the rest); bit 1:
+                              // no coherence counters (clean phase timing)
+#endif
+constexpr int K3B_BINS = 1024 + 2;  // grid cell mod 1024, off-grid, no slot
+constexpr int K3B_KT = 3;           // psi terms a point keeps in registers (more: re-walk)
+constexpr uint8_t K3B_HIT = 1, K3B_REWALK = 7;  // flags: bit 0 hit, bits 1-3 term count
+
+__device__ __forceinline__ int k3b_key(int slot, int gx) {
+    if (slot < 0) return 1025;
+    if (slot >= gx * gx) return 1024;
+    return slot & 1023;  // row-major cell; cells 1024 apart share a bin (only coherence suffers)
+}
+
+// exclusive scan of h[0..n) in place by the whole block (nt threads, nt % 64 == 0); returns
+// the total.  part: >= nt / 64 + 1 ints of scratch.
+__device__ __forceinline__ int block_excl_scan(int32_t* h, int n, int32_t* part) {
+    const int t = threadIdx.x, nt = blockDim.x, per = (n + nt - 1) / nt;
+    const int lo = min(n, t * per), hi = min(n, lo + per);
+    int32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += h[i];
+    int32_t inc = sum;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t v = __shfl_up(inc, o, 64);
+        if ((t & 63) >= o) inc += v;
+    }
+    if ((t & 63) == 63) part[t >> 6] = inc;
+    __syncthreads();
+    if (t == 0) {
+        int32_t run = 0;
+        for (int w = 0; w < nt / 64; ++w) {
+            const int32_t v = part[w];
+            part[w] = run;
+            run += v;
+        }
+        part[nt / 64] = run;
+    }
+    __syncthreads();
+    int32_t run = part[t >> 6] + inc - sum;
+    for (int i = lo; i < hi; ++i) {
+        const int32_t v = h[i];
+        h[i] = run;
+        run += v;
+    }
+    const int32_t total = part[nt / 64];
+    __syncthreads();
+    return total;
+}
+
+// Per-point results of the evaluation phase.
+template <int CPL>
+struct K3bRes {
+    double pen[CPL];
+    double tm[CPL][K3B_KT];  // the first nonzero obstacle psi terms, list order
+    int cnt[CPL];            // nonzero terms (may exceed K3B_KT)
+    bool hit[CPL];
+#ifdef UAM_K3B_DIAG
+    unsigned long long cyc0, cyc1;  // s_memtime cycles of the two walks
+#endif
+};
+
+// Phi, the nonzero obstacle psi terms and the collision bit of each lane's CPL points (whole
+// wave active, uniform control flow; slot -2 = no point).  Same terms in the same order as
+// total_penalty / eval_path's psi loop / collides (the walk of k_raster_build_cells).
+template <int CPL>
+__device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
+                                           const double (&x)[CPL], const double (&y)[CPL],
+                                           const int (&slot)[CPL], K3bRes<CPL>& R) {
+    const bool pen_smooth = p.penalty_smooth != 0, obs_smooth = p.obstacle_smooth != 0;
+    double t[CPL], wc[CPL];  // wc: the weight of the lane's current region (rc)
+    int rc[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) R.pen[k] = t[k] = wc[k] = 0.0, rc[k] = -1;
+#ifdef UAM_K3B_DIAG
+    unsigned long long dg[4] = {0, 0, 0, 0};
+#endif
+#ifdef UAM_K3B_DIAG
+    unsigned long long e0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef UAM_K3B_DIAG
+    int slot0[CPL];  // bit 2: skip the table-0 walk; bit 3: skip the obstacle walk
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) slot0[k] = (g_k3b_skip & 4) ? -2 : slot[k];
+#else
+    const int(&slot0)[CPL] = slot;
+#endif
+#ifdef UAM_K3B_DIAG
+    int slot1[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) slot1[k] = (g_k3b_skip & 8) ? -2 : slot[k];
+    unsigned long long e1 = 0;
+#else
+    const int(&slot1)[CPL] = slot;
+#endif
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        R.cnt[k] = 0;
+        R.hit[k] = false;
+#pragma unroll
+        for (int m = 0; m < K3B_KT; ++m) R.tm[k][m] = 0.0;
+    }
+    auto k3b_finish_pen = [&]() {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (rc[k] >= 0) R.pen[k] = R.pen[k] + wc[k] * t[k];
+    };
+    auto add_term = [&](int k, double v) {  // v nonzero or NaN: a term the no-fly chain adds
+#pragma unroll
+        for (int m = 0; m < K3B_KT; ++m)
+            if (R.cnt[k] == m) R.tm[k][m] = v;
+        ++R.cnt[k];
+    };
+    auto body0 = [&](int s, uint32_t mine) {
+#ifdef UAM_K3B_DIAG
+        dg[0] += 1;
+        dg[1] += __builtin_popcount(mine);
+#endif
+        if (!mine) return;
+        const DevShape sh = uload(g.shape, s);
+        uint32_t need = 0;
+        const double wnew = p.weights[sh.region];  // wave-uniform region: a scalar read
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (!((mine >> k) & 1u)) continue;
+            if (sh.region != rc[k]) {
+                if (rc[k] >= 0) R.pen[k] = R.pen[k] + wc[k] * t[k];
+                rc[k] = sh.region;
+                wc[k] = wnew;
+                t[k] = 0.0;
+            }
+            if (!((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, x[k], y[k])))
+                need |= 1u << k;
+        }
+        if (!need) return;
+        double r[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) r[k] = 1.0;
+        for_ineqs_u(g, sh, [&](const DevIneq& q) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const double h = ineq_h(&q, x[k], y[k]);
+                if (pen_smooth) {
+                    const double m = fmin(h - p.enlargement, 0.0);
+                    r[k] = r[k] * (m * m);
+                } else {
+                    r[k] = r[k] * fmin(p.enlargement - h, 0.0);
+                }
+            }
+        });
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if ((need >> k) & 1u) t[k] = sh.has_center ? t[k] + r[k] / sh.norm_pen : t[k] + r[k];
+    };
+
+    auto body1 = [&](int s, uint32_t m1, uint32_t m2) {
+#ifdef UAM_K3B_DIAG
+        dg[2] += 1;
+        dg[3] += __builtin_popcount(m1 | m2);
+#endif
+        if (!(m1 | m2)) return;
+        const DevShape sh = uload(g.shape, s);
+        uint32_t n1 = 0, n2 = 0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const bool out = outside(sh.box_obs, x[k], y[k]);
+            if (((m1 >> k) & 1u) && !((sh.flags & SHAPE_CULL_PSI) && out)) n1 |= 1u << k;
+            if (((m2 >> k) & 1u) && !((sh.flags & SHAPE_CULL_HIT) && out)) n2 |= 1u << k;
+        }
+        if (!(n1 | n2)) return;
+        double r[CPL];
+        bool in[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) r[k] = 1.0, in[k] = true;
+        for_ineqs_u(g, sh, [&](const DevIneq& q) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const double h = ineq_h(&q, x[k], y[k]);
+                if (obs_smooth) {
+                    const double m = fmin(h - 0.0, 0.0);
+                    r[k] = r[k] * (m * m);
+                } else {
+                    r[k] = r[k] * fmin(0.0 - h, 0.0);
+                }
+                in[k] = in[k] && !(h > 1e-14);
+            }
+        });
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (((n1 >> k) & 1u) && !(r[k] == 0.0)) add_term(k, r[k]);
+            if ((n2 >> k) & 1u) R.hit[k] = R.hit[k] || in[k];
+        }
+    };
+    // mask words of all three tables loaded at once, before either walk (tables of <= 128
+    // shapes with masks); otherwise the generic walkers
+    const KShapeGrid& gr = g.grid;
+    const bool fast = gr.mask[0] && gr.mask[1] && gr.mask[2] && gr.mw[0] >= 1 && gr.mw[0] <= 2 &&
+                      gr.mw[1] >= 1 && gr.mw[1] <= 2 && gr.mw[2] == gr.mw[1] &&
+                      gr.mbase[2] == gr.mbase[1];
+    uint64_t mk0[CPL][2], mk1[CPL][2], mk2[CPL][2];
+    if (fast) {
+        const int mw0 = gr.mw[0], mw1 = gr.mw[1];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                mk0[k][w] = (slot0[k] >= 0 && w < mw0) ? gr.mask[0][(int64_t)slot0[k] * mw0 + w]
+                                                       : 0ull;
+                mk1[k][w] = (slot1[k] >= 0 && w < mw1) ? gr.mask[1][(int64_t)slot1[k] * mw1 + w]
+                                                       : 0ull;
+                mk2[k][w] = (slot1[k] >= 0 && w < mw1) ? gr.mask[2][(int64_t)slot1[k] * mw1 + w]
+                                                       : 0ull;
+            }
+        uint64_t any0[2] = {0ull, 0ull}, any1[2] = {0ull, 0ull};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) any0[w] |= mk0[k][w], any1[w] |= mk1[k][w] | mk2[k][w];
+        const uint64_t u00 = wave_or_u64(any0[0]), u01 = mw0 > 1 ? wave_or_u64(any0[1]) : 0ull;
+        const uint64_t u10 = wave_or_u64(any1[0]), u11 = mw1 > 1 ? wave_or_u64(any1[1]) : 0ull;
+#pragma unroll
+        for (int w = 0; w < 2; ++w)
+            for (uint64_t bb = w ? u01 : u00; bb; bb &= bb - 1) {
+                const int bit = __builtin_ctzll(bb);
+                uint32_t mine = 0;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) mine |= (uint32_t)((mk0[k][w] >> bit) & 1ull) << k;
+                body0(gr.mbase[0] + 64 * w + bit, mine);
+            }
+        k3b_finish_pen();
+#ifdef UAM_K3B_DIAG
+        e1 = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+        for (int w = 0; w < 2; ++w)
+            for (uint64_t bb = w ? u11 : u10; bb; bb &= bb - 1) {
+                const int bit = __builtin_ctzll(bb);
+                uint32_t a1 = 0, a2 = 0;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    a1 |= (uint32_t)((mk1[k][w] >> bit) & 1ull) << k;
+                    a2 |= (uint32_t)((mk2[k][w] >> bit) & 1ull) << k;
+                }
+                body1(gr.mbase[1] + 64 * w + bit, a1, a2);
+            }
+    } else {
+        wave_walk_cells<0, CPL>(g, slot0, body0);
+        k3b_finish_pen();
+#ifdef UAM_K3B_DIAG
+        e1 = __builtin_amdgcn_s_memtime();
+#endif
+        wave_walk_obs_cells<CPL>(g, slot1, body1);
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        if (slot[k] == -1) {  // no index slot (no grid, NaN point): eval_path's per-point loops
+            R.pen[k] = total_penalty(g, p, x[k], y[k]);
+            R.cnt[k] = 0;
+            for (int s = 0; s < g.n_obstacles; ++s) {
+                const double v = obstacle_psi(g, p, s, x[k], y[k]);
+                if (!(v == 0.0)) add_term(k, v);
+            }
+            R.hit[k] = collides(g, x[k], y[k]);
+        }
+    }
+#ifdef UAM_K3B_DIAG
+    {
+        const unsigned long long e2 = __builtin_amdgcn_s_memtime();
+        R.cyc0 = e1 - e0;
+        R.cyc1 = e2 - e1;
+    }
+    if (g_k3b_skip & 2) return;  // timing run: no counters
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        int nd = 0;  // distinct slots of the wave's valid points k (whole wave active here)
+        uint64_t act = __ballot(slot[k] != -2);
+        while (act) {
+            const int l0 = __builtin_ctzll(act);
+            const int s0 = __shfl(slot[k], l0, 64);
+            act &= ~__ballot(slot[k] == s0);
+            ++nd;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_k3b_diag[0], 1ull);
+            atomicAdd(&g_k3b_diag[1], (unsigned long long)nd);
+        }
+    }
+    atomicAdd(&g_k3b_diag[3], dg[1]);
+    atomicAdd(&g_k3b_diag[5], dg[3]);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_k3b_diag[2], dg[0] * CPL);
+        atomicAdd(&g_k3b_diag[4], dg[2] * CPL);
+    }
+#endif
+}
+
+// eval_path's no-fly terms of one point, added in its order (a point K3b could not park)
+__device__ __forceinline__ double k3b_psi_chain(const KGeom& g, const KParams& p, double x0,
+                                                double x1, double acc) {
+    const int slot = g.grid.gx ? grid_slot(g.grid, x0, x1) : -1;
+    if (slot >= 0) {
+        const int k1 = g.grid.start[1][slot + 1];
+        for (int k = g.grid.start[1][slot]; k < k1; ++k) {
+            const DevShape& sh = g.shape[g.grid.items[1][k]];
+            if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x0, x1)) continue;
+            acc = acc + psi(g, sh, x0, x1, p.obstacle_smooth != 0, 0.0);
+        }
+        return acc;
+    }
+    for (int s = 0; s < g.n_obstacles; ++s) acc = acc + obstacle_psi(g, p, s, x0, x1);
+    return acc;
+}
+
+// LDS of K3b (D displacements, segment S): per point Phi (f64), its first psi term (f64), the
+// index of its further terms (u16), sorted order (u16), flags (u8); the list of further terms
+// (NPT / 2 doubles) and its fill counter; all of it
+// overlaid at the end by k_eval_pairs' output staging (64 D x (6 f64 + 3 i32)).  Then the
+// histogram, the scan parts, the block's pairs and the segment's unit-arc rows.
+__host__ __device__ __forceinline__ int k3b_tcap(int npt) { return npt / 2 > 64 ? npt / 2 : 64; }
+__host__ __device__ __forceinline__ size_t k3b_seg_bytes(int D, int S) {
+    const size_t npt = (size_t)64 * D * S;
+    const size_t seg = npt * (8 + 8 + 2 + 2 + 1) + 16 + (size_t)k3b_tcap((int)npt) * 8;
+    const size_t stage = (size_t)64 * D * (6 * 8 + 3 * 4);
+    return ((seg > stage ? seg : stage) + 15) & ~(size_t)15;
+}
+__host__ __device__ __forceinline__ size_t k3b_mid_bytes(int D) {  // histogram + scan parts
+    return ((size_t)K3B_BINS * 4 + (size_t)(D + 2) * 4 + 15) & ~(size_t)15;
+}
+__host__ __device__ __forceinline__ size_t k3b_lds_bytes(int D, int S) {
+    return k3b_seg_bytes(D, S) + k3b_mid_bytes(D) + 64 * 32 + (size_t)D * S * 16;
+}
+
+template <int S, int CPL>
+__global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
+                                                         const double* __restrict__ pairs,
+                                                         int64_t n_pairs,
+                                                         const double* __restrict__ utab, int D,
+                                                         KOut out, int32_t* __restrict__ best_f,
+                                                         int32_t* __restrict__ best_l,
+                                                         const int32_t* __restrict__ order) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int BP = 64 * D, NPT = BP * S, TCAP = k3b_tcap(NPT);
+    char* base = reinterpret_cast<char*>(smem);
+    double* s_phi = reinterpret_cast<double*>(base);
+    double* s_psi = s_phi + NPT;
+    double* s_term = s_psi + NPT;
+    uint16_t* s_tix = reinterpret_cast<uint16_t*>(s_term + TCAP);
+    uint16_t* s_ord = s_tix + NPT;
+    uint8_t* s_fl = reinterpret_cast<uint8_t*>(s_ord + NPT);
+    int32_t* s_tcnt =  // after the flags (k3b_seg_bytes keeps 16 B for it)
+        reinterpret_cast<int32_t*>(base + (((size_t)NPT * 21 + (size_t)TCAP * 8 + 3) & ~(size_t)3));
+    int32_t* s_hist = reinterpret_cast<int32_t*>(base + k3b_seg_bytes(D, S));
+    int32_t* s_part = s_hist + K3B_BINS;
+    double4* s_pair = reinterpret_cast<double4*>(base + k3b_seg_bytes(D, S) + k3b_mid_bytes(D));
+    double2* s_u = reinterpret_cast<double2*>(s_pair + 64);
+    const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const bool ordered = order != nullptr;
+    const int64_t q0 = 64 * (ordered ? xcd_chunk(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
+    const bool in = q0 + lane < n_pairs;
+    const int64_t q = (ordered && in) ? (int64_t)order[q0 + lane] : q0 + lane;
+    const int N = p.N, W = N + 2;
+    const double dN = (double)N;
+    PathSrc<true> src;
+    src.W = W;
+    src.wp = nullptr;
+    src.x0 = src.y0 = src.xf = src.yf = 0.0;
+    src.za = src.zb = 0.0;
+    if (in) {
+        const double4 pr = reinterpret_cast<const double4*>(pairs)[q];
+        src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    }
+    if (d == 0) s_pair[lane] = make_double4(src.x0, src.y0, src.xf, src.yf);
+    src.u = utab + (int64_t)d * N * 2;
+    PathAcc a;
+    a.L = a.len = a.ksum = 0.0;
+#ifdef UAM_K3B_DIAG
+    unsigned long long evc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime();
+#define K3B_STAMP(k)                                                \
+    do {                                                            \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+        ph[k] += tn - tp;                                           \
+        tp = tn;                                                    \
+    } while (0)
+#else
+#define K3B_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+    if (in) path_pass1<true>(p, src, nullptr, a);
+    K3B_STAMP(0);
+    a.cost = (double)(N + 1) * a.L;
+    a.nsum = 0.0;
+    a.nh = 0;
+    a.off = 0;
+    a.below = 0;
+    a.hmax = -INFINITY;
+    a.cmin = INFINITY;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int wave = tid >> 6, nwaves = nt >> 6;
+    int j0 = 0;
+    // point tt of the segment of path-thread th (block-local pair th & 63, displacement th >> 6)
+    auto seg_point = [&](int th, int tt, double& x, double& y) {
+        const double4 pr = s_pair[th & 63];
+        const int j = j0 + tt;
+        if (j == 0) {
+            x = pr.x, y = pr.y;
+        } else if (j == W - 1) {
+            x = pr.z, y = pr.w;
+        } else {
+            const double2 u = s_u[(th >> 6) * S + tt];
+            arc_point(pr.x, pr.y, pr.z, pr.w, u.x, u.y, x, y);
+        }
+    };
+    for (; j0 < W; j0 += S) {
+        const int sn = min(S, W - j0);
+        for (int i = tid; i < K3B_BINS; i += nt) s_hist[i] = 0;
+        if (tid == 0) *s_tcnt = 0;
+        for (int i = tid; i < D * S; i += nt) {  // the segment's unit-arc rows (j = 1..N)
+            const int dd = i / S, jj = j0 + (i - dd * S);
+            if (jj >= 1 && jj <= N) {
+                const double* u = utab + ((int64_t)dd * N + (jj - 1)) * 2;
+                s_u[i] = make_double2(u[0], u[1]);
+            }
+        }
+        __syncthreads();
+        // A: key and in-bin rank of this lane's sn points
+        int key[S], rank[S];
+#pragma unroll
+        for (int t = 0; t < S; ++t) {
+            key[t] = -1;
+            rank[t] = 0;
+            if (in && t < sn) {
+                double x, y;
+                seg_point(tid, t, x, y);
+                const int slot = g.grid.gx ? grid_slot(g.grid, x, y) : -1;
+                key[t] = k3b_key(slot, g.grid.gx);
+                rank[t] = atomicAdd(&s_hist[key[t]], 1);
+            }
+        }
+        __syncthreads();
+        K3B_STAMP(1);
+        const int npts = block_excl_scan(s_hist, K3B_BINS, s_part);
+        int pos[S];  // sorted position of each of this lane's points (rank reused)
+#pragma unroll
+        for (int t = 0; t < S; ++t) {
+            pos[t] = key[t] >= 0 ? s_hist[key[t]] + rank[t] : 0;
+            if (key[t] >= 0) s_ord[pos[t]] = (uint16_t)(tid * S + t);
+        }
+        __syncthreads();
+        K3B_STAMP(2);
+        // B: evaluate 64 CPL consecutive sorted points per wave step (wave-uniform trip count)
+#ifdef UAM_K3B_DIAG
+        const int npts_b = (g_k3b_skip & 1) ? 0 : npts;
+        if (g_k3b_skip & 1)
+            for (int i = tid; i < NPT; i += nt) s_fl[i] = 0, s_phi[i] = 0.0;
+#else
+        const int npts_b = npts;
+#endif
+        for (int c0 = wave * 64 * CPL; c0 < npts_b; c0 += nwaves * 64 * CPL) {
+#ifdef UAM_K3B_DIAG
+            const unsigned long long b0 = __builtin_amdgcn_s_memtime();
+#endif
+            double x[CPL], y[CPL];
+            int slot[CPL], id[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int pos = c0 + k * 64 + lane;
+                x[k] = y[k] = 0.0;
+                slot[k] = -2;
+                id[k] = -1;
+                if (pos < npts) {
+                    id[k] = s_ord[pos];
+                    const int th = id[k] / S;
+                    seg_point(th, id[k] - th * S, x[k], y[k]);
+                    slot[k] = g.grid.gx ? grid_slot(g.grid, x[k], y[k]) : -1;
+                }
+            }
+            K3bRes<CPL> R;
+#ifdef UAM_K3B_DIAG
+            const unsigned long long b1 = __builtin_amdgcn_s_memtime();
+#endif
+            k3b_points<CPL>(g, p, x, y, slot, R);
+#ifdef UAM_K3B_DIAG
+            const unsigned long long b2 = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (id[k] < 0) continue;
+                const int ps = c0 + k * 64 + lane;  // results at the sorted position
+                int c = R.cnt[k];
+#ifdef UAM_K3B_DIAG
+                if (!(g_k3b_skip & 2)) {
+                    if (c > 0) atomicAdd(&g_k3b_diag[14], 1ull);
+                    atomicAdd(&g_k3b_diag[15], (unsigned long long)c);
+                    if (c > K3B_KT) atomicAdd(&g_k3b_diag[7], 1ull);
+                }
+#endif
+                if (c > K3B_KT) {
+                    c = K3B_REWALK;
+                } else if (c > 1) {  // terms 2..c go to the segment's list
+                    const int b = atomicAdd(s_tcnt, c - 1);
+                    if (b + c - 1 > TCAP) {
+                        c = K3B_REWALK;
+                    } else {
+                        s_tix[ps] = (uint16_t)b;
+#pragma unroll
+                        for (int m = 1; m < K3B_KT; ++m)
+                            if (m < c) s_term[b + m - 1] = R.tm[k][m];
+                    }
+                }
+                s_psi[ps] = R.tm[k][0];
+                s_phi[ps] = R.pen[k];
+                s_fl[ps] = (uint8_t)((R.hit[k] ? K3B_HIT : 0) | (c << 1));
+            }
+#ifdef UAM_K3B_DIAG
+            const unsigned long long b3 = __builtin_amdgcn_s_memtime();
+            evc[0] += R.cyc0;
+            evc[1] += R.cyc1;
+            evc[2] += b1 - b0;
+            evc[3] += b2 - b1;
+            evc[4] += b3 - b2;
+            evc[5] += 1;
+#endif
+        }
+        __syncthreads();
+        K3B_STAMP(3);
+        // C: the path's lane adds its points in waypoint order (eval_path's chains)
+        if (in) {
+#pragma unroll
+            for (int t = 0; t < S; ++t) {
+                if (t >= sn) break;
+                const int id = pos[t];
+                a.cost = a.cost + s_phi[id] / dN;
+                const uint8_t fl = s_fl[id];
+                const int c = (fl >> 1) & 7;
+                if (c == K3B_REWALK) {
+                    double x, y;
+                    seg_point(tid, t, x, y);
+                    a.nsum = k3b_psi_chain(g, p, x, y, a.nsum);
+#ifdef UAM_K3B_DIAG
+                    atomicAdd(&g_k3b_diag[6], 1ull);
+#endif
+                } else if (c) {
+                    a.nsum = a.nsum + s_psi[id];
+                    if (c > 1) {
+                        const int b = s_tix[id];
+                        for (int m = 1; m < c; ++m) a.nsum = a.nsum + s_term[b + m - 1];
+                    }
+                }
+                a.nh += (fl & K3B_HIT) ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        K3B_STAMP(4);
+    }
+    // outputs staged through LDS exactly as k_eval_pairs does (the segment arrays are dead)
+    double* s_cost = smem;
+    double* s_L = s_cost + BP;
+    double* s_len = s_L + BP;
+    double* s_k = s_len + BP;
+    double* s_n = s_k + BP;
+    double* s_clr = s_n + BP;
+    int32_t* s_nh = reinterpret_cast<int32_t*>(s_clr + BP);
+    int32_t* s_off = s_nh + BP;
+    int32_t* s_bel = s_off + BP;
+    const int slot = d * 64 + lane;
+    if (in) {
+        s_cost[slot] = a.cost;
+        s_L[slot] = a.L;
+        s_len[slot] = a.len;
+        s_k[slot] = a.ksum;
+        s_n[slot] = a.nsum;
+        s_clr[slot] = clearance(p, UAM_MODE_ANALYTIC, a);
+        s_nh[slot] = a.nh;
+        s_off[slot] = a.off;
+        s_bel[slot] = a.below;
+    }
+    __syncthreads();
+    const int qi = tid / D, di = tid - qi * D;
+    if (q0 + qi < n_pairs) {
+        const int64_t gp = (ordered ? (int64_t)order[q0 + qi] : q0 + qi) * D + di;
+        const int s = di * 64 + qi;
+        if (out.cost) out.cost[gp] = s_cost[s];
+        if (out.length_q) out.length_q[gp] = s_L[s];
+        if (out.length) out.length[gp] = s_len[s];
+        if (out.kin_sum) out.kin_sum[gp] = s_k[s];
+        if (out.nfz_sum) out.nfz_sum[gp] = s_n[s];
+        if (out.min_clearance) out.min_clearance[gp] = s_clr[s];
+        if (out.nfz_hits) out.nfz_hits[gp] = s_nh[s];
+        if (out.offmap) out.offmap[gp] = s_off[s];
+        if (out.below_terrain) out.below_terrain[gp] = s_bel[s];
+    }
+    if (d == 0 && in) {
+        if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
+        if (best_l) best_l[q] = select_best(s_len + lane, 64, D, false);
+    }
+#ifdef UAM_K3B_DIAG
+    K3B_STAMP(5);
+    if (tid == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_k3b_diag[8 + k], ph[k]);
+    if (lane == 0 && (g_k3b_skip & 2))
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_k3b_ev[k], evc[k]);
+#endif
+#undef K3B_STAMP
 }
 
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
@@ -4045,6 +4690,10 @@ struct uam_ctx {
     bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
     int k8_nstreams = 4;        // K8 large regions: streams they are spread over (UAM_K8_STREAMS)
     bool pair_order = true;     // K3: evaluate pairs in a spatial order (UAM_PAIR_ORDER=0: off)
+    int k3b_seg = 8;            // K3b segment (waypoints sorted together; UAM_K3B_SEG: 2/4/8/16,
+                                // 0 = the lane-per-path K3)
+    int k3b_cpl = 1;            // K3b points per lane in the evaluation phase (UAM_K3B_CPL: 1, 2)
+    bool k3b_attrs = false;     // K3b dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
@@ -4166,6 +4815,8 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
     if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
     if (const char* e = std::getenv("UAM_PAIR_ORDER")) c->pair_order = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_K3B_SEG")) c->k3b_seg = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K3B_CPL")) c->k3b_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K8_STREAMS"))
         c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
     *out = c;
@@ -4602,6 +5253,19 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
     return UAM_OK;
 }
 
+#ifdef UAM_K3B_DIAG
+// diagnostics build only: read and clear the K3b counters; set the phase-skip mask
+int uam_k3b_diag(uint64_t* out8, int32_t skip) {
+    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_k3b_diag), 16 * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpyFromSymbol(out8 + 16, HIP_SYMBOL(g_k3b_ev), 8 * sizeof(uint64_t)));
+    const uint64_t z[16] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_ev), z, 8 * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_diag), z, sizeof(z)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_skip), &skip, sizeof(skip)));
+    return UAM_OK;
+}
+#endif
+
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
     ctx->ktime_on = enable != 0;
@@ -4965,7 +5629,45 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
                        best_f, best_l, order)
     st = ktime_begin(ctx, s);
     if (st) return st;
-    if (mode == UAM_MODE_ANALYTIC) {
+    if (mode == UAM_MODE_ANALYTIC && !ko.g_rows && ctx->k3b_seg > 0) {
+        int S = ctx->k3b_seg >= 16 ? 16
+                : ctx->k3b_seg >= 8 ? 8 : ctx->k3b_seg >= 6 ? 6 : ctx->k3b_seg >= 4 ? 4 : 2;
+        while (S > 2 && k3b_lds_bytes(D, S) > 160 * 1024) S = S == 6 ? 4 : S / 2;
+        const int CPL = ctx->k3b_cpl >= 2 ? 2 : 1;
+        const size_t l3 = k3b_lds_bytes(D, S);
+        if (!ctx->k3b_attrs) {  // per context = per device (DeviceGuard active)
+            const void* fns[] = {(const void*)k_eval_pairs_k3b<2, 1>,
+                                 (const void*)k_eval_pairs_k3b<4, 1>,
+                                 (const void*)k_eval_pairs_k3b<8, 1>,
+                                 (const void*)k_eval_pairs_k3b<16, 1>,
+                                 (const void*)k_eval_pairs_k3b<6, 1>,
+                                 (const void*)k_eval_pairs_k3b<6, 2>,
+                                 (const void*)k_eval_pairs_k3b<2, 2>,
+                                 (const void*)k_eval_pairs_k3b<4, 2>,
+                                 (const void*)k_eval_pairs_k3b<8, 2>,
+                                 (const void*)k_eval_pairs_k3b<16, 2>};
+            for (const void* f : fns)
+                HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            160 * 1024));
+            ctx->k3b_attrs = true;
+        }
+#define UAM_LAUNCH_K3B(S_, C_)                                                                 \
+    hipLaunchKernelGGL((k_eval_pairs_k3b<S_, C_>), grid, block, l3, s, ctx->kg, ctx->kp, pairs,   \
+                       n_pairs, utab, D, ko, best_f, best_l, order)
+        switch (S * 4 + CPL) {
+            case 16 * 4 + 2: UAM_LAUNCH_K3B(16, 2); break;
+            case 8 * 4 + 2: UAM_LAUNCH_K3B(8, 2); break;
+            case 6 * 4 + 2: UAM_LAUNCH_K3B(6, 2); break;
+            case 6 * 4 + 1: UAM_LAUNCH_K3B(6, 1); break;
+            case 4 * 4 + 2: UAM_LAUNCH_K3B(4, 2); break;
+            case 2 * 4 + 2: UAM_LAUNCH_K3B(2, 2); break;
+            case 16 * 4 + 1: UAM_LAUNCH_K3B(16, 1); break;
+            case 8 * 4 + 1: UAM_LAUNCH_K3B(8, 1); break;
+            case 4 * 4 + 1: UAM_LAUNCH_K3B(4, 1); break;
+            default: UAM_LAUNCH_K3B(2, 1); break;
+        }
+#undef UAM_LAUNCH_K3B
+    } else if (mode == UAM_MODE_ANALYTIC) {
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
         if (kr.sum) {
