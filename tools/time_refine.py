@@ -17,6 +17,9 @@ def main():
     ap.add_argument("--inner", type=int, default=20)
     ap.add_argument("--nfz", type=int, default=0)
     ap.add_argument("--memory", type=int, default=8)
+    ap.add_argument("--set", action="append", default=[],
+                    help="refine setting override, e.g. --set c0=100 --set rho=10")
+    ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--empty", action="store_true",
                     help="same regions and weights, no shapes (isolates the geometry cost)")
     a = ap.parse_args()
@@ -36,9 +39,18 @@ def main():
     eng = Engine(0)
     eng.set_geometry(compile_map(build_region_map(spec)))
     eng.set_params(canonical_params(spec, N=a.N, anchor=tuple(spec["x_start"])))
-    wp = eng.gen_paths(torch.tensor(random_pairs(a.pairs, seed=3), device="cuda"),
-                       arc_table(a.N, displacements(5)))
+    pairs = random_pairs(a.pairs, seed=a.seed)
+    wp = eng.gen_paths(torch.tensor(pairs, device="cuda"), arc_table(a.N, displacements(5)))
     rp = {"n_outer": a.outer, "n_inner": a.inner, "memory": a.memory}
+    for kv in a.set:
+        k, v = kv.split("=")
+        rp[k] = float(v) if "." in v or "e" in v else int(v)
+    # endpoints inside a no-fly shape keep a path infeasible whatever the refinement does (the
+    # endpoint rows of get_nonlincon are fixed): report the feasible-endpoint paths separately
+    ends = torch.tensor(pairs.reshape(-1, 2), device="cuda")
+    pe = eng.eval_points(ends, want=("psi_raw", "collide"))
+    ok_end = ((pe["psi_raw"] == 0) & (pe["collide"] == 0)).reshape(-1, 2).all(dim=1)
+    ok_path = ok_end.repeat_interleave(5)
     eng.refine(wp[:64], rp)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -56,7 +68,21 @@ def main():
                       "steps_per_s": float(out["iters"].double().sum()) / (ms / 1e3),
                       "cost_before_mean": float(c0.mean()), "cost_after_mean": float(c1.mean()),
                       "improved_frac": float((c1 < c0).double().mean()),
-                      "infeas_median": float(out["infeas"].median())}))
+                      "infeas_median": float(out["infeas"].median()),
+                      "settings": rp,
+                      "feasible_endpoint_share": float(ok_path.double().mean()),
+                      "infeas_median_feasible_endpoints": float(out["infeas"][ok_path].median()),
+                      "infeas_p90_feasible_endpoints": float(out["infeas"][ok_path].quantile(0.9)),
+                      "share_le_1e-3_feasible_endpoints":
+                          float((out["infeas"][ok_path] <= 1e-3).double().mean()),
+                      "improved_frac_feasible_endpoints":
+                          float((c1[ok_path] < c0[ok_path]).double().mean()),
+                      # the reference keeps the best of a pair's 5 candidates (main.py:175-180)
+                      "pair_best_infeas_median_feasible_endpoints":
+                          float(out["infeas"].reshape(-1, 5).min(dim=1).values[ok_end].median()),
+                      "pair_share_le_1e-3_feasible_endpoints":
+                          float((out["infeas"].reshape(-1, 5).min(dim=1).values[ok_end] <= 1e-3)
+                                .double().mean())}))
 
 
 if __name__ == "__main__":
