@@ -14,7 +14,8 @@ import numpy as np
 from .geometry import MAX_REGIONS, FlatGeometry, compile_spec  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# UAM_ORACLE_LIB: another build of the same source (tools/sanitize_host.sh: ASan + UBSan)
+LIB_PATH = os.environ.get("UAM_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _f64p = ctypes.POINTER(ctypes.c_double)

@@ -11,7 +11,7 @@
  *
  * Every routine restates, in plain float64 C with the reference's operation order, one
  * reference function (file:line relative to /root/reference/geo_simulation_project/):
- *   ineq_h          polygon.py:69-71,98  ball.py:209-213(func)  square.py:266-288
+ *   ineq_h          polygon.py:69-71,98  ball.py:33-37(func)  square.py:29-52(right/left/top/bottom)
  *   psi             path_generation/quadratic_obstacle.py:27-39  (penalty_function)
  *   contains        path_generation/quadratic_obstacle.py:89-94, map.py:41-43 (collides)
  *   region_penalty  path_generation/problem.py:59-82 (get_penalty_function)

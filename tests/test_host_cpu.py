@@ -159,3 +159,27 @@ def test_synthetic_dem_statistics():
     v = dem[valid].astype(np.float64)
     assert v.min() >= S.DEM_MIN - 1e-3 and v.max() <= S.DEM_MAX + 1e-3
     assert abs(v.mean() - S.DEM_MEAN) < 15 and abs(v.std() - S.DEM_STD) < 15
+
+
+def test_function_compose_host():
+    """Function.compose (function.py:122-157): h(A x + b) on the host callables, the
+    reference's shape errors, and the device spec dropped (map compilation rejects it)."""
+    import numpy as np
+    import pytest
+
+    from uam_path_planning_amd.geometry import compile_shapes
+    from uam_path_planning_amd.path_generation import ball
+
+    obs = ball([1.0, 2.0], 1.0, 2.0)
+    h = obs.inequalities[0]
+    x = np.array([[3.0], [1.0]])
+    ref = float(np.asarray(h(np.array([[3.0 * 2.0 + 0.5], [1.0 * 2.0 - 1.0]]))).reshape(-1)[0])
+    h.compose(np.array([[2.0]]), np.array([[0.5], [-1.0]]))
+    assert float(np.asarray(h(x)).reshape(-1)[0]) == ref
+    assert h.spec is None
+    with pytest.raises(ValueError):
+        compile_shapes([obs], [])
+    with pytest.raises(ValueError, match="translation vector"):
+        ball([0.0, 0.0], 1.0).inequalities[0].compose(np.eye(2), np.zeros(2))
+    with pytest.raises(ValueError, match="scaling matrix"):
+        ball([0.0, 0.0], 1.0).inequalities[0].compose(np.eye(3))

@@ -14,6 +14,13 @@
 //   final filter -> Polygon(box).area > min_approx_polygon_area
 // Pinned: the reference's data/raw/populated_area -> data/processed/populated_area.txt
 // (29/29 rectangles, vertex order included; tests/test_polygons_cpu.py).
+//
+// Attribution: calipers() and min_area_rect_box() below follow the rotating-calipers routine of
+// OpenCV (modules/imgproc/src/rotcalipers.cpp, cv::minAreaRect / rotatingCalipers) step by
+// step -- the same variable roles and control flow -- because float32 bit-parity with
+// cv2.minAreaRect is the requirement.  OpenCV is distributed under the Apache License 2.0
+// (4.5 and later; the 3-clause BSD license before): Copyright (C) 2000-2022 Intel
+// Corporation, Willow Garage Inc., Itseez Inc., OpenCV Foundation and other contributors.
 #include "polyproc.h"
 
 #include <algorithm>

@@ -4,6 +4,7 @@ PyTorch is plumbing here (allocation, streams, H2D/D2H); every arithmetic step o
 runs in the hand-written HIP kernels of csrc/uampath.hip.  There is no CPU fallback: without a
 visible GPU or without libuampath.so, constructing an Engine raises.
 """
+import collections
 import ctypes
 from dataclasses import dataclass, field
 
@@ -555,10 +556,27 @@ def default_engine(device=None):
 
 
 # ---- single-shape helpers used by the drop-in classes (scratch contexts) ------------------
+# The reference evaluates psi / contains / collides point by point (problem.py:72-80 calls
+# psi(x) per shape per point).  Each distinct (geometry, options) pair gets one context with its
+# geometry and parameters uploaded once, kept in a small LRU cache, so a per-point loop costs
+# one copy in, one launch and one copy out per call -- no allocation, upload or k_prepare.
+_SCRATCH_MAX = 64
+_scratch_cache = collections.OrderedDict()
+
+
 def _scratch(geom, params):
-    eng = Engine(default_engine().device)
+    dev = default_engine().device
+    key = (dev, geom.signature(), repr(params))
+    eng = _scratch_cache.get(key)
+    if eng is not None:
+        _scratch_cache.move_to_end(key)
+        return eng
+    eng = Engine(dev)
     eng.set_geometry(geom)
     eng.set_params(params)
+    _scratch_cache[key] = eng
+    if len(_scratch_cache) > _SCRATCH_MAX:
+        _scratch_cache.popitem(last=False)
     return eng
 
 

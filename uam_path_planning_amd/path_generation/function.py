@@ -53,16 +53,29 @@ class Function:
         return self.f(x)
 
     def compose(self, A, b=None):
-        """h(A x + b).  Shape checks follow function.py:142-157 (a (2,) translation raises the
-        reference's ValueError); affine composition itself is not part of the device path."""
+        """In place, h(x) -> h(A x + b) with grad A^T grad h(A x + b) and hessian A H(x) A^T
+        (the reference's own expression), as function.py:122-157 (a 1 x 1 A scales the identity; b defaults to
+        0 and must be (m, 1), else the reference's ValueError).  The result is a host callable
+        only: its device spec is dropped, so a shape holding it is rejected when a map is
+        compiled for the device (the kernels evaluate the three shape kinds as built)."""
         A = np.asarray(A)
         m, n = A.shape
         if m == 1 and n == 1:
             m = len(b) if b is not None else self.n
+            n = m
+            A = A * np.eye(m)
         elif self._n is not None and self.n != m:
             raise ValueError(f"Size mismatch between function '{self.n}' and scaling matrix A "
                              f"'{A.shape}'")
-        if b is not None and np.asarray(b).shape != (m, 1):
+        b = np.zeros((m, 1)) if b is None else b
+        if np.asarray(b).shape != (m, 1):
             raise ValueError(f"Size mismatch between scaling matrix A '{A.shape}' and "
                              f"translation vector '{np.asarray(b).shape}'")
-        raise NotImplementedError("affine composition of shapes is outside the device hot path")
+        f0, g0, h0 = self.f, self.grad, self.hess
+        self.f = lambda x: f0(A @ x + b)
+        if g0 is not None:
+            self.grad = lambda x: A.T @ g0(A @ x + b)
+            if h0 is not None:
+                self.hess = (lambda x: A @ h0(x) @ A.T) if callable(h0) else A @ h0 @ A.T
+        self._n = n
+        self.spec = None
