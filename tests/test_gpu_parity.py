@@ -691,3 +691,55 @@ def test_raster_summary_table(eng, oracle_mod):
     big = raster_geo(4096)
     with pytest.raises(ValueError):
         eng.raster_summary(type(raster)(big, None), 8)
+
+
+@pytest.mark.parametrize("mode", ["analytic", "raster"])
+def test_pair_order_two_streams(oracle_mod, mode):
+    """The pair-order scratch is owned by the context: two batches of >= 4096 pairs
+    enqueued on two streams of the same context, with no host synchronisation in between, must
+    both come out exactly as the oracle says (a shared, unordered scratch would hand one launch
+    the other's order: pairs evaluated twice or never)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import (CONFIGS, build_region_map, canonical_params,
+                                                canonical_spec, displacements, raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    e = Engine(0)
+    spec = canonical_spec(nfz_polygons=CONFIGS["cfg3"]["nfz_polygons"])
+    params = canonical_params(spec, N=40, altitude=320.0)
+    e.set_geometry(compile_map(build_region_map(spec)))
+    e.set_params(params)
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), params.N, spec["options"],
+                            spec["maxratio"], spec["maxalpha"], spec["enlargement"],
+                            spec["weights"], altitude=params.altitude)
+    D = 5
+    ut = arc_table(params.N, displacements(D))
+    kw, okw = {}, {}
+    if mode == "raster":
+        geo = raster_geo(512)
+        raster = e.raster_build(geo, synthetic_dem(512))
+        kw = {"raster": raster}
+        okw = {"mode": "raster",
+               "rdesc": oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx,
+                                                      geo.dy, geo.nodata, geo.dem_threshold),
+               "rec": raster.rec.cpu().numpy().view(np.float32)}
+    pa, pb = random_pairs(6000, seed=31), random_pairs(4500, seed=32)
+    ta = e.tensor(pa, torch.float64)
+    tb = e.tensor(pb, torch.float64)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):  # several rounds so the launches overlap
+        with torch.cuda.stream(s1):
+            ga = e.eval_generated(ta, ut, **kw)
+        with torch.cuda.stream(s2):
+            gb = e.eval_generated(tb, ut, **kw)
+        outs.append((ga, gb))
+    torch.cuda.synchronize()
+    ra = orc.eval_paths(oracle_mod.gen_paths(pa, ut), **okw)
+    rb = orc.eval_paths(oracle_mod.gen_paths(pb, ut), **okw)
+    for ga, gb in outs:
+        _assert_paths_equal(ga, ra, raster=mode == "raster")
+        _assert_paths_equal(gb, rb, raster=mode == "raster")
