@@ -519,16 +519,23 @@ __device__ __forceinline__ int32_t raster_cell_skip(const KRaster& rs, const uin
 // in flight, consumed in waypoint order exactly as consume_chunk does.  (Compacting each chunk
 // to the lane's next 8 needed waypoints measured 3x slower: the per-slot forward scans
 // diverge.)
+#ifndef UAM_SKIP_CHUNK
+#define UAM_SKIP_CHUNK 8  // gathers per chunk (tuning builds: -DUAM_SKIP_CHUNK=...)
+#endif
+#ifndef UAM_SKIP_MINW
+#define UAM_SKIP_MINW 5   // waves per SIMD the skip kernel is compiled for
+#endif
 template <bool GEN>
 __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4* __restrict__ rec,
                                                   const uint32_t* bits, const PathSrc<GEN>& src,
                                                   int W, int32_t* cells, double dN, PathAcc& a) {
+    constexpr int CH = UAM_SKIP_CHUNK;
     bool anyskip = false;
-    for (int j0 = 0; j0 < W; j0 += 8) {
-        uint4 r[8];
+    for (int j0 = 0; j0 < W; j0 += CH) {
+        uint4 r[CH];
         uint32_t inb = 0, need = 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < CH; ++t) {
             if (j0 + t < W) {
                 double x0, x1;
                 src.at(j0 + t, x0, x1);
@@ -546,7 +553,7 @@ __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4
         }
         anyskip = anyskip || (inb & ~need);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < CH; ++t) {
             if (j0 + t >= W) break;
             if (!((inb >> t) & 1u)) {
                 ++a.off;
@@ -5671,7 +5678,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
         if (kr.sum) {
-            UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, 8, false, 5);  // occupancy 5 (6 spilled)
+            UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, 8, false, UAM_SKIP_MINW);  // 5 (6 spilled)
         } else switch (v) {
             case 2: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 1); break;
             case 3: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 1); break;
