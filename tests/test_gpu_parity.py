@@ -743,3 +743,36 @@ def test_pair_order_two_streams(oracle_mod, mode):
     for ga, gb in outs:
         _assert_paths_equal(ga, ra, raster=mode == "raster")
         _assert_paths_equal(gb, rb, raster=mode == "raster")
+
+
+@pytest.mark.parametrize("order", ["1", "0"])
+def test_volume_pair_order(oracle_mod, monkeypatch, order):
+    """Config 5's kernel with the raster pair order over the volume's x/y extent (batches of
+    >= 4096 pairs; UAM_PAIR_ORDER on and off): every output and the selection bit-exact vs
+    the oracle -- each pair is still read and written at its own index."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.scenario import (canonical_spec, displacements, layer_weights,
+                                                raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs3d, synthetic_dem
+
+    monkeypatch.setenv("UAM_PAIR_ORDER", order)
+    e = Engine(0)
+    spec = canonical_spec(nfz_polygons=8)
+    orc = _setup(e, oracle_mod, spec, 24, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"])
+    R, nz, z0, dz = 256, 32, 0.0, 20.0
+    geo = raster_geo(R)
+    r2 = e.raster_build(geo, synthetic_dem(R))
+    lw = layer_weights(nz)
+    vol = e.volume_build(r2, nz, z0, dz, lw)
+    vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, z0, dz)
+    ref_vol = oracle_mod.volume_build(vd, _np(r2.rec).view(np.float32), lw)
+    pairs = random_pairs3d(5000, seed=9, zmin=-50.0, zmax=700.0)
+    ut = arc_table(24, displacements(5))
+    ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    for gk, ok in PATH_KEYS + (("below_terrain", "below"), ("min_clearance", "min_clearance")):
+        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+    np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                  oracle_mod.argmin(ref["cost"], 5, True))

@@ -4597,16 +4597,20 @@ __device__ __forceinline__ uint32_t rorder_key(const double4 pr, const KOrdBox& 
     return k;
 }
 
+// pairs [n][4] (x0, y0, xf, yf), or [n][6] (x0, y0, z0, xf, yf, zf) when vol (config 5)
 __global__ __launch_bounds__(256) void k_rorder_hist(const double* __restrict__ pairs, int64_t n,
                                                      KOrdBox box, uint16_t* __restrict__ key,
-                                                     int32_t* __restrict__ H) {
+                                                     int32_t* __restrict__ H, int vol) {
     __shared__ int32_t h[RORD_BINS];
     const int t = threadIdx.x, blk = blockIdx.x;
     for (int b = t; b < RORD_BINS; b += 256) h[b] = 0;
     __syncthreads();
     const int64_t lo = n * blk / RORD_NB, hi = n * (blk + 1) / RORD_NB;
     for (int64_t i = lo + t; i < hi; i += 256) {
-        const uint32_t k = rorder_key(reinterpret_cast<const double4*>(pairs)[i], box);
+        const double4 pr =
+            vol ? make_double4(pairs[6 * i], pairs[6 * i + 1], pairs[6 * i + 3], pairs[6 * i + 4])
+                : reinterpret_cast<const double4*>(pairs)[i];
+        const uint32_t k = rorder_key(pr, box);
         key[i] = (uint16_t)k;
         atomicAdd(&h[k], 1);
     }
@@ -5355,7 +5359,7 @@ static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t 
 
 // K2 pair order over the raster extent (k_rorder_hist / k_rorder_scatter)
 static int raster_pair_order(uam_ctx* ctx, const KRaster& kr, const double* pairs, int64_t n,
-                             hipStream_t s, const int32_t** order) {
+                             hipStream_t s, const int32_t** order, int vol = 0) {
     *order = nullptr;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t b_h = al((size_t)RORD_BINS * RORD_NB * 4), b_key = al((size_t)n * 2),
@@ -5369,7 +5373,7 @@ static int raster_pair_order(uam_ctx* ctx, const KRaster& kr, const double* pair
     const double ex = kr.nx * kr.dx, ey = kr.ny * kr.dy;
     const KOrdBox box{kr.x0, kr.y_top - ey, (double)(1 << RORD_BITS) / ex,
                       (double)(1 << RORD_BITS) / ey};
-    hipLaunchKernelGGL(k_rorder_hist, dim3(RORD_NB), dim3(256), 0, s, pairs, n, box, key, H);
+    hipLaunchKernelGGL(k_rorder_hist, dim3(RORD_NB), dim3(256), 0, s, pairs, n, box, key, H, vol);
     hipLaunchKernelGGL(k_rorder_scatter, dim3(RORD_NB), dim3(256), 0, s, (const uint16_t*)key, n,
                        (const int32_t*)H, ord);
     HIP_TRY(hipGetLastError());
@@ -5802,14 +5806,25 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    // the raster pair order over the volume's x/y extent (results do not depend on it)
+    const int32_t* order = nullptr;
+    if (ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
+        KRaster kxy{};
+        kxy.nx = kv.nx, kxy.ny = kv.ny, kxy.x0 = kv.x0, kxy.y_top = kv.y_top;
+        kxy.dx = vd->dx, kxy.dy = vd->dy;
+        st = raster_pair_order(ctx, kxy, pairs6, n_pairs, (hipStream_t)stream, &order, 1);
+        if (st) return st;
+    }
     st = ktime_begin(ctx, (hipStream_t)stream);
     if (st) return st;
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
-                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l,
-                       nullptr);
+                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l, order);
     HIP_TRY(hipGetLastError());
-    return ktime_end(ctx, (hipStream_t)stream);
+    st = ktime_end(ctx, (hipStream_t)stream);
+    if (st) return st;
+    if (order) return order_done(ctx, (hipStream_t)stream);
+    return UAM_OK;
 }
 
 static int refine_memory(const uam_refine_params* rp) {
