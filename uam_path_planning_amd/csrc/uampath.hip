@@ -79,7 +79,7 @@ struct alignas(16) DevShape {  // 128 B
     double box_obs[4];
     int32_t region;     // region of a region shape, -1 for obstacles
     int32_t pad0;
-    double pad1;
+    double wreg;        // weight of its region (uam_set_params; 0 for obstacles)
 };
 
 __host__ __device__ __forceinline__ bool outside(const double* b, double x0, double x1) {
@@ -1756,10 +1756,10 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
             slot[k] = valid[k] ? (g.grid.gx ? grid_slot(g.grid, xc, yc[k]) : -1) : -2;
         }
         // Φ: total_penalty's region loop, per cell
-        double pen[CPL], t[CPL];
+        double pen[CPL], t[CPL], wc[CPL];  // wc: the weight of the cell's current region
         int rc[CPL];
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) pen[k] = t[k] = 0.0, rc[k] = -1;
+        for (int k = 0; k < CPL; ++k) pen[k] = t[k] = wc[k] = 0.0, rc[k] = -1;
         wave_walk_cells<0, CPL>(g, slot, [&](int s, uint32_t mine) {
             if (!mine) return;
             const DevShape sh = uload(g.shape, s);
@@ -1768,8 +1768,9 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
             for (int k = 0; k < CPL; ++k) {
                 if (!((mine >> k) & 1u)) continue;
                 if (sh.region != rc[k]) {
-                    if (rc[k] >= 0) pen[k] = pen[k] + p.weights[rc[k]] * t[k];
+                    if (rc[k] >= 0) pen[k] = pen[k] + wc[k] * t[k];
                     rc[k] = sh.region;
+                    wc[k] = sh.wreg;  // p.weights[sh.region], from the shape record
                     t[k] = 0.0;
                 }
                 if (!((sh.flags & SHAPE_CULL_PEN) && outside(sh.box_pen, xc, yc[k])))
@@ -1800,7 +1801,7 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
         });
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
-            if (rc[k] >= 0) pen[k] = pen[k] + p.weights[rc[k]] * t[k];
+            if (rc[k] >= 0) pen[k] = pen[k] + wc[k] * t[k];
         // Σψ_nfz (obstacle_psi_sum, e = 0) and Map.collides, one h per inequality for both
         double acc[CPL];
         bool hit[CPL];
@@ -2020,7 +2021,7 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
         if (!mine) return;
         const DevShape sh = uload(g.shape, s);
         uint32_t need = 0;
-        const double wnew = p.weights[sh.region];  // wave-uniform region: a scalar read
+        const double wnew = sh.wreg;  // the region's weight, in the same record load
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             if (!((mine >> k) & 1u)) continue;
@@ -5083,6 +5084,10 @@ int uam_set_params(uam_ctx* ctx, const uam_params* prm, uam_stream stream) {
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
         HIP_TRY(hipMemcpy(ctx->h_shape.data(), ctx->d_shape, sizeof(DevShape) * ctx->n_shapes,
                           hipMemcpyDeviceToHost));
+        // each region shape carries its region's weight (p.weights[region], bit for bit)
+        for (DevShape& d : ctx->h_shape) d.wreg = d.region >= 0 ? k.weights[d.region] : 0.0;
+        HIP_TRY(hipMemcpy(ctx->d_shape, ctx->h_shape.data(), sizeof(DevShape) * ctx->n_shapes,
+                          hipMemcpyHostToDevice));
     }
     st = build_shape_grid(ctx);
     if (st) return st;
