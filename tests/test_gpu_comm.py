@@ -86,3 +86,32 @@ def test_bcast_raster_group_single_process(eng):
     eng.bcast_raster(t, root=0)
     torch.cuda.synchronize()
     assert torch.equal(t.cpu(), torch.arange(4096, dtype=torch.int32))
+
+
+def test_kernel_timing_events(eng):
+    """uam_kernel_timing / uam_kernel_time (bench.py's kernel_ms): one event pair per launch of
+    the dominant kernel on the launch stream, none while stopped, reset by each query."""
+    import numpy as np
+
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import (build_region_map, canonical_params,
+                                                canonical_spec, displacements, raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    spec = canonical_spec()
+    eng.set_geometry(compile_map(build_region_map(spec)))
+    eng.set_params(canonical_params(spec, N=40))
+    ut = arc_table(40, displacements(5))
+    raster = eng.raster_build(raster_geo(256), synthetic_dem(256))
+    pairs = random_pairs(5000, seed=1)
+    eng.kernel_timing(True)
+    for _ in range(3):
+        eng.eval_generated(pairs, ut, raster=raster)
+    eng.eval_generated(pairs, ut)               # analytic (K3b) counts too
+    ms, n = eng.kernel_time()
+    assert n == 4 and np.isfinite(ms) and ms > 0.0
+    assert eng.kernel_time() == (0.0, 0)        # the query resets
+    eng.kernel_timing(False)
+    eng.eval_generated(pairs, ut, raster=raster)
+    assert eng.kernel_time() == (0.0, 0)

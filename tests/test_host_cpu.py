@@ -183,3 +183,20 @@ def test_function_compose_host():
         ball([0.0, 0.0], 1.0).inequalities[0].compose(np.eye(2), np.zeros(2))
     with pytest.raises(ValueError, match="scaling matrix"):
         ball([0.0, 0.0], 1.0).inequalities[0].compose(np.eye(3))
+
+
+def test_bench_roofline_bookkeeping():
+    """bench.py's roofline fields are recomputable from the line alone: frac = (16 W + 16) B x
+    paths / kernel_ms / 8 TB/s, traffic and its ratio from the PMC record."""
+    import bench
+
+    prof = {"l2_fabric_bytes_per_launch": 4.264e9, "l2_hit_rate": 0.14, "source": "x"}
+    r = bench.gather_roofline(prof, 500_000, 82, 0.7105, "k")
+    assert r["algorithmic_bytes_per_path"] == 1328
+    assert r["algorithmic_bytes_per_launch"] == 1328 * 500_000
+    assert abs(r["frac"] - 1328 * 500_000 / 0.7105e-3 / 1e9 / 8000.0) < 1e-4
+    assert r["traffic"] == 4.264e9 and abs(r["traffic_over_algorithmic"] - 6.42) < 0.01
+    assert "Infinity-Cache" in r["traffic_label"]
+    a = bench.analytic_roofline({"f64_flop_per_launch": 1.3e10}, 500_000, 3.55, "k3b")
+    assert a["unit"] == "TFLOP/s" and abs(a["achieved"] - 1.3e10 / 3.55e-3 / 1e12) < 1e-3
+    assert bench.analytic_roofline({}, 1, 1.0, "k")["frac"] is None
