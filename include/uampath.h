@@ -209,11 +209,10 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
 /* K2 gather skip (build-defined; no reference counterpart; results unchanged).  A bitmap
  * summary of a record raster: one bit per block x block cells (blocks row-major, nby x nbx;
  * bit b in 32-bit word b / 32), set when every cell of the block has phi == +-0,
- * psi_nfz == +-0, no no-fly flag and a terrain <= 0 (dem, 0 on nodata cells; NaN clears it).
- * K2 keeps the bitmap in LDS and does not gather the records of waypoints in set blocks (they
- * add exactly nothing to cost, no-fly sum and hits); when a path skipped some and the terrain
- * maximum of the rest is < 0, it fetches those too, so every output stays bit-identical to
- * uam_eval_generated.  block: a power of two in [1, 1024] with at most 65536 blocks, or 0 =
+ * psi_nfz == +-0, no no-fly flag and a terrain that reads +0.0 (a nodata cell, or a dem value
+ * of +0.0f).  K2 / K2s keep the bitmap in LDS and do not gather the records of waypoints in set
+ * blocks: they add exactly nothing to cost, no-fly sum and hits, and +0.0 to the terrain
+ * maximum, so every output stays bit-identical to uam_eval_generated.  block: a power of two in [1, 1024] with at most 65536 blocks, or 0 =
  * automatic (8, doubled until the blocks fit).  The bitmap holds ceil(nbx * nby / 32) words and
  * must be rebuilt whenever rec changes. */
 int uam_raster_summary_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,

@@ -492,13 +492,15 @@ __device__ __forceinline__ void consume_chunk(const Chunk<C>& ch, int j0, int W,
 
 // ---- K2 gather skip (uam_raster_summary; build-defined, no reference counterpart) --------
 // A bitmap with one bit per B x B cell block, set when every cell of the block has phi == +-0,
-// psi == +-0, no no-fly flag and a terrain <= 0 (0 on nodata cells, as consume_chunk reads it;
-// NaN terrain clears the bit).  A waypoint in a set block adds exactly nothing to the cost and
-// no-fly sums (x + (+-0) == x for every accumulator, none of which is ever -0) and nothing to
-// nfz_hits, and its terrain cannot raise a path maximum that is >= 0.  K2 holds the bitmap in
-// LDS (<= 8 KiB), so the test costs no memory request; it gathers only the other waypoints and,
-// when it skipped some and the maximum it gathered is < 0 (or none), fetches the skipped
-// records too.  Every output is bit-identical to gathering every waypoint.
+// psi == +-0, no no-fly flag and a terrain that reads +0.0 (a nodata cell, as consume_chunk
+// reads it, or a DEM value of +0.0f: open sea).  A waypoint in a set block adds exactly nothing
+// to the cost and no-fly sums (x + (+-0) == x for every accumulator, none of which is ever -0)
+// and nothing to nfz_hits, and its terrain is exactly +0.0, so the path maximum takes
+// fmax(hmax, +0.0) with no memory request.  K2 holds the bitmap in LDS (<= 8 KiB), so the test
+// costs no memory request either; it gathers only the other waypoints.  Every output is
+// bit-identical to gathering every waypoint.  (Round 2's first form also set the bit over
+// terrain < 0 and re-fetched the skipped records of paths whose gathered maximum stayed < 0;
+// those re-walks cost K2s 50-60 us per cfg3 launch and are gone with the +0.0 rule.)
 constexpr int SKIP_MAX_BITS = 65536;  // 8 KiB of LDS
 
 // raster cell of a point (uampath.h convention: float64 floor of the scaled offset; -1 off the
@@ -530,7 +532,6 @@ __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4
                                                   const uint32_t* bits, const PathSrc<GEN>& src,
                                                   int W, int32_t* cells, double dN, PathAcc& a) {
     constexpr int CH = UAM_SKIP_CHUNK;
-    bool anyskip = false;
     for (int j0 = 0; j0 < W; j0 += CH) {
         uint4 r[CH];
         uint32_t inb = 0, need = 0;
@@ -551,7 +552,6 @@ __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4
                 }
             }
         }
-        anyskip = anyskip || (inb & ~need);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             if (j0 + t >= W) break;
@@ -560,24 +560,16 @@ __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4
                 a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
                 continue;
             }
-            if (!((need >> t) & 1u)) continue;  // adds +-0: an exact no-op
+            if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
+                a.hmax = fmax(a.hmax, 0.0);
+                continue;
+            }
             a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
             a.nsum = a.nsum + (double)__uint_as_float(r[t].y);
             a.nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
             const double terrain =
                 (r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r[t].z);
             a.hmax = fmax(a.hmax, terrain);
-        }
-    }
-    if (anyskip && !(a.hmax >= 0.0)) {  // a skipped terrain (<= 0) may be the maximum
-        for (int j = 0; j < W; ++j) {
-            double x0, x1;
-            src.at(j, x0, x1);
-            bool sk;
-            const int32_t cl = raster_cell_skip(rs, bits, x0, x1, sk);
-            if (!sk) continue;
-            const uint4 r = rec[cl];
-            a.hmax = fmax(a.hmax, (r.w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r.z));
         }
     }
 }
@@ -598,9 +590,8 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
         for (int iy = y0; iy < y1 && skip; ++iy)
             for (int ix = x0; ix < x1; ++ix) {
                 const uint4 r = rec[(int64_t)iy * nx + ix];
-                const float t = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
-                if ((r.x & 0x7fffffffu) || (r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ) ||
-                    !(t <= 0.0f)) {
+                const uint32_t t = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
+                if ((r.x & 0x7fffffffu) || (r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ) || t) {
                     skip = false;
                     break;
                 }
@@ -4660,6 +4651,303 @@ __global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restri
     for (int64_t i = lo + t; i < hi; i += 256) order[atomicAdd(&off[key[i]], 1)] = (int32_t)i;
 }
 
+// ---- K2s: segment-sorted raster evaluation (build-defined; no reference counterpart) --------
+// K2 (one lane walks one path's W waypoints) is bound by scattered 128-B record lines: 14% L2
+// hits and 6.4x the algorithmic bytes across the fabric (profiles/r02/final).  K2s cuts every
+// path into nseg segments of L = ceil(W / nseg) waypoints and evaluates segment k of all paths
+// in one launch, the (path, segment) items sorted by the Morton key of the 64 x 64-tile raster
+// tile under the segment's middle waypoint, so the workgroups an XCD runs together gather from
+// one region of the raster.  Between launches a path's running sums live in a 32-B SegState;
+// every waypoint is still added in waypoint order with raster_pass2_skip's arithmetic (the
+// order of the items changes which lane does the work, never the operations a path sees), so
+// every output is bit-identical to K2's.  Launches (default form): k_seg_hist -> scan ->
+// k_seg_scatter for segment 0's order, then segment 0 (k_seg_eval<.., FIRST>: the lane runs
+// the path's pass 1 too, so its ALU work overlaps the gathers as in K2) while the other
+// segments' orders are sorted on the side stream, then segments 1.. (workgroups per CU capped
+// through an LDS floor, UAM_K2S_LDS), then k_seg_final (outputs, the main.py:175-180
+// selection).  UAM_K2S_FUSE=0 runs pass 1 as its own kernel (k_seg_pass1) on the side stream
+// instead, optionally part by part (UAM_K2S_SPLIT).  Measured on cfg3: DESIGN.md §4 K2s.
+#ifndef UAM_SEG_TBITS
+#define UAM_SEG_TBITS 6  // tuning builds: -DUAM_SEG_TBITS=5 (32 x 32 tiles)
+#endif
+constexpr int SEG_TBITS = UAM_SEG_TBITS;               // 64 x 64 tiles over the raster
+constexpr int SEG_BINS = (1 << (2 * SEG_TBITS)) + 1;   // + one bin for off-raster / NaN
+constexpr int SEG_NBK = 256;                           // partitions of a segment's items
+constexpr int SEG_MAX = 8;                             // segments per path
+constexpr int SEG_MAXSPLIT = 4;                        // path parts (KSeg::nsplit)
+
+struct SegState {  // 32 B per path
+    double cost, nsum, hmax;
+    int32_t nh, off;
+};
+
+struct KSeg {
+    const double* __restrict__ pairs;
+    const double* __restrict__ utab;
+    int64_t n_pairs;
+    int32_t P, D, W, nseg, L, F, tshift;  // segment 0 = [0, F), then segments of L
+    int32_t nsplit;             // path parts [P h / nsplit, P (h+1) / nsplit), sorted apart
+    int32_t g0;                 // sort launches: first group (blockIdx.y = g - g0)
+    int64_t obase;              // sort launches: order index of group g0's first item
+    SegState* __restrict__ st;  // [P]
+    double4* __restrict__ p1;   // [P] pass 1: (L, length, kinematic sum, 0)
+    uint16_t* __restrict__ key; // [nseg][P] sort keys
+    int32_t* __restrict__ cnt;  // [nsplit][nseg][SEG_BINS][SEG_NBK] counts -> offsets
+    int32_t* __restrict__ tot;  // scan block totals
+    int32_t* __restrict__ order;  // [nsplit][nseg][part] path of each sorted item
+    __device__ __forceinline__ void bounds(int s, int& j0, int& j1) const {
+        j0 = s == 0 ? 0 : F + (s - 1) * L;
+        j1 = min(s == 0 ? F : F + s * L, W);
+    }
+    __device__ __forceinline__ int32_t part_lo(int h) const {
+        return (int32_t)((int64_t)P * h / nsplit);
+    }
+};
+
+__device__ __forceinline__ PathSrc<true> seg_src(const KSeg& ks, int N, int32_t path) {
+    const int32_t q = path / ks.D, d = path - q * ks.D;
+    const double4 pr = reinterpret_cast<const double4*>(ks.pairs)[q];
+    PathSrc<true> src;
+    src.W = N + 2;
+    src.wp = nullptr;
+    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    src.u = ks.utab + (int64_t)d * N * 2;
+    src.za = src.zb = 0.0;
+    return src;
+}
+
+// pass 1 of every path (path_pass1: L, length, kinematic sum) and its state seed
+// cost = (N+1) L (eval_path), thread = path in natural order (coalesced stores)
+__global__ __launch_bounds__(256) void k_seg_pass1(KParams p, KSeg ks, KOut out, int32_t p0,
+                                                   int32_t p1) {
+    const int64_t i = p0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= p1) return;
+    const PathSrc<true> src = seg_src(ks, p.N, (int32_t)i);
+    PathAcc a;
+    path_pass1<true>(p, src, nullptr, a);
+    ks.p1[i] = make_double4(a.L, a.len, a.ksum, 0.0);
+    SegState s;
+    s.cost = (double)(p.N + 1) * a.L;
+    s.nsum = 0.0;
+    s.hmax = -INFINITY;
+    s.nh = 0;
+    s.off = 0;
+    ks.st[i] = s;
+}
+
+// sort key of segment s of path i: Morton code of the tile under its middle waypoint
+__device__ __forceinline__ uint32_t seg_key(const KSeg& ks, const KRaster& rs, int N, int32_t i,
+                                            int s) {
+    int j0, j1;
+    ks.bounds(s, j0, j1);
+    const PathSrc<true> src = seg_src(ks, N, i);
+    double x0, x1;
+    src.at((j0 + j1 - 1) >> 1, x0, x1);
+    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+    if (!((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)))
+        return SEG_BINS - 1;
+    const uint32_t tx = (uint32_t)fx >> ks.tshift, ty = (uint32_t)fy >> ks.tshift;
+    uint32_t k = 0;
+#pragma unroll
+    for (int b = SEG_TBITS - 1; b >= 0; --b) k = (k << 2) | (((ty >> b) & 1u) << 1) | ((tx >> b) & 1u);
+    return k;
+}
+
+// counting sort, launch 1: block (b, g) keys partition b of group g = (part h, segment s)'s
+// items and stores its LDS histogram bin-major, so the scan of cnt yields each
+// (group, bin, partition)'s offset; group g's items land in one contiguous run of order
+__device__ __forceinline__ void seg_group(const KSeg& ks, int g, int b, int& s, int32_t& lo,
+                                          int32_t& hi) {
+    const int h = g / ks.nseg;
+    s = g - h * ks.nseg;
+    const int32_t p0 = ks.part_lo(h), n = ks.part_lo(h + 1) - p0;
+    lo = p0 + (int32_t)((int64_t)n * b / SEG_NBK);
+    hi = p0 + (int32_t)((int64_t)n * (b + 1) / SEG_NBK);
+}
+
+__global__ __launch_bounds__(256) void k_seg_hist(KParams p, KRaster rs, KSeg ks) {
+    __shared__ int32_t h[SEG_BINS];
+    const int t = threadIdx.x, b = blockIdx.x, g = blockIdx.y + ks.g0;
+    for (int k = t; k < SEG_BINS; k += 256) h[k] = 0;
+    __syncthreads();
+    int s;
+    int32_t lo, hi;
+    seg_group(ks, g, b, s, lo, hi);
+    uint16_t* key = ks.key + (int64_t)s * ks.P;
+    for (int32_t i = lo + t; i < hi; i += 256) {
+        const uint32_t k = seg_key(ks, rs, p.N, i, s);
+        key[i] = (uint16_t)k;
+        atomicAdd(&h[k], 1);
+    }
+    __syncthreads();
+    for (int k = t; k < SEG_BINS; k += 256)
+        ks.cnt[((int64_t)blockIdx.y * SEG_BINS + k) * SEG_NBK + b] = h[k];
+}
+
+// launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors = scanned offset + block
+// total, items scattered in partition order
+__global__ __launch_bounds__(256) void k_seg_scatter(KSeg ks) {
+    __shared__ int32_t cur[SEG_BINS];
+    const int t = threadIdx.x, b = blockIdx.x, g = blockIdx.y + ks.g0;
+    for (int k = t; k < SEG_BINS; k += 256) {
+        const int64_t c = ((int64_t)blockIdx.y * SEG_BINS + k) * SEG_NBK + b;
+        cur[k] = ks.cnt[c] + ks.tot[c / (256 * SCAN_ITEMS)];
+    }
+    __syncthreads();
+    int s;
+    int32_t lo, hi;
+    seg_group(ks, g, b, s, lo, hi);
+    const uint16_t* key = ks.key + (int64_t)s * ks.P;
+    int32_t* order = ks.order + ks.obase;
+    for (int32_t i = lo + t; i < hi; i += 256) order[atomicAdd(&cur[key[i]], 1)] = i;
+}
+
+// waypoints [j0, j1) of one path: raster_pass2_skip's chunks, cell arithmetic and sums
+// (SKIP = false: no bitmap, every in-raster waypoint gathered, as consume_chunk)
+template <bool SKIP>
+__device__ __forceinline__ void seg_pass2(const KRaster& rs, const uint4* __restrict__ rec,
+                                          const uint32_t* bits, const PathSrc<true>& src,
+                                          int j0, int j1, double dN, PathAcc& a) {
+    constexpr int CH = UAM_SKIP_CHUNK;
+    for (int jc = j0; jc < j1; jc += CH) {
+        uint4 r[CH];
+        uint32_t inb = 0, need = 0;
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            if (jc + t < j1) {
+                double x0, x1;
+                src.at(jc + t, x0, x1);
+                bool sk = false;
+                int32_t cl;
+                if (SKIP) {
+                    cl = raster_cell_skip(rs, bits, x0, x1, sk);
+                } else {
+                    int ix, iy;
+                    cl = raster_cell(rs, x0, x1, ix, iy) ? iy * rs.nx + ix : -1;
+                }
+                if (cl >= 0) {
+                    inb |= 1u << t;
+                    if (!sk) {
+                        need |= 1u << t;
+                        r[t] = rec[cl];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            if (jc + t >= j1) break;
+            if (!((inb >> t) & 1u)) {
+                ++a.off;
+                a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
+                continue;
+            }
+            if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
+                a.hmax = fmax(a.hmax, 0.0);
+                continue;
+            }
+            a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
+            a.nsum = a.nsum + (double)__uint_as_float(r[t].y);
+            a.nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+            const double terrain =
+                (r[t].w & UAM_FLAG_NODATA) ? 0.0 : (double)__uint_as_float(r[t].z);
+            a.hmax = fmax(a.hmax, terrain);
+        }
+    }
+}
+
+// segment s of every path, items in sorted order; workgroup b takes the sorted chunk
+// xcd_chunk(b), so an XCD's workgroups cover one contiguous run of tiles.  Dynamic LDS: the
+// skip bitmap, padded to the context's floor (UAM_K2S_LDS) to cap the workgroups per CU.
+// FIRST (segment 0 with UAM_K2S_FUSE): the lane runs the path's pass 1 itself and seeds the
+// state, so pass 1's ALU work overlaps the gathers as in K2.
+// pord (optional, segment 0): items in K2's pair order instead, item i = path
+// pord[i / D] * D + i % D (no per-path sort on the critical path)
+template <bool SKIP, bool FIRST>
+__global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks,
+                                                  const uint4* __restrict__ rec, int s,
+                                                  int64_t base, int32_t n,
+                                                  const int32_t* __restrict__ pord) {
+    extern __shared__ uint32_t s_bits[];
+    if (SKIP) {
+        for (int i = threadIdx.x; i < rs.swords; i += 256) s_bits[i] = rs.sum[i];
+        __syncthreads();
+    }
+    const int64_t i = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    int32_t path;
+    if (pord) {
+        const int32_t qi = (int32_t)i / ks.D;
+        path = pord[qi] * ks.D + ((int32_t)i - qi * ks.D);
+    } else {
+        path = ks.order[base + i];
+    }
+    const PathSrc<true> src = seg_src(ks, p.N, path);
+    PathAcc a;
+    if (FIRST) {
+        path_pass1<true>(p, src, nullptr, a);
+        ks.p1[path] = make_double4(a.L, a.len, a.ksum, 0.0);
+        a.cost = (double)(p.N + 1) * a.L;
+        a.nsum = 0.0;
+        a.hmax = -INFINITY;
+        a.nh = 0;
+        a.off = 0;
+    } else {
+        const SegState st = ks.st[path];
+        a.cost = st.cost;
+        a.nsum = st.nsum;
+        a.hmax = st.hmax;
+        a.nh = st.nh;
+        a.off = st.off;
+    }
+    int j0, j1;
+    ks.bounds(s, j0, j1);
+    seg_pass2<SKIP>(rs, rec, s_bits, src, j0, j1, (double)p.N, a);
+    SegState o;
+    o.cost = a.cost;
+    o.nsum = a.nsum;
+    o.hmax = a.hmax;
+    o.nh = a.nh;
+    o.off = a.off;
+    ks.st[path] = o;
+}
+
+// outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout) and the selection
+// over each pair's D paths
+__global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out,
+                                                    int32_t* __restrict__ best_f,
+                                                    int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int D = ks.D, t = threadIdx.x;
+    double* s_cost = smem;
+    double* s_len = smem + 64 * D;
+
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int qi = t / D, di = t - qi * D;
+    if (q0 + qi < ks.n_pairs) {
+        const int64_t gp = (q0 + qi) * D + di;
+        const SegState st = ks.st[gp];
+        const double4 q1 = ks.p1[gp];
+        if (out.cost) out.cost[gp] = st.cost;
+        if (out.length_q) out.length_q[gp] = q1.x;
+        if (out.length) out.length[gp] = q1.y;
+        if (out.kin_sum) out.kin_sum[gp] = q1.z;
+        if (out.nfz_sum) out.nfz_sum[gp] = st.nsum;
+        if (out.min_clearance) out.min_clearance[gp] = p.altitude - st.hmax;
+        if (out.nfz_hits) out.nfz_hits[gp] = st.nh;
+        if (out.offmap) out.offmap[gp] = st.off;
+        if (out.below_terrain) out.below_terrain[gp] = 0;
+        s_cost[di * 64 + qi] = st.cost;
+        s_len[di * 64 + qi] = q1.y;
+    }
+    __syncthreads();
+    if (t < 64 && q0 + t < ks.n_pairs) {
+        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -4706,6 +4994,19 @@ struct uam_ctx {
                                 // 0 = the lane-per-path K3)
     int k3b_cpl = 1;            // K3b points per lane in the evaluation phase (UAM_K3B_CPL: 1, 2)
     bool k3b_attrs = false;     // K3b dynamic-LDS attributes raised on this context's device
+    int k2s_segs = 2;           // K2s segments per path (UAM_K2S_SEGS: 2..8; 0 or 1 = K2)
+    int k2s_lds = 80 * 1024;    // K2s segment launches: dynamic-LDS floor per workgroup, which
+                                // caps the workgroups resident per CU (UAM_K2S_LDS)
+    int64_t k2s_min = 65536;    // K2s: smallest batch in paths it takes (UAM_K2S_MIN)
+    int k2s_split = 1;          // K2s path parts whose pass 1 is pipelined (UAM_K2S_SPLIT, 1..4)
+    bool k2s_fuse = true;       // K2s: segment 0's launch runs pass 1 (UAM_K2S_FUSE=0: a pass-1
+                                // kernel on the side stream, beside the sort)
+    int k2s_lds0 = 0;           // K2s: LDS floor of the fused segment-0 launch (UAM_K2S_LDS0)
+    int k2s_first = 0;          // K2s: waypoints in segment 0 (UAM_K2S_FIRST; 0 = equal split)
+    bool k2s_order0 = false;    // K2s: segment 0 in K2's pair order instead of sorted by its own
+                                // key (UAM_K2S_ORDER0=1; cfg3: 376 vs 298 us, not the default)
+    hipEvent_t k2s_ev[4] = {};  // K2s: pass 1 of part h done (side stream)
+    bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
@@ -4829,6 +5130,14 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_PAIR_ORDER")) c->pair_order = std::atoi(e) != 0;
     if (const char* e = std::getenv("UAM_K3B_SEG")) c->k3b_seg = std::atoi(e);
     if (const char* e = std::getenv("UAM_K3B_CPL")) c->k3b_cpl = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K2S_SEGS")) c->k2s_segs = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K2S_LDS")) c->k2s_lds = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("UAM_K2S_MIN")) c->k2s_min = std::atoll(e);
+    if (const char* e = std::getenv("UAM_K2S_SPLIT")) c->k2s_split = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K2S_FUSE")) c->k2s_fuse = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_K2S_FIRST")) c->k2s_first = std::atoi(e);
+    if (const char* e = std::getenv("UAM_K2S_ORDER0")) c->k2s_order0 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_K2S_LDS0")) c->k2s_lds0 = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("UAM_K8_STREAMS"))
         c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
     *out = c;
@@ -4850,6 +5159,8 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    for (hipEvent_t e : ctx->k2s_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ktime_ev) {
         (void)hipEventSynchronize(e.second);
         (void)hipEventDestroy(e.first);
@@ -5363,15 +5674,23 @@ static int pair_order(uam_ctx* ctx, const double* pairs, int64_t n, hipStream_t 
 }
 
 // K2 pair order over the raster extent (k_rorder_hist / k_rorder_scatter)
+static size_t raster_pair_order_bytes(int64_t n) {
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    return al((size_t)RORD_BINS * RORD_NB * 4) + al((size_t)n * 2) + al((size_t)n * 4);
+}
+
+// w_in: caller-owned scratch of raster_pair_order_bytes(n) (null: the context's order scratch)
 static int raster_pair_order(uam_ctx* ctx, const KRaster& kr, const double* pairs, int64_t n,
-                             hipStream_t s, const int32_t** order, int vol = 0) {
+                             hipStream_t s, const int32_t** order, int vol = 0,
+                             char* w_in = nullptr) {
     *order = nullptr;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_h = al((size_t)RORD_BINS * RORD_NB * 4), b_key = al((size_t)n * 2),
-                 b_ord = al((size_t)n * 4);
-    char* w = nullptr;
-    const int st = order_scratch(ctx, b_h + b_key + b_ord, s, &w);
-    if (st) return st;
+    const size_t b_h = al((size_t)RORD_BINS * RORD_NB * 4), b_key = al((size_t)n * 2);
+    char* w = w_in;
+    if (!w) {
+        const int st = order_scratch(ctx, raster_pair_order_bytes(n), s, &w);
+        if (st) return st;
+    }
     int32_t* H = (int32_t*)w;
     uint16_t* key = (uint16_t*)(w + b_h);
     int32_t* ord = (int32_t*)(w + b_h + b_key);
@@ -5529,6 +5848,161 @@ static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const 
     return 1;
 }
 
+// K2s launch (segment-sorted raster evaluation); returns 1 if launched, 0 if the batch is not
+// one it takes (the caller runs K2).  Scratch: the pair-order scratch (order_scratch), so two
+// streams sharing the context serialise on it.
+static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
+                            int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
+                            int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    const int64_t W = ctx->kp.N + 2;
+    const int want = std::min(ctx->k2s_segs, SEG_MAX);
+    if (want < 2 || ko.cells || ko.g_rows || D > 16) return 0;
+    // segment 0 = [0, F) (UAM_K2S_FIRST; default: the common length), then segments of L
+    int L = (int)((W + want - 1) / want), F = L;
+    if (ctx->k2s_first > 0 && ctx->k2s_first < W) {
+        F = ctx->k2s_first;
+        L = (int)((W - F + want - 2) / (want - 1));
+    }
+    const int nseg = 1 + (int)((W - F + L - 1) / L);  // e.g. W = 10 in 4: 3, 3, 3, 1
+    if (nseg < 2) return 0;
+    if (n_pairs > (INT32_MAX / SEG_MAX) / D) return 0;
+    const int64_t P = n_pairs * D;
+    if (P < ctx->k2s_min) return 0;
+    const int H = std::max(1, std::min(ctx->k2s_split, SEG_MAXSPLIT));
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const int64_t ncnt = (int64_t)H * nseg * SEG_BINS * SEG_NBK;
+    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    if (nsb > 4096) return 0;
+    const size_t b_st = al((size_t)P * sizeof(SegState)), b_len = al((size_t)P * 32),
+                 b_key = al((size_t)nseg * P * 2), b_cnt = al((size_t)ncnt * 4),
+                 b_tot = al(4096 * 4), b_ord = al((size_t)nseg * P * 4),
+                 b_po = al(raster_pair_order_bytes(n_pairs));
+    char* w = nullptr;
+    int st = order_scratch(ctx, b_st + b_len + b_key + b_cnt + b_tot + b_ord + b_po, s, &w);
+    if (st) return st;
+    KSeg ks{};
+    ks.pairs = pairs;
+    ks.utab = utab;
+    ks.n_pairs = n_pairs;
+    ks.P = (int32_t)P;
+    ks.D = D;
+    ks.W = (int32_t)W;
+    ks.nseg = nseg;
+    ks.L = L;
+    ks.F = F;
+    ks.nsplit = H;
+    int tshift = 0;
+    while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << SEG_TBITS)) ++tshift;
+    ks.tshift = tshift;
+    ks.st = (SegState*)w;
+    ks.p1 = (double4*)(w + b_st);
+    ks.key = (uint16_t*)(w + b_st + b_len);
+    ks.cnt = (int32_t*)(w + b_st + b_len + b_key);
+    ks.tot = (int32_t*)(w + b_st + b_len + b_key + b_cnt);
+    ks.order = (int32_t*)(w + b_st + b_len + b_key + b_cnt + b_tot);
+    const size_t lds_min = kr.sum ? (size_t)kr.swords * 4 : 0;
+    const size_t lds = std::max(lds_min, (size_t)std::min(ctx->k2s_lds, 160 * 1024));
+    const size_t lds0 = std::max(lds_min, (size_t)std::min(ctx->k2s_lds0, 160 * 1024));
+    if (!ctx->k2s_attrs) {  // per context = per device (the caller's DeviceGuard is active)
+        const void* fns[] = {(const void*)k_seg_eval<true, false>,
+                             (const void*)k_seg_eval<false, false>,
+                             (const void*)k_seg_eval<true, true>,
+                             (const void*)k_seg_eval<false, true>};
+        for (const void* f : fns)
+            HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+        ctx->k2s_attrs = true;
+    }
+    if (!ctx->s2) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    for (int h = 0; h < H; ++h)
+        if (!ctx->k2s_ev[h]) HIP_TRY(hipEventCreateWithFlags(&ctx->k2s_ev[h], hipEventDisableTiming));
+    // kernel timing brackets the whole sequence (sort included).  Pass 1 (ALU-bound) runs part
+    // by part on the side stream: part h's first segment launch waits only for part h's pass 1,
+    // so the later parts' pass 1 overlaps the (latency-bound) gathers of the earlier ones.
+    // With UAM_K2S_FUSE (default) segment 0's launch runs pass 1 in the same lanes instead.
+    const bool fuse = ctx->k2s_fuse;
+    st = ktime_begin(ctx, s);
+    if (st) return st;
+    if (!fuse) {
+        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+        for (int h = 0; h < H; ++h) {
+            const int32_t p0 = (int32_t)(P * h / H), p1 = (int32_t)(P * (h + 1) / H);
+            hipLaunchKernelGGL(k_seg_pass1, dim3((unsigned)((p1 - p0 + 255) / 256)), dim3(256),
+                               0, ctx->s2, ctx->kp, ks, ko, p0, p1);
+            HIP_TRY(hipEventRecord(ctx->k2s_ev[h], ctx->s2));
+        }
+    }
+    // counting sort of the groups [g0, g0 + ng) on stream q (cnt / tot: its own count and
+    // block-total scratch); order positions start at group g0's (g0 * P: H == 1 or g0 == 0)
+    auto sort_groups = [&](int g0, int ng, hipStream_t q, int32_t* cnt, int32_t* tot) {
+        KSeg kq = ks;
+        kq.g0 = g0;
+        kq.obase = (int64_t)g0 * P;
+        kq.cnt = cnt;
+        kq.tot = tot;
+        const int64_t nc = (int64_t)ng * SEG_BINS * SEG_NBK;
+        const int64_t nb = (nc + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+        hipLaunchKernelGGL(k_seg_hist, dim3(SEG_NBK, ng), dim3(256), 0, q, ctx->kp, kr, kq);
+        hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nb), dim3(256), 0, q, cnt, nc, cnt, tot);
+        hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, q, tot, (int)nb);
+        hipLaunchKernelGGL(k_seg_scatter, dim3(SEG_NBK, ng), dim3(256), 0, q, kq);
+    };
+    // fused pass 1, one part: segment 0's order first on s, the other segments' orders on the
+    // side stream beside segment 0's launch (joined before segment 1)
+    // (UAM_K2S_ORDER0=1, default: segment 0 in K2's pair order, no sort before it)
+    const bool two = fuse && H == 1;
+    const int32_t* pord = nullptr;
+    if (two) {
+        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+        if (ctx->k2s_order0 && n_pairs < INT32_MAX) {
+            st = raster_pair_order(ctx, kr, pairs, n_pairs, s, &pord, 0,
+                                   w + b_st + b_len + b_key + b_cnt + b_tot + b_ord);
+            if (st) return st;
+        } else {
+            sort_groups(0, 1, s, ks.cnt, ks.tot);
+        }
+        sort_groups(1, nseg - 1, ctx->s2, ks.cnt + (int64_t)SEG_BINS * SEG_NBK, ks.tot + 2048);
+        HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+    } else {
+        sort_groups(0, H * nseg, s, ks.cnt, ks.tot);
+    }
+    (void)nsb;
+    const dim3 gf((unsigned)((n_pairs + 63) / 64));
+    for (int k = 0; k < nseg; ++k)
+        for (int h = 0; h < H; ++h) {
+            const int32_t n = (int32_t)(P * (h + 1) / H - P * h / H);
+            // group (h, k) = h * nseg + k; the groups before it hold nseg * part_lo(h) + k * n
+            const int64_t base = (P * h / H) * (int64_t)nseg + (int64_t)k * n;
+            if (k == 0 && !fuse) HIP_TRY(hipStreamWaitEvent(s, ctx->k2s_ev[h], 0));
+            if (k == 1 && h == 0 && two) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+            const dim3 ge((unsigned)((n + 255) / 256));
+#define UAM_LAUNCH_SEG(SK_, F_, LDS_)                                                          \
+    hipLaunchKernelGGL((k_seg_eval<SK_, F_>), ge, dim3(256), LDS_, s, ctx->kp, kr, ks,         \
+                       (const uint4*)rec, k, base, n, k == 0 ? pord : nullptr)
+            if (k == 0 && fuse) {
+                if (kr.sum) UAM_LAUNCH_SEG(true, true, lds0);
+                else UAM_LAUNCH_SEG(false, true, lds0);
+            } else {
+                if (kr.sum) UAM_LAUNCH_SEG(true, false, lds);
+                else UAM_LAUNCH_SEG(false, false, lds);
+            }
+#undef UAM_LAUNCH_SEG
+        }
+    const size_t lf = (size_t)2 * 64 * D * sizeof(double);
+    hipLaunchKernelGGL(k_seg_final, gf, dim3(64 * D), lf, s, ctx->kp, ks, ko, best_f, best_l);
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "segmented evaluation launch");
+    st = ktime_end(ctx, s);
+    if (st) return st;
+    st = order_done(ctx, s);
+    return st ? st : 1;
+}
+
 } // extern "C"
 
 static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shift,
@@ -5600,7 +6074,12 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         if (st < 0) return st;
         if (st == 1) return UAM_OK;
     }
-    int v = (ctx->variant == 0 || ctx->variant >= UAM_TUNING_WAVE) ? UAM_TUNING_DEFAULT
+    if (mode == UAM_MODE_RASTER && ctx->variant == 0 && ctx->k2s_segs > 1) {
+        st = launch_segmented(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
+        if (st < 0) return st;
+        if (st == 1) return UAM_OK;
+    }
+    int v =(ctx->variant == 0 || ctx->variant >= UAM_TUNING_WAVE) ? UAM_TUNING_DEFAULT
                                                                    : ctx->variant;
     if (D > 16) v = 1;  // the block-of-pairs kernels hold all D waves in one workgroup
     if (v == 1) {
