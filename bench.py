@@ -263,13 +263,19 @@ def main():
 
     total_paths = Q_total * D * args.steps
     value = total_paths / elapsed
-    wave = mode != "analytic" and (args.variant == 9 or (args.variant == 0 and P <= 16384))
+    last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
+    wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    ktag = "wave" if wave else ("raster+skip" if skip else mode)
-    if raster_mode and not skip and not wave:
-        ktag += f"-v{args.variant or 2}"
-    kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
-                   f"k_eval_pairs<{ktag}>")
+    if last.startswith("K2s"):
+        ktag = last.lower()
+        kernel_name = ("K2s sequence (k_seg_hist / k_scan / k_seg_scatter, k_seg_eval<FIRST> "
+                       "fused with pass 1, k_seg_eval, k_seg_final)")
+    else:
+        ktag = "wave" if wave else ("raster+skip" if skip else mode)
+        if raster_mode and not skip and not wave:
+            ktag += f"-v{args.variant or 2}"
+        kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
+                       f"k_eval_pairs<{ktag}>")
     pkey = f"{args.workload}:{mode}:R{R}:Q{Q}:{ktag}"
     prof = {}
     if os.path.exists(args.traffic_json):
@@ -283,9 +289,11 @@ def main():
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name)
     roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
-                                    "launch of the kernel, on its launch stream "
-                                    "(uam_kernel_timing)" if kern_timed else
+                                    "launch of the kernel (K2s: around its whole launch "
+                                    "sequence), on its launch stream (uam_kernel_timing)"
+                                    if kern_timed else
                                     "torch events around the whole step (multi-launch variant)")
+    roofline["library_kernel"] = last
     roofline["step_event_ms"] = round(step_ev_ms, 4)
     roofline["profile_key"] = pkey
     result = {
@@ -411,8 +419,9 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name):
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
          "note": "each 16-B record gather that misses L2 moves one 128-B line (PMC); the "
-                 "measured random-gather ceiling (tools/gather_ceiling.hip) bounds the kernel, "
-                 "DESIGN.md §5"}
+                 "measured random-gather ceiling (tools/gather_ceiling.hip) bounds a kernel "
+                 "gathering in random order (K2); K2s's tile-sorted segments pass it through "
+                 "L2 reuse (l2_hit_rate), DESIGN.md §4-5"}
     return r
 
 

@@ -360,6 +360,11 @@ int uam_set_tuning(uam_ctx* ctx, int32_t variant);
  * kernel time and the launch count since the last call (then resets the count). */
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable);
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
+/* The path evaluation the last uam_eval_generated / uam_eval_generated3d call on ctx ran:
+ * "K2s+skip" / "K2s" (segment-sorted raster), "K2+skip" / "K2" (lane per path), "K2w" (wave per
+ * path), "K2b", "K2t", "K2v1", "K3b", "K3", "K3v1", "K4", "K4w"; "" before the first call.  The
+ * string is static (never freed).  For benchmarks and tests: which kernel a number belongs to. */
+const char* uam_last_kernel(const uam_ctx* ctx);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */
 int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,

@@ -104,8 +104,10 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
         else:
             e.raster_summary(raster, block)
         gpu = e.eval_generated(pairs, ut, raster=raster)
+        assert e.last_kernel() == ("K2s" if block is None else "K2s+skip")
         _check(gpu, ref, oracle_mod, D)
         g2 = k2.eval_generated(pairs, ut, raster=raster)
+        assert k2.last_kernel() == ("K2" if block is None else "K2+skip")
         for gk, _ in KEYS:
             np.testing.assert_array_equal(gpu[gk].cpu().numpy(), g2[gk].cpu().numpy(),
                                           err_msg=gk)
@@ -129,6 +131,7 @@ def test_k2s_displacements_and_short_paths(oracle_mod, monkeypatch, D, N):
     pairs = random_pairs(1037 if D > 1 else 17037, seed=3)  # above the wave kernel's 16384
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
     gpu = e.eval_generated(pairs, ut, raster=raster)
+    assert e.last_kernel() == "K2s+skip"
     _check(gpu, ref, oracle_mod, D)
 
 

@@ -323,6 +323,7 @@ def test_full_size_cfg3_properties(eng, oracle_mod):
     oracle on a 2k-pair subsample (bit-exact), size-independent properties on the rest."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 4096, 100_000, 80, nfz=64)
     gpu = eng.eval_generated(pairs, ut, raster=raster)
+    assert eng.last_kernel().startswith("K2s")     # the default for this batch size
     sub = np.random.default_rng(7).choice(len(pairs), 2000, replace=False)
     sub.sort()
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs[sub], ut), mode="raster", rdesc=rd, rec=rec)

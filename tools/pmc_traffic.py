@@ -17,6 +17,11 @@ Optional passes: --tcc (TCC_HIT_sum, TCC_MISS_sum, TCC_EA0_RDREQ_128B_sum) -> L2
 usage: tools/pmc_traffic.py --key cfg3:raster:R4096:Q100000:raster+skip --kernel k_eval_pairs \
           [--fetch DIR] [--write DIR] [--tcc DIR] [--sq DIR] [--flops DIR] [--source TEXT]
 Each DIR holds rocprofv3's *counter_collection.csv of one counter pass.
+
+A multi-launch evaluation (K2s: sorts, two segment launches, output launch) is summarised per
+step: --kernel takes comma-separated name patterns, and --per names the kernel launched once per
+step; each counter is then the sum over every matching dispatch / the number of --per
+dispatches (e.g. --kernel k_seg_,k_scan_ --per k_seg_final).
 """
 import argparse
 import csv
@@ -26,14 +31,26 @@ import os
 import statistics
 
 
+PER = None  # --per: the once-per-step kernel of a multi-launch evaluation
+
+
 def load(d, kernel, counter):
-    vals = []
+    pats = kernel.split(",")
+    vals, steps = [], set()
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if r["Counter_Name"] != counter:
+                continue
+            if any(p in r["Kernel_Name"] for p in pats):
                 vals.append(float(r["Counter_Value"]))
+            if PER and PER in r["Kernel_Name"]:
+                steps.add(r.get("Dispatch_Id", len(steps)))
     if not vals:
         raise SystemExit(f"no {counter} rows for kernel '{kernel}' in {d}")
+    if PER:
+        if not steps:
+            raise SystemExit(f"no {counter} rows for the per-step kernel '{PER}' in {d}")
+        return sum(vals) / len(steps), len(steps)
     return statistics.median(vals), len(vals)
 
 
@@ -41,6 +58,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--key", required=True)
     ap.add_argument("--kernel", required=True)
+    ap.add_argument("--per", default=None)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--tcc")
@@ -49,7 +67,11 @@ def main():
     ap.add_argument("--source", default=None)
     ap.add_argument("--out", default="profiles/traffic.json")
     a = ap.parse_args()
+    global PER
+    PER = a.per
     rec = {"kernel": a.kernel, "source": a.source}
+    if a.per:
+        rec["per_step_of"] = a.per
     if a.fetch and a.write:
         fetch_kib, n1 = load(a.fetch, a.kernel, "FETCH_SIZE")
         write_kib, n2 = load(a.write, a.kernel, "WRITE_SIZE")

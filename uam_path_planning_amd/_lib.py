@@ -126,6 +126,7 @@ SIGNATURES = {
     "uam_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "uam_kernel_time": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_int64)]),
+    "uam_last_kernel": (ctypes.c_char_p, [_vp]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,

@@ -4655,7 +4655,7 @@ __global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restri
 // K2 (one lane walks one path's W waypoints) is bound by scattered 128-B record lines: 14% L2
 // hits and 6.4x the algorithmic bytes across the fabric (profiles/r02/final).  K2s cuts every
 // path into nseg segments of L = ceil(W / nseg) waypoints and evaluates segment k of all paths
-// in one launch, the (path, segment) items sorted by the Morton key of the 64 x 64-tile raster
+// in one launch, the (path, segment) items sorted by the Morton key of the 16 x 16-tile raster
 // tile under the segment's middle waypoint, so the workgroups an XCD runs together gather from
 // one region of the raster.  Between launches a path's running sums live in a 32-B SegState;
 // every waypoint is still added in waypoint order with raster_pass2_skip's arithmetic (the
@@ -4667,10 +4667,12 @@ __global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restri
 // through an LDS floor, UAM_K2S_LDS), then k_seg_final (outputs, the main.py:175-180
 // selection).  UAM_K2S_FUSE=0 runs pass 1 as its own kernel (k_seg_pass1) on the side stream
 // instead, optionally part by part (UAM_K2S_SPLIT).  Measured on cfg3: DESIGN.md §4 K2s.
+// tile grid of the sort key: 2^TBITS x 2^TBITS tiles over the raster.  cfg3 K2s time by TBITS
+// (tools/k2s_tbits.sh): 6 0.630, 5 0.603, 4 0.595, 3 0.613 ms
 #ifndef UAM_SEG_TBITS
-#define UAM_SEG_TBITS 6  // tuning builds: -DUAM_SEG_TBITS=5 (32 x 32 tiles)
+#define UAM_SEG_TBITS 4
 #endif
-constexpr int SEG_TBITS = UAM_SEG_TBITS;               // 64 x 64 tiles over the raster
+constexpr int SEG_TBITS = UAM_SEG_TBITS;               // 16 x 16 tiles over the raster
 constexpr int SEG_BINS = (1 << (2 * SEG_TBITS)) + 1;   // + one bin for off-raster / NaN
 constexpr int SEG_NBK = 256;                           // partitions of a segment's items
 constexpr int SEG_MAX = 8;                             // segments per path
@@ -5014,6 +5016,7 @@ struct uam_ctx {
     bool ord_pending = false;
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
+    const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
 };
 
 namespace {
@@ -5600,6 +5603,8 @@ int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
     return UAM_OK;
 }
 
+const char* uam_last_kernel(const uam_ctx* ctx) { return ctx ? ctx->last_kernel : ""; }
+
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
     if (!ctx || !ms_total || !launches) return fail(UAM_E_INVALID, "NULL argument");
     DeviceGuard dg(ctx->device);
@@ -6062,27 +6067,40 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         st = launch_wave(ctx, mode, true, kr, kv, rec, nullptr, pairs, utab, D, n_pairs * D, ko,
                          best_f, best_l, s);
         if (st < 0) return st;
-        if (st == 1) return UAM_OK;
+        if (st == 1) {
+            ctx->last_kernel = "K2w";
+            return UAM_OK;
+        }
     }
     if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_BINNED) {
         st = launch_binned(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
-        if (st == 1) return UAM_OK;
+        if (st == 1) {
+            ctx->last_kernel = "K2b";
+            return UAM_OK;
+        }
     }
     if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_TILED) {
         st = launch_tiled(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
-        if (st == 1) return UAM_OK;
+        if (st == 1) {
+            ctx->last_kernel = "K2t";
+            return UAM_OK;
+        }
     }
     if (mode == UAM_MODE_RASTER && ctx->variant == 0 && ctx->k2s_segs > 1) {
         st = launch_segmented(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
-        if (st == 1) return UAM_OK;
+        if (st == 1) {
+            ctx->last_kernel = kr.sum ? "K2s+skip" : "K2s";
+            return UAM_OK;
+        }
     }
     int v =(ctx->variant == 0 || ctx->variant >= UAM_TUNING_WAVE) ? UAM_TUNING_DEFAULT
                                                                    : ctx->variant;
     if (D > 16) v = 1;  // the block-of-pairs kernels hold all D waves in one workgroup
     if (v == 1) {
+        ctx->last_kernel = mode == UAM_MODE_RASTER ? "K2v1" : "K3v1";
         const int64_t n_waves = ((n_pairs + 63) / 64) * D;
         const int64_t blocks = (n_waves + 3) / 4;
         if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
@@ -6149,6 +6167,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
 #define UAM_LAUNCH_K3B(S_, C_)                                                                 \
     hipLaunchKernelGGL((k_eval_pairs_k3b<S_, C_>), grid, block, l3, s, ctx->kg, ctx->kp, pairs,   \
                        n_pairs, utab, D, ko, best_f, best_l, order)
+        ctx->last_kernel = "K3b";
         switch (S * 4 + CPL) {
             case 16 * 4 + 2: UAM_LAUNCH_K3B(16, 2); break;
             case 8 * 4 + 2: UAM_LAUNCH_K3B(8, 2); break;
@@ -6163,8 +6182,10 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         }
 #undef UAM_LAUNCH_K3B
     } else if (mode == UAM_MODE_ANALYTIC) {
+        ctx->last_kernel = "K3";
         UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
     } else {
+        ctx->last_kernel = kr.sum ? "K2+skip" : "K2";
         if (kr.sum) {
             UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, 8, false, UAM_SKIP_MINW);  // 5 (6 spilled)
         } else switch (v) {
@@ -6281,7 +6302,9 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     int32_t* best_l = out ? out->best_length_idx : nullptr;
     DeviceGuard dg(ctx->device);
     const KRaster kr{};
+    ctx->last_kernel = "K4";
     if (want_wave(ctx, n_pairs * D)) {
+        ctx->last_kernel = "K4w";
         st = launch_wave(ctx, UAM_MODE_VOLUME, true, kr, kv, vol, nullptr, pairs6, utab, D,
                          n_pairs * D, ko, best_f, best_l, (hipStream_t)stream);
         if (st < 0) return st;

@@ -269,9 +269,10 @@ class Engine:
         _lib.check(self.lib.uam_set_tuning(self._ctx, int(variant)), "uam_set_tuning")
 
     def kernel_timing(self, enable=True):
-        """Start (and reset) or stop HIP-event timing of the dominant path kernel: the context
-        records an event pair on the launch stream around every k_eval_pairs / k_eval_wave
-        launch (not around the pair order or selection kernels)."""
+        """Start (and reset) or stop HIP-event timing of the path evaluation: the context records
+        an event pair on the launch stream around every k_eval_pairs / k_eval_wave launch (not
+        around K2's pair order or the selection kernels), and around the whole K2s sequence
+        (its sorts, segment launches and output launch)."""
         _lib.check(self.lib.uam_kernel_timing(self._ctx, 1 if enable else 0),
                    "uam_kernel_timing")
 
@@ -281,6 +282,11 @@ class Engine:
         _lib.check(self.lib.uam_kernel_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)),
                    "uam_kernel_time")
         return ms.value, n.value
+
+    def last_kernel(self):
+        """Which path evaluation the last eval_generated / eval_generated3d ran (uam_last_kernel:
+        "K2s+skip", "K2+skip", "K2w", "K3b", ...)."""
+        return self.lib.uam_last_kernel(self._ctx).decode()
 
     def _outputs(self, P, W, mode, want_cells, want_g, n_pairs=None):
         torch = _torch()
