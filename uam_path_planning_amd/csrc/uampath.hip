@@ -4672,6 +4672,13 @@ __global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restri
 #ifndef UAM_SEG_TBITS
 #define UAM_SEG_TBITS 4
 #endif
+#ifndef UAM_SEG_CH0
+#define UAM_SEG_CH0 6   // gathers per chunk in segment 0 (tuning builds: -DUAM_SEG_CH0=...)
+#endif
+#ifndef UAM_SEG_CH1
+#define UAM_SEG_CH1 6   // gathers per chunk in the later segments (cfg3, tools/k2s_tbits.sh:
+                        // 6/6 0.590, 8/8 0.598, 8/4 0.592, 4/4 0.595, 8/16 0.755 ms)
+#endif
 constexpr int SEG_TBITS = UAM_SEG_TBITS;               // 16 x 16 tiles over the raster
 constexpr int SEG_BINS = (1 << (2 * SEG_TBITS)) + 1;   // + one bin for off-raster / NaN
 constexpr int SEG_NBK = 256;                           // partitions of a segment's items
@@ -4807,11 +4814,10 @@ __global__ __launch_bounds__(256) void k_seg_scatter(KSeg ks) {
 
 // waypoints [j0, j1) of one path: raster_pass2_skip's chunks, cell arithmetic and sums
 // (SKIP = false: no bitmap, every in-raster waypoint gathered, as consume_chunk)
-template <bool SKIP>
+template <bool SKIP, int CH>
 __device__ __forceinline__ void seg_pass2(const KRaster& rs, const uint4* __restrict__ rec,
                                           const uint32_t* bits, const PathSrc<true>& src,
                                           int j0, int j1, double dN, PathAcc& a) {
-    constexpr int CH = UAM_SKIP_CHUNK;
     for (int jc = j0; jc < j1; jc += CH) {
         uint4 r[CH];
         uint32_t inb = 0, need = 0;
@@ -4905,7 +4911,10 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     }
     int j0, j1;
     ks.bounds(s, j0, j1);
-    seg_pass2<SKIP>(rs, rec, s_bits, src, j0, j1, (double)p.N, a);
+    // gathers in flight per lane: the capped later segments (2 waves per SIMD) have the
+    // registers for more
+    seg_pass2<SKIP, FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
+                                                        (double)p.N, a);
     SegState o;
     o.cost = a.cost;
     o.nsum = a.nsum;
