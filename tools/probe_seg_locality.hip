@@ -145,4 +145,36 @@ int probe_seg(const void* rec, const int32_t* cells, int W, int j0, int j1,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the same segment launch over an 8-B record table (the first two words of each record)
+__global__ __launch_bounds__(256) void k_probe_seg8(const uint2* __restrict__ rec,
+                                                    const int32_t* __restrict__ cells, int W,
+                                                    int j0, int j1,
+                                                    const int32_t* __restrict__ order, int64_t P,
+                                                    double* __restrict__ acc) {
+    const int64_t i = xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int64_t p = order[i];
+    const int32_t* c = cells + p * W;
+    double s = j0 == 0 ? 0.0 : acc[p];
+    for (int j = j0; j < j1; j += 8) {
+        uint2 r[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int32_t cl = (j + t < j1) ? c[j + t] : -1;
+            r[t] = cl >= 0 ? rec[cl] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s = s + (double)__uint_as_float(r[t].x);
+    }
+    acc[p] = s;
+}
+
+int probe_seg8(const void* rec, const int32_t* cells, int W, int j0, int j1,
+               const int32_t* order, int64_t P, double* acc, int lds_pad, void* stream) {
+    hipLaunchKernelGGL(k_probe_seg8, dim3((unsigned)((P + 255) / 256)), dim3(256),
+                       (size_t)lds_pad, (hipStream_t)stream, (const uint2*)rec, cells, W, j0, j1,
+                       order, P, acc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // extern "C"
