@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
     ap.add_argument("--no-skip", action="store_true",
                     help="K2 without the gather-skip bitmap (A/B; results are identical)")
+    ap.add_argument("--pack", action="store_true",
+                    help="K2s gathers from the packed copy (uam_raster_pack: 8-B phi/terrain "
+                         "plane outside the no-fly blocks; A/B, results are identical)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -201,7 +204,8 @@ def main():
             setup["raster_bytes"] = table.numel() * 4
         if raster_mode and not args.no_skip:
             t1 = time.perf_counter()
-            eng.raster_summary(raster)         # every rank derives the skip bitmap locally
+            # every rank derives the skip bitmap (and K2s's packed copy) locally
+            eng.raster_summary(raster, packed=args.pack)
             torch.cuda.synchronize()
             setup["skip_bitmap_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
             setup["skip_block"] = raster.block

@@ -225,6 +225,26 @@ int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* 
                          int64_t n_pairs, const double* utab_dev, int32_t D,
                          const uam_path_outputs* out, uam_stream stream);
 
+/* K2s packed raster (build-defined; no reference counterpart; results unchanged).  A derived
+ * copy of rec for the segment-sorted evaluation: a 2-bit code per summary block (0 = nothing
+ * to gather, the gather-skip rule above; 1 = phi/terrain only, every cell has psi_nfz == +-0
+ * and no no-fly flag; 3 = the full 16-B record, read from rec) followed by one 8-B plane
+ * {phi, terrain read as the evaluation reads it} in blocks of 4 x 4 cells (one 128-B line).
+ * uam_raster_pack_shape gives the bytes of the caller's buffer (256-B aligned; 8 B per cell
+ * plus the codes, padded to whole blocks); block as uam_raster_summary (0 = automatic), and the
+ * same block must be passed to uam_eval_generated_p.  Rebuild the copy whenever rec changes.
+ * uam_eval_generated_p = uam_eval_generated_s whose K2s launches gather from packed_dev
+ * (NULL = from rec); the other kernels still read rec and summary_dev.  Replaces the same
+ * reference call as uam_eval_generated (problem.py:38-44 per candidate, main.py:158-196). */
+int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
+                          int64_t* bytes);
+int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
+                    int32_t block, void* packed_dev, uam_stream stream);
+int uam_eval_generated_p(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
+                         const uint32_t* summary_dev, int32_t block, const void* packed_dev,
+                         const double* pairs_dev, int64_t n_pairs, const double* utab_dev,
+                         int32_t D, const uam_path_outputs* out, uam_stream stream);
+
 /* K5: per group of G consecutive values, the reference's selection rule (main.py:175-180):
  * compare sqrt(v) when take_sqrt (fval = sqrt(cost), solver.py:48), else v. */
 int uam_argmin(uam_ctx* ctx, const double* values_dev, int64_t groups, int32_t G,

@@ -5,7 +5,8 @@ HBM) -- against the CPU oracle, bit for bit, and against the lane-per-path K2
 
 What is exercised: pass 1 fused into the first segment launch or not (UAM_K2S_FUSE), 1 and
 3 path parts (UAM_K2S_SPLIT), 2, 3, 4 and 8 segments (ragged last segment; W = 3 where a segment is one
-waypoint), D = 1, 5 and 16, the gather-skip bitmap off / automatic / 4-cell blocks, all region
+waypoint), D = 1, 5 and 16, the gather-skip bitmap off / automatic / 4-cell blocks, the
+packed raster (uam_raster_pack) or the 16-B records, all region
 weights 0 over a below-sea-level DEM (maxima < 0 from gathered land, and exactly +0.0 from
 skipped sea), NaN pairs and paths that leave the raster, and two streams sharing one
 context.  UAM_K2S_MIN=0 makes K2s take these small batches; BASELINE's cfg3 size runs
@@ -77,7 +78,8 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
     6 x 7), pass 1 fused into segment 0's launch (segment 0 in K2's pair order or sorted by
     its own key) or run as its own kernel on the side stream,
     the paths in 1 or 3 parts (pass 1 pipelined part by part; 22500 / 3 items each),
-    skip bitmap off, automatic and 4-cell blocks; some paths leave the raster and two pairs
+    skip bitmap off, automatic and 4-cell blocks, with and without the packed copy
+    (uam_raster_pack: 8-B planes, 2-bit block codes); some paths leave the raster and two pairs
     are NaN.  Every output and both selections equal the oracle's, and K2's."""
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.scenario import displacements
@@ -98,13 +100,14 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
     k2 = Engine(0)
     k2.set_geometry(e.geometry)
     k2.set_params(e.params)
-    for block in (None, 0, 4):
+    for block, pack in ((None, False), (0, False), (4, False), (0, True), (4, True)):
         if block is None:
-            raster.summary = None
+            raster.summary = raster.packed = None
         else:
-            e.raster_summary(raster, block)
+            e.raster_summary(raster, block, packed=pack)
         gpu = e.eval_generated(pairs, ut, raster=raster)
-        assert e.last_kernel() == ("K2s" if block is None else "K2s+skip")
+        assert e.last_kernel() == ("K2s" if block is None else
+                                   "K2s+pack" if pack else "K2s+skip")
         _check(gpu, ref, oracle_mod, D)
         g2 = k2.eval_generated(pairs, ut, raster=raster)
         assert k2.last_kernel() == ("K2" if block is None else "K2+skip")
@@ -125,13 +128,13 @@ def test_k2s_displacements_and_short_paths(oracle_mod, monkeypatch, D, N):
     from uam_path_planning_amd.synthetic import random_pairs
 
     e, orc, raster, rd, rec = _case(oracle_mod, monkeypatch, 4, N)
-    e.raster_summary(raster, 0)
+    e.raster_summary(raster, 0, packed=True)
     ds = np.linspace(-1.0, 1.0, D) if D > 1 else np.array([0.3])
     ut = arc_table(N, ds)
     pairs = random_pairs(1037 if D > 1 else 17037, seed=3)  # above the wave kernel's 16384
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
     gpu = e.eval_generated(pairs, ut, raster=raster)
-    assert e.last_kernel() == "K2s+skip"
+    assert e.last_kernel() == "K2s+pack"
     _check(gpu, ref, oracle_mod, D)
 
 

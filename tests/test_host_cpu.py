@@ -52,6 +52,14 @@ def test_invalid_calls_fail_loudly(lib):
     assert (b.value, nbx.value, nby.value) == (16, 256, 256)    # 65536-bit LDS bitmap
     assert lib.uam_raster_summary_shape(ctypes.byref(rd), 8, None, None, None) == \
         _lib.UAM_E_INVALID                                        # 262144 blocks: too many
+    nbytes = ctypes.c_int64()
+    assert lib.uam_raster_pack_shape(ctypes.byref(rd), 0, ctypes.byref(b),
+                                     ctypes.byref(nbytes)) == _lib.UAM_OK
+    # 2-bit codes of 65536 blocks (16 KiB), then one 8-B plane of 4096^2 cells
+    assert (b.value, nbytes.value) == (16, 16384 + 8 * 4096 * 4096)
+    assert lib.uam_raster_pack(None, None, None, 0, None, None) == _lib.UAM_E_INVALID
+    assert lib.uam_eval_generated_p(None, None, None, None, 0, None, None, 0, None, 5, None,
+                                    None) == _lib.UAM_E_INVALID
 
 
 def _specs():

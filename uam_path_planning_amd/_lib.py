@@ -117,6 +117,13 @@ SIGNATURES = {
     "uam_eval_generated_s": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp,
                                             ctypes.c_int32, _vp, ctypes.c_int64, _vp,
                                             ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
+    "uam_raster_pack_shape": (ctypes.c_int, [ctypes.POINTER(RasterDesc), ctypes.c_int32,
+                                             _i32p, ctypes.POINTER(ctypes.c_int64)]),
+    "uam_raster_pack": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, ctypes.c_int32,
+                                       _vp, _vp]),
+    "uam_eval_generated_p": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp,
+                                            ctypes.c_int32, _vp, _vp, ctypes.c_int64, _vp,
+                                            ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
     "uam_argmin": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp,
                                   _vp]),
     "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,

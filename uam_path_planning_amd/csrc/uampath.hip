@@ -138,6 +138,12 @@ struct KRaster {
     // blocks per row, swords 32-bit words; null = gather every waypoint
     const uint32_t* __restrict__ sum;
     int32_t sshift, snbx, swords;
+    // K2s packed raster (uam_raster_pack; null = K2s gathers rec): a 2-bit code per summary
+    // block (pmap, pwords words) and plane A {phi, terrain} of 8 B per cell in a blocked layout
+    // of 2^phb x 2^pwb cells per block, pnbx blocks per row
+    const uint32_t* __restrict__ pmap;
+    const uint2* __restrict__ pa;
+    int32_t pwords, phb, pwb, pnbx;
 };
 
 struct KVolume {
@@ -602,6 +608,72 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
     const int32_t w = blk >> 5;  // lanes 0 and 32 write the wave's two words
     if ((lane & 31) == 0 && blk < n_blocks)
         out[w] = (uint32_t)(lane ? (m >> 32) : m);
+}
+
+// ---- K2s packed raster (uam_raster_pack; build-defined, no reference counterpart) --------
+// K2s's gathers are bound by 128-B lines, of which a 16-B record uses one eighth.  Outside the
+// no-fly zones a waypoint needs only phi and the terrain, so the packed copy keeps them as an
+// 8-B plane A = {phi, terrain as consume_chunk reads it (+0.0 on a nodata cell)}, stored in
+// blocks of 2^phb x 2^pwb cells: half the table, twice the cells per line.  A 2-bit code per
+// summary block says what a waypoint there needs: 0 = nothing (the gather-skip rule), 1 = plane
+// A only (every cell of the block has psi == +-0 and no no-fly flag: the psi term is an exact
+// no-op and the hit count adds 0), 3 = the full 16-B record from rec.  Every path sees exactly
+// the values and the operations of raster_pass2_skip, so the outputs are bit-identical.
+__device__ __forceinline__ int32_t pk_addr(const KRaster& rs, int32_t ix, int32_t iy) {
+    const int32_t blk = (iy >> rs.phb) * rs.pnbx + (ix >> rs.pwb);
+    return (blk << (rs.phb + rs.pwb)) | ((iy & ((1 << rs.phb) - 1)) << rs.pwb) |
+           (ix & ((1 << rs.pwb) - 1));
+}
+
+// spread the 16 low bits of v to the even bits of the result
+__device__ __forceinline__ uint32_t spread16(uint32_t v) {
+    v &= 0xffffu;
+    v = (v | (v << 8)) & 0x00ff00ffu;
+    v = (v | (v << 4)) & 0x0f0f0f0fu;
+    v = (v | (v << 2)) & 0x33333333u;
+    v = (v | (v << 1)) & 0x55555555u;
+    return v;
+}
+
+// one thread per cell, rows coalesced: plane A at its blocked address
+__global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ rec, KRaster rs,
+                                                     uint2* __restrict__ pa) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= (int64_t)rs.nx * rs.ny) return;
+    const int32_t iy = (int32_t)(c / rs.nx), ix = (int32_t)(c - (int64_t)iy * rs.nx);
+    const uint4 r = rec[c];
+    const int32_t a = pk_addr(rs, ix, iy);
+    pa[a] = make_uint2(r.x, (r.w & UAM_FLAG_NODATA) ? 0u : r.z);
+}
+
+// one thread per summary block: its 2-bit code; lanes 0/16/32/48 write the wave's 4 words
+__global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict__ rec,
+                                                         int32_t nx, int32_t ny, int32_t shift,
+                                                         int32_t nbx, int32_t n_blocks,
+                                                         uint32_t* __restrict__ out) {
+    const int32_t blk = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t code = 0;
+    if (blk < n_blocks) {
+        const int B = 1 << shift;
+        const int bx = blk % nbx, by = blk / nbx;
+        const int x0 = bx << shift, y0 = by << shift;
+        const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+        bool skip = true, needb = false;
+        for (int iy = y0; iy < y1; ++iy)
+            for (int ix = x0; ix < x1; ++ix) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                const uint32_t t = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
+                if ((r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ)) needb = true;
+                if ((r.x & 0x7fffffffu) || t) skip = false;
+            }
+        code = needb ? 3u : skip ? 0u : 1u;
+    }
+    const uint64_t lo = __ballot(code & 1u), hi = __ballot(code >> 1);
+    const int lane = threadIdx.x & 63;
+    if ((lane & 15) == 0 && blk < n_blocks) {
+        const int sh = lane;  // this lane's 16 blocks are bits [lane, lane + 16) of the ballots
+        out[blk >> 4] = spread16((uint32_t)(lo >> sh)) | (spread16((uint32_t)(hi >> sh)) << 1);
+    }
 }
 
 // Records mode (internal, binned raster evaluation K2b): the waypoint's record was already
@@ -4865,6 +4937,67 @@ __device__ __forceinline__ void seg_pass2(const KRaster& rs, const uint4* __rest
     }
 }
 
+// waypoints [j0, j1) of one path from the packed raster (KRaster::pmap/pa, the 2-bit block
+// codes in LDS): raster_pass2_skip's cell arithmetic, values and sums.  A code-1 waypoint
+// gathers its 8-B plane-A entry (its psi term is +-0 and its hit 0 there: exact no-ops, not
+// added); a code-3 waypoint gathers its whole 16-B record from rec, so no waypoint costs more
+// than one request.
+template <int CH>
+__device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* __restrict__ rec,
+                                               const uint32_t* map, const PathSrc<true>& src,
+                                               int j0, int j1, double dN, PathAcc& a) {
+    for (int jc = j0; jc < j1; jc += CH) {
+        uint4 r[CH];
+        uint32_t inb = 0, need = 0, full = 0;
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            if (jc + t < j1) {
+                double x0, x1;
+                src.at(jc + t, x0, x1);
+                const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+                const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+                if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
+                    inb |= 1u << t;
+                    const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
+                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                    const uint32_t code = (map[b >> 4] >> ((b & 15) * 2)) & 3u;
+                    if (code & 2u) {
+                        need |= 1u << t;
+                        full |= 1u << t;
+                        r[t] = rec[iy * rs.nx + ix];
+                    } else if (code) {
+                        need |= 1u << t;
+                        const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
+                        r[t].x = v.x;
+                        r[t].z = v.y;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            if (jc + t >= j1) break;
+            if (!((inb >> t) & 1u)) {
+                ++a.off;
+                a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
+                continue;
+            }
+            if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
+                a.hmax = fmax(a.hmax, 0.0);
+                continue;
+            }
+            a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
+            double terrain = (double)__uint_as_float(r[t].z);
+            if ((full >> t) & 1u) {
+                a.nsum = a.nsum + (double)__uint_as_float(r[t].y);
+                a.nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
+                if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0;
+            }
+            a.hmax = fmax(a.hmax, terrain);
+        }
+    }
+}
+
 // segment s of every path, items in sorted order; workgroup b takes the sorted chunk
 // xcd_chunk(b), so an XCD's workgroups cover one contiguous run of tiles.  Dynamic LDS: the
 // skip bitmap, padded to the context's floor (UAM_K2S_LDS) to cap the workgroups per CU.
@@ -4872,13 +5005,17 @@ __device__ __forceinline__ void seg_pass2(const KRaster& rs, const uint4* __rest
 // state, so pass 1's ALU work overlaps the gathers as in K2.
 // pord (optional, segment 0): items in K2's pair order instead, item i = path
 // pord[i / D] * D + i % D (no per-path sort on the critical path)
-template <bool SKIP, bool FIRST>
+// PACK: the packed raster (seg_pass2_pack; SKIP ignored), its block codes in LDS.
+template <bool SKIP, bool FIRST, bool PACK = false>
 __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks,
                                                   const uint4* __restrict__ rec, int s,
                                                   int64_t base, int32_t n,
                                                   const int32_t* __restrict__ pord) {
     extern __shared__ uint32_t s_bits[];
-    if (SKIP) {
+    if (PACK) {
+        for (int i = threadIdx.x; i < rs.pwords; i += 256) s_bits[i] = rs.pmap[i];
+        __syncthreads();
+    } else if (SKIP) {
         for (int i = threadIdx.x; i < rs.swords; i += 256) s_bits[i] = rs.sum[i];
         __syncthreads();
     }
@@ -4913,8 +5050,12 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     ks.bounds(s, j0, j1);
     // gathers in flight per lane: the capped later segments (2 waves per SIMD) have the
     // registers for more
-    seg_pass2<SKIP, FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
-                                                        (double)p.N, a);
+    if (PACK)
+        seg_pass2_pack<FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
+                                                          (double)p.N, a);
+    else
+        seg_pass2<SKIP, FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
+                                                            (double)p.N, a);
     SegState o;
     o.cost = a.cost;
     o.nsum = a.nsum;
@@ -5914,14 +6055,16 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     ks.cnt = (int32_t*)(w + b_st + b_len + b_key);
     ks.tot = (int32_t*)(w + b_st + b_len + b_key + b_cnt);
     ks.order = (int32_t*)(w + b_st + b_len + b_key + b_cnt + b_tot);
-    const size_t lds_min = kr.sum ? (size_t)kr.swords * 4 : 0;
+    const size_t lds_min = kr.pmap ? (size_t)kr.pwords * 4 : kr.sum ? (size_t)kr.swords * 4 : 0;
     const size_t lds = std::max(lds_min, (size_t)std::min(ctx->k2s_lds, 160 * 1024));
     const size_t lds0 = std::max(lds_min, (size_t)std::min(ctx->k2s_lds0, 160 * 1024));
     if (!ctx->k2s_attrs) {  // per context = per device (the caller's DeviceGuard is active)
         const void* fns[] = {(const void*)k_seg_eval<true, false>,
                              (const void*)k_seg_eval<false, false>,
                              (const void*)k_seg_eval<true, true>,
-                             (const void*)k_seg_eval<false, true>};
+                             (const void*)k_seg_eval<false, true>,
+                             (const void*)k_seg_eval<false, true, true>,
+                             (const void*)k_seg_eval<false, false, true>};
         for (const void* f : fns)
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
@@ -5996,15 +6139,18 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
             if (k == 0 && !fuse) HIP_TRY(hipStreamWaitEvent(s, ctx->k2s_ev[h], 0));
             if (k == 1 && h == 0 && two) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
             const dim3 ge((unsigned)((n + 255) / 256));
-#define UAM_LAUNCH_SEG(SK_, F_, LDS_)                                                          \
-    hipLaunchKernelGGL((k_seg_eval<SK_, F_>), ge, dim3(256), LDS_, s, ctx->kp, kr, ks,         \
+#define UAM_LAUNCH_SEG(SK_, F_, LDS_, PK_)                                                     \
+    hipLaunchKernelGGL((k_seg_eval<SK_, F_, PK_>), ge, dim3(256), LDS_, s, ctx->kp, kr, ks,    \
                        (const uint4*)rec, k, base, n, k == 0 ? pord : nullptr)
-            if (k == 0 && fuse) {
-                if (kr.sum) UAM_LAUNCH_SEG(true, true, lds0);
-                else UAM_LAUNCH_SEG(false, true, lds0);
+            if (kr.pmap) {
+                if (k == 0 && fuse) UAM_LAUNCH_SEG(false, true, lds0, true);
+                else UAM_LAUNCH_SEG(false, false, lds, true);
+            } else if (k == 0 && fuse) {
+                if (kr.sum) UAM_LAUNCH_SEG(true, true, lds0, false);
+                else UAM_LAUNCH_SEG(false, true, lds0, false);
             } else {
-                if (kr.sum) UAM_LAUNCH_SEG(true, false, lds);
-                else UAM_LAUNCH_SEG(false, false, lds);
+                if (kr.sum) UAM_LAUNCH_SEG(true, false, lds, false);
+                else UAM_LAUNCH_SEG(false, false, lds, false);
             }
 #undef UAM_LAUNCH_SEG
         }
@@ -6040,10 +6186,53 @@ static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shi
     return UAM_OK;
 }
 
+// packed-raster layout (uam_raster_pack): 2^hb x 2^wb cells per block.  Default 2 x 2 (4 x 4
+// cells of 8 B = one 128-B line); UAM_PACK_HB / UAM_PACK_WB (0..4, tuning builds) are read
+// once per process, so packing and evaluation always agree.
+static void pack_layout(int32_t* hb, int32_t* wb) {
+    static const std::pair<int32_t, int32_t> hw = [] {
+        int32_t h = 2, w = 2;
+        if (const char* e = std::getenv("UAM_PACK_HB")) h = std::max(0, std::min(4, std::atoi(e)));
+        if (const char* e = std::getenv("UAM_PACK_WB")) w = std::max(0, std::min(4, std::atoi(e)));
+        return std::make_pair(h, w);
+    }();
+    *hb = hw.first;
+    *wb = hw.second;
+}
+
+struct PackDims {
+    int32_t sh, nbx, nby, words, hb, wb, lnbx;
+    int64_t off_a, bytes;
+};
+
+static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
+    int st = summary_dims(desc, block, &d->sh, &d->nbx, &d->nby);
+    if (st) return st;
+    d->words = (int32_t)(((int64_t)d->nbx * d->nby * 2 + 31) / 32);
+    pack_layout(&d->hb, &d->wb);
+    d->lnbx = (desc->nx + (1 << d->wb) - 1) >> d->wb;
+    const int64_t lnby = (desc->ny + (1 << d->hb) - 1) >> d->hb;
+    const int64_t cells = ((int64_t)d->lnbx * lnby) << (d->hb + d->wb);
+    if (cells >= ((int64_t)1 << 31)) return fail(UAM_E_INVALID, "packed raster too large");
+    d->off_a = ((int64_t)d->words * 4 + 255) & ~(int64_t)255;
+    d->bytes = d->off_a + cells * 8;
+    return UAM_OK;
+}
+
+static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
+    kr->pmap = (const uint32_t*)packed;
+    kr->pa = (const uint2*)((const char*)packed + d.off_a);
+    kr->pwords = d.words;
+    kr->phb = d.hb;
+    kr->pwb = d.wb;
+    kr->pnbx = d.lnbx;
+}
+
 static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                           const void* rec, const uint32_t* summary, int32_t sblock,
                           const double* pairs, int64_t n_pairs, const double* utab, int32_t D,
-                          const uam_path_outputs* out, uam_stream stream) {
+                          const uam_path_outputs* out, uam_stream stream,
+                          const void* packed = nullptr) {
     int st = check_ctx(ctx, true);
     if (st) return st;
     if (n_pairs < 0 || D < 1) return fail(UAM_E_INVALID, "n_pairs < 0 or D < 1");
@@ -6062,6 +6251,14 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
             kr.sshift = sh;
             kr.snbx = nbx;
             kr.swords = (nbx * nby + 31) / 32;
+        }
+        if (packed) {
+            PackDims pd;
+            st = pack_dims(desc, sblock, &pd);
+            if (st) return st;
+            kr.sshift = pd.sh;  // the block codes use the summary's block grid
+            kr.snbx = pd.nbx;
+            set_kpack(&kr, pd, packed);
         }
     } else if (mode != UAM_MODE_ANALYTIC) {
         return fail(UAM_E_INVALID, "unknown mode %d", mode);
@@ -6101,7 +6298,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         st = launch_segmented(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
         if (st == 1) {
-            ctx->last_kernel = kr.sum ? "K2s+skip" : "K2s";
+            ctx->last_kernel = kr.pmap ? "K2s+pack" : kr.sum ? "K2s+skip" : "K2s";
             return UAM_OK;
         }
     }
@@ -6230,6 +6427,49 @@ int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* 
                          const uam_path_outputs* out, uam_stream stream) {
     return eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs, n_pairs, utab,
                           D, out, stream);
+}
+
+int uam_eval_generated_p(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
+                         const uint32_t* summary, int32_t block, const void* packed,
+                         const double* pairs, int64_t n_pairs, const double* utab, int32_t D,
+                         const uam_path_outputs* out, uam_stream stream) {
+    return eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs, n_pairs, utab,
+                          D, out, stream, packed);
+}
+
+int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
+                          int64_t* bytes) {
+    PackDims d;
+    const int st = pack_dims(desc, block, &d);
+    if (st) return st;
+    if (block_out) *block_out = 1 << d.sh;
+    if (bytes) *bytes = d.bytes;
+    return UAM_OK;
+}
+
+int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, int32_t block,
+                    void* packed, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    KRaster kr{};
+    int st = make_kraster(desc, &kr);
+    if (st) return st;
+    if (!rec || !packed) return fail(UAM_E_INVALID, "rec/packed is NULL");
+    if ((uintptr_t)packed & 255) return fail(UAM_E_INVALID, "packed must be 256-B aligned");
+    PackDims d;
+    st = pack_dims(desc, block, &d);
+    if (st) return st;
+    set_kpack(&kr, d, packed);
+    DeviceGuard dg(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t nb = d.nbx * d.nby;
+    hipLaunchKernelGGL(k_raster_pack_map, dim3(grid_for(nb, 256)), dim3(256), 0, s,
+                       (const uint4*)rec, kr.nx, kr.ny, d.sh, d.nbx, nb, (uint32_t*)packed);
+    // padding cells of the blocked layout are never addressed; the plane holds every cell
+    const int64_t cells = (int64_t)kr.nx * kr.ny;
+    hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s,
+                       (const uint4*)rec, kr, (uint2*)((char*)packed + d.off_a));
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
 }
 
 int uam_raster_summary_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,

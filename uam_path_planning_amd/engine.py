@@ -78,12 +78,14 @@ class RasterGeo:
 class CostRaster:
     """Device record raster: rec [ny, nx, 4] int32 view of {phi f32, psi f32, dem f32, flags};
     summary: the K2 gather-skip bitmap of rec (uam_raster_summary, one bit per block x block
-    cells; None = K2 gathers every waypoint).  Rebuild it (Engine.raster_summary) after rec
-    changes."""
+    cells; None = K2 gathers every waypoint); packed: the K2s packed copy of rec
+    (uam_raster_pack, 8-B planes in 4 x 4-cell blocks; None = K2s gathers rec).  Rebuild both
+    (Engine.raster_summary) after rec changes."""
     geo: RasterGeo
     rec: object = field(repr=False)
     summary: object = field(default=None, repr=False)
     block: int = 0
+    packed: object = field(default=None, repr=False)  # uam_raster_pack copy for K2s (or None)
 
     @property
     def nbytes(self):
@@ -223,18 +225,20 @@ class Engine:
         return out
 
     # -- raster ---------------------------------------------------------------------------
-    def raster_build(self, geo, dem=None, out=None, summary=True):
-        """K1 record raster (+ its K2 gather-skip summary unless summary=False)."""
+    def raster_build(self, geo, dem=None, out=None, summary=True, packed=False):
+        """K1 record raster (+ its K2 gather-skip summary and, with packed, the K2s packed copy,
+        unless summary=False)."""
         torch = _torch()
         d = None if dem is None else self.tensor(dem, torch.float32).reshape(geo.ny, geo.nx)
         rec = out if out is not None else self.empty((geo.ny, geo.nx, 4), torch.int32)
         _lib.check(self.lib.uam_raster_build(self._ctx, ctypes.byref(geo.as_struct()), _ptr(d),
                                              _ptr(rec), self.stream), "uam_raster_build")
         r = CostRaster(geo, rec)
-        return self.raster_summary(r) if summary else r
+        return self.raster_summary(r, packed=packed) if summary else r
 
-    def raster_summary(self, raster, block=0):
-        """(Re)build raster.summary from raster.rec (block 0 = automatic); returns raster."""
+    def raster_summary(self, raster, block=0, packed=False):
+        """(Re)build raster.summary (and raster.packed unless packed=False; else it is dropped)
+        from raster.rec (block 0 = automatic); returns raster."""
         torch = _torch()
         g = raster.geo.as_struct()
         b, nbx, nby = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
@@ -245,7 +249,17 @@ class Engine:
         _lib.check(self.lib.uam_raster_summary(self._ctx, ctypes.byref(g), _ptr(raster.rec),
                                                b.value, _ptr(sm), self.stream),
                    "uam_raster_summary")
-        raster.summary, raster.block = sm, b.value
+        raster.summary, raster.block, raster.packed = sm, b.value, None
+        if packed:
+            nbytes = ctypes.c_int64()
+            _lib.check(self.lib.uam_raster_pack_shape(ctypes.byref(g), b.value, None,
+                                                      ctypes.byref(nbytes)),
+                       "uam_raster_pack_shape")
+            pk = self.empty(((nbytes.value + 255) // 256, 256), torch.uint8)
+            _lib.check(self.lib.uam_raster_pack(self._ctx, ctypes.byref(g), _ptr(raster.rec),
+                                                b.value, _ptr(pk), self.stream),
+                       "uam_raster_pack")
+            raster.packed = pk
         return raster
 
     def dem_mosaic(self, tiles, xoff, yoff, nx, ny, fill=-9999.0, dem=None):
@@ -341,6 +355,12 @@ class Engine:
             o, s = outputs
             _check_outputs(o, Q * D, Q, self.params.N + 2)
         geo = None if raster is None else ctypes.byref(raster.geo.as_struct())
+        if raster is not None and raster.packed is not None:
+            _lib.check(self.lib.uam_eval_generated_p(
+                self._ctx, geo, _ptr(raster.rec), _ptr(raster.summary), int(raster.block),
+                _ptr(raster.packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
+                "uam_eval_generated_p")
+            return o
         if raster is not None and raster.summary is not None:
             _lib.check(self.lib.uam_eval_generated_s(
                 self._ctx, geo, _ptr(raster.rec), _ptr(raster.summary), int(raster.block),
