@@ -72,9 +72,10 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
     ap.add_argument("--no-skip", action="store_true",
                     help="K2 without the gather-skip bitmap (A/B; results are identical)")
-    ap.add_argument("--pack", action="store_true",
-                    help="K2s gathers from the packed copy (uam_raster_pack: 8-B phi/terrain "
-                         "plane outside the no-fly blocks; A/B, results are identical)")
+    ap.add_argument("--no-pack", action="store_true",
+                    help="K2s gathers the 16-B records instead of the packed copy "
+                         "(uam_raster_pack: 8-B phi/terrain plane outside the no-fly blocks; "
+                         "A/B, results are identical)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -205,7 +206,7 @@ def main():
         if raster_mode and not args.no_skip:
             t1 = time.perf_counter()
             # every rank derives the skip bitmap (and K2s's packed copy) locally
-            eng.raster_summary(raster, packed=args.pack)
+            eng.raster_summary(raster, packed=not args.no_pack)
             torch.cuda.synchronize()
             setup["skip_bitmap_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
             setup["skip_block"] = raster.block
@@ -291,7 +292,7 @@ def main():
     if mode == "analytic":
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
-        roofline = gather_roofline(prof, P, W, kern_ms, kernel_name)
+        roofline = gather_roofline(prof, P, W, kern_ms, kernel_name, packed=last == "K2s+pack")
     roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
                                     "launch of the kernel (K2s: around its whole launch "
                                     "sequence), on its launch stream (uam_kernel_timing)"
@@ -397,7 +398,7 @@ def main():
         dist.destroy_process_group()
 
 
-def gather_roofline(prof, P, W, kern_ms, kernel_name):
+def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False):
     """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
     definition used in SURVEY, DESIGN §4 and here): one 16-B record gather per waypoint + 16 B
     of outputs per path = 16 W + 16 B/path.  `traffic`: L2->fabric bytes per launch of the same
@@ -422,6 +423,10 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name):
          "l2_hit_rate": prof.get("l2_hit_rate"),
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
+         "record_source": ("packed (uam_raster_pack): 8-B {phi, terrain} entries outside "
+                           "the no-fly blocks, 16-B records inside them; the algorithmic bytes "
+                           "keep SURVEY's 16 B per waypoint, the information each waypoint "
+                           "consumes" if packed else "16-B records"),
          "note": "each 16-B record gather that misses L2 moves one 128-B line (PMC); the "
                  "measured random-gather ceiling (tools/gather_ceiling.hip) bounds a kernel "
                  "gathering in random order (K2); K2s's tile-sorted segments pass it through "

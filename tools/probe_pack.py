@@ -29,7 +29,7 @@ def main():
     e.set_geometry(compile_map(build_region_map(spec)))
     e.set_params(canonical_params(spec, N=80, altitude=320.0))
     R = 4096
-    raster = e.raster_build(raster_geo(R), synthetic_dem(R))
+    raster = e.raster_build(raster_geo(R), synthetic_dem(R), packed=True)
     pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
     g = e.eval_generated(pairs, arc_table(80, displacements(5)), raster=raster, want_cells=True)
     cells = g["cells"].reshape(-1).long()

@@ -4881,6 +4881,8 @@ __global__ __launch_bounds__(256) void k_seg_scatter(KSeg ks) {
     seg_group(ks, g, b, s, lo, hi);
     const uint16_t* key = ks.key + (int64_t)s * ks.P;
     int32_t* order = ks.order + ks.obase;
+    // (loading 8 strides' keys together made the segment-0 scatter 6.5 -> 5.4 us and the side
+    // stream's 85 -> 115 us beside segment 0's launch: no net change, not kept)
     for (int32_t i = lo + t; i < hi; i += 256) order[atomicAdd(&cur[key[i]], 1)] = i;
 }
 
@@ -5149,6 +5151,10 @@ struct uam_ctx {
     int k2s_segs = 2;           // K2s segments per path (UAM_K2S_SEGS: 2..8; 0 or 1 = K2)
     int k2s_lds = 80 * 1024;    // K2s segment launches: dynamic-LDS floor per workgroup, which
                                 // caps the workgroups resident per CU (UAM_K2S_LDS)
+    int k2s_lds_pack = 40 * 1024;  // the same from the packed raster (a smaller table: a wider
+                                   // window fits L2; cfg3 kernel ms by floor: 40 KiB 0.541,
+                                   // 48 0.542-0.545, 56 0.555, 64 0.555, 80 0.555; UAM_K2S_LDS
+                                   // sets both)
     int64_t k2s_min = 65536;    // K2s: smallest batch in paths it takes (UAM_K2S_MIN)
     int k2s_split = 1;          // K2s path parts whose pass 1 is pipelined (UAM_K2S_SPLIT, 1..4)
     bool k2s_fuse = true;       // K2s: segment 0's launch runs pass 1 (UAM_K2S_FUSE=0: a pass-1
@@ -5284,7 +5290,8 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_K3B_SEG")) c->k3b_seg = std::atoi(e);
     if (const char* e = std::getenv("UAM_K3B_CPL")) c->k3b_cpl = std::atoi(e);
     if (const char* e = std::getenv("UAM_K2S_SEGS")) c->k2s_segs = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K2S_LDS")) c->k2s_lds = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("UAM_K2S_LDS"))
+        c->k2s_lds = c->k2s_lds_pack = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("UAM_K2S_MIN")) c->k2s_min = std::atoll(e);
     if (const char* e = std::getenv("UAM_K2S_SPLIT")) c->k2s_split = std::atoi(e);
     if (const char* e = std::getenv("UAM_K2S_FUSE")) c->k2s_fuse = std::atoi(e) != 0;
@@ -6056,7 +6063,8 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     ks.tot = (int32_t*)(w + b_st + b_len + b_key + b_cnt);
     ks.order = (int32_t*)(w + b_st + b_len + b_key + b_cnt + b_tot);
     const size_t lds_min = kr.pmap ? (size_t)kr.pwords * 4 : kr.sum ? (size_t)kr.swords * 4 : 0;
-    const size_t lds = std::max(lds_min, (size_t)std::min(ctx->k2s_lds, 160 * 1024));
+    const size_t lds = std::max(
+        lds_min, (size_t)std::min(kr.pmap ? ctx->k2s_lds_pack : ctx->k2s_lds, 160 * 1024));
     const size_t lds0 = std::max(lds_min, (size_t)std::min(ctx->k2s_lds0, 160 * 1024));
     if (!ctx->k2s_attrs) {  // per context = per device (the caller's DeviceGuard is active)
         const void* fns[] = {(const void*)k_seg_eval<true, false>,

@@ -225,7 +225,7 @@ class Engine:
         return out
 
     # -- raster ---------------------------------------------------------------------------
-    def raster_build(self, geo, dem=None, out=None, summary=True, packed=False):
+    def raster_build(self, geo, dem=None, out=None, summary=True, packed=True):
         """K1 record raster (+ its K2 gather-skip summary and, with packed, the K2s packed copy,
         unless summary=False)."""
         torch = _torch()
@@ -236,7 +236,7 @@ class Engine:
         r = CostRaster(geo, rec)
         return self.raster_summary(r, packed=packed) if summary else r
 
-    def raster_summary(self, raster, block=0, packed=False):
+    def raster_summary(self, raster, block=0, packed=True):
         """(Re)build raster.summary (and raster.packed unless packed=False; else it is dropped)
         from raster.rec (block 0 = automatic); returns raster."""
         torch = _torch()
