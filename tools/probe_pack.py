@@ -50,6 +50,16 @@ def main():
                                          for v in (0, 1, 3)))
     print(f"gathers per waypoint {h['1'] + h['3']:.3f}; bytes per waypoint packed "
           f"{8 * h['1'] + 16 * h['3']:.2f}, 16-B form {16 * (h['1'] + h['3']):.2f}")
+    # a finer "needs the full record" map: the share of gathered waypoints that would still
+    # read 16 B if the psi / no-fly test were made per F x F cells (F = 1: per cell)
+    rec = raster.rec.reshape(R, R, 4)
+    need = ((rec[..., 1] & 0x7fffffff) != 0) | ((rec[..., 3] & 1) != 0)
+    gathered = code > 0
+    for F in (16, 8, 4, 1):
+        nf = need.reshape(R // F, F, R // F, F).any(3).any(1)
+        cf = nf[(c // R) // F, (c % R) // F] & gathered
+        print(f"need-full map at {F:2d}x{F:<2d} cells: {float(cf.sum()) / n:.3f} of waypoints "
+              f"read 16 B ({(R // F) ** 2 // 8 // 1024} KiB as a bitmap)")
 
 
 if __name__ == "__main__":
