@@ -271,10 +271,11 @@ def main():
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    if last.startswith("K2s"):
+    if last.startswith("K2s") or last == "K4s":
         ktag = last.lower()
-        kernel_name = ("K2s sequence (k_seg_hist / k_scan / k_seg_scatter, k_seg_eval<FIRST> "
-                       "fused with pass 1, k_seg_eval, k_seg_final)")
+        ev = "k_seg_eval_vol" if last == "K4s" else "k_seg_eval"
+        kernel_name = (f"{last} sequence (k_seg_hist / k_scan / k_seg_scatter, {ev}<FIRST> "
+                       f"fused with pass 1, {ev}, k_seg_final)")
     else:
         ktag = "wave" if wave else ("raster+skip" if skip else mode)
         if raster_mode and not skip and not wave:

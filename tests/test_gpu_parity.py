@@ -831,3 +831,55 @@ def test_volume_pair_order(oracle_mod, monkeypatch, order):
         np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
     np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
                                   oracle_mod.argmin(ref["cost"], 5, True))
+
+
+@pytest.mark.parametrize("segs", ["2", "3", "4"])
+def test_volume_k4s(oracle_mod, monkeypatch, segs):
+    """K4s, the segment-sorted volume evaluation (launch_segmented with a KVolume: paths cut
+    into segments, each segment's (path, segment) items sorted by the x/y tile under their
+    middle waypoint, 40-B running states in HBM), against the oracle and against K4
+    (UAM_K4S=0, the default), bit for bit: every output incl. below_terrain / min_clearance
+    and both selections.  UAM_K4S=1 selects it, UAM_K2S_MIN=0 lets it take this batch (above
+    the wave kernel's 16384 paths); altitudes leave the volume's layers both ways, some paths
+    leave its x/y extent and one pair is NaN."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.scenario import (canonical_spec, displacements, layer_weights,
+                                                raster_geo)
+    from uam_path_planning_amd.synthetic import random_pairs3d, synthetic_dem
+
+    monkeypatch.setenv("UAM_K2S_MIN", "0")
+    monkeypatch.setenv("UAM_K2S_SEGS", segs)
+    monkeypatch.setenv("UAM_K4S", "1")
+    e = Engine(0)
+    spec = canonical_spec(nfz_polygons=8)
+    orc = _setup(e, oracle_mod, spec, 24, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"])
+    R, nz, z0, dz = 256, 32, 0.0, 20.0
+    geo = raster_geo(R)
+    r2 = e.raster_build(geo, synthetic_dem(R))
+    lw = layer_weights(nz)
+    vol = e.volume_build(r2, nz, z0, dz, lw)
+    vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, z0, dz)
+    ref_vol = oracle_mod.volume_build(vd, _np(r2.rec).view(np.float32), lw)
+    pairs = random_pairs3d(3500, seed=19, zmin=-50.0, zmax=700.0)
+    pairs[::89, 0] += 70.0
+    pairs[7] = np.nan
+    ut = arc_table(24, displacements(5))
+    ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4s"
+    monkeypatch.setenv("UAM_K4S", "0")
+    e4 = Engine(0)
+    e4.set_geometry(e.geometry)
+    e4.set_params(e.params)
+    g4 = e4.eval_generated3d(pairs, ut, vol)
+    assert e4.last_kernel() == "K4"
+    for gk, ok in PATH_KEYS + (("below_terrain", "below"), ("min_clearance", "min_clearance")):
+        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
+        np.testing.assert_array_equal(_np(gpu[gk]), _np(g4[gk]), err_msg=gk)
+    np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
+                                  oracle_mod.argmin(ref["cost"], 5, True))
+    np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
+                                  oracle_mod.argmin(ref["length"], 5, False))
+    assert (ref["below"] > 0).any() and (ref["offmap"] > 0).any()

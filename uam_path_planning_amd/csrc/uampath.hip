@@ -4762,12 +4762,19 @@ struct SegState {  // 32 B per path
     int32_t nh, off;
 };
 
+struct SegStateV {  // 40 B per volume path (K4s): cmin instead of hmax, plus below-terrain
+    double cost, nsum, cmin;
+    int32_t nh, off, below, pad;
+};
+
 struct KSeg {
     const double* __restrict__ pairs;
     const double* __restrict__ utab;
     int64_t n_pairs;
     int32_t P, D, W, nseg, L, F, tshift;  // segment 0 = [0, F), then segments of L
     int32_t nsplit;             // path parts [P h / nsplit, P (h+1) / nsplit), sorted apart
+    int32_t vol;                // volume paths (K4s): pairs [Q][6], SegStateV states, kv
+    KVolume kv;
     int32_t g0;                 // sort launches: first group (blockIdx.y = g - g0)
     int64_t obase;              // sort launches: order index of group g0's first item
     SegState* __restrict__ st;  // [P]
@@ -4787,13 +4794,19 @@ struct KSeg {
 
 __device__ __forceinline__ PathSrc<true> seg_src(const KSeg& ks, int N, int32_t path) {
     const int32_t q = path / ks.D, d = path - q * ks.D;
-    const double4 pr = reinterpret_cast<const double4*>(ks.pairs)[q];
     PathSrc<true> src;
     src.W = N + 2;
     src.wp = nullptr;
-    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    if (ks.vol) {  // pairs [Q][6] = (x0, y0, z0, xf, yf, zf), as k_eval_pairs reads them
+        const double* pr = ks.pairs + 6 * (int64_t)q;
+        src.x0 = pr[0], src.y0 = pr[1], src.za = pr[2];
+        src.xf = pr[3], src.yf = pr[4], src.zb = pr[5];
+    } else {
+        const double4 pr = reinterpret_cast<const double4*>(ks.pairs)[q];
+        src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+        src.za = src.zb = 0.0;
+    }
     src.u = ks.utab + (int64_t)d * N * 2;
-    src.za = src.zb = 0.0;
     return src;
 }
 
@@ -5067,6 +5080,57 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     ks.st[path] = o;
 }
 
+// K4s: segment s of every volume path (BASELINE cfg5), items in sorted order like k_seg_eval;
+// the waypoints of [j0, j1) go through issue_chunk_vol / consume_chunk_vol, k_eval_pairs's
+// volume arithmetic, so the outputs are bit-identical to K4's.  FIRST: pass 1 in the lane.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_seg_eval_vol(KParams p, KSeg ks,
+                                                      const uint4* __restrict__ vol, int s,
+                                                      int64_t base, int32_t n) {
+    const int64_t i = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int32_t path = ks.order[base + i];
+    const PathSrc<true> src = seg_src(ks, p.N, path);
+    SegStateV* stv = reinterpret_cast<SegStateV*>(ks.st);
+    PathAcc a;
+    if (FIRST) {
+        path_pass1<true>(p, src, nullptr, a);
+        ks.p1[path] = make_double4(a.L, a.len, a.ksum, 0.0);
+        a.cost = (double)(p.N + 1) * a.L;
+        a.nsum = 0.0;
+        a.cmin = INFINITY;
+        a.nh = 0;
+        a.off = 0;
+        a.below = 0;
+    } else {
+        const SegStateV st = stv[path];
+        a.cost = st.cost;
+        a.nsum = st.nsum;
+        a.cmin = st.cmin;
+        a.nh = st.nh;
+        a.off = st.off;
+        a.below = st.below;
+    }
+    int j0, j1;
+    ks.bounds(s, j0, j1);
+    const double dN = (double)p.N;
+    constexpr int CH = FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1;
+    for (int jc = j0; jc < j1; jc += CH) {
+        Chunk<CH> ch;
+        issue_chunk_vol<true, CH>(ks.kv, vol, src, jc, j1, nullptr, ch);
+        consume_chunk_vol<true, CH>(ch, src, jc, j1, dN, a);
+    }
+    SegStateV o;
+    o.cost = a.cost;
+    o.nsum = a.nsum;
+    o.cmin = a.cmin;
+    o.nh = a.nh;
+    o.off = a.off;
+    o.below = a.below;
+    o.pad = 0;
+    stv[path] = o;
+}
+
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout) and the selection
 // over each pair's D paths
 __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out,
@@ -5081,18 +5145,28 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
     const int qi = t / D, di = t - qi * D;
     if (q0 + qi < ks.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
-        const SegState st = ks.st[gp];
         const double4 q1 = ks.p1[gp];
-        if (out.cost) out.cost[gp] = st.cost;
+        double cost, nsum, clr;
+        int32_t nh, off, below;
+        if (ks.vol) {  // K4s: clearance(p, UAM_MODE_VOLUME, a) = cmin
+            const SegStateV st = reinterpret_cast<const SegStateV*>(ks.st)[gp];
+            cost = st.cost, nsum = st.nsum, clr = st.cmin;
+            nh = st.nh, off = st.off, below = st.below;
+        } else {
+            const SegState st = ks.st[gp];
+            cost = st.cost, nsum = st.nsum, clr = p.altitude - st.hmax;
+            nh = st.nh, off = st.off, below = 0;
+        }
+        if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = q1.x;
         if (out.length) out.length[gp] = q1.y;
         if (out.kin_sum) out.kin_sum[gp] = q1.z;
-        if (out.nfz_sum) out.nfz_sum[gp] = st.nsum;
-        if (out.min_clearance) out.min_clearance[gp] = p.altitude - st.hmax;
-        if (out.nfz_hits) out.nfz_hits[gp] = st.nh;
-        if (out.offmap) out.offmap[gp] = st.off;
-        if (out.below_terrain) out.below_terrain[gp] = 0;
-        s_cost[di * 64 + qi] = st.cost;
+        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
+        if (out.min_clearance) out.min_clearance[gp] = clr;
+        if (out.nfz_hits) out.nfz_hits[gp] = nh;
+        if (out.offmap) out.offmap[gp] = off;
+        if (out.below_terrain) out.below_terrain[gp] = below;
+        s_cost[di * 64 + qi] = cost;
         s_len[di * 64 + qi] = q1.y;
     }
     __syncthreads();
@@ -5165,6 +5239,8 @@ struct uam_ctx {
                                 // key (UAM_K2S_ORDER0=1; cfg3: 376 vs 298 us, not the default)
     hipEvent_t k2s_ev[4] = {};  // K2s: pass 1 of part h done (side stream)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
+    bool k4s = false;           // UAM_K4S=1: volume batches of >= k2s_min paths through K4s
+                                // (cfg5: 0.803 ms vs K4's 0.794, so K4 stays the default)
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
@@ -5297,6 +5373,7 @@ int uam_ctx_create(int device, uam_ctx** out) {
     if (const char* e = std::getenv("UAM_K2S_FUSE")) c->k2s_fuse = std::atoi(e) != 0;
     if (const char* e = std::getenv("UAM_K2S_FIRST")) c->k2s_first = std::atoi(e);
     if (const char* e = std::getenv("UAM_K2S_ORDER0")) c->k2s_order0 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("UAM_K4S")) c->k4s = std::atoi(e) != 0;
     if (const char* e = std::getenv("UAM_K2S_LDS0")) c->k2s_lds0 = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("UAM_K8_STREAMS"))
         c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
@@ -6013,9 +6090,11 @@ static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const 
 // K2s launch (segment-sorted raster evaluation); returns 1 if launched, 0 if the batch is not
 // one it takes (the caller runs K2).  Scratch: the pair-order scratch (order_scratch), so two
 // streams sharing the context serialise on it.
+// kv (K4s): a volume evaluation, kr then carries only the volume's x/y grid for the sort keys
 static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
                             int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
-                            int32_t* best_f, int32_t* best_l, hipStream_t s) {
+                            int32_t* best_f, int32_t* best_l, hipStream_t s,
+                            const KVolume* kv = nullptr) {
     const int64_t W = ctx->kp.N + 2;
     const int want = std::min(ctx->k2s_segs, SEG_MAX);
     if (want < 2 || ko.cells || ko.g_rows || D > 16) return 0;
@@ -6031,11 +6110,13 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     const int64_t P = n_pairs * D;
     if (P < ctx->k2s_min) return 0;
     const int H = std::max(1, std::min(ctx->k2s_split, SEG_MAXSPLIT));
+    if (kv && (H != 1 || !ctx->k2s_fuse)) return 0;  // K4s: the fused single-part form only
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)H * nseg * SEG_BINS * SEG_NBK;
     const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
     if (nsb > 4096) return 0;
-    const size_t b_st = al((size_t)P * sizeof(SegState)), b_len = al((size_t)P * 32),
+    const size_t b_st = al((size_t)P * (kv ? sizeof(SegStateV) : sizeof(SegState))),
+                 b_len = al((size_t)P * 32),
                  b_key = al((size_t)nseg * P * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)nseg * P * 4),
                  b_po = al(raster_pair_order_bytes(n_pairs));
@@ -6053,6 +6134,8 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     ks.L = L;
     ks.F = F;
     ks.nsplit = H;
+    ks.vol = kv ? 1 : 0;
+    if (kv) ks.kv = *kv;
     int tshift = 0;
     while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << SEG_TBITS)) ++tshift;
     ks.tshift = tshift;
@@ -6072,7 +6155,9 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
                              (const void*)k_seg_eval<true, true>,
                              (const void*)k_seg_eval<false, true>,
                              (const void*)k_seg_eval<false, true, true>,
-                             (const void*)k_seg_eval<false, false, true>};
+                             (const void*)k_seg_eval<false, false, true>,
+                             (const void*)k_seg_eval_vol<true>,
+                             (const void*)k_seg_eval_vol<false>};
         for (const void* f : fns)
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
@@ -6125,7 +6210,7 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     if (two) {
         HIP_TRY(hipEventRecord(ctx->ev_fork, s));
         HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-        if (ctx->k2s_order0 && n_pairs < INT32_MAX) {
+        if (ctx->k2s_order0 && !kv && n_pairs < INT32_MAX) {
             st = raster_pair_order(ctx, kr, pairs, n_pairs, s, &pord, 0,
                                    w + b_st + b_len + b_key + b_cnt + b_tot + b_ord);
             if (st) return st;
@@ -6147,6 +6232,15 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
             if (k == 0 && !fuse) HIP_TRY(hipStreamWaitEvent(s, ctx->k2s_ev[h], 0));
             if (k == 1 && h == 0 && two) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
             const dim3 ge((unsigned)((n + 255) / 256));
+            if (kv) {
+                if (k == 0)
+                    hipLaunchKernelGGL(k_seg_eval_vol<true>, ge, dim3(256), lds0, s, ctx->kp, ks,
+                                       (const uint4*)rec, k, base, n);
+                else
+                    hipLaunchKernelGGL(k_seg_eval_vol<false>, ge, dim3(256), lds, s, ctx->kp, ks,
+                                       (const uint4*)rec, k, base, n);
+                continue;
+            }
 #define UAM_LAUNCH_SEG(SK_, F_, LDS_, PK_)                                                     \
     hipLaunchKernelGGL((k_seg_eval<SK_, F_, PK_>), ge, dim3(256), LDS_, s, ctx->kp, kr, ks,    \
                        (const uint4*)rec, k, base, n, k == 0 ? pord : nullptr)
@@ -6570,6 +6664,18 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    if (ctx->variant == 0 && ctx->k2s_segs > 1 && ctx->k4s) {  // K4s: segment-sorted (cfg5)
+        KRaster kxy{};
+        kxy.nx = kv.nx, kxy.ny = kv.ny, kxy.x0 = kv.x0, kxy.y_top = kv.y_top;
+        kxy.dx = vd->dx, kxy.dy = vd->dy, kxy.inv_dx = kv.inv_dx, kxy.inv_dy = kv.inv_dy;
+        st = launch_segmented(ctx, kxy, vol, pairs6, n_pairs, utab, D, ko, best_f, best_l,
+                              (hipStream_t)stream, &kv);
+        if (st < 0) return st;
+        if (st == 1) {
+            ctx->last_kernel = "K4s";
+            return UAM_OK;
+        }
+    }
     // the raster pair order over the volume's x/y extent (results do not depend on it)
     const int32_t* order = nullptr;
     if (ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
