@@ -367,8 +367,13 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
  * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
  * UAM_PAIR_ORDER=0 (uam_eval_generated without the spatial pair order it applies to
- * batches of >= 4096 pairs; raster batches then also skip the XCD placement).  None of them
- * changes results.  (K2t's result-changing diagnostics, UAM_TB_DBG, exist only in a
+ * batches of >= 4096 pairs; raster batches then also skip the XCD placement), UAM_K2S_SEGS
+ * (segment-sorted K2s: segments per path, 0 = K2), UAM_K2S_MIN (smallest K2s batch in paths),
+ * UAM_K2S_LDS / UAM_K2S_LDS0 (LDS floors of K2s's later / first segment launch),
+ * UAM_K2S_SPLIT / UAM_K2S_FUSE / UAM_K2S_FIRST / UAM_K2S_ORDER0 (K2s pass-1 placement and
+ * segment-0 forms), UAM_K4S=1 (volume batches through the segment-sorted K4s), and, read once
+ * per process, UAM_PACK_HB / UAM_PACK_WB (the packed raster's 2^hb x 2^wb-cell blocks; pack
+ * and evaluate under the same setting).  None of them changes results.  (K2t's result-changing diagnostics, UAM_TB_DBG, exist only in a
  * -DUAM_TB_DIAG build of the library.) */
 int uam_set_tuning(uam_ctx* ctx, int32_t variant);
 
