@@ -70,6 +70,9 @@ def parse():
                          "OMP_NUM_THREADS capped by the affinity mask and 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
+    ap.add_argument("--group", type=int, default=None,
+                    help="K2g waypoints per group (uam_set_option UAM_OPT_GROUP; 0 = K2s); "
+                         "default: the library's")
     ap.add_argument("--no-skip", action="store_true",
                     help="K2 without the gather-skip bitmap (A/B; results are identical)")
     ap.add_argument("--no-pack", action="store_true",
@@ -228,6 +231,8 @@ def main():
     o = outs[0]
     if args.variant:
         eng.set_tuning(args.variant)
+    if args.group is not None:
+        eng.set_option("group", args.group)
 
     def step(ev=None):
         # one launch: pair order + arc generation + gather + cost reduction + selection
@@ -271,7 +276,11 @@ def main():
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    if last.startswith("K2s") or last == "K4s":
+    if last.startswith("K2g"):
+        ktag = last.lower()
+        kernel_name = ("K2g sequence (k_g_hist / k_scan / k_g_scatter, k_g_eval over every "
+                       "(path, group) item, k_g_final; k_g_pass1 on the side stream)")
+    elif last.startswith("K2s") or last == "K4s":
         ktag = last.lower()
         ev = "k_seg_eval_vol" if last == "K4s" else "k_seg_eval"
         kernel_name = (f"{last} sequence (k_seg_hist / k_scan / k_seg_scatter, {ev}<FIRST> "
@@ -293,13 +302,16 @@ def main():
     if mode == "analytic":
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
-        roofline = gather_roofline(prof, P, W, kern_ms, kernel_name, packed=last == "K2s+pack")
+        roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
+                                   packed=last in ("K2s+pack", "K2g+pack"))
     roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
-                                    "launch of the kernel (K2s: around its whole launch "
+                                    "launch of the kernel (K2g / K2s: around the whole launch "
                                     "sequence), on its launch stream (uam_kernel_timing)"
                                     if kern_timed else
                                     "torch events around the whole step (multi-launch variant)")
     roofline["library_kernel"] = last
+    group = eng.last_group()   # the sum order the library used (0 = sequential)
+    roofline["sum_group"] = group
     roofline["step_event_ms"] = round(step_ev_ms, 4)
     roofline["profile_key"] = pkey
     result = {
@@ -321,7 +333,9 @@ def main():
                    "displacements": D, "waypoints_per_path": W, "paths_total": Q_total * D,
                    "mode": mode, "no_fly_shapes": geom.n_obstacles,
                    "region_shapes": int(geom.region_first[-1] - geom.region_first[0]),
-                   "parallelism": f"pair-sharded dp{n_gpus}, raster broadcast once"},
+                   "parallelism": (f"pair-sharded dp{world}, raster broadcast once" +
+                                   (f" ({world} ranks on {n_gpus} GPU(s), rehearsal)"
+                                    if world != n_gpus else ""))},
         "waypoint_evals_per_s": round(value * W, 1),
         "roofline": roofline,
         "setup": setup,
@@ -332,14 +346,15 @@ def main():
     # ---- parity at N > 1: every rank checks the first pairs of its shard --------------------
     if world > 1:
         mism = rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_host, o,
-                           D, N)
+                           D, N, group)
         t = torch.tensor(mism, dtype=torch.float64,
                          device=eng.torch_device if backend == "nccl" else "cpu")
         dist.all_reduce(t)
         m = [int(x) for x in t.cpu()]
         result["parity"] = {"paths_checked": m[0], "cost_mismatches": m[1],
                             "best_index_mismatches": m[2], "ranks": world,
-                            "rule": f"bit-exact float64 vs CPU oracle, first "
+                            "rule": f"bit-exact float64 vs CPU oracle (sum order: "
+                                    f"{order_name(group)}), first "
                                     f"{PARITY_PAIRS_PER_RANK} pairs of every rank's shard"}
 
     # ---- CPU baseline + parity sample (rank 0, N=1 only) ----------------------------------
@@ -354,11 +369,16 @@ def main():
         gpu_best = o["best_fval_idx"].cpu().numpy()
         chunk = 50 if mode == "analytic" else 2000
         done, t_cpu, mism, bmis = 0, 0.0, 0, 0
+        seq_rel = None
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
-            r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox)
+            r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, group)
             t_cpu += time.perf_counter() - ts
+            if group and seq_rel is None:   # grouped vs the reference's sequential order
+                rs = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, 0)
+                seq_rel = float(np.max(np.abs(r["cost"] - rs["cost"]) /
+                                       np.maximum(np.abs(rs["cost"]), 1e-300)))
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
             done += len(sl)
@@ -391,7 +411,11 @@ def main():
                       f"shards, {passes} pass(es) in {wall:.2f} s; 1 thread: {t_cpu:.1f} s"}
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
                             "best_index_mismatches": bmis,
-                            "rule": "bit-exact float64 vs CPU oracle"}
+                            "rule": f"bit-exact float64 vs CPU oracle (sum order: "
+                                    f"{order_name(group)})"}
+        if seq_rel is not None:
+            result["parity"]["max_rel_cost_vs_sequential_order"] = seq_rel
+            result["parity"]["tolerance_vs_reference"] = 1e-5
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -467,13 +491,20 @@ def oracle_inputs(O, geo, raster, volume, mode):
     return rd, rec, vd, vox
 
 
-def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox):
+def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0):
     if mode == "volume":
         return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
-    return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec)
+    return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec,
+                          group=group)
 
 
-def rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_host, o, D, N):
+def order_name(group):
+    return (f"per-path partial sums over groups of {group} waypoints, added in group order "
+            f"(oracle orc_eval_paths_g)" if group else "sequential, the reference's")
+
+
+def rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_host, o, D, N,
+                group=0):
     """[paths checked, cost mismatches, best-index mismatches] of this rank's first pairs
     against the CPU oracle (the checker; run after the timed region)."""
     from oracle import oracle as O
@@ -483,7 +514,7 @@ def rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_hos
                    altitude=params.altitude)
     n = min(PARITY_PAIRS_PER_RANK, len(pairs_host))
     rd, rec, vd, vox = oracle_inputs(O, geo, raster, volume, mode)
-    r = oracle_eval(O, orc, pairs_host[:n], ut_host, mode, rd, rec, vd, vox)
+    r = oracle_eval(O, orc, pairs_host[:n], ut_host, mode, rd, rec, vd, vox, group)
     cost = o["cost"][:n * D].cpu().numpy()
     best = o["best_fval_idx"][:n].cpu().numpy()
     return [float(n * D), float(np.sum(r["cost"] != cost)),

@@ -347,49 +347,67 @@ int uam_process_polygons(const double* xy, const int64_t* ring_start, int32_t n_
  * pieces by a second labelling on the grid refined at the box edges.  Output as
  * uam_process_polygons (regions in raster order of their first cell).  Definition:
  * oracle/uam_oracle.c orc_dem_polygons.  Work is enqueued on `stream` and, for the large
- * regions, on up to 3 side streams the context owns (UAM_K8_STREAMS, 1-8, default 4 in all);
+ * regions, on up to 3 side streams the context owns (UAM_OPT_K8_STREAMS, 1-8, 4 in all);
  * the call synchronises all of them before it returns. */
 int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* desc,
                      float threshold, double unit_m, const uam_polyproc_params* params,
                      int64_t* rect_xy, int32_t max_rects, int32_t* n_rects, uam_stream stream);
 
-/* Kernel variant for the raster/volume evaluations (0 = automatic).  1 = one wave per
- * (displacement, 64 pairs), direct stores, separate selection kernels; 2..8 = one workgroup
- * per 64 pairs x D (D <= 16) with LDS-staged coalesced stores and the selection fused,
- * differing in gathers per chunk / software pipelining / occupancy; 9 = one wave per path
- * (lanes over waypoints; small batches); 10 = never one wave per path; 11 = binned raster
- * evaluation (K2b); 12 = tile-sorted raster evaluation (K2t: waypoints binned by raster
- * tile, XCD-pinned gathers from L2, per-block LDS reduction; pass 1 on a side stream).
- * 0 picks the wave per path kernel for batches up to 16384 paths and variant 2 above.  All
- * variants return bit-identical results.
- *
- * Tuning experiments only (read once, by uam_ctx_create; unset = the defaults): UAM_K1_CPL
- * (raster build rows per lane: 1, 2, 4, 8; default 2), UAM_K1_GRID (raster build workgroup
- * cap), UAM_TB_PB / UAM_TB_K (K2t pairs per path-block / gather workgroups per XCD),
- * UAM_PAIR_ORDER=0 (uam_eval_generated without the spatial pair order it applies to
- * batches of >= 4096 pairs; raster batches then also skip the XCD placement), UAM_K2S_SEGS
- * (segment-sorted K2s: segments per path, 0 = K2), UAM_K2S_MIN (smallest K2s batch in paths),
- * UAM_K2S_LDS / UAM_K2S_LDS0 (LDS floors of K2s's later / first segment launch),
- * UAM_K2S_SPLIT / UAM_K2S_FUSE / UAM_K2S_FIRST / UAM_K2S_ORDER0 (K2s pass-1 placement and
- * segment-0 forms), UAM_K4S=1 (volume batches through the segment-sorted K4s), and, read once
- * per process, UAM_PACK_HB / UAM_PACK_WB (the packed raster's 2^hb x 2^wb-cell blocks; pack
- * and evaluate under the same setting).  None of them changes results.  (K2t's result-changing diagnostics, UAM_TB_DBG, exist only in a
- * -DUAM_TB_DIAG build of the library.) */
-int uam_set_tuning(uam_ctx* ctx, int32_t variant);
-
 /* Measurement (bench.py's roofline; build-defined).  uam_kernel_timing(ctx, 1) resets and
  * starts timing, 0 stops it: while on, the context records a HIP event pair on the launch
- * stream around every launch of the dominant path kernel (k_eval_pairs / k_eval_wave of
- * uam_eval_generated, uam_eval_generated_s and uam_eval_generated3d), excluding the pair order
- * and selection launches.  uam_kernel_time waits for those events and returns the summed
- * kernel time and the launch count since the last call (then resets the count). */
+ * stream around every timed path evaluation of uam_eval_generated* -- around the whole launch
+ * sequence of K2g and K2s (sorts, evaluation, output launch; K2g's pass 1 on the side stream is
+ * joined inside it), around the k_eval_pairs / k_eval_wave launch of the other forms (excluding
+ * their pair order and selection launches).  uam_kernel_time waits for those events and returns
+ * the summed time and the count since the last call (then resets the count).  At most 4096
+ * events pairs are pending: query at least that often (further timed calls fail UAM_E_STATE). */
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable);
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
-/* The path evaluation the last uam_eval_generated / uam_eval_generated3d call on ctx ran:
- * "K2s+skip" / "K2s" (segment-sorted raster), "K2+skip" / "K2" (lane per path), "K2w" (wave per
- * path), "K2b", "K2t", "K2v1", "K3b", "K3", "K3v1", "K4", "K4w"; "" before the first call.  The
- * string is static (never freed).  For benchmarks and tests: which kernel a number belongs to. */
+/* The path evaluation the last uam_eval_generated* call on ctx ran: "K2g+pack" (segment-grouped
+ * raster, the default for packed rasters and batches >= UAM_OPT_SORTED_MIN_PATHS paths),
+ * "K2s+pack" / "K2s+skip" / "K2s" (segment-sorted raster, sequential sums), "K2+skip" / "K2"
+ * (lane per path), "K2w" (wave per path), "K2d" (D > 16), "K3b", "K3", "K3d", "K4", "K4w";
+ * "" before the first call.  The string is static (never freed).  For benchmarks and tests:
+ * which kernel a number belongs to. */
 const char* uam_last_kernel(const uam_ctx* ctx);
+
+/* Waypoint-group length of the per-path sums of the last uam_eval_generated* call on ctx: G > 0
+ * when the segment-grouped raster evaluation K2g ran (cost and nfz_sum formed as per-group
+ * partial sums over waypoints [kG, (k+1)G) added in group order; oracle/uam_oracle.c
+ * orc_eval_paths_g), 0 for the reference's sequential order (problem.py:42-43). */
+int32_t uam_last_group(const uam_ctx* ctx);
+
+/* Context options: which kernel form runs (results never depend on them, except for the sum
+ * order UAM_OPT_GROUP selects, which uam_last_group reports).  Read by the calls that follow.
+ *   UAM_OPT_GROUP                K2g waypoints per group, 1..16 (default 8); 0 = no K2g (the
+ *                                raster batches it takes run K2s: the reference's sum order)
+ *   UAM_OPT_SORTED_MIN_PATHS     smallest raster batch (paths) the sorted forms K2g / K2s take
+ *                                (default 65536; smaller batches run K2 / K2w)
+ *   UAM_OPT_K2S_SEGMENTS         K2s segments per path, 2..8 (default 2)
+ *   UAM_OPT_WAVE_MAX_PATHS       batches of up to this many paths run one wave per path (K2w /
+ *                                K4w; default 16384; 0 = never)
+ *   UAM_OPT_PAIR_ORDER           1 (default): batches of >= 4096 pairs through the lane-per-path
+ *                                kernels in a spatial pair order; 0: in index order
+ *   UAM_OPT_K1_ROWS              raster build: cells (rows) per lane, 1, 2 (default), 4, 8
+ *   UAM_OPT_K3B_SEGMENT          analytic K3b: waypoints sorted together, 2/4/6/8 (default)/16;
+ *                                0 = the lane-per-path K3
+ *   UAM_OPT_K3B_POINTS_PER_LANE  analytic K3b evaluation phase: 1 (default) or 2
+ *   UAM_OPT_K8_TILED             DEM polygons: 1 (default) tile labelling in LDS, 0 cell-parallel
+ *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4) */
+enum {
+    UAM_OPT_GROUP = 1,
+    UAM_OPT_SORTED_MIN_PATHS = 2,
+    UAM_OPT_K2S_SEGMENTS = 3,
+    UAM_OPT_WAVE_MAX_PATHS = 4,
+    UAM_OPT_PAIR_ORDER = 5,
+    UAM_OPT_K1_ROWS = 6,
+    UAM_OPT_K3B_SEGMENT = 7,
+    UAM_OPT_K3B_POINTS_PER_LANE = 8,
+    UAM_OPT_K8_TILED = 9,
+    UAM_OPT_K8_STREAMS = 10
+};
+int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
+int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);
 
 /* Workspace bytes uam_refine needs for n_paths (after uam_set_geometry/uam_set_params). */
 int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,

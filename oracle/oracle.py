@@ -178,7 +178,7 @@ def lib():
             build()
         _lib = ctypes.CDLL(LIB_PATH)
         for name in ("orc_eval_points", "orc_gen_paths", "orc_raster_build", "orc_eval_paths",
-                     "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d",
+                     "orc_eval_paths_g", "orc_argmin", "orc_volume_build", "orc_gen_paths3d", "orc_eval_paths3d",
                      "orc_refine"):
             getattr(_lib, name).restype = ctypes.c_int
         _lib.orc_dem_polygons.restype = ctypes.c_int64
@@ -280,7 +280,10 @@ class Oracle:
 
     # -- paths -----------------------------------------------------------------------------
     def eval_paths(self, wp, mode="analytic", rdesc=None, rec=None, want_cells=False,
-                   want_g=False):
+                   want_g=False, group=0):
+        """group > 0 (raster mode): the segment-grouped summation order of K2g (partial sums
+        over waypoint groups of `group`, added in group order; uam_oracle.c orc_eval_paths_g);
+        0 = the reference's sequential order."""
         W = self.N + 2
         wp = np.ascontiguousarray(wp, dtype=np.float64).reshape(-1, W, 2)
         P = wp.shape[0]
@@ -293,14 +296,15 @@ class Oracle:
         m = 0 if mode == "analytic" else 1
         if m == 1:
             rec = np.ascontiguousarray(rec, dtype=np.float32)
-        lib().orc_eval_paths(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.c_int32(m),
-                             None if rdesc is None else ctypes.byref(rdesc),
-                             _ptr(rec if m == 1 else None, _f32p), _ptr(wp, _f64p),
-                             ctypes.c_int64(P), _ptr(out["cost"], _f64p),
-                             _ptr(out["lq"], _f64p), _ptr(out["length"], _f64p),
-                             _ptr(out["kin"], _f64p), _ptr(out["nfz"], _f64p),
-                             _ptr(out["nfz_hits"], _i32p), _ptr(out["min_clearance"], _f64p),
-                             _ptr(out["offmap"], _i32p), _ptr(cells, _i32p), _ptr(g, _f64p))
+        lib().orc_eval_paths_g(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.c_int32(m),
+                               None if rdesc is None else ctypes.byref(rdesc),
+                               _ptr(rec if m == 1 else None, _f32p), _ptr(wp, _f64p),
+                               ctypes.c_int64(P), _ptr(out["cost"], _f64p),
+                               _ptr(out["lq"], _f64p), _ptr(out["length"], _f64p),
+                               _ptr(out["kin"], _f64p), _ptr(out["nfz"], _f64p),
+                               _ptr(out["nfz_hits"], _i32p), _ptr(out["min_clearance"], _f64p),
+                               _ptr(out["offmap"], _i32p), _ptr(cells, _i32p), _ptr(g, _f64p),
+                               ctypes.c_int32(int(group)))
         if want_cells:
             out["cells"] = cells
         if want_g:

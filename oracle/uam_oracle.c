@@ -249,10 +249,17 @@ static double nrm_of(double d2, int smooth) {
     return smooth ? n * n : n; /* problem.py:94,132: norm_2(.)**2 when smooth */
 }
 
-int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const orc_raster* rs,
-                   const float* rec, const double* wp, int64_t P, double* cost, double* lq,
-                   double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
-                   int32_t* offmap, int32_t* cells, double* g_rows) {
+/* group > 0 (raster mode only): the grouped summation order of the segment-grouped raster
+ * evaluation K2g (build-defined, no reference counterpart).  The waypoints are
+ * cut into groups [kG, min((k+1)G, W)); per group a partial Φ/N sum and a partial ψ sum are
+ * formed in waypoint order from +0.0, and the partials are added to cost = (N+1)·L and to
+ * nsum = 0.0 in group order (one group when group >= W).  group = 0 is the reference's
+ * sequential order (problem.py:42-43): cost + Φ_0/N + Φ_1/N + ...  Both sum the same terms and differ by
+ * rounding only (≤ 1e-12 relative on the cfg3 batch, tests/test_oracle_golden.py). */
+int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const orc_raster* rs,
+                     const float* rec, const double* wp, int64_t P, double* cost, double* lq,
+                     double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
+                     int32_t* offmap, int32_t* cells, double* g_rows, int32_t group) {
     const int N = p->N, W = N + 2;
     const double mincos = cos(p->maxalpha);
     const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
@@ -331,8 +338,16 @@ int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const o
         double c = (double)(N + 1) * L;
         double nsum = 0.0, hmax = -INFINITY;
         int32_t nh = 0, off = 0;
+        const int grouped = (mode == 1) && group > 0;
+        double gc = 0.0, gn = 0.0; /* partials of the current group (grouped order) */
         for (int j = 0; j < W; ++j) {
             double x0 = z[2 * j], x1 = z[2 * j + 1];
+            if (grouped && j > 0 && j % group == 0) { /* group boundary: flush the partials */
+                c = c + gc;
+                nsum = nsum + gn;
+                gc = 0.0;
+                gn = 0.0;
+            }
             if (mode == 0) {
                 c = c + total_penalty(g, p, x0, x1) / (double)N;
                 for (int s = 0; s < g->n_obstacles; ++s) {
@@ -357,12 +372,21 @@ int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const o
                 const float* rc = rec + 4 * cell;
                 uint32_t fl;
                 memcpy(&fl, &rc[3], 4);
-                c = c + (double)rc[0] / (double)N;
-                nsum = nsum + (double)rc[1];
+                if (grouped) {
+                    gc = gc + (double)rc[0] / (double)N;
+                    gn = gn + (double)rc[1];
+                } else {
+                    c = c + (double)rc[0] / (double)N;
+                    nsum = nsum + (double)rc[1];
+                }
                 nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
                 double terrain = (fl & ORC_FLAG_NODATA) ? 0.0 : (double)rc[2];
                 if (terrain > hmax) hmax = terrain;
             }
+        }
+        if (grouped) { /* the last group */
+            c = c + gc;
+            nsum = nsum + gn;
         }
         if (cost) cost[pi] = c;
         if (lq) lq[pi] = L;
@@ -374,6 +398,14 @@ int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const o
         if (minclr) minclr[pi] = (mode == 1) ? p->altitude - hmax : NAN;
     }
     return 0;
+}
+
+int orc_eval_paths(const orc_geom* g, const orc_params* p, int32_t mode, const orc_raster* rs,
+                   const float* rec, const double* wp, int64_t P, double* cost, double* lq,
+                   double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
+                   int32_t* offmap, int32_t* cells, double* g_rows) {
+    return orc_eval_paths_g(g, p, mode, rs, rec, wp, P, cost, lq, length, kin, nfz, hits, minclr,
+                            offmap, cells, g_rows, 0);
 }
 
 /* main.py:175-180 over groups of G consecutive paths.  The reference keeps index i when

@@ -110,7 +110,6 @@ def test_cfg4_geotiff_tiles_8192(eng, oracle_mod, tmp_path):
     pairs = random_pairs(cfg["pairs"], seed=0)[lo:hi]
     assert len(pairs) * D == 125_000
     ut = arc_table(N, displacements(D))
-    eng.set_tuning(0)
 
     def launch(pr):
         return eng.eval_generated(pr, ut, raster=raster)
@@ -120,7 +119,7 @@ def test_cfg4_geotiff_tiles_8192(eng, oracle_mod, tmp_path):
     rd = oracle_mod.Oracle.raster_desc(g.nx, g.ny, g.x0, g.y_top, g.dx, g.dy, g.nodata,
                                        g.dem_threshold)
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs[sub], ut), mode="raster", rdesc=rd,
-                         rec=rec.view(np.float32))
+                         rec=rec.view(np.float32), group=eng.last_group())
     _check_subsample(oracle_mod, gpu, ref, sub, D)
     assert (ref["nfz_hits"] > 0).any()
     _check_properties(eng, oracle_mod, launch, pairs, gpu, D)
@@ -153,7 +152,6 @@ def test_cfg5_volume_1024x1024x64(eng, oracle_mod):
     np.testing.assert_array_equal(vox, ref_vol.view(np.int32))      # all 67M voxels
     pairs = random_pairs3d(Q, seed=0)
     ut = arc_table(N, displacements(D))
-    eng.set_tuning(0)
 
     def launch(pr):
         return eng.eval_generated3d(pr, ut, vol)

@@ -1,16 +1,15 @@
 """K2s -- the segment-sorted raster evaluation (launch_segmented: paths cut into segments, each
 segment index one launch over its items sorted by raster tile, per-path running sums carried in
 HBM) -- against the CPU oracle, bit for bit, and against the lane-per-path K2
-(UAM_K2S_SEGS=0).
+(UAM_OPT_SORTED_MIN_PATHS above the batch).  K2s is the fast form of the reference's
+sequential sum order (UAM_OPT_GROUP = 0; the default K2g is tests/test_gpu_k2g.py).
 
-What is exercised: pass 1 fused into the first segment launch or not (UAM_K2S_FUSE), 1 and
-3 path parts (UAM_K2S_SPLIT), 2, 3, 4 and 8 segments (ragged last segment; W = 3 where a segment is one
-waypoint), D = 1, 5 and 16, the gather-skip bitmap off / automatic / 4-cell blocks, the
+What is exercised: 2, 3, 4 and 8 segments (UAM_OPT_K2S_SEGMENTS; ragged last segment; W = 3
+where a segment is one waypoint), D = 1, 5 and 16, the gather-skip bitmap off / automatic / 4-cell blocks, the
 packed raster (uam_raster_pack) or the 16-B records, all region
 weights 0 over a below-sea-level DEM (maxima < 0 from gathered land, and exactly +0.0 from
 skipped sea), NaN pairs and paths that leave the raster, and two streams sharing one
-context.  UAM_K2S_MIN=0 makes K2s take these small batches; BASELINE's cfg3 size runs
-through it by default (test_gpu_parity.py::test_full_size_cfg3_properties).  Reference rule:
+context.  UAM_OPT_SORTED_MIN_PATHS = 0 makes K2s take these small batches.  Reference rule:
 problem.py:38-44 (cost), main.py:175-180 (selection)."""
 import numpy as np
 import pytest
@@ -24,8 +23,7 @@ KEYS = (("cost", "cost"), ("length_q", "lq"), ("length", "length"), ("kin_sum", 
         ("min_clearance", "min_clearance"))
 
 
-def _case(oracle_mod, monkeypatch, segs, N, weights="canonical", R=1024, nfz=16, split=1,
-          fuse=1, order0=1):
+def _case(oracle_mod, segs, N, weights="canonical", R=1024, nfz=16):
     from uam_path_planning_amd import build
     from uam_path_planning_amd.engine import Engine, PathParams
     from uam_path_planning_amd.geometry import compile_map
@@ -35,12 +33,10 @@ def _case(oracle_mod, monkeypatch, segs, N, weights="canonical", R=1024, nfz=16,
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
     build.build_library()
-    monkeypatch.setenv("UAM_K2S_SEGS", str(segs))
-    monkeypatch.setenv("UAM_K2S_MIN", "0")
-    monkeypatch.setenv("UAM_K2S_SPLIT", str(split))
-    monkeypatch.setenv("UAM_K2S_FUSE", str(fuse))
-    monkeypatch.setenv("UAM_K2S_ORDER0", str(order0))
     e = Engine(0)
+    e.set_option("group", 0)   # K2s, not the segment-grouped K2g (tests/test_gpu_k2g.py)
+    e.set_option("k2s_segments", segs)
+    e.set_option("sorted_min_paths", 0)
     spec = canonical_spec(nfz_polygons=nfz)
     w = spec["weights"] if weights == "canonical" else [0.0] * len(spec["weights"])
     opts = spec["options"]
@@ -70,14 +66,11 @@ def _check(gpu, ref, oracle_mod, D):
                                   oracle_mod.argmin(ref["length"], D, False))
 
 
-@pytest.mark.parametrize("split,fuse,order0", [(1, 1, 1), (1, 1, 0), (1, 0, 1), (3, 0, 1)])
 @pytest.mark.parametrize("weights", ["canonical", "zero"])
 @pytest.mark.parametrize("segs", [2, 3, 4, 8])
-def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fuse, order0):
+def test_k2s_vs_oracle_and_k2(oracle_mod, segs, weights):
     """4500 pairs x 5 over a 1024^2 raster, N = 40 (W = 42: 21/21, 14 x 3, 11/11/11/9,
-    6 x 7), pass 1 fused into segment 0's launch (segment 0 in K2's pair order or sorted by
-    its own key) or run as its own kernel on the side stream,
-    the paths in 1 or 3 parts (pass 1 pipelined part by part; 22500 / 3 items each),
+    6 x 7), pass 1 fused into segment 0's launch,
     skip bitmap off, automatic and 4-cell blocks, with and without the packed copy
     (uam_raster_pack: 8-B planes, 2-bit block codes); some paths leave the raster and two pairs
     are NaN.  Every output and both selections equal the oracle's, and K2's."""
@@ -85,8 +78,7 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
     from uam_path_planning_amd.scenario import displacements
     from uam_path_planning_amd.synthetic import random_pairs
 
-    e, orc, raster, rd, rec = _case(oracle_mod, monkeypatch, segs, 40, weights, split=split,
-                                    fuse=fuse, order0=order0)
+    e, orc, raster, rd, rec = _case(oracle_mod, segs, 40, weights)
     D = 5
     ut = arc_table(40, displacements(D))
     pairs = random_pairs(4500, seed=12)
@@ -94,10 +86,11 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
     pairs[5, 1] = np.nan
     pairs[77] = np.nan
     ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
-    monkeypatch.setenv("UAM_K2S_SEGS", "0")
     from uam_path_planning_amd.engine import Engine
 
     k2 = Engine(0)
+    k2.set_option("group", 0)
+    k2.set_option("wave_max_paths", 0)     # the lane-per-path K2 at this batch size
     k2.set_geometry(e.geometry)
     k2.set_params(e.params)
     for block, pack in ((None, False), (0, False), (4, False), (0, True), (4, True)):
@@ -120,14 +113,14 @@ def test_k2s_vs_oracle_and_k2(oracle_mod, monkeypatch, segs, weights, split, fus
 
 @pytest.mark.parametrize("D", [1, 16])
 @pytest.mark.parametrize("N", [1, 80])
-def test_k2s_displacements_and_short_paths(oracle_mod, monkeypatch, D, N):
+def test_k2s_displacements_and_short_paths(oracle_mod, D, N):
     """D = 1 (blockDim 64 in the output launch) and 16 (1024), N = 1 (W = 3: four segments
     become three of one waypoint) and N = 80 (cfg3's W = 82), ragged pair counts above the
     wave-per-path kernel's automatic range."""
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.synthetic import random_pairs
 
-    e, orc, raster, rd, rec = _case(oracle_mod, monkeypatch, 4, N)
+    e, orc, raster, rd, rec = _case(oracle_mod, 4, N)
     e.raster_summary(raster, 0, packed=True)
     ds = np.linspace(-1.0, 1.0, D) if D > 1 else np.array([0.3])
     ut = arc_table(N, ds)
@@ -138,7 +131,7 @@ def test_k2s_displacements_and_short_paths(oracle_mod, monkeypatch, D, N):
     _check(gpu, ref, oracle_mod, D)
 
 
-def test_k2s_two_streams(oracle_mod, monkeypatch):
+def test_k2s_two_streams(oracle_mod):
     """Two K2s batches enqueued on two streams of one context without host synchronisation:
     the segment state, keys and orders live in the context's order scratch, so the second
     launch waits for the first one's last read -- both must come out exactly as the oracle
@@ -147,7 +140,7 @@ def test_k2s_two_streams(oracle_mod, monkeypatch):
     from uam_path_planning_amd.scenario import displacements
     from uam_path_planning_amd.synthetic import random_pairs
 
-    e, orc, raster, rd, rec = _case(oracle_mod, monkeypatch, 4, 40)
+    e, orc, raster, rd, rec = _case(oracle_mod, 4, 40)
     e.raster_summary(raster, 0)
     D = 5
     ut = arc_table(40, displacements(D))

@@ -1,6 +1,6 @@
 """K3b -- analytic-mode evaluation with the block's waypoints sorted by shape-grid cell
 (k_eval_pairs_k3b, the default for uam_eval_generated in analytic mode without g rows) -- against
-the CPU oracle, bit for bit, and against the lane-per-path K3 (UAM_K3B_SEG=0).
+the CPU oracle, bit for bit, and against the lane-per-path K3 (UAM_OPT_K3B_SEGMENT = 0).
 
 What is exercised: segment lengths 2/4/8/16 with W not a multiple of the segment (ragged last
 segment), D = 1, 5, 16 (blockDim 64..1024; the LDS picks a shorter segment at D = 16), the pair
@@ -29,9 +29,9 @@ def _engine(monkeypatch, seg, spec, params, cpl=2):
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
     build.build_library()
-    monkeypatch.setenv("UAM_K3B_SEG", str(seg))
-    monkeypatch.setenv("UAM_K3B_CPL", str(cpl))
     e = Engine(0)
+    e.set_option("k3b_segment", seg)
+    e.set_option("k3b_points_per_lane", cpl)
     e.set_geometry(compile_map(build_region_map(spec)))
     e.set_params(params)
     return e

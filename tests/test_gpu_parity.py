@@ -194,8 +194,8 @@ def test_raster_build_list_walk_and_partial_waves(eng, oracle_mod):
 @pytest.mark.parametrize("cpl", [1, 2, 4, 8])
 @pytest.mark.parametrize("big", [False, True])
 def test_raster_build_cells_per_lane(oracle_mod, cpl, big, monkeypatch):
-    """K1 with 1 (single-cell kernel), 2, 4 and 8 rows per lane (UAM_K1_CPL, read when the
-    context is created) on a 333 x 251 raster: partial strips in both directions, lanes whose
+    """K1 with 1 (single-cell kernel), 2, 4 and 8 rows per lane (UAM_OPT_K1_ROWS) on a
+    333 x 251 raster: partial strips in both directions, lanes whose
     cells fall in different grid slots, the merged psi/contains walk (masks) and -- big: 306
     obstacles and a >256-shape region table -- the per-cell list cursors.  Non-smooth penalty
     and obstacle options take the other psi branch."""
@@ -203,8 +203,8 @@ def test_raster_build_cells_per_lane(oracle_mod, cpl, big, monkeypatch):
     from uam_path_planning_amd.scenario import canonical_spec
     from uam_path_planning_amd.synthetic import random_convex_polygons, synthetic_dem
 
-    monkeypatch.setenv("UAM_K1_CPL", str(cpl))
     e2 = Engine(0)
+    e2.set_option("k1_rows", cpl)
     spec = canonical_spec(nfz_polygons=300 if big else 64, seed=4)
     if big:
         spec["regions"][1]["shapes"] = spec["regions"][1]["shapes"] + [
@@ -247,14 +247,15 @@ def _raster_case(eng, oracle_mod, R, Q, N, nfz, seed=0, D=5, geo=None):
 
 @pytest.mark.parametrize("R,Q,N", [(256, 300, 80), (2048, 200, 254), (512, 64, 1)])
 def test_raster_eval_generated_vs_oracle(eng, oracle_mod, R, Q, N):
-    """Both the wave-per-path kernel (tuning 9, what 0 picks for these batch sizes) and the
-    lane-per-path kernels (tuning 10) against the oracle, generated and explicit paths."""
+    """Both the wave-per-path kernel (what the default picks for these batch sizes) and the
+    lane-per-path kernels (UAM_OPT_WAVE_MAX_PATHS = 0) against the oracle, generated and
+    explicit paths."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, R, Q, N, nfz=4)
     wp = oracle_mod.gen_paths(pairs, ut)
     ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, want_cells=True)
     try:
-        for v in (9, 10):
-            eng.set_tuning(v)
+        for wmax in (1 << 40, 0):
+            eng.set_option("wave_max_paths", wmax)
             gpu = eng.eval_generated(pairs, ut, raster=raster, want_cells=True)
             _assert_paths_equal(gpu, ref, raster=True)
             np.testing.assert_array_equal(_np(gpu["cells"]), ref["cells"])
@@ -267,7 +268,7 @@ def test_raster_eval_generated_vs_oracle(eng, oracle_mod, R, Q, N):
             _assert_paths_equal(gpu2, ref, raster=True)
             np.testing.assert_array_equal(_np(gpu2["cells"]), ref["cells"])
     finally:
-        eng.set_tuning(0)
+        eng.set_option("wave_max_paths", 16384)
 
 
 def test_raster_matches_reference_at_snapped_centres(eng, oracle_mod):
@@ -323,13 +324,19 @@ def test_full_size_cfg3_properties(eng, oracle_mod):
     oracle on a 2k-pair subsample (bit-exact), size-independent properties on the rest."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 4096, 100_000, 80, nfz=64)
     gpu = eng.eval_generated(pairs, ut, raster=raster)
-    assert eng.last_kernel().startswith("K2s")     # the default for this batch size
+    assert eng.last_kernel() == "K2g+pack"     # the default for this batch size
+    group = eng.last_group()
+    assert group > 0
     sub = np.random.default_rng(7).choice(len(pairs), 2000, replace=False)
     sub.sort()
-    ref = orc.eval_paths(oracle_mod.gen_paths(pairs[sub], ut), mode="raster", rdesc=rd, rec=rec)
+    wp = oracle_mod.gen_paths(pairs[sub], ut)
+    ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, group=group)
     idx = (sub[:, None] * 5 + np.arange(5)).reshape(-1)
     for gk, ok in PATH_KEYS:
         np.testing.assert_array_equal(_np(gpu[gk])[idx], ref[ok], err_msg=gk)
+    # the grouped sums against the reference's sequential order: rounding only (bar 1e-5)
+    seq = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
+    np.testing.assert_allclose(_np(gpu["cost"])[idx], seq["cost"], rtol=1e-12, atol=0)
     cost, lq = _np(gpu["cost"]), _np(gpu["length_q"])
     assert np.isfinite(cost).all()
     assert (cost >= 81 * lq - 1e-9).all()                 # penalties are non-negative
@@ -385,58 +392,39 @@ def test_dropin_problem_and_solver(eng):
 
 
 @pytest.mark.parametrize("D", [5, 3, 17])
-def test_kernel_variants_bit_identical(eng, oracle_mod, D):
-    """Every uam_set_tuning variant returns the same bits (and the fused selection matches the
-    oracle's rule); D=17 exercises the fallback to the per-wave kernel + separate selection."""
+def test_raster_kernels_bit_identical(eng, oracle_mod, D):
+    """The raster forms return the same bits: the wave-per-path kernel, the lane-per-path K2
+    (with the skip bitmap), K2s and K2g (against the grouped oracle), and the fused selection
+    matches the oracle's rule; D = 17 exercises the fallback to the per-wave kernel + separate
+    selection (K2d / K3d)."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 512, 333, 80, nfz=4, D=D)
-    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
+    wp = oracle_mod.gen_paths(pairs, ut)
+    ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
+    seen = set()
     try:
-        for v in range(0, 13):
-            eng.set_tuning(v)
+        for wmax, smin, group in ((1 << 40, 65536, 8), (0, 65536, 8), (0, 0, 0), (0, 0, 8)):
+            eng.set_option("wave_max_paths", wmax)
+            eng.set_option("sorted_min_paths", smin)
+            eng.set_option("group", group)
             gpu = eng.eval_generated(pairs, ut, raster=raster)
-            _assert_paths_equal(gpu, ref, raster=True)
+            seen.add(eng.last_kernel())
+            r = ref if eng.last_group() == 0 else orc.eval_paths(
+                wp, mode="raster", rdesc=rd, rec=rec, group=eng.last_group())
+            _assert_paths_equal(gpu, r, raster=True)
             np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
-                                          oracle_mod.argmin(ref["cost"], D, True))
+                                          oracle_mod.argmin(r["cost"], D, True))
             np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
-                                          oracle_mod.argmin(ref["length"], D, False))
-            ga = eng.eval_generated(pairs[:50], ut)      # analytic path of the same variant
+                                          oracle_mod.argmin(r["length"], D, False))
+            ga = eng.eval_generated(pairs[:50], ut)      # analytic path of the same settings
             ra = orc.eval_paths(oracle_mod.gen_paths(pairs[:50], ut))
             _assert_paths_equal(ga, ra)
     finally:
-        eng.set_tuning(0)
+        eng.set_option("wave_max_paths", 16384)
+        eng.set_option("sorted_min_paths", 65536)
+        eng.set_option("group", 8)
+    assert seen == ({"K2w", "K2d"} if D > 16 else {"K2w", "K2+skip", "K2s+pack", "K2g+pack"})
     with pytest.raises(ValueError):
-        eng.set_tuning(99)
-
-
-@pytest.mark.parametrize("R,Q,N,D,crop", [(512, 1003, 80, 5, False), (700, 257, 80, 3, True),
-                                            (2048, 333, 254, 5, False), (300, 77, 1, 16, True),
-                                            (8192, 2000, 80, 5, False)])
-def test_tiled_eval_vs_oracle(eng, oracle_mod, R, Q, N, D, crop):
-    """K2t (tuning 12: tile-binned, LDS-sorted, XCD-pinned gathers, block reduction) against
-    the oracle: partial edge tiles, rasters that do not cover the paths (off-raster bin),
-    ragged last path-blocks, W = 3 and W = 256 (smaller path-blocks), D = 16, 8192^2."""
-    from uam_path_planning_amd.engine import RasterGeo
-
-    geo = None
-    if crop:   # R x R/2 cells over part of the map: many waypoints fall off the raster
-        geo = RasterGeo(nx=R, ny=R // 2, x0=8.0, y_top=5.0, dx=40.0 / R, dy=40.0 / R,
-                        nodata=-9999.0, dem_threshold=0.0)
-    orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, R, Q, N, nfz=4, D=D,
-                                                   geo=geo)
-    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec)
-    if crop:
-        assert (ref["offmap"] > 0).any() and (ref["offmap"] < N + 2).any()
-    try:
-        eng.set_tuning(12)
-        for _ in range(2):   # second launch reuses the grown scratch
-            gpu = eng.eval_generated(pairs, ut, raster=raster)
-            _assert_paths_equal(gpu, ref, raster=True)
-            np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
-                                          oracle_mod.argmin(ref["cost"], D, True))
-            np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
-                                          oracle_mod.argmin(ref["length"], D, False))
-    finally:
-        eng.set_tuning(0)
+        eng.set_option("wave_max_paths", -1)
 
 
 @pytest.mark.parametrize("enl", [-0.5, -1e-3, 0.0, 1e-3, 0.3, 2.0])
@@ -529,14 +517,14 @@ def test_volume_mode_vs_oracle(eng, oracle_mod):
     ut = arc_table(40, displacements(5))
     ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
     try:
-        for v in (10, 9):   # lane-per-path, then wave-per-path (the auto pick at this size)
-            eng.set_tuning(v)
+        for wmax in (0, 1 << 40):   # lane-per-path, then wave-per-path (the auto pick here)
+            eng.set_option("wave_max_paths", wmax)
             gpu = eng.eval_generated3d(pairs, ut, vol)
             for gk, ok in PATH_KEYS + (("below_terrain", "below"),
                                        ("min_clearance", "min_clearance")):
-                np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=f"{gk} v{v}")
+                np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=f"{gk} w{wmax}")
     finally:
-        eng.set_tuning(0)
+        eng.set_option("wave_max_paths", 16384)
     assert (_np(gpu["offmap"]) > 0).any() and (_np(gpu["below_terrain"]) > 0).any()
     np.testing.assert_array_equal(_np(gpu["best_fval_idx"]), oracle_mod.argmin(ref["cost"], 5, True))
 
@@ -571,7 +559,7 @@ def test_shape_grid_index_is_exact(eng, oracle_mod):
 @pytest.mark.parametrize("order", ["1", "0"])
 def test_generated_analytic_pair_order(oracle_mod, monkeypatch, order):
     """K3 evaluates batches of >= 4096 pairs in a spatial (Morton) order of the pairs
-    (UAM_PAIR_ORDER, default on) and writes every result at its pair's own index: the outputs
+    (UAM_OPT_PAIR_ORDER, default on) and writes every result at its pair's own index: the outputs
     and the selection equal the oracle's, bit for bit, with the order on and off."""
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import Engine
@@ -580,8 +568,8 @@ def test_generated_analytic_pair_order(oracle_mod, monkeypatch, order):
                                                 canonical_spec, displacements)
     from uam_path_planning_amd.synthetic import random_pairs
 
-    monkeypatch.setenv("UAM_PAIR_ORDER", order)
     e2 = Engine(0)
+    e2.set_option("pair_order", int(order))
     spec = canonical_spec(nfz_polygons=CONFIGS["cfg3"]["nfz_polygons"])
     params = canonical_params(spec, N=40, altitude=320.0)
     e2.set_geometry(compile_map(build_region_map(spec)))
@@ -605,7 +593,7 @@ def test_generated_analytic_pair_order(oracle_mod, monkeypatch, order):
 @pytest.mark.parametrize("weights", ["canonical", "zero"])
 def test_raster_pair_order_and_gather_skip(oracle_mod, monkeypatch, order, weights):
     """K2 (raster, lane per path) with the spatial pair order + XCD placement on and off
-    (UAM_PAIR_ORDER) and with the gather-skip bitmap at several block sizes and without it:
+    (UAM_OPT_PAIR_ORDER) and with the gather-skip bitmap at several block sizes and without it:
     every output, the cells and the selection equal the oracle's bit for bit.  With all region
     weights 0 and every land cell below sea level, Phi is +0 everywhere: the sea blocks are
     skipped (terrain +0.0 enters the maximum without a gather) while the below-sea-level land
@@ -615,8 +603,8 @@ def test_raster_pair_order_and_gather_skip(oracle_mod, monkeypatch, order, weigh
     from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
     from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
 
-    monkeypatch.setenv("UAM_PAIR_ORDER", order)
     e2 = Engine(0)
+    e2.set_option("pair_order", int(order))
     spec = canonical_spec(nfz_polygons=16)
     w = spec["weights"] if weights == "canonical" else [0.0] * len(spec["weights"])
     orc = _setup(e2, oracle_mod, spec, 40, spec["options"], spec["maxratio"], spec["maxalpha"],
@@ -803,7 +791,7 @@ def test_pair_order_two_streams(oracle_mod, mode):
 @pytest.mark.parametrize("order", ["1", "0"])
 def test_volume_pair_order(oracle_mod, monkeypatch, order):
     """Config 5's kernel with the raster pair order over the volume's x/y extent (batches of
-    >= 4096 pairs; UAM_PAIR_ORDER on and off): every output and the selection bit-exact vs
+    >= 4096 pairs; UAM_OPT_PAIR_ORDER on and off): every output and the selection bit-exact vs
     the oracle -- each pair is still read and written at its own index."""
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import Engine
@@ -811,8 +799,8 @@ def test_volume_pair_order(oracle_mod, monkeypatch, order):
                                                 raster_geo)
     from uam_path_planning_amd.synthetic import random_pairs3d, synthetic_dem
 
-    monkeypatch.setenv("UAM_PAIR_ORDER", order)
     e = Engine(0)
+    e.set_option("pair_order", int(order))
     spec = canonical_spec(nfz_polygons=8)
     orc = _setup(e, oracle_mod, spec, 24, spec["options"], spec["maxratio"], spec["maxalpha"],
                  spec["enlargement"], spec["weights"])
@@ -831,55 +819,3 @@ def test_volume_pair_order(oracle_mod, monkeypatch, order):
         np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
     np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
                                   oracle_mod.argmin(ref["cost"], 5, True))
-
-
-@pytest.mark.parametrize("segs", ["2", "3", "4"])
-def test_volume_k4s(oracle_mod, monkeypatch, segs):
-    """K4s, the segment-sorted volume evaluation (launch_segmented with a KVolume: paths cut
-    into segments, each segment's (path, segment) items sorted by the x/y tile under their
-    middle waypoint, 40-B running states in HBM), against the oracle and against K4
-    (UAM_K4S=0, the default), bit for bit: every output incl. below_terrain / min_clearance
-    and both selections.  UAM_K4S=1 selects it, UAM_K2S_MIN=0 lets it take this batch (above
-    the wave kernel's 16384 paths); altitudes leave the volume's layers both ways, some paths
-    leave its x/y extent and one pair is NaN."""
-    from uam_path_planning_amd.arcs import arc_table
-    from uam_path_planning_amd.engine import Engine
-    from uam_path_planning_amd.scenario import (canonical_spec, displacements, layer_weights,
-                                                raster_geo)
-    from uam_path_planning_amd.synthetic import random_pairs3d, synthetic_dem
-
-    monkeypatch.setenv("UAM_K2S_MIN", "0")
-    monkeypatch.setenv("UAM_K2S_SEGS", segs)
-    monkeypatch.setenv("UAM_K4S", "1")
-    e = Engine(0)
-    spec = canonical_spec(nfz_polygons=8)
-    orc = _setup(e, oracle_mod, spec, 24, spec["options"], spec["maxratio"], spec["maxalpha"],
-                 spec["enlargement"], spec["weights"])
-    R, nz, z0, dz = 256, 32, 0.0, 20.0
-    geo = raster_geo(R)
-    r2 = e.raster_build(geo, synthetic_dem(R))
-    lw = layer_weights(nz)
-    vol = e.volume_build(r2, nz, z0, dz, lw)
-    vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, z0, dz)
-    ref_vol = oracle_mod.volume_build(vd, _np(r2.rec).view(np.float32), lw)
-    pairs = random_pairs3d(3500, seed=19, zmin=-50.0, zmax=700.0)
-    pairs[::89, 0] += 70.0
-    pairs[7] = np.nan
-    ut = arc_table(24, displacements(5))
-    ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)
-    gpu = e.eval_generated3d(pairs, ut, vol)
-    assert e.last_kernel() == "K4s"
-    monkeypatch.setenv("UAM_K4S", "0")
-    e4 = Engine(0)
-    e4.set_geometry(e.geometry)
-    e4.set_params(e.params)
-    g4 = e4.eval_generated3d(pairs, ut, vol)
-    assert e4.last_kernel() == "K4"
-    for gk, ok in PATH_KEYS + (("below_terrain", "below"), ("min_clearance", "min_clearance")):
-        np.testing.assert_array_equal(_np(gpu[gk]), ref[ok], err_msg=gk)
-        np.testing.assert_array_equal(_np(gpu[gk]), _np(g4[gk]), err_msg=gk)
-    np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
-                                  oracle_mod.argmin(ref["cost"], 5, True))
-    np.testing.assert_array_equal(_np(gpu["best_length_idx"]),
-                                  oracle_mod.argmin(ref["length"], 5, False))
-    assert (ref["below"] > 0).any() and (ref["offmap"] > 0).any()

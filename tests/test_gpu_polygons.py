@@ -111,15 +111,15 @@ def test_population_pipeline_reproduces_reference(eng, tmp_path):
 @pytest.mark.parametrize("tiled", ["1", "0"])
 @pytest.mark.parametrize("nx,ny,thr", [(700, 450, 0.0), (129, 1000, 150.0), (1000, 63, 0.0)])
 def test_dem_polygons_tile_edges(oracle_mod, monkeypatch, tiled, nx, ny, thr):
-    """Tile labelling (UAM_K8_TILE=1, the default: 64 x 64 LDS tiles + edge joins) and the
+    """Tile labelling (UAM_OPT_K8_TILED = 1, the default: 64 x 64 LDS tiles + edge joins) and the
     cell-parallel merge (0) on rasters that are not multiples of the tile: partial tiles on
     both edges, a single tile row, components crossing many tile edges, large regions split
     into box pieces (cuts inside and across tiles)."""
     from uam_path_planning_amd.engine import Engine, RasterGeo
     from uam_path_planning_amd.synthetic import synthetic_dem
 
-    monkeypatch.setenv("UAM_K8_TILE", tiled)
     e2 = Engine(0)
+    e2.set_option("k8_tiled", int(tiled))
     dx = 60.0 / max(nx, ny)
     geo = RasterGeo(nx=nx, ny=ny, x0=0.0, y_top=20.0, dx=dx, dy=dx, nodata=-9999.0,
                     dem_threshold=thr)
@@ -133,14 +133,14 @@ def test_dem_polygons_tile_edges(oracle_mod, monkeypatch, tiled, nx, ny, thr):
 
 @pytest.mark.parametrize("streams", ["1", "2", "8"])
 def test_dem_polygons_region_streams(oracle_mod, monkeypatch, streams):
-    """The large regions spread over 1, 2 or 8 streams (UAM_K8_STREAMS; default 4): same
+    """The large regions spread over 1, 2 or 8 streams (UAM_OPT_K8_STREAMS; default 4): same
     rectangles in the same order as the oracle."""
     from uam_path_planning_amd.engine import Engine
     from uam_path_planning_amd.scenario import raster_geo
     from uam_path_planning_amd.synthetic import synthetic_dem
 
-    monkeypatch.setenv("UAM_K8_STREAMS", streams)
     e2 = Engine(0)
+    e2.set_option("k8_streams", int(streams))
     geo = raster_geo(1024)
     dem = synthetic_dem(1024, seed=5)
     got = _arr(e2.dem_polygons(dem, geo, 0.0))

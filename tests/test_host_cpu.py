@@ -27,7 +27,8 @@ def test_header_symbols_exported(lib):
 
     with open(os.path.join(ROOT, "include", "uampath.h")) as f:
         text = f.read()
-    declared = set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(uam_\w+)\s*\(", text, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int32_t|int64_t|void|const char\*)\s+(uam_\w+)\s*\(", text,
+                              re.M))
     assert len(declared) >= 15
     for name in declared:
         assert hasattr(lib, name), name

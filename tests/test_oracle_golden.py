@@ -140,3 +140,65 @@ def test_geometry_errors(oracle_mod):
     with pytest.raises(ValueError) as ei:
         oracle_mod.arc_table(4, [1.5])
     assert str(ei.value) == errs["arc_displacement_gt1"]["message"]
+
+
+def _grouped_restatement(wp, rec, rd, N, group):
+    """Pure-Python statement of the K2g sum order (independent of uam_oracle.c): per path and
+    group k the raster terms Φ/N and ψ of waypoints [kG, (k+1)G) summed from +0.0 in waypoint
+    order.  Returns the per-path lists of (Φ/N partial, ψ partial); the caller adds them to
+    (N+1)·L and to 0.0 in group order."""
+    W = N + 2
+    out_pen, out_n = [], []
+    for z in wp:
+        parts = []
+        for k0 in range(0, W, group):
+            gc, gn = 0.0, 0.0
+            for j in range(k0, min(k0 + group, W)):
+                fx = np.floor((z[j, 0] - rd.x0) * (1.0 / rd.dx))
+                fy = np.floor((rd.y_top - z[j, 1]) * (1.0 / rd.dy))
+                if not (0.0 <= fx < rd.nx and 0.0 <= fy < rd.ny):
+                    continue
+                r = rec[int(fy), int(fx)]
+                gc = gc + float(r[0]) / float(N)
+                gn = gn + float(r[1])
+            parts.append((gc, gn))
+        out_pen.append(parts)
+    return out_pen
+
+
+@pytest.mark.parametrize("group", [1, 3, 8, 16, 200])
+def test_grouped_sum_order(oracle_mod, group):
+    """The grouped order of the segment-grouped raster evaluation (K2g; orc_eval_paths_g):
+    the C oracle equals a pure-Python statement of it bit for bit, and differs from the
+    reference's sequential order (problem.py:42-43; orc_eval_paths) by rounding only, far
+    inside the north_star's 1e-5 -- every order-free output is identical."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=8)
+    N = 40
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                            spec["maxalpha"], spec["enlargement"], spec["weights"],
+                            altitude=320.0)
+    geo = raster_geo(256)
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                       geo.nodata, geo.dem_threshold)
+    rec = orc.raster_build(rd, synthetic_dem(256))
+    pairs = random_pairs(60, seed=4)
+    pairs[::7, 0] += 40.0          # some waypoints off the raster
+    wp = oracle_mod.gen_paths(pairs, arc_table(N, displacements(5)))
+    seq = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
+    grp = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, group=group)
+    parts = _grouped_restatement(wp, rec, rd, N, group)
+    for i, pp in enumerate(parts):
+        c, n = float(N + 1) * grp["lq"][i], 0.0
+        for gc, gn in pp:
+            c = c + gc
+            n = n + gn
+        assert c == grp["cost"][i] and n == grp["nfz"][i]
+    for k in ("lq", "length", "kin", "nfz_hits", "offmap", "min_clearance"):
+        np.testing.assert_array_equal(grp[k], seq[k], err_msg=k)
+    np.testing.assert_allclose(grp["cost"], seq["cost"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(grp["nfz"], seq["nfz"], rtol=1e-12, atol=1e-300)
+    assert (seq["offmap"] > 0).any() and (seq["nfz"] > 0).any()

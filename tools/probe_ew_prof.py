@@ -33,7 +33,7 @@ def main():
     raster = eng.raster_build(raster_geo(2048), synthetic_dem(2048))
     pairs = torch.tensor(random_pairs(200, seed=0), device="cuda")
     ut = arc_table(254, displacements(5))
-    eng.set_tuning(9)
+    eng.set_option("wave_max_paths", 1 << 40)
     for _ in range(5):
         eng.eval_generated(pairs, ut, raster=raster)
     torch.cuda.synchronize()

@@ -28,8 +28,6 @@ def main():
         subprocess.run([B.hipcc(), *B.HIPCC_FLAGS, "-DUAM_K3B_DIAG", "-o", out, *B.SRCS],
                        check=True)
     os.environ["UAM_LIB_PATH"] = out
-    os.environ["UAM_K3B_SEG"] = str(a.seg)
-    os.environ["UAM_K3B_CPL"] = str(a.cpl)
     import torch
     from uam_path_planning_amd import _lib
     from uam_path_planning_amd.arcs import arc_table
@@ -45,6 +43,8 @@ def main():
     spec = canonical_spec(nfz_polygons=CONFIGS["cfg3"]["nfz_polygons"])
     params = canonical_params(spec, N=80, altitude=320.0)
     e = Engine(0)
+    e.set_option("k3b_segment", a.seg)
+    e.set_option("k3b_points_per_lane", a.cpl)
     e.set_geometry(compile_map(build_region_map(spec)))
     e.set_params(params)
     ut = e.tensor(arc_table(80, displacements(5)), torch.float64)

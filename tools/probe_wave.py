@@ -1,5 +1,5 @@
 """Lane-per-path (tuning 2) vs wave-per-path (tuning 9) raster evaluation across batch sizes,
-to place the automatic crossover (uampath.hip UAM_WAVE_AUTO_PATHS).
+to place the automatic crossover (UAM_OPT_WAVE_MAX_PATHS, default 16384).
 usage: python tools/probe_wave.py [--R 4096] [--N 80]"""
 import argparse
 import json
@@ -35,8 +35,8 @@ def main():
         outd = out[0]
         row = {"pairs": Q, "paths": Q * 5, "N": a.N, "R": a.R}
         res = {}
-        for v in (2, 9):
-            eng.set_tuning(v)
+        for v, wmax in ((2, 0), (9, 1 << 40)):   # 2 = lane per path, 9 = wave per path
+            eng.set_option("wave_max_paths", wmax)
             for _ in range(3):
                 eng.eval_generated(pairs, ut, raster=raster, outputs=out)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,7 +51,7 @@ def main():
             row[f"paths_per_s_v{v}"] = Q * 5 / (ms / 1e3)
             res[v] = {k: t.clone() for k, t in outd.items()}
         row["identical"] = all(torch.equal(res[2][k], res[9][k]) for k in res[2])
-        eng.set_tuning(0)
+        eng.set_option("wave_max_paths", 16384)
         print(json.dumps(row), flush=True)
 
 

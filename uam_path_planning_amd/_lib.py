@@ -18,6 +18,10 @@ RECORD_BYTES = 16
 COMM_ID_BYTES = 128
 
 UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
+# uam_set_option keys (include/uampath.h)
+OPTIONS = {"group": 1, "sorted_min_paths": 2, "k2s_segments": 3, "wave_max_paths": 4,
+           "pair_order": 5, "k1_rows": 6, "k3b_segment": 7, "k3b_points_per_lane": 8,
+           "k8_tiled": 9, "k8_streams": 10}
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
 MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
 FLAG_NFZ, FLAG_MASK, FLAG_NODATA, FLAG_BELOW_TERRAIN = 1, 2, 4, 8
@@ -129,11 +133,13 @@ SIGNATURES = {
     "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _vp, _vp]),
     "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
-    "uam_set_tuning": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "uam_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "uam_kernel_time": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_int64)]),
     "uam_last_kernel": (ctypes.c_char_p, [_vp]),
+    "uam_last_group": (ctypes.c_int32, [_vp]),
+    "uam_set_option": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.c_int64]),
+    "uam_get_option": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,

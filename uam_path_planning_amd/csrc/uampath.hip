@@ -40,13 +40,6 @@
 #include "../../include/uampath.h"
 #include "polyproc.h"
 
-#define UAM_TUNING_MAX 12
-#define UAM_TUNING_BINNED 11    // binned raster evaluation (K2b)
-#define UAM_TUNING_TILED 12     // tile-sorted raster evaluation (K2t)
-#define UAM_TUNING_WAVE 9       // force the wave-per-path kernel (K2w)
-#define UAM_TUNING_LANE 10      // never pick K2w automatically
-#define UAM_WAVE_AUTO_PATHS 16384  // auto: K2w up to here (tools/probe_wave.py crossover)
-#define UAM_TUNING_DEFAULT 2
 
 namespace {
 
@@ -527,17 +520,14 @@ __device__ __forceinline__ int32_t raster_cell_skip(const KRaster& rs, const uin
 // in flight, consumed in waypoint order exactly as consume_chunk does.  (Compacting each chunk
 // to the lane's next 8 needed waypoints measured 3x slower: the per-slot forward scans
 // diverge.)
-#ifndef UAM_SKIP_CHUNK
-#define UAM_SKIP_CHUNK 8  // gathers per chunk (tuning builds: -DUAM_SKIP_CHUNK=...)
-#endif
-#ifndef UAM_SKIP_MINW
-#define UAM_SKIP_MINW 5   // waves per SIMD the skip kernel is compiled for
-#endif
+// (chunks of 4-16 at 4-8 waves per SIMD measured 4-36% slower on cfg3, r02)
+constexpr int SKIP_CHUNK = 8;  // gathers per chunk
+constexpr int SKIP_MINW = 5;   // waves per SIMD the skip kernel is compiled for (6 spills)
 template <bool GEN>
 __device__ __forceinline__ void raster_pass2_skip(const KRaster& rs, const uint4* __restrict__ rec,
                                                   const uint32_t* bits, const PathSrc<GEN>& src,
                                                   int W, int32_t* cells, double dN, PathAcc& a) {
-    constexpr int CH = UAM_SKIP_CHUNK;
+    constexpr int CH = SKIP_CHUNK;
     for (int j0 = 0; j0 < W; j0 += CH) {
         uint4 r[CH];
         uint32_t inb = 0, need = 0;
@@ -676,30 +666,9 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
     }
 }
 
-// Records mode (internal, binned raster evaluation K2b): the waypoint's record was already
-// gathered into recs[path * W + j] (bit 31 of .w set = off the raster); the pass-2 sums are
-// eval_path's, so outputs are bit-identical to the gathering kernels.
-constexpr int MODE_RECORDS = 3;
 // Raster mode with the gather skip (internal; KRaster::sum set, raster_pass2_skip): its own
 // kernel instantiation, so the plain raster kernel keeps its register budget.
 constexpr int MODE_RASTER_SKIP = 4;
-constexpr uint32_t REC_OFF = 0x80000000u;
-
-template <int C>
-__device__ __forceinline__ void issue_chunk_rec(const uint4* __restrict__ recs, int64_t base,
-                                                int j0, int W, Chunk<C>& ch) {
-#pragma unroll
-    for (int t = 0; t < C; ++t) {
-        const int j = j0 + t;
-        ch.in[t] = false;
-        ch.r[t] = make_uint4(0, 0, 0, 0);
-        if (j < W) {
-            const uint4 r = recs[base + j];
-            ch.in[t] = !(r.w & REC_OFF);
-            ch.r[t] = r;
-        }
-    }
-}
 
 // Volume mode (BASELINE config 5, no reference counterpart): the waypoint's voxel
 // (ix, iy as in raster mode, iz = floor((z - z0) / dz)) holds {risk f32, psi_nfz f32,
@@ -812,9 +781,8 @@ __device__ __forceinline__ void path_pass1(const KParams& p, const PathSrc<GEN>&
 }
 
 // One path: pass 1 = geometry-only terms (length_of, true length, kinematic rows), pass 2 =
-// per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk,
-// PIPE = issue chunk k+1's gathers before consuming chunk k (two chunks in flight).
-template <int MODE, bool GEN, int C, bool PIPE>
+// per-waypoint penalty (analytic formulas or the record gather).  C = gathers per chunk.
+template <int MODE, bool GEN, int C>
 __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, const KRaster& rs,
                                              const KVolume& vs, const uint4* __restrict__ rec,
                                              const PathSrc<GEN>& src, int64_t path,
@@ -864,35 +832,15 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
             }
             a.nh += collides(g, x0, x1) ? 1 : 0;
         }
-    } else if (MODE == MODE_RECORDS) {
-        for (int j0 = 0; j0 < W; j0 += C) {
-            Chunk<C> ch;
-            issue_chunk_rec<C>(rec, path * (int64_t)W, j0, W, ch);
-            consume_chunk<C>(ch, j0, W, dN, a);
-        }
     } else if (MODE == MODE_RASTER_SKIP) {
         raster_pass2_skip<GEN>(rs, rec, sbits, src, W, out.cells ? out.cells + path * W : nullptr,
                                dN, a);
     } else {
         int32_t* cells = out.cells ? out.cells + path * W : nullptr;
-        if (!PIPE) {
-            for (int j0 = 0; j0 < W; j0 += C) {
-                Chunk<C> ch;
-                issue_chunk<GEN, C>(rs, rec, src, j0, W, cells, ch);
-                consume_chunk<C>(ch, j0, W, dN, a);
-            }
-        } else {
-            Chunk<C> ca, cb;
-            issue_chunk<GEN, C>(rs, rec, src, 0, W, cells, ca);
-            for (int j0 = 0; j0 < W; j0 += 2 * C) {
-                if (j0 + C < W) issue_chunk<GEN, C>(rs, rec, src, j0 + C, W, cells, cb);
-                consume_chunk<C>(ca, j0, W, dN, a);
-                if (j0 + C < W) {
-                    if (j0 + 2 * C < W)
-                        issue_chunk<GEN, C>(rs, rec, src, j0 + 2 * C, W, cells, ca);
-                    consume_chunk<C>(cb, j0 + C, W, dN, a);
-                }
-            }
+        for (int j0 = 0; j0 < W; j0 += C) {
+            Chunk<C> ch;
+            issue_chunk<GEN, C>(rs, rec, src, j0, W, cells, ch);
+            consume_chunk<C>(ch, j0, W, dN, a);
         }
     }
     return a;
@@ -901,7 +849,7 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
 // raster: cruise altitude - highest terrain under the waypoints; volume: min over waypoints of
 // (waypoint altitude - terrain of its column); analytic: NaN (no DEM)
 __device__ __forceinline__ double clearance(const KParams& p, int mode, const PathAcc& a) {
-    return (mode == UAM_MODE_RASTER || mode == MODE_RECORDS || mode == MODE_RASTER_SKIP)
+    return (mode == UAM_MODE_RASTER || mode == MODE_RASTER_SKIP)
                ? p.altitude - a.hmax
                                    : (mode == UAM_MODE_VOLUME ? a.cmin : (double)NAN);
 }
@@ -947,12 +895,13 @@ __global__ __launch_bounds__(256) void k_eval_waypoints(KGeom g, KParams p, KRas
     src.x0 = src.y0 = src.xf = src.yf = 0.0;
     src.za = src.zb = 0.0;
     const KVolume vs{};
-    const PathAcc a = eval_path<MODE, false, 8, false>(g, p, rs, vs, rec, src, path, out);
+    const PathAcc a = eval_path<MODE, false, 8>(g, p, rs, vs, rec, src, path, out);
     write_path(out, p, MODE, path, a);
 }
 
-// Variant 1 (first version): global wave w -> displacement d = w % D (wave-uniform),
-// pairs [(w / D)*64, +64); outputs stored straight from registers (stride-D stores).
+// D > 16 (the block-of-pairs kernels hold all D waves of a pair in one workgroup): global wave
+// w -> displacement d = w % D (wave-uniform), pairs [(w / D)*64, +64); outputs stored straight
+// from registers (stride-D stores), selection by k_argmin afterwards.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRaster rs,
                                                         const uint4* __restrict__ rec,
@@ -978,7 +927,7 @@ __global__ __launch_bounds__(256) void k_eval_generated(KGeom g, KParams p, KRas
     src.u = utab + (int64_t)d * p.N * 2;
     src.za = src.zb = 0.0;
     const KVolume vs{};
-    const PathAcc a = eval_path<MODE, true, 8, false>(g, p, rs, vs, rec, src, q * D + d, out);
+    const PathAcc a = eval_path<MODE, true, 8>(g, p, rs, vs, rec, src, q * D + d, out);
     write_path(out, p, MODE, q * D + d, a);
 }
 
@@ -993,7 +942,7 @@ __device__ __forceinline__ int64_t xcd_chunk(int64_t b, int64_t nb) {
 // lane = pair).  Results are staged in LDS and written with unit-stride (coalesced) stores
 // over the block's contiguous path range [b*64*D, (b+1)*64*D); the candidate selection
 // (main.py:175-180) runs in the same launch on the staged costs / lengths.
-template <int MODE, int C, bool PIPE, int MINW>
+template <int MODE, int MINW>
 __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, KRaster rs,
                                                            KVolume vs,
                                                            const uint4* __restrict__ rec,
@@ -1048,7 +997,7 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
         }
         src.u = utab + (int64_t)d * p.N * 2;
         const PathAcc a =
-            eval_path<MODE, true, C, PIPE>(g, p, rs, vs, rec, src, q * D + d, out, s_bits);
+            eval_path<MODE, true, 8>(g, p, rs, vs, rec, src, q * D + d, out, s_bits);
         s_cost[slot] = a.cost;
         s_L[slot] = a.L;
         s_len[slot] = a.len;
@@ -3759,90 +3708,8 @@ __global__ __launch_bounds__(256) void k_fill_segs_i32(int32_t* __restrict__ p, 
     for (int k = 0; k < nseg; ++k) p[k * n + i] = fs.v[k];
 }
 
-// ----------------------------------------------------------------------------------------
-// K2b: binned raster evaluation (tuning 11).  Every waypoint gather of K2 misses L2 and moves
-// a 128-B line for a 16-B record.  Here the waypoints are first binned by
-// raster tile (BIN_TS x BIN_TS cells = 1 MiB of records), each tile's gathers then run on one
-// XCD while the tile sits in that XCD's 4-MiB L2, and the per-path reduction reads the
-// gathered records contiguously.  Record values and summation order are K2's.
-constexpr int BIN_TS = 256;     // tile side (cells)
-constexpr int BIN_ITEMS = 16;   // waypoints per thread in the binning kernels (4096 per block)
-
-struct KBin {
-    const double* pairs;
-    const double* utab;
-    int32_t D, W;
-    int64_t n_wp;      // P * W
-    int32_t tiles_x, n_tiles;  // n_tiles real tiles; bucket n_tiles = off the raster
-    int32_t n_blocks;  // binning blocks
-};
-
-__device__ __forceinline__ void bin_point(const KBin& kb, const KRaster& rs, int64_t g,
-                                          int32_t& tile, int32_t& cell) {
-    const int64_t path = g / kb.W;
-    const int j = (int)(g - path * kb.W);
-    const int64_t q = path / kb.D;
-    const int d = (int)(path - q * kb.D);
-    const double4 pr = reinterpret_cast<const double4*>(kb.pairs)[q];
-    double x, y;
-    if (j == 0) {
-        x = pr.x, y = pr.y;
-    } else if (j == kb.W - 1) {
-        x = pr.z, y = pr.w;
-    } else {
-        const double* u = kb.utab + ((int64_t)d * (kb.W - 2) + (j - 1)) * 2;
-        arc_point(pr.x, pr.y, pr.z, pr.w, u[0], u[1], x, y);
-    }
-    const double fx = floor((x - rs.x0) * rs.inv_dx);
-    const double fy = floor((rs.y_top - y) * rs.inv_dy);
-    const bool in = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny);
-    if (!in) {
-        tile = kb.n_tiles;
-        cell = -1;
-        return;
-    }
-    const int ix = (int)fx, iy = (int)fy;
-    tile = (iy / BIN_TS) * kb.tiles_x + ix / BIN_TS;
-    cell = iy * rs.nx + ix;
-}
-
-__global__ __launch_bounds__(256) void k_bin_count(KBin kb, KRaster rs,
-                                                   int32_t* __restrict__ counts) {
-    extern __shared__ int32_t hist[];
-    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256) hist[t] = 0;
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * 256 * BIN_ITEMS;
-    for (int it = 0; it < BIN_ITEMS; ++it) {
-        const int64_t g = base + (int64_t)it * 256 + threadIdx.x;
-        if (g >= kb.n_wp) break;
-        int32_t tile, cell;
-        bin_point(kb, rs, g, tile, cell);
-        atomicAdd(&hist[tile], 1);
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256)
-        counts[(int64_t)t * kb.n_blocks + blockIdx.x] = hist[t];  // tile-major
-}
-
-__global__ __launch_bounds__(256) void k_bin_scatter(KBin kb, KRaster rs,
-                                                     const int32_t* __restrict__ offs,
-                                                     uint2* __restrict__ bucket) {
-    extern __shared__ int32_t cur[];
-    for (int t = threadIdx.x; t <= kb.n_tiles; t += 256)
-        cur[t] = offs[(int64_t)t * kb.n_blocks + blockIdx.x];
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * 256 * BIN_ITEMS;
-    for (int it = 0; it < BIN_ITEMS; ++it) {
-        const int64_t g = base + (int64_t)it * 256 + threadIdx.x;
-        if (g >= kb.n_wp) break;
-        int32_t tile, cell;
-        bin_point(kb, rs, g, tile, cell);
-        const int32_t pos = atomicAdd(&cur[tile], 1);
-        bucket[pos] = make_uint2((uint32_t)g, (uint32_t)cell);
-    }
-}
-
-// exclusive scan of n int32 (n < 2^31): per-block scan, block-total scan, add
+// exclusive scan of n int32 (n < 2^31): per-block scan, then the block-total scan; the
+// consumers add the scanned block total themselves
 constexpr int SCAN_ITEMS = 16;
 __global__ __launch_bounds__(256) void k_scan_local(const int32_t* __restrict__ in, int64_t n,
                                                     int32_t* __restrict__ out,
@@ -3909,105 +3776,6 @@ __global__ __launch_bounds__(1024) void k_scan_totals(int32_t* __restrict__ tota
     }
 }
 
-__global__ __launch_bounds__(256) void k_scan_add(int32_t* __restrict__ out, int64_t n,
-                                                  const int32_t* __restrict__ totals) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    out[i] += totals[i / (256 * SCAN_ITEMS)];
-}
-
-// XCD-pinned gather: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch);
-// group x = b % 8 walks the tiles t == x (mod 8), its K blocks splitting each tile's bucket,
-// so a tile's 1 MiB of records is fetched into one XCD's L2 and served from there.
-constexpr int GATHER_CH = 2048;  // entries per block step (8 per thread)
-__global__ __launch_bounds__(256) void k_bin_gather(const uint2* __restrict__ bucket,
-                                                    const int32_t* __restrict__ offs,
-                                                    int32_t n_tiles, int32_t n_blocks_bin,
-                                                    int64_t n_wp,
-                                                    const uint4* __restrict__ rec,
-                                                    uint4* __restrict__ recs, int K) {
-    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
-    for (int t = x; t <= n_tiles; t += 8) {
-        const int64_t b0 = offs[(int64_t)t * n_blocks_bin];
-        const int64_t b1 = t < n_tiles ? offs[(int64_t)(t + 1) * n_blocks_bin] : n_wp;
-        for (int64_t c0 = b0 + (int64_t)r * GATHER_CH; c0 < b1; c0 += (int64_t)K * GATHER_CH) {
-            uint2 e[GATHER_CH / 256];
-            uint4 v[GATHER_CH / 256];
-#pragma unroll
-            for (int k = 0; k < GATHER_CH / 256; ++k) {
-                const int64_t i = c0 + (int64_t)k * 256 + threadIdx.x;
-                e[k] = i < b1 ? bucket[i] : make_uint2(0xffffffffu, 0);
-            }
-#pragma unroll
-            for (int k = 0; k < GATHER_CH / 256; ++k) {
-                if (e[k].x == 0xffffffffu) continue;
-                v[k] = (t < n_tiles) ? rec[e[k].y] : make_uint4(0, 0, 0, REC_OFF);
-            }
-#pragma unroll
-            for (int k = 0; k < GATHER_CH / 256; ++k)
-                if (e[k].x != 0xffffffffu) recs[e[k].x] = v[k];
-        }
-    }
-}
-
-// ----------------------------------------------------------------------------------------
-// K2t: tile-sorted raster evaluation (tuning 12).  K2's waypoint gathers are random 16-B
-// reads, each moving a 128-B line out of HBM, so K2 sits at the fabric's
-// random-line rate.  K2t moves every waypoint through on-chip caches instead, in four
-// launches that only stream:
-//   A1 k_tb_count    K2's pass 1 (L, length, kinematic sum) per path, plus a histogram of
-//                    each path-block's waypoints over 256x256-cell raster tiles (1 MiB).
-//   S1 k_tb_rowscan  per-tile exclusive scan over the blocks (bin offsets).
-//   A2 k_tb_scatter  one workgroup per path-block: regenerate the waypoints, sort them by
-//                    tile in LDS, write them as contiguous runs into the tile-major bins.
-//   B  k_tb_gather   XCD-pinned: tiles t == x (mod 8) on XCD x, so a tile's records are
-//                    fetched into one L2 once and served from there; each gathered record
-//                    goes back, tagged with its slot, into its path-block's region as a
-//                    contiguous run (one run per (tile, block)).
-//   C  k_tb_reduce   one workgroup per path-block: the region is read contiguously and
-//                    placed in LDS by slot, then each lane sums its path in waypoint order.
-// Every order-dependent float64 sum runs in eval_path's order over the same values, and the
-// terms eval_path skips (off the raster) are stored as +0, an exact no-op on accumulators
-// that start at +0 (cost = (N+1)L >= +0), so K2t is bit-identical to K2.
-constexpr int TB_TS = 256;            // tile side in cells (256^2 x 16 B = 1 MiB of records)
-constexpr int TB_MAX_NTB = 4096;      // tiles + 1 (off-raster bin)
-constexpr uint32_t TB_OFF = 0x8000u;  // record flag: waypoint off the raster
-constexpr int TB_CH = 2048;           // entries per gather step of one workgroup
-
-// nontemporal (streaming) 8-/16-B loads and stores: the builtins take clang vector types
-typedef uint32_t tb_u2 __attribute__((ext_vector_type(2)));
-typedef uint32_t tb_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint2 tb_ldnt(const uint2* p) {
-    const tb_u2 v = __builtin_nontemporal_load(reinterpret_cast<const tb_u2*>(p));
-    return make_uint2(v.x, v.y);
-}
-__device__ __forceinline__ uint4 tb_ldnt(const uint4* p) {
-    const tb_u4 v = __builtin_nontemporal_load(reinterpret_cast<const tb_u4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void tb_stnt(uint4 v, uint4* p) {
-    tb_u4 w;
-    w.x = v.x, w.y = v.y, w.z = v.z, w.w = v.w;
-    __builtin_nontemporal_store(w, reinterpret_cast<tb_u4*>(p));
-}
-
-struct KTile {
-    const double* pairs;
-    const double* utab;
-    int64_t n_pairs, P;
-    int32_t D, W, PB, NB, SB;       // pairs per block, blocks, slot capacity per block
-    int32_t tiles_x, NT, NTB;       // NTB = NT + 1; bin NT = off the raster
-    int32_t* cnt;                   // [NTB][NB]: counts, then per-row exclusive prefix
-    int32_t* rowtot;                // [NTB] row totals
-    int32_t* tstart;                // [NTB + 1] start of each tile's bin (k_tb_tstart)
-    int32_t dbg;                    // diagnostics (UAM_TB_DBG): 1 = B skips gathers, 2 = B
-                                    // skips stores
-    int32_t* boff;                  // [NB][NTB] block-local exclusive prefix over tiles
-    uint2* ent;                     // tile-major bins {slot<<16 | tile cell, dest}
-    uint4* recb;                    // [NB][SB] gathered records, slot in w's high half
-    double* kin;                    // [3][P] L, length, kinematic sum
-};
-
 // raster cell of a point (uampath.h convention, exactly issue_chunk's arithmetic)
 __device__ __forceinline__ bool raster_cell(const KRaster& rs, double x0, double x1, int& ix,
                                             int& iy) {
@@ -4017,317 +3785,6 @@ __device__ __forceinline__ bool raster_cell(const KRaster& rs, double x0, double
     ix = in ? (int)fx : 0;
     iy = in ? (int)fy : 0;
     return in;
-}
-
-// exclusive scan of n <= TB_MAX_NTB ints into s[0..n] (s[n] = total), by wave 0 of the block
-__device__ __forceinline__ void tb_scan_small(const int32_t* __restrict__ v, int n,
-                                              int32_t* s) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        int32_t carry = 0;
-        for (int t0 = 0; t0 < n; t0 += 64) {
-            const int t = t0 + lane;
-            const int32_t x0 = t < n ? v[t] : 0;
-            int32_t x = x0;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (t < n) s[t] = carry + x - x0;
-            carry += __shfl(x, 63, 64);
-        }
-        if (lane == 0) s[n] = carry;
-    }
-    __syncthreads();
-}
-
-// K2 pass 1 for every path (L, length, kinematic sum -> kin), one lane per path in K2's layout
-// (wave = displacement, lane = pair).  ALU-bound; it runs on a second stream beside A1..B.
-__global__ __launch_bounds__(1024) void k_tb_kin(KParams p, KTile kt) {
-    const int d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t q = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    if (q >= kt.n_pairs) return;
-    const double4 pr = reinterpret_cast<const double4*>(kt.pairs)[q];
-    PathSrc<true> src;
-    src.W = kt.W;
-    src.wp = nullptr;
-    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
-    src.za = src.zb = 0.0;
-    src.u = kt.utab + (int64_t)d * p.N * 2;
-    PathAcc a;
-    path_pass1<true>(p, src, nullptr, a);
-    const int64_t path = q * kt.D + d;
-    kt.kin[path] = a.L;
-    kt.kin[kt.P + path] = a.len;
-    kt.kin[2 * kt.P + path] = a.ksum;
-}
-
-// waypoint i (slot = path_local * W + j) of path-block b, exactly PathSrc<true>::at
-__device__ __forceinline__ void tb_point(const KParams& p, const KTile& kt, int64_t b, int i,
-                                         double& x, double& y) {
-    const int W = kt.W, D = kt.D;
-    const int pl = i / W, j = i - pl * W;
-    const int ql = pl / D, d = pl - ql * D;
-    const double4 pr = reinterpret_cast<const double4*>(kt.pairs)[b * kt.PB + ql];
-    if (j == 0) {
-        x = pr.x, y = pr.y;
-    } else if (j == W - 1) {
-        x = pr.z, y = pr.w;
-    } else {
-        const double* u = kt.utab + ((int64_t)d * p.N + (j - 1)) * 2;
-        arc_point(pr.x, pr.y, pr.z, pr.w, u[0], u[1], x, y);
-    }
-}
-
-// A1: histogram of one path-block's waypoints over the tiles (one workgroup per block):
-// cnt[t][b] (tile-major, for S1) and the block-local exclusive prefix boff[b][t].
-__global__ __launch_bounds__(256) void k_tb_count(KParams p, KRaster rs, KTile kt) {
-    extern __shared__ int32_t tb_hist[];  // [NTB]
-    const int NTB = kt.NTB;
-    for (int i = threadIdx.x; i < NTB; i += blockDim.x) tb_hist[i] = 0;
-    __syncthreads();
-    const int64_t b = blockIdx.x;
-    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
-    const int nwp = npair * kt.D * kt.W;
-    for (int i = threadIdx.x; i < nwp; i += blockDim.x) {
-        double x, y;
-        tb_point(p, kt, b, i, x, y);
-        int ix, iy;
-        const int t = raster_cell(rs, x, y, ix, iy) ? (iy / TB_TS) * kt.tiles_x + ix / TB_TS
-                                                    : kt.NT;
-        atomicAdd(&tb_hist[t], 1);
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < NTB; t += blockDim.x)
-        kt.cnt[(int64_t)t * kt.NB + b] = tb_hist[t];
-    if (threadIdx.x < 64) {  // block-local exclusive prefix over tiles
-        const int lane = threadIdx.x;
-        int32_t carry = 0;
-        for (int t0 = 0; t0 < NTB; t0 += 64) {
-            const int t = t0 + lane;
-            const int32_t v = t < NTB ? tb_hist[t] : 0;
-            int32_t x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (t < NTB) kt.boff[b * NTB + t] = carry + x - v;
-            carry += __shfl(x, 63, 64);
-        }
-    }
-}
-
-// S1: exclusive scan of each tile row cnt[t][0..NB) in place; rowtot[t] = the row's total.
-__global__ __launch_bounds__(1024) void k_tb_rowscan(KTile kt) {
-    __shared__ int32_t wsum[16];
-    int32_t* row = kt.cnt + (int64_t)blockIdx.x * kt.NB;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int32_t carry = 0;
-    for (int i0 = 0; i0 < kt.NB; i0 += 4096) {
-        int32_t v[4], run = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = i0 + threadIdx.x * 4 + k;
-            v[k] = i < kt.NB ? row[i] : 0;
-            const int32_t t = v[k];
-            v[k] = run;
-            run += t;
-        }
-        int32_t x = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[wv] = x;
-        __syncthreads();
-        int32_t woff = 0, tot = 0;
-        for (int k = 0; k < 16; ++k) {
-            const int32_t w = k < (int)(blockDim.x >> 6) ? wsum[k] : 0;
-            woff += k < wv ? w : 0;
-            tot += w;
-        }
-        const int32_t excl = carry + woff + x - run;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = i0 + threadIdx.x * 4 + k;
-            if (i < kt.NB) row[i] = v[k] + excl;
-        }
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) kt.rowtot[blockIdx.x] = carry;
-}
-
-// S2: tile bin starts = exclusive scan of the row totals (one wave).
-__global__ __launch_bounds__(64) void k_tb_tstart(KTile kt) {
-    tb_scan_small(kt.rowtot, kt.NTB, kt.tstart);
-}
-
-// A2: one workgroup per path-block.  Slot i = path_local * W + j (path_local = pair_local * D
-// + d, the global path order).
-__global__ __launch_bounds__(256) void k_tb_scatter(KParams p, KRaster rs, KTile kt) {
-    extern __shared__ __attribute__((aligned(16))) int32_t tb_s[];
-    const int NTB = kt.NTB;
-    int32_t* base = tb_s;                     // [NTB + 1] tile starts, then run bases
-    int32_t* cur = base + NTB + 1;            // [NTB] LDS cursors
-    uint2* el = reinterpret_cast<uint2*>(tb_s + ((2 * NTB + 2) & ~1));  // [SB]
-    uint16_t* tl = reinterpret_cast<uint16_t*>(el + kt.SB);               // [SB]
-    const int64_t b = blockIdx.x;
-    for (int t = threadIdx.x; t < NTB; t += blockDim.x) {
-        const int32_t bo = kt.boff[b * NTB + t];
-        base[t] = kt.tstart[t] + kt.cnt[(int64_t)t * kt.NB + b] - bo;
-        cur[t] = bo;
-    }
-    __syncthreads();
-    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
-    const int nwp = npair * kt.D * kt.W;
-    for (int i = threadIdx.x; i < nwp; i += blockDim.x) {
-        double x, y;
-        tb_point(p, kt, b, i, x, y);
-        int ix, iy, t;
-        uint32_t tc = 0;
-        if (raster_cell(rs, x, y, ix, iy)) {
-            t = (iy / TB_TS) * kt.tiles_x + ix / TB_TS;
-            tc = (uint32_t)((iy % TB_TS) * TB_TS + ix % TB_TS);
-        } else {
-            t = kt.NT;
-        }
-        const int pos = atomicAdd(&cur[t], 1);
-        // entry: slot and tile cell; destination of the gathered record = block region + the
-        // entry's rank in the block's tile-sorted order (the order B writes the runs in)
-        el[pos] = make_uint2(((uint32_t)i << 16) | tc, (uint32_t)(b * kt.SB + pos));
-        tl[pos] = (uint16_t)t;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nwp; i += blockDim.x) kt.ent[base[tl[i]] + i] = el[i];
-}
-
-// B: XCD-pinned gather (blocks b and b + 8 share an XCD).  Group x = blockIdx % 8 walks the
-// tiles t == x (mod 8); its K workgroups split each tile's bin in TB_CH-entry steps.
-__global__ __launch_bounds__(256) void k_tb_gather(KRaster rs, KTile kt,
-                                                   const uint4* __restrict__ rec, int K) {
-    __shared__ int32_t tst[TB_MAX_NTB + 1];
-    const int NTB = kt.NTB;
-    for (int t = threadIdx.x; t <= NTB; t += blockDim.x) tst[t] = kt.tstart[t];
-    __syncthreads();
-    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
-    constexpr int E = TB_CH / 256;
-    for (int t = x; t < NTB; t += 8) {
-        const int64_t s0 = tst[t], s1 = tst[t + 1];
-        const bool on = t < kt.NT;
-        const int64_t tbase = on ? (int64_t)(t / kt.tiles_x) * TB_TS * rs.nx +
-                                       (int64_t)(t % kt.tiles_x) * TB_TS
-                                 : 0;
-        for (int64_t c0 = s0 + (int64_t)r * TB_CH; c0 < s1; c0 += (int64_t)K * TB_CH) {
-            uint2 e[E];
-            uint4 v[E];
-#pragma unroll
-            for (int k = 0; k < E; ++k) {
-                const int64_t i = c0 + k * 256 + threadIdx.x;
-                e[k] = i < s1 ? tb_ldnt(kt.ent + i) : make_uint2(0u, 0xffffffffu);
-            }
-#pragma unroll
-            for (int k = 0; k < E; ++k) {
-                const uint32_t tc = e[k].x & 0xffffu;
-                v[k] = (on && e[k].y != 0xffffffffu && !(kt.dbg & 1))
-                           ? rec[tbase + (int64_t)(tc / TB_TS) * rs.nx + tc % TB_TS]
-                           : make_uint4(0u, 0u, 0u, TB_OFF);
-            }
-#pragma unroll
-            for (int k = 0; k < E; ++k) {
-                if (e[k].y == 0xffffffffu || (kt.dbg & 2)) continue;
-                const uint32_t slot = e[k].x >> 16;
-                tb_stnt(make_uint4(v[k].x, v[k].y, v[k].z, (v[k].w & 0xffffu) | (slot << 16)),
-                        kt.recb + e[k].y);
-            }
-        }
-    }
-}
-
-// C: one workgroup per path-block.  LDS holds Φ, Σψ and the terrain term per slot (row
-// stride Ws = W | 1, odd, so the lanes' column walk is bank-conflict free).
-__global__ __launch_bounds__(256) void k_tb_reduce(KParams p, KTile kt, KOut out,
-                                                   int32_t* __restrict__ best_f,
-                                                   int32_t* __restrict__ best_l) {
-    extern __shared__ __attribute__((aligned(16))) double tb_d[];
-    const int W = kt.W, D = kt.D, Ws = W | 1, PBD = kt.PB * D;
-    double* s_cost = tb_d;                  // [PBD]
-    double* s_len = s_cost + PBD;           // [PBD]
-    float* phi = reinterpret_cast<float*>(s_len + PBD);
-    float* psi = phi + PBD * Ws;
-    float* ter = psi + PBD * Ws;
-    int32_t* nh = reinterpret_cast<int32_t*>(ter + PBD * Ws);
-    int32_t* off = nh + PBD;
-    for (int i = threadIdx.x; i < PBD; i += blockDim.x) nh[i] = off[i] = 0;
-    __syncthreads();
-    const int64_t b = blockIdx.x;
-    const int npair = (int)min((int64_t)kt.PB, kt.n_pairs - b * kt.PB);
-    const int npath = npair * D, nwp = npath * W;
-    const uint4* __restrict__ src = kt.recb + b * kt.SB;
-    constexpr int E = 8;  // records in flight per thread
-    for (int i0 = 0; i0 < nwp; i0 += E * 256) {
-        uint4 r[E];
-#pragma unroll
-        for (int k = 0; k < E; ++k) {
-            const int i = i0 + k * 256 + (int)threadIdx.x;
-            r[k] = i < nwp ? tb_ldnt(src + i) : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int k = 0; k < E; ++k) {
-            if (i0 + k * 256 + (int)threadIdx.x >= nwp) break;
-            const int slot = (int)(r[k].w >> 16);
-            const int pl = slot / W, j = slot - pl * W;
-            const int s = pl * Ws + j;
-            if (r[k].w & TB_OFF) {
-                phi[s] = 0.0f;
-                psi[s] = 0.0f;
-                ter[s] = 0.0f;  // off the raster counts as sea level (consume_chunk)
-                atomicAdd(&off[pl], 1);
-            } else {
-                phi[s] = __uint_as_float(r[k].x);
-                psi[s] = __uint_as_float(r[k].y);
-                ter[s] = (r[k].w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r[k].z);
-                if (r[k].w & UAM_FLAG_NFZ) atomicAdd(&nh[pl], 1);
-            }
-        }
-    }
-    __syncthreads();
-    const int l = threadIdx.x;
-    if (l < npath) {
-        const int64_t path = b * PBD + l;
-        const double L = kt.kin[path], len = kt.kin[kt.P + path],
-                     ks = kt.kin[2 * kt.P + path];
-        const double dN = (double)p.N;
-        double cost = (double)(p.N + 1) * L, nsum = 0.0, hmax = -INFINITY;
-        const float* fp = phi + l * Ws;
-        const float* fs = psi + l * Ws;
-        const float* ft = ter + l * Ws;
-        for (int j = 0; j < W; ++j) {
-            cost = cost + (double)fp[j] / dN;
-            nsum = nsum + (double)fs[j];
-            hmax = fmax(hmax, (double)ft[j]);
-        }
-        if (out.cost) out.cost[path] = cost;
-        if (out.length_q) out.length_q[path] = L;
-        if (out.length) out.length[path] = len;
-        if (out.kin_sum) out.kin_sum[path] = ks;
-        if (out.nfz_sum) out.nfz_sum[path] = nsum;
-        if (out.nfz_hits) out.nfz_hits[path] = nh[l];
-        if (out.offmap) out.offmap[path] = off[l];
-        if (out.min_clearance) out.min_clearance[path] = p.altitude - hmax;
-        if (out.below_terrain) out.below_terrain[path] = 0;
-        s_cost[l] = cost;
-        s_len[l] = len;
-    }
-    __syncthreads();
-    if (l < npair) {
-        const int64_t q = b * kt.PB + l;
-        if (best_f) best_f[q] = select_best(s_cost + l * D, 1, D, true);
-        if (best_l) best_l[q] = select_best(s_len + l * D, 1, D, false);
-    }
 }
 
 __global__ __launch_bounds__(256) void k_gen_paths(const double* __restrict__ pairs,
@@ -4732,63 +4189,42 @@ __global__ __launch_bounds__(256) void k_rorder_scatter(const uint16_t* __restri
 // one region of the raster.  Between launches a path's running sums live in a 32-B SegState;
 // every waypoint is still added in waypoint order with raster_pass2_skip's arithmetic (the
 // order of the items changes which lane does the work, never the operations a path sees), so
-// every output is bit-identical to K2's.  Launches (default form): k_seg_hist -> scan ->
-// k_seg_scatter for segment 0's order, then segment 0 (k_seg_eval<.., FIRST>: the lane runs
-// the path's pass 1 too, so its ALU work overlaps the gathers as in K2) while the other
-// segments' orders are sorted on the side stream, then segments 1.. (workgroups per CU capped
-// through an LDS floor, UAM_K2S_LDS), then k_seg_final (outputs, the main.py:175-180
-// selection).  UAM_K2S_FUSE=0 runs pass 1 as its own kernel (k_seg_pass1) on the side stream
-// instead, optionally part by part (UAM_K2S_SPLIT).  Measured on cfg3: DESIGN.md §4 K2s.
-// tile grid of the sort key: 2^TBITS x 2^TBITS tiles over the raster.  cfg3 K2s time by TBITS
-// (tools/k2s_tbits.sh): 6 0.630, 5 0.603, 4 0.595, 3 0.613 ms
-#ifndef UAM_SEG_TBITS
-#define UAM_SEG_TBITS 4
-#endif
-#ifndef UAM_SEG_CH0
-#define UAM_SEG_CH0 6   // gathers per chunk in segment 0 (tuning builds: -DUAM_SEG_CH0=...)
-#endif
-#ifndef UAM_SEG_CH1
-#define UAM_SEG_CH1 6   // gathers per chunk in the later segments (cfg3, tools/k2s_tbits.sh:
-                        // 6/6 0.590, 8/8 0.598, 8/4 0.592, 4/4 0.595, 8/16 0.755 ms)
-#endif
-constexpr int SEG_TBITS = UAM_SEG_TBITS;               // 16 x 16 tiles over the raster
+// every output is bit-identical to K2's.  Launches: k_seg_hist -> scan -> k_seg_scatter for
+// segment 0's order, then segment 0 (k_seg_eval<.., FIRST>: the lane runs the path's pass 1
+// too, so its ALU work overlaps the gathers as in K2) while the other segments' orders are
+// sorted on the side stream, then segments 1.. (workgroups per CU capped through an LDS
+// floor), then k_seg_final (outputs, the main.py:175-180 selection).  K2s is the fast form
+// of the reference's sequential order (UAM_OPT_GROUP = 0); K2g (below) is the default.
+// Measured on cfg3: DESIGN.md §4 K2s.  Tile grid of the sort key: 16 x 16 tiles over the
+// raster (cfg3 K2s ms by tile bits, r02: 6 0.630, 5 0.603, 4 0.595, 3 0.613); 6 gathers per
+// chunk (6/6 0.590, 8/8 0.598, 8/4 0.592, 4/4 0.595, 8/16 0.755 ms).
+constexpr int SEG_TBITS = 4;                           // 16 x 16 tiles over the raster
 constexpr int SEG_BINS = (1 << (2 * SEG_TBITS)) + 1;   // + one bin for off-raster / NaN
 constexpr int SEG_NBK = 256;                           // partitions of a segment's items
 constexpr int SEG_MAX = 8;                             // segments per path
-constexpr int SEG_MAXSPLIT = 4;                        // path parts (KSeg::nsplit)
+constexpr int SEG_CH = 6;                              // gathers per chunk
 
 struct SegState {  // 32 B per path
     double cost, nsum, hmax;
     int32_t nh, off;
 };
 
-struct SegStateV {  // 40 B per volume path (K4s): cmin instead of hmax, plus below-terrain
-    double cost, nsum, cmin;
-    int32_t nh, off, below, pad;
-};
-
 struct KSeg {
     const double* __restrict__ pairs;
     const double* __restrict__ utab;
     int64_t n_pairs;
-    int32_t P, D, W, nseg, L, F, tshift;  // segment 0 = [0, F), then segments of L
-    int32_t nsplit;             // path parts [P h / nsplit, P (h+1) / nsplit), sorted apart
-    int32_t vol;                // volume paths (K4s): pairs [Q][6], SegStateV states, kv
-    KVolume kv;
+    int32_t P, D, W, nseg, L, tshift;  // segments of L waypoints
     int32_t g0;                 // sort launches: first group (blockIdx.y = g - g0)
     int64_t obase;              // sort launches: order index of group g0's first item
     SegState* __restrict__ st;  // [P]
     double4* __restrict__ p1;   // [P] pass 1: (L, length, kinematic sum, 0)
     uint16_t* __restrict__ key; // [nseg][P] sort keys
-    int32_t* __restrict__ cnt;  // [nsplit][nseg][SEG_BINS][SEG_NBK] counts -> offsets
+    int32_t* __restrict__ cnt;  // [nseg][SEG_BINS][SEG_NBK] counts -> offsets
     int32_t* __restrict__ tot;  // scan block totals
-    int32_t* __restrict__ order;  // [nsplit][nseg][part] path of each sorted item
+    int32_t* __restrict__ order;  // [nseg][P] path of each sorted item
     __device__ __forceinline__ void bounds(int s, int& j0, int& j1) const {
-        j0 = s == 0 ? 0 : F + (s - 1) * L;
-        j1 = min(s == 0 ? F : F + s * L, W);
-    }
-    __device__ __forceinline__ int32_t part_lo(int h) const {
-        return (int32_t)((int64_t)P * h / nsplit);
+        j0 = s * L;
+        j1 = min(j0 + L, W);
     }
 };
 
@@ -4797,36 +4233,11 @@ __device__ __forceinline__ PathSrc<true> seg_src(const KSeg& ks, int N, int32_t 
     PathSrc<true> src;
     src.W = N + 2;
     src.wp = nullptr;
-    if (ks.vol) {  // pairs [Q][6] = (x0, y0, z0, xf, yf, zf), as k_eval_pairs reads them
-        const double* pr = ks.pairs + 6 * (int64_t)q;
-        src.x0 = pr[0], src.y0 = pr[1], src.za = pr[2];
-        src.xf = pr[3], src.yf = pr[4], src.zb = pr[5];
-    } else {
-        const double4 pr = reinterpret_cast<const double4*>(ks.pairs)[q];
-        src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
-        src.za = src.zb = 0.0;
-    }
+    const double4 pr = reinterpret_cast<const double4*>(ks.pairs)[q];
+    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    src.za = src.zb = 0.0;
     src.u = ks.utab + (int64_t)d * N * 2;
     return src;
-}
-
-// pass 1 of every path (path_pass1: L, length, kinematic sum) and its state seed
-// cost = (N+1) L (eval_path), thread = path in natural order (coalesced stores)
-__global__ __launch_bounds__(256) void k_seg_pass1(KParams p, KSeg ks, KOut out, int32_t p0,
-                                                   int32_t p1) {
-    const int64_t i = p0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= p1) return;
-    const PathSrc<true> src = seg_src(ks, p.N, (int32_t)i);
-    PathAcc a;
-    path_pass1<true>(p, src, nullptr, a);
-    ks.p1[i] = make_double4(a.L, a.len, a.ksum, 0.0);
-    SegState s;
-    s.cost = (double)(p.N + 1) * a.L;
-    s.nsum = 0.0;
-    s.hmax = -INFINITY;
-    s.nh = 0;
-    s.off = 0;
-    ks.st[i] = s;
 }
 
 // sort key of segment s of path i: Morton code of the tile under its middle waypoint
@@ -4848,16 +4259,14 @@ __device__ __forceinline__ uint32_t seg_key(const KSeg& ks, const KRaster& rs, i
     return k;
 }
 
-// counting sort, launch 1: block (b, g) keys partition b of group g = (part h, segment s)'s
-// items and stores its LDS histogram bin-major, so the scan of cnt yields each
-// (group, bin, partition)'s offset; group g's items land in one contiguous run of order
+// counting sort, launch 1: block (b, g) keys partition b of segment g's items and stores its
+// LDS histogram bin-major, so the scan of cnt yields each (segment, bin, partition)'s offset;
+// segment g's items land in one contiguous run of order
 __device__ __forceinline__ void seg_group(const KSeg& ks, int g, int b, int& s, int32_t& lo,
                                           int32_t& hi) {
-    const int h = g / ks.nseg;
-    s = g - h * ks.nseg;
-    const int32_t p0 = ks.part_lo(h), n = ks.part_lo(h + 1) - p0;
-    lo = p0 + (int32_t)((int64_t)n * b / SEG_NBK);
-    hi = p0 + (int32_t)((int64_t)n * (b + 1) / SEG_NBK);
+    s = g;
+    lo = (int32_t)((int64_t)ks.P * b / SEG_NBK);
+    hi = (int32_t)((int64_t)ks.P * (b + 1) / SEG_NBK);
 }
 
 __global__ __launch_bounds__(256) void k_seg_hist(KParams p, KRaster rs, KSeg ks) {
@@ -5015,17 +4424,14 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
 
 // segment s of every path, items in sorted order; workgroup b takes the sorted chunk
 // xcd_chunk(b), so an XCD's workgroups cover one contiguous run of tiles.  Dynamic LDS: the
-// skip bitmap, padded to the context's floor (UAM_K2S_LDS) to cap the workgroups per CU.
-// FIRST (segment 0 with UAM_K2S_FUSE): the lane runs the path's pass 1 itself and seeds the
-// state, so pass 1's ALU work overlaps the gathers as in K2.
-// pord (optional, segment 0): items in K2's pair order instead, item i = path
-// pord[i / D] * D + i % D (no per-path sort on the critical path)
+// skip bitmap, padded to a floor that caps the workgroups per CU (later segments).
+// FIRST (segment 0): the lane runs the path's pass 1 itself and seeds the state, so pass 1's
+// ALU work overlaps the gathers as in K2.
 // PACK: the packed raster (seg_pass2_pack; SKIP ignored), its block codes in LDS.
 template <bool SKIP, bool FIRST, bool PACK = false>
 __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks,
                                                   const uint4* __restrict__ rec, int s,
-                                                  int64_t base, int32_t n,
-                                                  const int32_t* __restrict__ pord) {
+                                                  int64_t base, int32_t n) {
     extern __shared__ uint32_t s_bits[];
     if (PACK) {
         for (int i = threadIdx.x; i < rs.pwords; i += 256) s_bits[i] = rs.pmap[i];
@@ -5036,13 +4442,7 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     }
     const int64_t i = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (i >= n) return;
-    int32_t path;
-    if (pord) {
-        const int32_t qi = (int32_t)i / ks.D;
-        path = pord[qi] * ks.D + ((int32_t)i - qi * ks.D);
-    } else {
-        path = ks.order[base + i];
-    }
+    const int32_t path = ks.order[base + i];
     const PathSrc<true> src = seg_src(ks, p.N, path);
     PathAcc a;
     if (FIRST) {
@@ -5066,11 +4466,9 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     // gathers in flight per lane: the capped later segments (2 waves per SIMD) have the
     // registers for more
     if (PACK)
-        seg_pass2_pack<FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
-                                                          (double)p.N, a);
+        seg_pass2_pack<SEG_CH>(rs, rec, s_bits, src, j0, j1, (double)p.N, a);
     else
-        seg_pass2<SKIP, FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1>(rs, rec, s_bits, src, j0, j1,
-                                                            (double)p.N, a);
+        seg_pass2<SKIP, SEG_CH>(rs, rec, s_bits, src, j0, j1, (double)p.N, a);
     SegState o;
     o.cost = a.cost;
     o.nsum = a.nsum;
@@ -5078,57 +4476,6 @@ __global__ __launch_bounds__(256) void k_seg_eval(KParams p, KRaster rs, KSeg ks
     o.nh = a.nh;
     o.off = a.off;
     ks.st[path] = o;
-}
-
-// K4s: segment s of every volume path (BASELINE cfg5), items in sorted order like k_seg_eval;
-// the waypoints of [j0, j1) go through issue_chunk_vol / consume_chunk_vol, k_eval_pairs's
-// volume arithmetic, so the outputs are bit-identical to K4's.  FIRST: pass 1 in the lane.
-template <bool FIRST>
-__global__ __launch_bounds__(256) void k_seg_eval_vol(KParams p, KSeg ks,
-                                                      const uint4* __restrict__ vol, int s,
-                                                      int64_t base, int32_t n) {
-    const int64_t i = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int32_t path = ks.order[base + i];
-    const PathSrc<true> src = seg_src(ks, p.N, path);
-    SegStateV* stv = reinterpret_cast<SegStateV*>(ks.st);
-    PathAcc a;
-    if (FIRST) {
-        path_pass1<true>(p, src, nullptr, a);
-        ks.p1[path] = make_double4(a.L, a.len, a.ksum, 0.0);
-        a.cost = (double)(p.N + 1) * a.L;
-        a.nsum = 0.0;
-        a.cmin = INFINITY;
-        a.nh = 0;
-        a.off = 0;
-        a.below = 0;
-    } else {
-        const SegStateV st = stv[path];
-        a.cost = st.cost;
-        a.nsum = st.nsum;
-        a.cmin = st.cmin;
-        a.nh = st.nh;
-        a.off = st.off;
-        a.below = st.below;
-    }
-    int j0, j1;
-    ks.bounds(s, j0, j1);
-    const double dN = (double)p.N;
-    constexpr int CH = FIRST ? UAM_SEG_CH0 : UAM_SEG_CH1;
-    for (int jc = j0; jc < j1; jc += CH) {
-        Chunk<CH> ch;
-        issue_chunk_vol<true, CH>(ks.kv, vol, src, jc, j1, nullptr, ch);
-        consume_chunk_vol<true, CH>(ch, src, jc, j1, dN, a);
-    }
-    SegStateV o;
-    o.cost = a.cost;
-    o.nsum = a.nsum;
-    o.cmin = a.cmin;
-    o.nh = a.nh;
-    o.off = a.off;
-    o.below = a.below;
-    o.pad = 0;
-    stv[path] = o;
 }
 
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout) and the selection
@@ -5146,17 +4493,9 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
     if (q0 + qi < ks.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         const double4 q1 = ks.p1[gp];
-        double cost, nsum, clr;
-        int32_t nh, off, below;
-        if (ks.vol) {  // K4s: clearance(p, UAM_MODE_VOLUME, a) = cmin
-            const SegStateV st = reinterpret_cast<const SegStateV*>(ks.st)[gp];
-            cost = st.cost, nsum = st.nsum, clr = st.cmin;
-            nh = st.nh, off = st.off, below = st.below;
-        } else {
-            const SegState st = ks.st[gp];
-            cost = st.cost, nsum = st.nsum, clr = p.altitude - st.hmax;
-            nh = st.nh, off = st.off, below = 0;
-        }
+        const SegState st = ks.st[gp];
+        const double cost = st.cost, nsum = st.nsum, clr = p.altitude - st.hmax;
+        const int32_t nh = st.nh, off = st.off, below = 0;
         if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = q1.x;
         if (out.length) out.length[gp] = q1.y;
@@ -5171,6 +4510,238 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
     }
     __syncthreads();
     if (t < 64 && q0 + t < ks.n_pairs) {
+        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+    }
+}
+
+// ---- K2g: segment-grouped raster evaluation (build-defined; no reference counterpart) -------
+// K2s keeps each path's sums in waypoint order, so its segments run one launch after another
+// and stay long (41 waypoints, ~13 km): its gathers reach 46% L2 hits and move 4.5x the
+// algorithmic bytes (profiles/r02/pack_final).  K2g restates the per-path sums in a grouped
+// order (oracle/uam_oracle.c orc_eval_paths_g): the waypoints are cut into groups of G
+// (default 8, ~2.6 km), each group's Phi/N and psi partial sums are formed from +0.0 in
+// waypoint order, and the partials are added to cost = (N+1) L and nsum = 0 in group order;
+// the terrain maximum, hits and off-raster counts are order-free.  Every (path, group) item is
+// then independent, so ONE counting sort on the 64 x 64-tile Morton key of the item's middle
+// waypoint and ONE launch evaluate all of them with the XCD-placed sorted order: the items an
+// XCD runs together cover a few tiles, whose lines stay in its L2.  The partials go to a
+// 16-B slot per item; k_g_final combines them in group order with pass 1 (computed beside the
+// sort and the evaluation on the side stream) and runs the main.py:175-180 selection.
+// Against the sequential reference the grouped sums differ by rounding only (<= 1e-12
+// relative, tests/test_oracle_golden.py); against the grouped oracle they are bit-exact.
+constexpr int G_TBITS = 6;                            // 64 x 64 tiles over the raster
+constexpr int G_BINS = (1 << (2 * G_TBITS)) + 1;      // + one bin for off-raster / NaN
+constexpr int G_NBK = 256;                            // partitions of the counting sort
+constexpr int G_MAXLEN = 16;                          // longest group
+
+struct GSlot {       // 16 B per (path, group)
+    double cost;     // partial sum of Phi/N in waypoint order from +0.0
+    float hmax;      // max terrain of the group's waypoints as consume_chunk reads it
+    uint32_t cnt;    // nfz hits | off-raster << 8 | (psi partial stored) << 16
+};
+
+struct KGrp {
+    const double* __restrict__ pairs;
+    const double* __restrict__ utab;
+    int64_t n_pairs;
+    int32_t P, D, W, G, nseg, tshift;
+    int64_t n_items;               // P * nseg; item i = path * nseg + group
+    uint16_t* __restrict__ key;    // [n_items]
+    int32_t* __restrict__ cnt;     // [G_BINS][G_NBK] counts -> offsets
+    int32_t* __restrict__ tot;     // scan block totals
+    int32_t* __restrict__ order;   // [n_items] item of each sorted position
+    GSlot* __restrict__ slot;      // [P][nseg]
+    double* __restrict__ psi;      // [P][nseg] psi partial (read only where flagged)
+    double4* __restrict__ p1;      // [P] pass 1: (L, length, kinematic sum, 0)
+};
+
+__device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
+    const int32_t q = path / kg.D, d = path - q * kg.D;
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    PathSrc<true> src;
+    src.W = N + 2;
+    src.wp = nullptr;
+    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
+    src.za = src.zb = 0.0;
+    src.u = kg.utab + (int64_t)d * N * 2;
+    return src;
+}
+
+// counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
+// groups (Morton code of the 64 x 64-tile tile under the group's middle waypoint) and the
+// partition's histogram, stored bin-major so the scan yields each (bin, partition)'s offset
+__global__ __launch_bounds__(256) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
+    __shared__ int32_t h[G_BINS];
+    const int t = threadIdx.x, b = blockIdx.x;
+    for (int k = t; k < G_BINS; k += 256) h[k] = 0;
+    __syncthreads();
+    const int32_t lo = (int32_t)((int64_t)kg.P * b / G_NBK);
+    const int32_t hi = (int32_t)((int64_t)kg.P * (b + 1) / G_NBK);
+    for (int32_t i = lo + t; i < hi; i += 256) {
+        const PathSrc<true> src = grp_src(kg, p.N, i);
+        for (int s = 0; s < kg.nseg; ++s) {
+            const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
+            double x0, x1;
+            src.at((j0 + j1 - 1) >> 1, x0, x1);
+            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+            uint32_t k = G_BINS - 1;
+            if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
+                const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
+                k = 0;
+#pragma unroll
+                for (int bit = G_TBITS - 1; bit >= 0; --bit)
+                    k = (k << 2) | (((ty >> bit) & 1u) << 1) | ((tx >> bit) & 1u);
+            }
+            kg.key[(int64_t)i * kg.nseg + s] = (uint16_t)k;
+            atomicAdd(&h[k], 1);
+        }
+    }
+    __syncthreads();
+    for (int k = t; k < G_BINS; k += 256) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
+}
+
+// launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered
+__global__ __launch_bounds__(256) void k_g_scatter(KGrp kg) {
+    __shared__ int32_t cur[G_BINS];
+    const int t = threadIdx.x, b = blockIdx.x;
+    for (int k = t; k < G_BINS; k += 256) {
+        const int64_t c = (int64_t)k * G_NBK + b;
+        cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
+    }
+    __syncthreads();
+    const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
+    const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
+    for (int64_t i = lo + t; i < hi; i += 256) kg.order[atomicAdd(&cur[kg.key[i]], 1)] = (int32_t)i;
+}
+
+// pass 1 of every path (path_pass1: L, length, kinematic sum), thread = path in natural order
+__global__ __launch_bounds__(256) void k_g_pass1(KParams p, KGrp kg) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= kg.P) return;
+    const PathSrc<true> src = grp_src(kg, p.N, (int32_t)i);
+    PathAcc a;
+    path_pass1<true>(p, src, nullptr, a);
+    kg.p1[i] = make_double4(a.L, a.len, a.ksum, 0.0);
+}
+
+// every (path, group) item in sorted order (workgroup b takes the sorted chunk xcd_chunk(b));
+// the group's waypoints from the packed raster exactly as seg_pass2_pack reads them (block
+// codes in LDS), all GL gathers issued before the first is consumed; the partials go to the
+// item's slot
+template <int GL>
+__global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
+                                                const uint4* __restrict__ rec) {
+    extern __shared__ uint32_t s_map[];
+    for (int i = threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
+    __syncthreads();
+    const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    if (pos >= kg.n_items) return;
+    const int32_t item = kg.order[pos];
+    const int32_t path = item / kg.nseg;
+    const int s = item - path * kg.nseg;
+    const PathSrc<true> src = grp_src(kg, p.N, path);
+    const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
+    uint4 r[GL];
+    uint32_t inb = 0, need = 0, full = 0;
+#pragma unroll
+    for (int t = 0; t < GL; ++t) {
+        if (j0 + t < j1) {
+            double x0, x1;
+            src.at(j0 + t, x0, x1);
+            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+            if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
+                inb |= 1u << t;
+                const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
+                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
+                if (code & 2u) {
+                    need |= 1u << t;
+                    full |= 1u << t;
+                    r[t] = rec[iy * rs.nx + ix];
+                } else if (code) {
+                    need |= 1u << t;
+                    const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
+                    r[t].x = v.x;
+                    r[t].z = v.y;
+                }
+            }
+        }
+    }
+    const double dN = (double)p.N;
+    double gc = 0.0, gn = 0.0;
+    float hmax = -INFINITY;
+    uint32_t nh = 0, off = 0;
+#pragma unroll
+    for (int t = 0; t < GL; ++t) {
+        if (j0 + t < j1) {
+            if (!((inb >> t) & 1u)) {
+                ++off;
+                hmax = fmaxf(hmax, 0.0f);  // off-raster counts as sea level
+            } else if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
+                hmax = fmaxf(hmax, 0.0f);
+            } else {
+                gc = gc + (double)__uint_as_float(r[t].x) / dN;
+                float terrain = __uint_as_float(r[t].z);
+                if ((full >> t) & 1u) {
+                    gn = gn + (double)__uint_as_float(r[t].y);
+                    nh += (r[t].w & UAM_FLAG_NFZ) ? 1u : 0u;
+                    if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0f;
+                }
+                hmax = fmaxf(hmax, terrain);
+            }
+        }
+    }
+    const int64_t si = (int64_t)path * kg.nseg + s;
+    GSlot o;
+    o.cost = gc;
+    o.hmax = hmax;
+    o.cnt = nh | (off << 8) | (full ? 1u << 16 : 0u);
+    kg.slot[si] = o;
+    if (full) kg.psi[si] = gn;
+}
+
+// outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout): the partials
+// combined in group order, and the selection over each pair's D paths
+__global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
+                                                  int32_t* __restrict__ best_f,
+                                                  int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int D = kg.D, t = threadIdx.x;
+    double* s_cost = smem;
+    double* s_len = smem + 64 * D;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int qi = t / D, di = t - qi * D;
+    if (q0 + qi < kg.n_pairs) {
+        const int64_t gp = (q0 + qi) * D + di;
+        const double4 q1 = kg.p1[gp];
+        double cost = (double)(p.N + 1) * q1.x, nsum = 0.0, hmax = -INFINITY;
+        int32_t nh = 0, off = 0;
+        const GSlot* sl = kg.slot + gp * kg.nseg;
+        for (int s = 0; s < kg.nseg; ++s) {
+            const GSlot g = sl[s];
+            cost = cost + g.cost;
+            if (g.cnt >> 16) nsum = nsum + kg.psi[gp * kg.nseg + s];
+            hmax = fmax(hmax, (double)g.hmax);
+            nh += (int32_t)(g.cnt & 255u);
+            off += (int32_t)((g.cnt >> 8) & 255u);
+        }
+        if (out.cost) out.cost[gp] = cost;
+        if (out.length_q) out.length_q[gp] = q1.x;
+        if (out.length) out.length[gp] = q1.y;
+        if (out.kin_sum) out.kin_sum[gp] = q1.z;
+        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
+        if (out.min_clearance) out.min_clearance[gp] = p.altitude - hmax;
+        if (out.nfz_hits) out.nfz_hits[gp] = nh;
+        if (out.offmap) out.offmap[gp] = off;
+        if (out.below_terrain) out.below_terrain[gp] = 0;
+        s_cost[di * 64 + qi] = cost;
+        s_len[di * 64 + qi] = q1.y;
+    }
+    __syncthreads();
+    if (t < 64 && q0 + t < kg.n_pairs) {
         if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
         if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
     }
@@ -5191,56 +4762,35 @@ struct uam_ctx {
     KGeom kg{};
     KParams kp{};
     bool have_geom = false, have_params = false;
-    int variant = 0;  // uam_set_tuning; 0 = default
     std::vector<DevIneq> h_ineq;
     std::vector<DevShape> h_shape;
     int32_t* d_grid = nullptr;  // shape-grid index (KShapeGrid), rebuilt by uam_set_params
-    void* d_ws = nullptr;       // grow-only scratch of the binned evaluation (K2b)
-    size_t ws_bytes = 0;
-    int tb_k = 0;               // K2t gather workgroups per XCD (0 = default; UAM_TB_K env)
-    int tb_pb = 0;              // K2t pairs per path-block (0 = default; UAM_TB_PB env)
-    int tb_dbg = 0;             // K2t diagnostics (KTile::dbg): read from UAM_TB_DBG only in a
-                                // -DUAM_TB_DIAG build (they change results)
-    bool tb_attrs = false;      // K2t dynamic-LDS attributes raised on this context's device
     // kernel timing (uam_kernel_timing): HIP event pairs around the dominant path kernel
     bool ktime_on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ktime_ev;
     size_t ktime_n = 0;
-    int k1_cpl = 0;             // K1 cells per lane: 0 = default (2), 1 = single-cell kernel,
-                                // 2 / 4 / 8 (UAM_K1_CPL env)
-    int k1_grid = 0;            // K1 workgroup cap (0 = one wave per strip; UAM_K1_GRID env)
-    hipStream_t s2 = nullptr;   // K2t side stream (pass 1 beside the streaming launches)
+    int k1_cpl = 2;             // K1 cells (rows) per lane: 1 = single-cell kernel, 2, 4, 8
+                                // (UAM_OPT_K1_ROWS)
+    hipStream_t s2 = nullptr;   // side stream (K2g / K2s: pass 1 and sorts beside the gathers)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
     double* d_tmtab = nullptr;  // K7 reprojection row / column tables (grow-only)
     size_t tmtab_n = 0;
-    bool k8_tiled = true;       // K8 tile labelling (UAM_K8_TILE=0: the cell-parallel merge)
-    int k8_nstreams = 4;        // K8 large regions: streams they are spread over (UAM_K8_STREAMS)
-    bool pair_order = true;     // K3: evaluate pairs in a spatial order (UAM_PAIR_ORDER=0: off)
-    int k3b_seg = 8;            // K3b segment (waypoints sorted together; UAM_K3B_SEG: 2/4/8/16,
-                                // 0 = the lane-per-path K3)
-    int k3b_cpl = 1;            // K3b points per lane in the evaluation phase (UAM_K3B_CPL: 1, 2)
+    bool k8_tiled = true;       // K8 tile labelling (UAM_OPT_K8_TILED = 0: cell-parallel merge)
+    int k8_nstreams = 4;        // K8 large regions: streams they are spread over
+                                // (UAM_OPT_K8_STREAMS)
+    bool pair_order = true;     // K2 / K3 / K4: pairs in a spatial order (UAM_OPT_PAIR_ORDER)
+    int k3b_seg = 8;            // K3b segment (waypoints sorted together; UAM_OPT_K3B_SEGMENT:
+                                // 2/4/6/8/16, 0 = the lane-per-path K3)
+    int k3b_cpl = 1;            // K3b points per lane in the evaluation phase
+                                // (UAM_OPT_K3B_POINTS_PER_LANE: 1, 2)
     bool k3b_attrs = false;     // K3b dynamic-LDS attributes raised on this context's device
-    int k2s_segs = 2;           // K2s segments per path (UAM_K2S_SEGS: 2..8; 0 or 1 = K2)
-    int k2s_lds = 80 * 1024;    // K2s segment launches: dynamic-LDS floor per workgroup, which
-                                // caps the workgroups resident per CU (UAM_K2S_LDS)
-    int k2s_lds_pack = 40 * 1024;  // the same from the packed raster (a smaller table: a wider
-                                   // window fits L2; cfg3 kernel ms by floor: 40 KiB 0.541,
-                                   // 48 0.542-0.545, 56 0.555, 64 0.555, 80 0.555; UAM_K2S_LDS
-                                   // sets both)
-    int64_t k2s_min = 65536;    // K2s: smallest batch in paths it takes (UAM_K2S_MIN)
-    int k2s_split = 1;          // K2s path parts whose pass 1 is pipelined (UAM_K2S_SPLIT, 1..4)
-    bool k2s_fuse = true;       // K2s: segment 0's launch runs pass 1 (UAM_K2S_FUSE=0: a pass-1
-                                // kernel on the side stream, beside the sort)
-    int k2s_lds0 = 0;           // K2s: LDS floor of the fused segment-0 launch (UAM_K2S_LDS0)
-    int k2s_first = 0;          // K2s: waypoints in segment 0 (UAM_K2S_FIRST; 0 = equal split)
-    bool k2s_order0 = false;    // K2s: segment 0 in K2's pair order instead of sorted by its own
-                                // key (UAM_K2S_ORDER0=1; cfg3: 376 vs 298 us, not the default)
-    hipEvent_t k2s_ev[4] = {};  // K2s: pass 1 of part h done (side stream)
+    int64_t wave_max = 16384;   // K2w / K4w for batches of up to this many paths
+                                // (UAM_OPT_WAVE_MAX_PATHS; tools/probe_wave.py crossover)
+    int k2s_segs = 2;           // K2s segments per path (UAM_OPT_K2S_SEGMENTS: 2..8)
+    int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
-    bool k4s = false;           // UAM_K4S=1: volume batches of >= k2s_min paths through K4s
-                                // (cfg5: 0.803 ms vs K4's 0.794, so K4 stays the default)
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
@@ -5249,6 +4799,8 @@ struct uam_ctx {
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
+    int32_t last_group = 0;     // uam_last_group: waypoint-group length of the last call's sums
+    int k2g_group = 8;          // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s)
 };
 
 namespace {
@@ -5265,6 +4817,8 @@ int check_ctx(uam_ctx* ctx, bool need_params) {
 // dominant path kernel; pairs are pooled and reused after uam_kernel_time / a reset.
 int ktime_begin(uam_ctx* ctx, hipStream_t s) {
     if (!ctx->ktime_on) return UAM_OK;
+    if (ctx->ktime_n >= 4096)
+        return fail(UAM_E_STATE, "kernel timing: 4096 event pairs pending, call uam_kernel_time");
     if (ctx->ktime_n == ctx->ktime_ev.size()) {
         hipEvent_t a, b;
         HIP_TRY(hipEventCreate(&a));
@@ -5354,29 +4908,6 @@ int uam_ctx_create(int device, uam_ctx** out) {
     uam_ctx* c = new (std::nothrow) uam_ctx();
     if (!c) return fail(UAM_E_NOMEM, "ctx allocation failed");
     c->device = device;
-    if (const char* e = std::getenv("UAM_TB_K")) c->tb_k = std::atoi(e);  // tuning experiments
-    if (const char* e = std::getenv("UAM_TB_PB")) c->tb_pb = std::atoi(e);
-#ifdef UAM_TB_DIAG
-    if (const char* e = std::getenv("UAM_TB_DBG")) c->tb_dbg = std::atoi(e);
-#endif
-    if (const char* e = std::getenv("UAM_K1_CPL")) c->k1_cpl = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K1_GRID")) c->k1_grid = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K8_TILE")) c->k8_tiled = std::atoi(e) != 0;
-    if (const char* e = std::getenv("UAM_PAIR_ORDER")) c->pair_order = std::atoi(e) != 0;
-    if (const char* e = std::getenv("UAM_K3B_SEG")) c->k3b_seg = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K3B_CPL")) c->k3b_cpl = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K2S_SEGS")) c->k2s_segs = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K2S_LDS"))
-        c->k2s_lds = c->k2s_lds_pack = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("UAM_K2S_MIN")) c->k2s_min = std::atoll(e);
-    if (const char* e = std::getenv("UAM_K2S_SPLIT")) c->k2s_split = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K2S_FUSE")) c->k2s_fuse = std::atoi(e) != 0;
-    if (const char* e = std::getenv("UAM_K2S_FIRST")) c->k2s_first = std::atoi(e);
-    if (const char* e = std::getenv("UAM_K2S_ORDER0")) c->k2s_order0 = std::atoi(e) != 0;
-    if (const char* e = std::getenv("UAM_K4S")) c->k4s = std::atoi(e) != 0;
-    if (const char* e = std::getenv("UAM_K2S_LDS0")) c->k2s_lds0 = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("UAM_K8_STREAMS"))
-        c->k8_nstreams = std::max(1, std::min(8, std::atoi(e)));
     *out = c;
     return UAM_OK;
 }
@@ -5390,14 +4921,11 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_ineq) (void)hipFree(ctx->d_ineq);
     if (ctx->d_shape) (void)hipFree(ctx->d_shape);
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
-    if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     if (ctx->ev_ord) (void)hipEventSynchronize(ctx->ev_ord);
     if (ctx->d_ord) (void)hipFree(ctx->d_ord);
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    for (hipEvent_t e : ctx->k2s_ev)
-        if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ktime_ev) {
         (void)hipEventSynchronize(e.second);
         (void)hipEventDestroy(e.first);
@@ -5669,9 +5197,9 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
     DeviceGuard dg(ctx->device);
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     const hipStream_t s = (hipStream_t)stream;
-    const int cpl = ctx->k1_cpl > 0 ? ctx->k1_cpl : 2;  // cells (rows) per lane
+    const int cpl = ctx->k1_cpl;  // cells (rows) per lane
     const int64_t strips = (int64_t)((kr.nx + 63) / 64) * ((kr.ny + cpl - 1) / cpl);
-    const dim3 gs(grid_for(strips * 64, 256, ctx->k1_grid > 0 ? ctx->k1_grid : (1 << 20)));
+    const dim3 gs(grid_for(strips * 64, 256, 1 << 20));
     switch (cpl) {
         case 1:  // the single-cell kernel
             hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0, s,
@@ -5766,10 +5294,7 @@ static int launch_wave(uam_ctx* ctx, int mode, bool gen, const KRaster& kr, cons
     return 1;
 }
 
-static bool want_wave(const uam_ctx* ctx, int64_t n_paths) {
-    if (ctx->variant == UAM_TUNING_WAVE) return true;
-    return ctx->variant == 0 && n_paths <= UAM_WAVE_AUTO_PATHS;
-}
+static bool want_wave(const uam_ctx* ctx, int64_t n_paths) { return n_paths <= ctx->wave_max; }
 
 int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec, const double* wp, int64_t n_paths,
@@ -5808,15 +5333,6 @@ int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     return UAM_OK;
 }
 
-int uam_set_tuning(uam_ctx* ctx, int32_t variant) {
-    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
-    if (variant < 0 || variant > UAM_TUNING_MAX)
-        return fail(UAM_E_INVALID, "tuning variant %d out of range [0, %d]", variant,
-                    UAM_TUNING_MAX);
-    ctx->variant = variant;
-    return UAM_OK;
-}
-
 #ifdef UAM_K3B_DIAG
 // diagnostics build only: read and clear the K3b counters; set the phase-skip mask
 int uam_k3b_diag(uint64_t* out8, int32_t skip) {
@@ -5838,6 +5354,83 @@ int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
 }
 
 const char* uam_last_kernel(const uam_ctx* ctx) { return ctx ? ctx->last_kernel : ""; }
+
+int32_t uam_last_group(const uam_ctx* ctx) { return ctx ? ctx->last_group : 0; }
+
+int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    switch (option) {
+        case UAM_OPT_GROUP:
+            if (value < 0 || value > G_MAXLEN)
+                return fail(UAM_E_INVALID, "UAM_OPT_GROUP %lld outside [0, %d]", (long long)value,
+                            G_MAXLEN);
+            ctx->k2g_group = (int)value;
+            return UAM_OK;
+        case UAM_OPT_SORTED_MIN_PATHS:
+            if (value < 0) return fail(UAM_E_INVALID, "UAM_OPT_SORTED_MIN_PATHS < 0");
+            ctx->k2s_min = value;
+            return UAM_OK;
+        case UAM_OPT_K2S_SEGMENTS:
+            if (value < 2 || value > SEG_MAX)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2S_SEGMENTS %lld outside [2, %d]",
+                            (long long)value, SEG_MAX);
+            ctx->k2s_segs = (int)value;
+            return UAM_OK;
+        case UAM_OPT_WAVE_MAX_PATHS:
+            if (value < 0) return fail(UAM_E_INVALID, "UAM_OPT_WAVE_MAX_PATHS < 0");
+            ctx->wave_max = value;
+            return UAM_OK;
+        case UAM_OPT_PAIR_ORDER:
+            ctx->pair_order = value != 0;
+            return UAM_OK;
+        case UAM_OPT_K1_ROWS:
+            if (value != 1 && value != 2 && value != 4 && value != 8)
+                return fail(UAM_E_INVALID, "UAM_OPT_K1_ROWS %lld not 1, 2, 4 or 8",
+                            (long long)value);
+            ctx->k1_cpl = (int)value;
+            return UAM_OK;
+        case UAM_OPT_K3B_SEGMENT:
+            if (value != 0 && value != 2 && value != 4 && value != 6 && value != 8 && value != 16)
+                return fail(UAM_E_INVALID, "UAM_OPT_K3B_SEGMENT %lld not 0, 2, 4, 6, 8 or 16",
+                            (long long)value);
+            ctx->k3b_seg = (int)value;
+            return UAM_OK;
+        case UAM_OPT_K3B_POINTS_PER_LANE:
+            if (value != 1 && value != 2)
+                return fail(UAM_E_INVALID, "UAM_OPT_K3B_POINTS_PER_LANE %lld not 1 or 2",
+                            (long long)value);
+            ctx->k3b_cpl = (int)value;
+            return UAM_OK;
+        case UAM_OPT_K8_TILED:
+            ctx->k8_tiled = value != 0;
+            return UAM_OK;
+        case UAM_OPT_K8_STREAMS:
+            if (value < 1 || value > 8)
+                return fail(UAM_E_INVALID, "UAM_OPT_K8_STREAMS %lld outside [1, 8]",
+                            (long long)value);
+            ctx->k8_nstreams = (int)value;
+            return UAM_OK;
+        default:
+            return fail(UAM_E_INVALID, "unknown option %d", option);
+    }
+}
+
+int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
+    if (!ctx || !value) return fail(UAM_E_INVALID, "NULL argument");
+    switch (option) {
+        case UAM_OPT_GROUP: *value = ctx->k2g_group; return UAM_OK;
+        case UAM_OPT_SORTED_MIN_PATHS: *value = ctx->k2s_min; return UAM_OK;
+        case UAM_OPT_K2S_SEGMENTS: *value = ctx->k2s_segs; return UAM_OK;
+        case UAM_OPT_WAVE_MAX_PATHS: *value = ctx->wave_max; return UAM_OK;
+        case UAM_OPT_PAIR_ORDER: *value = ctx->pair_order ? 1 : 0; return UAM_OK;
+        case UAM_OPT_K1_ROWS: *value = ctx->k1_cpl; return UAM_OK;
+        case UAM_OPT_K3B_SEGMENT: *value = ctx->k3b_seg; return UAM_OK;
+        case UAM_OPT_K3B_POINTS_PER_LANE: *value = ctx->k3b_cpl; return UAM_OK;
+        case UAM_OPT_K8_TILED: *value = ctx->k8_tiled ? 1 : 0; return UAM_OK;
+        case UAM_OPT_K8_STREAMS: *value = ctx->k8_nstreams; return UAM_OK;
+        default: return fail(UAM_E_INVALID, "unknown option %d", option);
+    }
+}
 
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
     if (!ctx || !ms_total || !launches) return fail(UAM_E_INVALID, "NULL argument");
@@ -5944,184 +5537,30 @@ static int raster_pair_order(uam_ctx* ctx, const KRaster& kr, const double* pair
     return UAM_OK;
 }
 
-// K2b launch; returns 1 if launched, 0 if the batch does not fit (caller falls back)
-static int launch_binned(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
-                         int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
-                         int32_t* best_f, int32_t* best_l, hipStream_t s) {
-    if (ko.cells || D > 16) return 0;
-    const int64_t W = ctx->kp.N + 2, P = n_pairs * D, n_wp = P * W;
-    if (n_wp >= INT32_MAX) return 0;
-    const int tiles_x = (kr.nx + BIN_TS - 1) / BIN_TS, tiles_y = (kr.ny + BIN_TS - 1) / BIN_TS;
-    const int64_t NT = (int64_t)tiles_x * tiles_y;
-    const int64_t NB = (n_wp + 256 * BIN_ITEMS - 1) / (256 * BIN_ITEMS);
-    const int64_t ncount = (NT + 1) * NB;
-    const int64_t nsb = (ncount + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
-    if (NT + 1 > 8192 || nsb > 4096) return 0;
-    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_counts = al(ncount * 4), b_offs = al(ncount * 4), b_tot = al(4096 * 4),
-                 b_bucket = al((size_t)n_wp * 8), b_recs = al((size_t)n_wp * 16);
-    const size_t need = b_counts + b_offs + b_tot + b_bucket + b_recs;
-    if (need > ctx->ws_bytes) {
-        if (ctx->d_ws) (void)hipFree(ctx->d_ws);
-        ctx->d_ws = nullptr;
-        ctx->ws_bytes = 0;
-        if (hipMalloc(&ctx->d_ws, need) != hipSuccess) return fail(UAM_E_NOMEM, "binned scratch");
-        ctx->ws_bytes = need;
-    }
-    char* w = (char*)ctx->d_ws;
-    int32_t* counts = (int32_t*)w;
-    int32_t* offs = (int32_t*)(w + b_counts);
-    int32_t* tot = (int32_t*)(w + b_counts + b_offs);
-    uint2* bucket = (uint2*)(w + b_counts + b_offs + b_tot);
-    uint4* recs = (uint4*)(w + b_counts + b_offs + b_tot + b_bucket);
-    KBin kb{pairs, utab, D, (int32_t)W, n_wp, tiles_x, (int32_t)NT, (int32_t)NB};
-    const size_t hist = (size_t)(NT + 1) * sizeof(int32_t);
-    hipLaunchKernelGGL(k_bin_count, dim3((unsigned)NB), dim3(256), hist, s, kb, kr, counts);
-    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, counts, ncount, offs,
-                       tot);
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, tot, (int)nsb);
-    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(ncount, 256, INT32_MAX)), dim3(256), 0, s, offs,
-                       ncount, tot);
-    hipLaunchKernelGGL(k_bin_scatter, dim3((unsigned)NB), dim3(256), hist, s, kb, kr, offs,
-                       bucket);
-    const int K = 128;  // blocks per XCD group
-    hipLaunchKernelGGL(k_bin_gather, dim3(8 * K), dim3(256), 0, s, bucket, offs, (int32_t)NT,
-                       (int32_t)NB, n_wp, (const uint4*)rec, recs, K);
-    const int64_t blocks = (n_pairs + 63) / 64;
-    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
-    const KVolume kv{};
-    hipLaunchKernelGGL((k_eval_pairs<MODE_RECORDS, 8, false, 1>), dim3((unsigned)blocks),
-                       dim3(64 * D), lds, s, ctx->kg, ctx->kp, kr, kv, (const uint4*)recs, pairs,
-                       n_pairs, utab, D, ko, best_f, best_l, nullptr);
-    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "binned evaluation launch");
-    return 1;
-}
-
-// K2t launch (tuning 12); returns 1 if launched, 0 if the batch does not fit (caller falls
-// back to K2).  Path-block size PB: the largest of 16, 8, 4, 2, 1 pairs whose LDS image
-// (12 B per slot in C, 10 B per slot in A2) fits kTbLds.
-static int launch_tiled(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
-                        int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
-                        int32_t* best_f, int32_t* best_l, hipStream_t s) {
-    if (ko.cells || ko.g_rows || D > 16) return 0;
-    const int64_t W = ctx->kp.N + 2, P = n_pairs * D, n_wp = P * W;
-    if (n_wp >= INT32_MAX) return 0;
-    const int tiles_x = (kr.nx + TB_TS - 1) / TB_TS, tiles_y = (kr.ny + TB_TS - 1) / TB_TS;
-    const int64_t NT = (int64_t)tiles_x * tiles_y, NTB = NT + 1;
-    if (NTB > TB_MAX_NTB) return 0;
-    constexpr size_t kTbLds = 96 * 1024;
-    const int64_t Ws = W | 1;
-    int PB = ctx->tb_pb > 0 ? ctx->tb_pb : 8;
-    auto lds_c = [&](int pb) { return (size_t)pb * D * (16 + 8 + 12 * Ws); };
-    auto lds_a2 = [&](int pb) { return (size_t)(2 * NTB + 2) * 4 + (size_t)pb * D * W * 10; };
-    while (PB > 1 && (lds_c(PB) > kTbLds || lds_a2(PB) > kTbLds || PB * D * W >= 65536))
-        PB /= 2;
-    if (lds_c(PB) > kTbLds || lds_a2(PB) > kTbLds || PB * D * W >= 65536) return 0;
-    const int64_t NB = (n_pairs + PB - 1) / PB, SB = (int64_t)PB * D * W;
-    if (NB >= INT32_MAX / NTB) return 0;
-    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_cnt = al(NTB * NB * 4), b_tot = al((2 * NTB + 1) * 4), b_boff = al(NB * NTB * 4),
-                 b_ent = al((size_t)n_wp * 8), b_recb = al((size_t)NB * SB * 16),
-                 b_kin = al((size_t)P * 24);
-    const size_t need = b_cnt + b_tot + b_boff + b_ent + b_recb + b_kin;
-    if (need > ctx->ws_bytes) {
-        if (ctx->d_ws) (void)hipFree(ctx->d_ws);
-        ctx->d_ws = nullptr;
-        ctx->ws_bytes = 0;
-        if (hipMalloc(&ctx->d_ws, need) != hipSuccess) return fail(UAM_E_NOMEM, "tiled scratch");
-        ctx->ws_bytes = need;
-    }
-    char* w = (char*)ctx->d_ws;
-    KTile kt{};
-    kt.pairs = pairs;
-    kt.utab = utab;
-    kt.n_pairs = n_pairs;
-    kt.P = P;
-    kt.D = D;
-    kt.W = (int32_t)W;
-    kt.PB = PB;
-    kt.NB = (int32_t)NB;
-    kt.SB = (int32_t)SB;
-    kt.tiles_x = tiles_x;
-    kt.NT = (int32_t)NT;
-    kt.NTB = (int32_t)NTB;
-    kt.cnt = (int32_t*)w;
-    kt.rowtot = (int32_t*)(w + b_cnt);
-    kt.tstart = kt.rowtot + NTB;
-    kt.dbg = ctx->tb_dbg;
-    kt.boff = (int32_t*)(w + b_cnt + b_tot);
-    kt.ent = (uint2*)(w + b_cnt + b_tot + b_boff);
-    kt.recb = (uint4*)(w + b_cnt + b_tot + b_boff + b_ent);
-    kt.kin = (double*)(w + b_cnt + b_tot + b_boff + b_ent + b_recb);
-    if (!ctx->tb_attrs) {  // per context = per device (the caller's DeviceGuard is active)
-        HIP_TRY(hipFuncSetAttribute((const void*)k_tb_scatter,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds));
-        HIP_TRY(hipFuncSetAttribute((const void*)k_tb_reduce,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTbLds));
-        ctx->tb_attrs = true;
-    }
-    // pass 1 (ALU-bound) on a second stream, beside the streaming launches A1..B
-    if (!ctx->s2) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
-    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-    if (!(kt.dbg & 4))
-        hipLaunchKernelGGL(k_tb_kin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D), 0,
-                           ctx->s2, ctx->kp, kt);
-    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
-    hipLaunchKernelGGL(k_tb_count, dim3((unsigned)NB), dim3(256), (size_t)NTB * 4, s, ctx->kp, kr,
-                       kt);
-    hipLaunchKernelGGL(k_tb_rowscan, dim3((unsigned)NTB), dim3(1024), 0, s, kt);
-    hipLaunchKernelGGL(k_tb_tstart, dim3(1), dim3(64), 0, s, kt);
-    hipLaunchKernelGGL(k_tb_scatter, dim3((unsigned)NB), dim3(256), lds_a2(PB), s, ctx->kp, kr,
-                       kt);
-    const int K = ctx->tb_k > 0 ? ctx->tb_k : 128;  // workgroups per XCD group
-    hipLaunchKernelGGL(k_tb_gather, dim3(8 * K), dim3(256), 0, s, kr, kt, (const uint4*)rec, K);
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
-    hipLaunchKernelGGL(k_tb_reduce, dim3((unsigned)NB), dim3(256), lds_c(PB), s, ctx->kp, kt, ko,
-                       best_f, best_l);
-    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "tiled evaluation launch");
-    return 1;
-}
-
-// K2s launch (segment-sorted raster evaluation); returns 1 if launched, 0 if the batch is not
-// one it takes (the caller runs K2).  Scratch: the pair-order scratch (order_scratch), so two
-// streams sharing the context serialise on it.
-// kv (K4s): a volume evaluation, kr then carries only the volume's x/y grid for the sort keys
+// K2s launch (segment-sorted raster evaluation, the reference's sequential sums); returns 1 if
+// launched, 0 if the batch is not one it takes (the caller runs K2).  Scratch: the pair-order
+// scratch (order_scratch), so two streams sharing the context serialise on it.
 static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
                             int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
-                            int32_t* best_f, int32_t* best_l, hipStream_t s,
-                            const KVolume* kv = nullptr) {
+                            int32_t* best_f, int32_t* best_l, hipStream_t s) {
     const int64_t W = ctx->kp.N + 2;
     const int want = std::min(ctx->k2s_segs, SEG_MAX);
     if (want < 2 || ko.cells || ko.g_rows || D > 16) return 0;
-    // segment 0 = [0, F) (UAM_K2S_FIRST; default: the common length), then segments of L
-    int L = (int)((W + want - 1) / want), F = L;
-    if (ctx->k2s_first > 0 && ctx->k2s_first < W) {
-        F = ctx->k2s_first;
-        L = (int)((W - F + want - 2) / (want - 1));
-    }
-    const int nseg = 1 + (int)((W - F + L - 1) / L);  // e.g. W = 10 in 4: 3, 3, 3, 1
+    const int L = (int)((W + want - 1) / want);
+    const int nseg = (int)((W + L - 1) / L);  // e.g. W = 10 in 4: 3, 3, 3, 1
     if (nseg < 2) return 0;
     if (n_pairs > (INT32_MAX / SEG_MAX) / D) return 0;
     const int64_t P = n_pairs * D;
     if (P < ctx->k2s_min) return 0;
-    const int H = std::max(1, std::min(ctx->k2s_split, SEG_MAXSPLIT));
-    if (kv && (H != 1 || !ctx->k2s_fuse)) return 0;  // K4s: the fused single-part form only
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const int64_t ncnt = (int64_t)H * nseg * SEG_BINS * SEG_NBK;
+    const int64_t ncnt = (int64_t)nseg * SEG_BINS * SEG_NBK;
     const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
     if (nsb > 4096) return 0;
-    const size_t b_st = al((size_t)P * (kv ? sizeof(SegStateV) : sizeof(SegState))),
-                 b_len = al((size_t)P * 32),
+    const size_t b_st = al((size_t)P * sizeof(SegState)), b_len = al((size_t)P * 32),
                  b_key = al((size_t)nseg * P * 2), b_cnt = al((size_t)ncnt * 4),
-                 b_tot = al(4096 * 4), b_ord = al((size_t)nseg * P * 4),
-                 b_po = al(raster_pair_order_bytes(n_pairs));
+                 b_tot = al(4096 * 4), b_ord = al((size_t)nseg * P * 4);
     char* w = nullptr;
-    int st = order_scratch(ctx, b_st + b_len + b_key + b_cnt + b_tot + b_ord + b_po, s, &w);
+    int st = order_scratch(ctx, b_st + b_len + b_key + b_cnt + b_tot + b_ord, s, &w);
     if (st) return st;
     KSeg ks{};
     ks.pairs = pairs;
@@ -6132,10 +5571,6 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     ks.W = (int32_t)W;
     ks.nseg = nseg;
     ks.L = L;
-    ks.F = F;
-    ks.nsplit = H;
-    ks.vol = kv ? 1 : 0;
-    if (kv) ks.kv = *kv;
     int tshift = 0;
     while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << SEG_TBITS)) ++tshift;
     ks.tshift = tshift;
@@ -6145,19 +5580,20 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     ks.cnt = (int32_t*)(w + b_st + b_len + b_key);
     ks.tot = (int32_t*)(w + b_st + b_len + b_key + b_cnt);
     ks.order = (int32_t*)(w + b_st + b_len + b_key + b_cnt + b_tot);
+    // the later segments' launches pad their dynamic LDS to a floor that caps the workgroups
+    // resident per CU, so an XCD's resident items cover a narrow range of the sorted order
+    // (cfg3 kernel ms by floor, packed: 40 KiB 0.541, 48 0.542-0.545, 56-80 0.555; 16-B
+    // records: 80 KiB); segment 0 carries pass 1 and needs its occupancy (no floor)
     const size_t lds_min = kr.pmap ? (size_t)kr.pwords * 4 : kr.sum ? (size_t)kr.swords * 4 : 0;
-    const size_t lds = std::max(
-        lds_min, (size_t)std::min(kr.pmap ? ctx->k2s_lds_pack : ctx->k2s_lds, 160 * 1024));
-    const size_t lds0 = std::max(lds_min, (size_t)std::min(ctx->k2s_lds0, 160 * 1024));
+    const size_t lds = std::max(lds_min, (size_t)(kr.pmap ? 40 : 80) * 1024);
+    const size_t lds0 = lds_min;
     if (!ctx->k2s_attrs) {  // per context = per device (the caller's DeviceGuard is active)
         const void* fns[] = {(const void*)k_seg_eval<true, false>,
                              (const void*)k_seg_eval<false, false>,
                              (const void*)k_seg_eval<true, true>,
                              (const void*)k_seg_eval<false, true>,
                              (const void*)k_seg_eval<false, true, true>,
-                             (const void*)k_seg_eval<false, false, true>,
-                             (const void*)k_seg_eval_vol<true>,
-                             (const void*)k_seg_eval_vol<false>};
+                             (const void*)k_seg_eval<false, false, true>};
         for (const void* f : fns)
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
@@ -6168,27 +5604,11 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
         HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     }
-    for (int h = 0; h < H; ++h)
-        if (!ctx->k2s_ev[h]) HIP_TRY(hipEventCreateWithFlags(&ctx->k2s_ev[h], hipEventDisableTiming));
-    // kernel timing brackets the whole sequence (sort included).  Pass 1 (ALU-bound) runs part
-    // by part on the side stream: part h's first segment launch waits only for part h's pass 1,
-    // so the later parts' pass 1 overlaps the (latency-bound) gathers of the earlier ones.
-    // With UAM_K2S_FUSE (default) segment 0's launch runs pass 1 in the same lanes instead.
-    const bool fuse = ctx->k2s_fuse;
+    // kernel timing brackets the whole sequence (sorts included)
     st = ktime_begin(ctx, s);
     if (st) return st;
-    if (!fuse) {
-        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-        for (int h = 0; h < H; ++h) {
-            const int32_t p0 = (int32_t)(P * h / H), p1 = (int32_t)(P * (h + 1) / H);
-            hipLaunchKernelGGL(k_seg_pass1, dim3((unsigned)((p1 - p0 + 255) / 256)), dim3(256),
-                               0, ctx->s2, ctx->kp, ks, ko, p0, p1);
-            HIP_TRY(hipEventRecord(ctx->k2s_ev[h], ctx->s2));
-        }
-    }
-    // counting sort of the groups [g0, g0 + ng) on stream q (cnt / tot: its own count and
-    // block-total scratch); order positions start at group g0's (g0 * P: H == 1 or g0 == 0)
+    // counting sort of the segments [g0, g0 + ng) on stream q (cnt / tot: its own count and
+    // block-total scratch); order positions start at segment g0's (g0 * P)
     auto sort_groups = [&](int g0, int ng, hipStream_t q, int32_t* cnt, int32_t* tot) {
         KSeg kq = ks;
         kq.g0 = g0;
@@ -6202,65 +5622,119 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
         hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, q, tot, (int)nb);
         hipLaunchKernelGGL(k_seg_scatter, dim3(SEG_NBK, ng), dim3(256), 0, q, kq);
     };
-    // fused pass 1, one part: segment 0's order first on s, the other segments' orders on the
-    // side stream beside segment 0's launch (joined before segment 1)
-    // (UAM_K2S_ORDER0=1, default: segment 0 in K2's pair order, no sort before it)
-    const bool two = fuse && H == 1;
-    const int32_t* pord = nullptr;
-    if (two) {
-        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-        if (ctx->k2s_order0 && !kv && n_pairs < INT32_MAX) {
-            st = raster_pair_order(ctx, kr, pairs, n_pairs, s, &pord, 0,
-                                   w + b_st + b_len + b_key + b_cnt + b_tot + b_ord);
-            if (st) return st;
-        } else {
-            sort_groups(0, 1, s, ks.cnt, ks.tot);
-        }
-        sort_groups(1, nseg - 1, ctx->s2, ks.cnt + (int64_t)SEG_BINS * SEG_NBK, ks.tot + 2048);
-        HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
-    } else {
-        sort_groups(0, H * nseg, s, ks.cnt, ks.tot);
-    }
-    (void)nsb;
-    const dim3 gf((unsigned)((n_pairs + 63) / 64));
-    for (int k = 0; k < nseg; ++k)
-        for (int h = 0; h < H; ++h) {
-            const int32_t n = (int32_t)(P * (h + 1) / H - P * h / H);
-            // group (h, k) = h * nseg + k; the groups before it hold nseg * part_lo(h) + k * n
-            const int64_t base = (P * h / H) * (int64_t)nseg + (int64_t)k * n;
-            if (k == 0 && !fuse) HIP_TRY(hipStreamWaitEvent(s, ctx->k2s_ev[h], 0));
-            if (k == 1 && h == 0 && two) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
-            const dim3 ge((unsigned)((n + 255) / 256));
-            if (kv) {
-                if (k == 0)
-                    hipLaunchKernelGGL(k_seg_eval_vol<true>, ge, dim3(256), lds0, s, ctx->kp, ks,
-                                       (const uint4*)rec, k, base, n);
-                else
-                    hipLaunchKernelGGL(k_seg_eval_vol<false>, ge, dim3(256), lds, s, ctx->kp, ks,
-                                       (const uint4*)rec, k, base, n);
-                continue;
-            }
+    // segment 0's order first on s, the other segments' orders on the side stream beside
+    // segment 0's launch (joined before segment 1)
+    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+    sort_groups(0, 1, s, ks.cnt, ks.tot);
+    sort_groups(1, nseg - 1, ctx->s2, ks.cnt + (int64_t)SEG_BINS * SEG_NBK, ks.tot + 2048);
+    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+    for (int k = 0; k < nseg; ++k) {
+        const int64_t base = (int64_t)k * P;
+        if (k == 1) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+        const dim3 ge((unsigned)((P + 255) / 256));
 #define UAM_LAUNCH_SEG(SK_, F_, LDS_, PK_)                                                     \
     hipLaunchKernelGGL((k_seg_eval<SK_, F_, PK_>), ge, dim3(256), LDS_, s, ctx->kp, kr, ks,    \
-                       (const uint4*)rec, k, base, n, k == 0 ? pord : nullptr)
-            if (kr.pmap) {
-                if (k == 0 && fuse) UAM_LAUNCH_SEG(false, true, lds0, true);
-                else UAM_LAUNCH_SEG(false, false, lds, true);
-            } else if (k == 0 && fuse) {
-                if (kr.sum) UAM_LAUNCH_SEG(true, true, lds0, false);
-                else UAM_LAUNCH_SEG(false, true, lds0, false);
-            } else {
-                if (kr.sum) UAM_LAUNCH_SEG(true, false, lds, false);
-                else UAM_LAUNCH_SEG(false, false, lds, false);
-            }
-#undef UAM_LAUNCH_SEG
+                       (const uint4*)rec, k, base, (int32_t)P)
+        if (kr.pmap) {
+            if (k == 0) UAM_LAUNCH_SEG(false, true, lds0, true);
+            else UAM_LAUNCH_SEG(false, false, lds, true);
+        } else if (k == 0) {
+            if (kr.sum) UAM_LAUNCH_SEG(true, true, lds0, false);
+            else UAM_LAUNCH_SEG(false, true, lds0, false);
+        } else {
+            if (kr.sum) UAM_LAUNCH_SEG(true, false, lds, false);
+            else UAM_LAUNCH_SEG(false, false, lds, false);
         }
+#undef UAM_LAUNCH_SEG
+    }
+    const dim3 gf((unsigned)((n_pairs + 63) / 64));
     const size_t lf = (size_t)2 * 64 * D * sizeof(double);
     hipLaunchKernelGGL(k_seg_final, gf, dim3(64 * D), lf, s, ctx->kp, ks, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "segmented evaluation launch");
     st = ktime_end(ctx, s);
     if (st) return st;
+    st = order_done(ctx, s);
+    return st ? st : 1;
+}
+
+// K2g launch (segment-grouped raster evaluation); returns 1 if launched, 0 if the batch is not
+// one it takes (the caller runs K2s / K2).  Needs the packed raster.  Scratch: the pair-order
+// scratch (order_scratch), so two streams sharing the context serialise on it.
+static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
+                          int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
+                          int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    const int G = ctx->k2g_group;
+    if (G < 1 || G > G_MAXLEN || !kr.pmap || ko.cells || ko.g_rows || D > 16) return 0;
+    const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
+    if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
+    const int nseg = (int)((W + G - 1) / G);
+    const int64_t n_items = P * nseg;
+    if (n_items >= INT32_MAX) return 0;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const int64_t ncnt = (int64_t)G_BINS * G_NBK;
+    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
+                 b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
+                 b_slot = al((size_t)n_items * sizeof(GSlot)), b_psi = al((size_t)n_items * 8),
+                 b_p1 = al((size_t)P * 32);
+    char* w = nullptr;
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_psi + b_p1, s, &w);
+    if (st) return st;
+    KGrp kg{};
+    kg.pairs = pairs;
+    kg.utab = utab;
+    kg.n_pairs = n_pairs;
+    kg.P = (int32_t)P;
+    kg.D = D;
+    kg.W = (int32_t)W;
+    kg.G = G;
+    kg.nseg = nseg;
+    int tshift = 0;
+    while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << G_TBITS)) ++tshift;
+    kg.tshift = tshift;
+    kg.n_items = n_items;
+    size_t o = 0;
+    kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first
+    kg.psi = (double*)(w + o), o += b_psi;
+    kg.p1 = (double4*)(w + o), o += b_p1;
+    kg.order = (int32_t*)(w + o), o += b_ord;
+    kg.cnt = (int32_t*)(w + o), o += b_cnt;
+    kg.tot = (int32_t*)(w + o), o += b_tot;
+    kg.key = (uint16_t*)(w + o);
+    if (!ctx->s2) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    st = ktime_begin(ctx, s);
+    if (st) return st;
+    // pass 1 (f64 ALU) on the side stream, beside the sort and the gathers
+    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+    hipLaunchKernelGGL(k_g_pass1, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, ctx->s2,
+                       ctx->kp, kg);
+    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(256), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
+                       kg.tot);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(256), 0, s, kg);
+    const size_t lds = (size_t)kr.pwords * 4;
+    const dim3 ge((unsigned)((n_items + 255) / 256));
+    if (G <= 8)
+        hipLaunchKernelGGL(k_g_eval<8>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    else if (G <= 12)
+        hipLaunchKernelGGL(k_g_eval<12>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    else
+        hipLaunchKernelGGL(k_g_eval<16>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
+                       (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
+    st = ktime_end(ctx, s);
+    if (st) return st;
+    ctx->last_group = G;
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -6288,18 +5762,11 @@ static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shi
     return UAM_OK;
 }
 
-// packed-raster layout (uam_raster_pack): 2^hb x 2^wb cells per block.  Default 2 x 2 (4 x 4
-// cells of 8 B = one 128-B line); UAM_PACK_HB / UAM_PACK_WB (0..4, tuning builds) are read
-// once per process, so packing and evaluation always agree.
+// packed-raster layout (uam_raster_pack): 2^hb x 2^wb cells per block, 2 x 2 = 4 x 4 cells of
+// 8 B = one 128-B line (row-major measured the same on cfg3: 0.554 vs 0.555 ms, r02)
 static void pack_layout(int32_t* hb, int32_t* wb) {
-    static const std::pair<int32_t, int32_t> hw = [] {
-        int32_t h = 2, w = 2;
-        if (const char* e = std::getenv("UAM_PACK_HB")) h = std::max(0, std::min(4, std::atoi(e)));
-        if (const char* e = std::getenv("UAM_PACK_WB")) w = std::max(0, std::min(4, std::atoi(e)));
-        return std::make_pair(h, w);
-    }();
-    *hb = hw.first;
-    *wb = hw.second;
+    *hb = 2;
+    *wb = 2;
 }
 
 struct PackDims {
@@ -6370,6 +5837,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
     int32_t* best_l = out ? out->best_length_idx : nullptr;
     DeviceGuard dg(ctx->device);
     hipStream_t s = (hipStream_t)stream;
+    ctx->last_group = 0;  // sequential sums unless K2g runs
     if (mode == UAM_MODE_RASTER && n_pairs <= INT64_MAX / D && want_wave(ctx, n_pairs * D)) {
         const KVolume kv{};
         st = launch_wave(ctx, mode, true, kr, kv, rec, nullptr, pairs, utab, D, n_pairs * D, ko,
@@ -6380,23 +5848,15 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
             return UAM_OK;
         }
     }
-    if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_BINNED) {
-        st = launch_binned(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
+    if (mode == UAM_MODE_RASTER && ctx->k2g_group > 0) {
+        st = launch_grouped(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
         if (st == 1) {
-            ctx->last_kernel = "K2b";
+            ctx->last_kernel = "K2g+pack";
             return UAM_OK;
         }
     }
-    if (mode == UAM_MODE_RASTER && ctx->variant == UAM_TUNING_TILED) {
-        st = launch_tiled(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
-        if (st < 0) return st;
-        if (st == 1) {
-            ctx->last_kernel = "K2t";
-            return UAM_OK;
-        }
-    }
-    if (mode == UAM_MODE_RASTER && ctx->variant == 0 && ctx->k2s_segs > 1) {
+    if (mode == UAM_MODE_RASTER) {
         st = launch_segmented(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
         if (st == 1) {
@@ -6404,11 +5864,8 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
             return UAM_OK;
         }
     }
-    int v =(ctx->variant == 0 || ctx->variant >= UAM_TUNING_WAVE) ? UAM_TUNING_DEFAULT
-                                                                   : ctx->variant;
-    if (D > 16) v = 1;  // the block-of-pairs kernels hold all D waves in one workgroup
-    if (v == 1) {
-        ctx->last_kernel = mode == UAM_MODE_RASTER ? "K2v1" : "K3v1";
+    if (D > 16) {  // the block-of-pairs kernels hold all D waves in one workgroup
+        ctx->last_kernel = mode == UAM_MODE_RASTER ? "K2d" : "K3d";
         const int64_t n_waves = ((n_pairs + 63) / 64) * D;
         const int64_t blocks = (n_waves + 3) / 4;
         if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
@@ -6424,7 +5881,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
         HIP_TRY(hipGetLastError());
         if (best_f || best_l) {  // selection needs the costs/lengths even if not requested
             if ((best_f && !ko.cost) || (best_l && !ko.length))
-                return fail(UAM_E_INVALID, "best_*_idx needs cost/length outputs (variant 1)");
+                return fail(UAM_E_INVALID, "best_*_idx needs cost/length outputs (D > 16)");
             const dim3 g2(grid_for(n_pairs, 256, INT32_MAX));
             if (best_f) hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.cost, n_pairs, D, 1, best_f);
             if (best_l) hipLaunchKernelGGL(k_argmin, g2, dim3(256), 0, s, ko.length, n_pairs, D, 0, best_l);
@@ -6444,10 +5901,10 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
                                        : raster_pair_order(ctx, kr, pairs, n_pairs, s, &order);
         if (st) return st;
     }
-#define UAM_LAUNCH_PAIRS(MODE_, C_, PIPE_, MINW_)                                          \
-    hipLaunchKernelGGL((k_eval_pairs<MODE_, C_, PIPE_, MINW_>), grid, block, lds, s, ctx->kg, \
-                       ctx->kp, kr, kv, (const uint4*)rec, pairs, n_pairs, utab, D, ko,      \
-                       best_f, best_l, order)
+#define UAM_LAUNCH_PAIRS(MODE_, MINW_)                                                     \
+    hipLaunchKernelGGL((k_eval_pairs<MODE_, MINW_>), grid, block, lds, s, ctx->kg, ctx->kp,   \
+                       kr, kv, (const uint4*)rec, pairs, n_pairs, utab, D, ko, best_f, best_l, \
+                       order)
     st = ktime_begin(ctx, s);
     if (st) return st;
     if (mode == UAM_MODE_ANALYTIC && !ko.g_rows && ctx->k3b_seg > 0) {
@@ -6491,20 +5948,13 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
 #undef UAM_LAUNCH_K3B
     } else if (mode == UAM_MODE_ANALYTIC) {
         ctx->last_kernel = "K3";
-        UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 8, false, 1);
+        UAM_LAUNCH_PAIRS(UAM_MODE_ANALYTIC, 1);
     } else {
+        // (r01: chunks of 2-8 gathers, software pipelining and 5-8 waves per SIMD measured within
+        // +-1% of each other on cfg3 -- the kernel sits at the random-gather ceiling)
         ctx->last_kernel = kr.sum ? "K2+skip" : "K2";
-        if (kr.sum) {
-            UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, 8, false, UAM_SKIP_MINW);  // 5 (6 spilled)
-        } else switch (v) {
-            case 2: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 1); break;
-            case 3: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 1); break;
-            case 4: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, true, 1); break;
-            case 5: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 8, false, 6); break;
-            case 6: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, true, 6); break;
-            case 7: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 2, true, 8); break;
-            default: UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 4, false, 8); break;  // 8
-        }
+        if (kr.sum) UAM_LAUNCH_PAIRS(MODE_RASTER_SKIP, SKIP_MINW);
+        else UAM_LAUNCH_PAIRS(UAM_MODE_RASTER, 1);
     }
 #undef UAM_LAUNCH_PAIRS
     HIP_TRY(hipGetLastError());
@@ -6654,6 +6104,7 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     DeviceGuard dg(ctx->device);
     const KRaster kr{};
     ctx->last_kernel = "K4";
+    ctx->last_group = 0;
     if (want_wave(ctx, n_pairs * D)) {
         ctx->last_kernel = "K4w";
         st = launch_wave(ctx, UAM_MODE_VOLUME, true, kr, kv, vol, nullptr, pairs6, utab, D,
@@ -6664,18 +6115,6 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
     const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
-    if (ctx->variant == 0 && ctx->k2s_segs > 1 && ctx->k4s) {  // K4s: segment-sorted (cfg5)
-        KRaster kxy{};
-        kxy.nx = kv.nx, kxy.ny = kv.ny, kxy.x0 = kv.x0, kxy.y_top = kv.y_top;
-        kxy.dx = vd->dx, kxy.dy = vd->dy, kxy.inv_dx = kv.inv_dx, kxy.inv_dy = kv.inv_dy;
-        st = launch_segmented(ctx, kxy, vol, pairs6, n_pairs, utab, D, ko, best_f, best_l,
-                              (hipStream_t)stream, &kv);
-        if (st < 0) return st;
-        if (st == 1) {
-            ctx->last_kernel = "K4s";
-            return UAM_OK;
-        }
-    }
     // the raster pair order over the volume's x/y extent (results do not depend on it)
     const int32_t* order = nullptr;
     if (ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
@@ -6687,7 +6126,7 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     }
     st = ktime_begin(ctx, (hipStream_t)stream);
     if (st) return st;
-    hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 8, false, 1>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
                        (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l, order);
     HIP_TRY(hipGetLastError());
@@ -7227,8 +6666,13 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     g_pinned->reset();
     g_devarena = (DevArena*)ctx->devarena;
     g_devarena->reset();
-    // UAM_K8_PROF=1: host timestamps of the phases (at the existing synchronisation points)
-    static const bool prof = std::getenv("UAM_K8_PROF") != nullptr;
+    // -DUAM_K8_PROF (diagnostics build): host timestamps of the phases (at the existing
+    // synchronisation points)
+#ifdef UAM_K8_PROF
+    constexpr bool prof = true;
+#else
+    constexpr bool prof = false;
+#endif
     const auto t_start = std::chrono::steady_clock::now();
     auto stamp = [&](const char* what) {
         if (prof)

@@ -47,26 +47,42 @@ def init_raster_comm(engine, group=None):
     engine.comm_init(obj[0], dist.get_world_size(group), dist.get_rank(group))
 
 
-def broadcast_raster(rec, src=0, group=None, engine=None):
-    """Broadcast the record raster tensor (in place) from src; returns seconds taken
-    (synchronised on the tensor's device before and after).  With an engine whose
-    communicator init_raster_comm set up, the bytes move by libuampath's RCCL broadcast
-    (uam_bcast_raster, xGMI on the GPU node); without one (CPU tensors: the gloo tests, or
-    several ranks sharing one GPU in a rehearsal) by torch.distributed.broadcast."""
+def broadcast_raster(raster, src=0, group=None, engine=None, rebuild=None):
+    """Broadcast the record raster in place from global rank src; returns seconds taken
+    (synchronised on the tensor's device before and after).
+
+    raster: a CostRaster, whose rec is broadcast and whose derived copies -- the gather-skip
+    bitmap (summary) and the packed copy K2g / K2s read (packed) -- were built from the
+    receiver's OLD records, so they are rebuilt from the broadcast records with `rebuild`
+    (default: `engine`) or, with no engine at hand, dropped (the evaluation then gathers rec);
+    or a bare tensor (rec of a CostRaster, a volume's voxels), broadcast as is -- its caller
+    owns any derived copy.  With an engine whose communicator init_raster_comm set up, the
+    bytes move by libuampath's RCCL broadcast (uam_bcast_raster, xGMI on the GPU node), whose
+    ranks are the process group's ranks (src is converted); without one (CPU tensors: the gloo
+    tests, or several ranks sharing one GPU in a rehearsal) by torch.distributed.broadcast."""
     import torch
 
     dist = _dist()
+    rec = getattr(raster, "rec", raster)
     dev = rec.device
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     if engine is not None:
-        engine.bcast_raster(rec, root=src)
+        root = dist.get_group_rank(group, src) if group is not None else src
+        engine.bcast_raster(rec, root=root)
     else:
         dist.broadcast(rec, src=src, group=group)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    return time.perf_counter() - t0
+    secs = time.perf_counter() - t0
+    if rec is not raster and (raster.summary is not None or raster.packed is not None):
+        eng = rebuild if rebuild is not None else engine
+        if eng is not None:
+            eng.raster_summary(raster, raster.block, packed=raster.packed is not None)
+        else:
+            raster.summary = raster.packed = None
+    return secs
 
 
 def max_over_ranks(values, device=None):

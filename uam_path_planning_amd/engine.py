@@ -279,9 +279,6 @@ class Engine:
         """Preallocated per-path (and per-pair best-index) outputs, reusable across launches."""
         return self._outputs(P, W, None, want_cells, want_g, n_pairs)
 
-    def set_tuning(self, variant):
-        _lib.check(self.lib.uam_set_tuning(self._ctx, int(variant)), "uam_set_tuning")
-
     def kernel_timing(self, enable=True):
         """Start (and reset) or stop HIP-event timing of the path evaluation: the context records
         an event pair on the launch stream around every k_eval_pairs / k_eval_wave launch (not
@@ -299,8 +296,26 @@ class Engine:
 
     def last_kernel(self):
         """Which path evaluation the last eval_generated / eval_generated3d ran (uam_last_kernel:
-        "K2s+skip", "K2+skip", "K2w", "K3b", ...)."""
+        "K2g+pack", "K2s+pack", "K2+skip", "K2w", "K3b", ...)."""
         return self.lib.uam_last_kernel(self._ctx).decode()
+
+    def last_group(self):
+        """Waypoint-group length of the last eval_generated's sums (uam_last_group): G > 0 when
+        the segment-grouped K2g ran (the oracle's orc_eval_paths_g order), 0 = sequential."""
+        return int(self.lib.uam_last_group(self._ctx))
+
+    def set_option(self, name, value):
+        """uam_set_option (include/uampath.h UAM_OPT_*): "group" (K2g waypoints per group,
+        0 = K2s), "sorted_min_paths", "k2s_segments", "wave_max_paths", "pair_order",
+        "k1_rows", "k3b_segment", "k3b_points_per_lane", "k8_tiled", "k8_streams"."""
+        _lib.check(self.lib.uam_set_option(self._ctx, _lib.OPTIONS[name], int(value)),
+                   "uam_set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        _lib.check(self.lib.uam_get_option(self._ctx, _lib.OPTIONS[name], ctypes.byref(v)),
+                   "uam_get_option")
+        return v.value
 
     def _outputs(self, P, W, mode, want_cells, want_g, n_pairs=None):
         torch = _torch()

@@ -145,7 +145,7 @@ class DataManager:
         dem, geo = DataManager(eng).load_dem(input_file, float(threshold_dem))
         eng.set_geometry(compile_shapes((), []))
         eng.set_params(PathParams(N=1))
-        rec = eng.raster_build(geo, dem).rec
+        rec = eng.raster_build(geo, dem, summary=False, packed=False).rec  # only the flags
         return ((rec[..., 3] & 2) != 0).cpu().numpy()
 
     def load_dem_polygons_from_geotiff(self, input_file, threshold_dem=0):
