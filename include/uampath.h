@@ -372,14 +372,15 @@ int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
 const char* uam_last_kernel(const uam_ctx* ctx);
 
 /* Waypoint-group length of the per-path sums of the last uam_eval_generated* call on ctx: G > 0
- * when the segment-grouped raster evaluation K2g ran (cost and nfz_sum formed as per-group
- * partial sums over waypoints [kG, (k+1)G) added in group order; oracle/uam_oracle.c
- * orc_eval_paths_g), 0 for the reference's sequential order (problem.py:42-43). */
+ * when the segment-grouped raster evaluation K2g ran (cost, length_q, length, kin_sum and
+ * nfz_sum formed as per-group partial sums, each term attached to a waypoint of the group
+ * [kG, (k+1)G), added in group order; oracle/uam_oracle.c orc_eval_paths_g), 0 for the
+ * reference's sequential order (problem.py:38-44, 84-114, 130-146). */
 int32_t uam_last_group(const uam_ctx* ctx);
 
 /* Context options: which kernel form runs (results never depend on them, except for the sum
  * order UAM_OPT_GROUP selects, which uam_last_group reports).  Read by the calls that follow.
- *   UAM_OPT_GROUP                K2g waypoints per group, 1..16 (default 8); 0 = no K2g (the
+ *   UAM_OPT_GROUP                K2g waypoints per group, 1..64 (default 21); 0 = no K2g (the
  *                                raster batches it takes run K2s: the reference's sum order)
  *   UAM_OPT_SORTED_MIN_PATHS     smallest raster batch (paths) the sorted forms K2g / K2s take
  *                                (default 65536; smaller batches run K2 / K2w)
@@ -393,7 +394,10 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                0 = the lane-per-path K3
  *   UAM_OPT_K3B_POINTS_PER_LANE  analytic K3b evaluation phase: 1 (default) or 2
  *   UAM_OPT_K8_TILED             DEM polygons: 1 (default) tile labelling in LDS, 0 cell-parallel
- *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4) */
+ *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4)
+ *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6 (4)
+ *   UAM_OPT_K2G_LDS_FLOOR        K2g evaluation: dynamic-LDS floor per workgroup in bytes, which
+ *                                caps the workgroups resident per CU (default 0) */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -404,7 +408,9 @@ enum {
     UAM_OPT_K3B_SEGMENT = 7,
     UAM_OPT_K3B_POINTS_PER_LANE = 8,
     UAM_OPT_K8_TILED = 9,
-    UAM_OPT_K8_STREAMS = 10
+    UAM_OPT_K8_STREAMS = 10,
+    UAM_OPT_K2G_TILE_BITS = 11,
+    UAM_OPT_K2G_LDS_FLOOR = 12
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

@@ -249,13 +249,55 @@ static double nrm_of(double d2, int smooth) {
     return smooth ? n * n : n; /* problem.py:94,132: norm_2(.)**2 when smooth */
 }
 
+/* Grouped summation (K2g; build-defined, no reference counterpart).  A per-path
+ * sum over terms indexed by waypoint: with G > 0 the terms of waypoints [kG, (k+1)G) form a
+ * partial sum from +0.0 in index order, and the partials are added to the sum's initial value
+ * in group order; with G = 0 every term is added to the running sum in index order, which is
+ * the reference's sequential order.  Terms arrive in non-decreasing index order. */
+typedef struct {
+    double tot, part;
+    int grp, G;
+} gacc;
+
+static void gacc_init(gacc* a, double init, int G) {
+    a->tot = init;
+    a->part = 0.0;
+    a->grp = 0;
+    a->G = G;
+}
+
+static void gacc_add(gacc* a, int idx, double v) {
+    if (a->G <= 0) {
+        a->tot = a->tot + v;
+        return;
+    }
+    const int g = idx / a->G;
+    if (g != a->grp) { /* group boundary: flush (empty groups add +0.0, an exact no-op) */
+        a->tot = a->tot + a->part;
+        a->part = 0.0;
+        a->grp = g;
+    }
+    a->part = a->part + v;
+}
+
+static double gacc_done(gacc* a) {
+    if (a->G > 0) {
+        a->tot = a->tot + a->part;
+        a->part = 0.0;
+        a->G = 0;
+    }
+    return a->tot;
+}
+
 /* group > 0 (raster mode only): the grouped summation order of the segment-grouped raster
- * evaluation K2g (build-defined, no reference counterpart).  The waypoints are
- * cut into groups [kG, min((k+1)G, W)); per group a partial Φ/N sum and a partial ψ sum are
- * formed in waypoint order from +0.0, and the partials are added to cost = (N+1)·L and to
- * nsum = 0.0 in group order (one group when group >= W).  group = 0 is the reference's
- * sequential order (problem.py:42-43): cost + Φ_0/N + Φ_1/N + ...  Both sum the same terms and differ by
- * rounding only (≤ 1e-12 relative on the cfg3 batch, tests/test_oracle_golden.py). */
+ * evaluation K2g.  The waypoints are cut into groups [kG, min((k+1)G, W)); every per-path sum
+ * is formed as per-group partials added in group order (gacc), with each term attached to a
+ * waypoint: the Φ/N and ψ terms of waypoint j to j; the length terms of segment p_{j-1} -> p_j
+ * (get_cost's L and the true length) to j, get_cost's anchor term to 0; kinematic row k
+ * (points k, k+1, k+2) to k + 1.  cost = (N+1)·L + the Φ/N partials.  group = 0 is the
+ * reference's sequential order (problem.py:38-44, 84-114, 130-146).  Both sum the same terms
+ * and differ by rounding only (≤ 1e-12 relative on the cfg3 batch,
+ * tests/test_oracle_golden.py). */
 int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const orc_raster* rs,
                      const float* rec, const double* wp, int64_t P, double* cost, double* lq,
                      double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
@@ -264,6 +306,7 @@ int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const
     const double mincos = cos(p->maxalpha);
     const double r = p->maxratio_smooth ? p->maxratio * p->maxratio : p->maxratio;
     const int n_rows = 3 * N + g->n_obstacles * W;
+    const int G = (mode == 1 && group > 0) ? group : 0;
     double inv_dx = 0, inv_dy = 0;
     if (mode == 1) {
         inv_dx = 1.0 / rs->dx;
@@ -274,20 +317,21 @@ int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const
         /* length_of (problem.py:130-146): y = [anchor, p_0..p_{N+1}, goal]; N+1 segments */
         double ax = p->anchor_mode ? p->anchor_x : z[0];
         double ay = p->anchor_mode ? p->anchor_y : z[1];
-        double L = 0.0;
+        gacc aL;
+        gacc_init(&aL, 0.0, G);
         if (p->quirk_length) {
             double dx = z[0] - ax, dy = z[1] - ay;
             double s = 0.0;
             s = s + dx * dx;
             s = s + dy * dy;
-            L = L + nrm_of(s, p->length_smooth);
+            gacc_add(&aL, 0, nrm_of(s, p->length_smooth));
             for (int k = 1; k <= N; ++k) {
                 dx = z[2 * k] - z[2 * k - 2];
                 dy = z[2 * k + 1] - z[2 * k - 1];
                 s = 0.0;
                 s = s + dx * dx;
                 s = s + dy * dy;
-                L = L + nrm_of(s, p->length_smooth);
+                gacc_add(&aL, k, nrm_of(s, p->length_smooth));
             }
         } else {
             for (int k = 1; k <= N + 1; ++k) {
@@ -295,20 +339,24 @@ int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const
                 double s = 0.0;
                 s = s + dx * dx;
                 s = s + dy * dy;
-                L = L + nrm_of(s, p->length_smooth);
+                gacc_add(&aL, k, nrm_of(s, p->length_smooth));
             }
         }
+        const double L = gacc_done(&aL);
         /* true polyline length (solver.py:49 length_of(x_sol), non-smooth, all segments) */
-        double len = 0.0;
+        gacc alen;
+        gacc_init(&alen, 0.0, G);
         for (int k = 1; k <= N + 1; ++k) {
             double dx = z[2 * k] - z[2 * k - 2], dy = z[2 * k + 1] - z[2 * k - 1];
             double s = 0.0;
             s = s + dx * dx;
             s = s + dy * dy;
-            len = len + sqrt(s);
+            gacc_add(&alen, k, sqrt(s));
         }
+        const double len = gacc_done(&alen);
         /* kinematic rows (problem.py:100-107) */
-        double ksum = 0.0;
+        gacc ak;
+        gacc_init(&ak, 0.0, G);
         double* grow = g_rows ? g_rows + pi * (int64_t)n_rows : 0;
         for (int k = 0; k < N; ++k) {
             double ax0 = z[2 * (k + 1)] - z[2 * k], ay0 = z[2 * (k + 1) + 1] - z[2 * k + 1];
@@ -325,34 +373,29 @@ int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const
             double c1 = fmax(0.0, nb - r * na);
             double c2 = fmax(0.0, na / r - nb);
             double c3 = fmax(0.0, mincos - dt / (na * nb));
-            ksum = ksum + c1;
-            ksum = ksum + c2;
-            ksum = ksum + c3;
+            gacc_add(&ak, k + 1, c1);
+            gacc_add(&ak, k + 1, c2);
+            gacc_add(&ak, k + 1, c3);
             if (grow) {
                 grow[3 * k] = c1;
                 grow[3 * k + 1] = c2;
                 grow[3 * k + 2] = c3;
             }
         }
+        const double ksum = gacc_done(&ak);
         /* per-waypoint penalty, no-fly rows, clearance */
-        double c = (double)(N + 1) * L;
-        double nsum = 0.0, hmax = -INFINITY;
+        gacc ac, an;
+        gacc_init(&ac, (double)(N + 1) * L, G);
+        gacc_init(&an, 0.0, G);
+        double hmax = -INFINITY;
         int32_t nh = 0, off = 0;
-        const int grouped = (mode == 1) && group > 0;
-        double gc = 0.0, gn = 0.0; /* partials of the current group (grouped order) */
         for (int j = 0; j < W; ++j) {
             double x0 = z[2 * j], x1 = z[2 * j + 1];
-            if (grouped && j > 0 && j % group == 0) { /* group boundary: flush the partials */
-                c = c + gc;
-                nsum = nsum + gn;
-                gc = 0.0;
-                gn = 0.0;
-            }
             if (mode == 0) {
-                c = c + total_penalty(g, p, x0, x1) / (double)N;
+                gacc_add(&ac, j, total_penalty(g, p, x0, x1) / (double)N);
                 for (int s = 0; s < g->n_obstacles; ++s) {
                     double v = psi(g, s, x0, x1, p->obstacle_smooth, 0.0);
-                    nsum = nsum + v;
+                    gacc_add(&an, j, v);
                     if (grow) grow[3 * N + s * W + j] = v;
                 }
                 nh += collides(g, x0, x1);
@@ -372,22 +415,14 @@ int orc_eval_paths_g(const orc_geom* g, const orc_params* p, int32_t mode, const
                 const float* rc = rec + 4 * cell;
                 uint32_t fl;
                 memcpy(&fl, &rc[3], 4);
-                if (grouped) {
-                    gc = gc + (double)rc[0] / (double)N;
-                    gn = gn + (double)rc[1];
-                } else {
-                    c = c + (double)rc[0] / (double)N;
-                    nsum = nsum + (double)rc[1];
-                }
+                gacc_add(&ac, j, (double)rc[0] / (double)N);
+                gacc_add(&an, j, (double)rc[1]);
                 nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
                 double terrain = (fl & ORC_FLAG_NODATA) ? 0.0 : (double)rc[2];
                 if (terrain > hmax) hmax = terrain;
             }
         }
-        if (grouped) { /* the last group */
-            c = c + gc;
-            nsum = nsum + gn;
-        }
+        const double c = gacc_done(&ac), nsum = gacc_done(&an);
         if (cost) cost[pi] = c;
         if (lq) lq[pi] = L;
         if (length) length[pi] = len;

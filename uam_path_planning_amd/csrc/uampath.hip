@@ -719,6 +719,32 @@ __device__ __forceinline__ void consume_chunk_vol(const Chunk<C>& ch, const Path
     }
 }
 
+// Kinematic row k of problem.py:100-107 from the norms pn, nk of segments k and k + 1 (the
+// squared norms when maxratio_smooth) and their dot product dt:
+//   c1 = max(0, nk - r pn), c2 = max(0, pn / r - nk), c3 = max(0, mincos - dt / (pn nk)).
+// The two f64 divisions (~10 VALU instructions each) are skipped where their outcome is
+// provably +0, which is every row of a path that keeps to the ratio and turn limits:
+//   c2: t = RN(nk r); pn <= RN(t (1 - 2^-50)) implies pn < nk r exactly, so pn / r < nk,
+//       RN(pn / r) <= nk and the difference is <= 0: c2 = +0;
+//   c3: q = RN(pn nk) in [1e-200, 1e200], mincos > 1e-100, dt >= RN(RN(mincos q) (1 + 2^-50))
+//       implies dt > mincos q exactly, so RN(dt / q) >= mincos and c3 = +0.
+// (RN's relative error is <= 2^-53 in that range, well inside the 2^-50 margins.)  Otherwise
+// the formula runs as written; NaN and infinite operands fail both tests.  Every value is
+// bit-identical to the plain formula.
+__device__ __forceinline__ void kin_row(const KParams& p, double pn, double nk, double dt,
+                                        double& c1, double& c2, double& c3) {
+    c1 = fmax(0.0, nk - p.r_eff * pn);
+    const double t2 = nk * p.r_eff;
+    c2 = (pn <= t2 * (1.0 - 0x1p-50)) ? 0.0 : fmax(0.0, pn / p.r_eff - nk);
+    const double q = pn * nk;
+    bool fast3 = false;
+    if (q >= 1e-200 && q <= 1e200 && p.mincos > 1e-100) {
+        const double t3 = p.mincos * q;
+        fast3 = dt >= t3 * (1.0 + 0x1p-50);
+    }
+    c3 = fast3 ? 0.0 : fmax(0.0, p.mincos - dt / q);
+}
+
 // Pass 1 of a path: get_cost's length term L (problem.py:130-146 with the quirk), the true
 // length (length_of, solver.py:49) and the sum of the 3N kinematic rows (problem.py:100-107),
 // optionally storing the rows.  Shared by every path kernel, so their bits agree.
@@ -757,9 +783,8 @@ __device__ __forceinline__ void path_pass1(const KParams& p, const PathSrc<GEN>&
             double dt = 0.0;
             dt = dt + pdx * dx;
             dt = dt + pdy * dy;
-            const double c1 = fmax(0.0, nk - p.r_eff * pn);
-            const double c2 = fmax(0.0, pn / p.r_eff - nk);
-            const double c3 = fmax(0.0, p.mincos - dt / (pn * nk));
+            double c1, c2, c3;
+            kin_row(p, pn, nk, dt, c1, c2, c3);
             ksum = ksum + c1;
             ksum = ksum + c2;
             ksum = ksum + c3;
@@ -3114,9 +3139,11 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
                 double dt = 0.0;
                 dt = dt + pdx * dx;
                 dt = dt + pdy * dy;
-                kn[3 * (j - 2)] = fmax(0.0, nk - p.r_eff * pn);
-                kn[3 * (j - 2) + 1] = fmax(0.0, pn / p.r_eff - nk);
-                kn[3 * (j - 2) + 2] = fmax(0.0, p.mincos - dt / (pn * nk));
+                double c1, c2, c3;
+                kin_row(p, pn, nk, dt, c1, c2, c3);
+                kn[3 * (j - 2)] = c1;
+                kn[3 * (j - 2) + 1] = c2;
+                kn[3 * (j - 2) + 2] = c3;
             }
         }
     }
@@ -4519,41 +4546,51 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
 // K2s keeps each path's sums in waypoint order, so its segments run one launch after another
 // and stay long (41 waypoints, ~13 km): its gathers reach 46% L2 hits and move 4.5x the
 // algorithmic bytes (profiles/r02/pack_final).  K2g restates the per-path sums in a grouped
-// order (oracle/uam_oracle.c orc_eval_paths_g): the waypoints are cut into groups of G
-// (default 8, ~2.6 km), each group's Phi/N and psi partial sums are formed from +0.0 in
-// waypoint order, and the partials are added to cost = (N+1) L and nsum = 0 in group order;
-// the terrain maximum, hits and off-raster counts are order-free.  Every (path, group) item is
-// then independent, so ONE counting sort on the 64 x 64-tile Morton key of the item's middle
-// waypoint and ONE launch evaluate all of them with the XCD-placed sorted order: the items an
-// XCD runs together cover a few tiles, whose lines stay in its L2.  The partials go to a
-// 16-B slot per item; k_g_final combines them in group order with pass 1 (computed beside the
-// sort and the evaluation on the side stream) and runs the main.py:175-180 selection.
-// Against the sequential reference the grouped sums differ by rounding only (<= 1e-12
-// relative, tests/test_oracle_golden.py); against the grouped oracle they are bit-exact.
-constexpr int G_TBITS = 6;                            // 64 x 64 tiles over the raster
-constexpr int G_BINS = (1 << (2 * G_TBITS)) + 1;      // + one bin for off-raster / NaN
-constexpr int G_NBK = 256;                            // partitions of the counting sort
-constexpr int G_MAXLEN = 16;                          // longest group
+// order (oracle/uam_oracle.c orc_eval_paths_g): the waypoints are cut into groups of G, each
+// group's Phi/N and psi partial sums are formed from +0.0 in waypoint order, and the partials
+// are added to cost = (N+1) L and nsum = 0 in group order; the terrain maximum, hits and
+// off-raster counts are order-free.  Every (path, group) item is then independent, so ONE
+// counting sort on the Morton key of the raster tile under the item's middle waypoint and ONE
+// launch evaluate all of them in the XCD-placed sorted order: the items an XCD runs together
+// cover a few tiles, whose lines stay in its L2.  The partials go to a 16-B slot per item;
+// k_g_final combines them in group order with pass 1 and runs the main.py:175-180 selection.
+// Every per-path sum is grouped the same way -- each term attached to a waypoint (Phi/N, psi
+// of waypoint j; the length terms of segment p_{j-1} -> p_j; kinematic row k to k + 1) -- so
+// an item also forms its group's share of pass 1 (get_cost's L, the true length, the
+// kinematic rows): that f64 work runs in the memory-bound evaluation launch, whose waves wait
+// on gathers with the VALU mostly idle (profiles/r03/k2g_order: pass 1 as its own launch beside
+// the evaluation cost ~90 us of its 130-150).  Against the sequential reference the grouped
+// sums differ by rounding only (<= 1e-12 relative, tests/test_oracle_golden.py); against the
+// grouped oracle they are bit-exact.
+constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles over the raster
+constexpr int G_BINS_MAX = (1 << (2 * G_TBITS_MAX)) + 1;  // + one bin for off-raster / NaN
+constexpr int G_NBK = 256;                              // partitions of the counting sort
+constexpr int G_MAXLEN = 64;                            // longest group
+constexpr int G_UTAB_LDS = 32 * 1024;                   // unit-arc table in LDS up to this size
 
-struct GSlot {       // 16 B per (path, group)
-    double cost;     // partial sum of Phi/N in waypoint order from +0.0
+struct alignas(16) GSlot {  // 48 B per (path, group), written by one lane
+    double cost;     // partial sums from +0.0 in waypoint order: Phi/N,
+    double psi;      //   the no-fly psi,
+    double L;        //   get_cost's length term (problem.py:130-146 with the quirk),
+    double len;      //   the true length (solver.py:49),
+    double ksum;     //   the kinematic rows (problem.py:100-107)
     float hmax;      // max terrain of the group's waypoints as consume_chunk reads it
-    uint32_t cnt;    // nfz hits | off-raster << 8 | (psi partial stored) << 16
+    uint32_t cnt;    // nfz hits | off-raster << 8
 };
 
 struct KGrp {
     const double* __restrict__ pairs;
     const double* __restrict__ utab;
     int64_t n_pairs;
-    int32_t P, D, W, G, nseg, tshift;
+    int32_t P, D, W, G, nseg, tshift, tbits, bins;
+    int32_t utab_lds;              // k_g_eval stages utab in LDS (D N 16 <= G_UTAB_LDS)
     int64_t n_items;               // P * nseg; item i = path * nseg + group
     uint16_t* __restrict__ key;    // [n_items]
-    int32_t* __restrict__ cnt;     // [G_BINS][G_NBK] counts -> offsets
+    int32_t* __restrict__ cnt;     // [bins][G_NBK] counts -> offsets
     int32_t* __restrict__ tot;     // scan block totals
     int32_t* __restrict__ order;   // [n_items] item of each sorted position
-    GSlot* __restrict__ slot;      // [P][nseg]
-    double* __restrict__ psi;      // [P][nseg] psi partial (read only where flagged)
-    double4* __restrict__ p1;      // [P] pass 1: (L, length, kinematic sum, 0)
+    GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
+                                   // a group's slots of consecutive paths contiguously
 };
 
 __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
@@ -4568,143 +4605,220 @@ __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t 
     return src;
 }
 
+// sort key of a point: Morton code of its 2^tbits x 2^tbits-grid tile, bins - 1 off the raster
+__device__ __forceinline__ uint32_t grp_key(const KGrp& kg, const KRaster& rs, double x0,
+                                            double x1) {
+    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+    if (!((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)))
+        return kg.bins - 1;
+    const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
+    uint32_t k = 0;
+    for (int bit = kg.tbits - 1; bit >= 0; --bit)
+        k = (k << 2) | (((ty >> bit) & 1u) << 1) | ((tx >> bit) & 1u);
+    return k;
+}
+
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
-// groups (Morton code of the 64 x 64-tile tile under the group's middle waypoint) and the
-// partition's histogram, stored bin-major so the scan yields each (bin, partition)'s offset
-__global__ __launch_bounds__(256) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
-    __shared__ int32_t h[G_BINS];
+// groups (the tile under the group's middle waypoint) and the partition's histogram, stored
+// bin-major so the scan yields each (bin, partition)'s offset
+__global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
+    __shared__ int32_t h[G_BINS_MAX];
     const int t = threadIdx.x, b = blockIdx.x;
-    for (int k = t; k < G_BINS; k += 256) h[k] = 0;
+    for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     __syncthreads();
-    const int32_t lo = (int32_t)((int64_t)kg.P * b / G_NBK);
-    const int32_t hi = (int32_t)((int64_t)kg.P * (b + 1) / G_NBK);
-    for (int32_t i = lo + t; i < hi; i += 256) {
-        const PathSrc<true> src = grp_src(kg, p.N, i);
-        for (int s = 0; s < kg.nseg; ++s) {
-            const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
-            double x0, x1;
-            src.at((j0 + j1 - 1) >> 1, x0, x1);
-            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
-            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
-            uint32_t k = G_BINS - 1;
-            if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
-                const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
-                k = 0;
-#pragma unroll
-                for (int bit = G_TBITS - 1; bit >= 0; --bit)
-                    k = (k << 2) | (((ty >> bit) & 1u) << 1) | ((tx >> bit) & 1u);
-            }
-            kg.key[(int64_t)i * kg.nseg + s] = (uint16_t)k;
-            atomicAdd(&h[k], 1);
-        }
+    // thread = item (consecutive threads: the groups of one path, then the next path's), so
+    // the key stores are coalesced and a path's pair is one broadcast load
+    const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
+    const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
+    for (int64_t i = lo + t; i < hi; i += 1024) {
+        const int32_t path = (int32_t)(i / kg.nseg);
+        const int s = (int)(i - (int64_t)path * kg.nseg);
+        const PathSrc<true> src = grp_src(kg, p.N, path);
+        const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
+        double x0, x1;
+        src.at((j0 + j1 - 1) >> 1, x0, x1);
+        const uint32_t k = grp_key(kg, rs, x0, x1);
+        kg.key[i] = (uint16_t)k;
+        atomicAdd(&h[k], 1);
     }
     __syncthreads();
-    for (int k = t; k < G_BINS; k += 256) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
+    for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
 // launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered
-__global__ __launch_bounds__(256) void k_g_scatter(KGrp kg) {
-    __shared__ int32_t cur[G_BINS];
+__global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
+    __shared__ int32_t cur[G_BINS_MAX];
     const int t = threadIdx.x, b = blockIdx.x;
-    for (int k = t; k < G_BINS; k += 256) {
+    for (int k = t; k < kg.bins; k += 1024) {
         const int64_t c = (int64_t)k * G_NBK + b;
         cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
     }
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
-    for (int64_t i = lo + t; i < hi; i += 256) kg.order[atomicAdd(&cur[kg.key[i]], 1)] = (int32_t)i;
-}
-
-// pass 1 of every path (path_pass1: L, length, kinematic sum), thread = path in natural order
-__global__ __launch_bounds__(256) void k_g_pass1(KParams p, KGrp kg) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= kg.P) return;
-    const PathSrc<true> src = grp_src(kg, p.N, (int32_t)i);
-    PathAcc a;
-    path_pass1<true>(p, src, nullptr, a);
-    kg.p1[i] = make_double4(a.L, a.len, a.ksum, 0.0);
+    for (int64_t i = lo + t; i < hi; i += 1024)
+        kg.order[atomicAdd(&cur[kg.key[i]], 1)] = (int32_t)i;
 }
 
 // every (path, group) item in sorted order (workgroup b takes the sorted chunk xcd_chunk(b));
 // the group's waypoints from the packed raster exactly as seg_pass2_pack reads them (block
-// codes in LDS), all GL gathers issued before the first is consumed; the partials go to the
-// item's slot
-template <int GL>
+// codes in LDS), CH gathers issued before the first of them is consumed; the unit-arc rows in
+// LDS (the items of a wave come from different groups and displacements: per-lane rows); the
+// partials go to the item's slot.  Dynamic LDS: the block codes, the unit-arc table, padded
+// to a floor that caps the workgroups per CU (UAM_OPT_K2G_LDS) so an XCD's resident items
+// cover a narrow range of the sorted order.
+template <int CH>
 __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                                                 const uint4* __restrict__ rec) {
-    extern __shared__ uint32_t s_map[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint32_t* s_map = s_dyn;
+    const int mapw = (rs.pwords + 3) & ~3;
+    const double2* s_u = reinterpret_cast<const double2*>(s_dyn + mapw);
     for (int i = threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
+    if (kg.utab_lds) {
+        double2* su = reinterpret_cast<double2*>(s_dyn + mapw);
+        const double2* gu = reinterpret_cast<const double2*>(kg.utab);
+        for (int i = threadIdx.x; i < kg.D * p.N; i += 256) su[i] = gu[i];
+    }
     __syncthreads();
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (pos >= kg.n_items) return;
     const int32_t item = kg.order[pos];
     const int32_t path = item / kg.nseg;
     const int s = item - path * kg.nseg;
-    const PathSrc<true> src = grp_src(kg, p.N, path);
-    const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
-    uint4 r[GL];
-    uint32_t inb = 0, need = 0, full = 0;
-#pragma unroll
-    for (int t = 0; t < GL; ++t) {
-        if (j0 + t < j1) {
-            double x0, x1;
-            src.at(j0 + t, x0, x1);
-            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
-            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
-            if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
-                inb |= 1u << t;
-                const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
-                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
-                if (code & 2u) {
-                    need |= 1u << t;
-                    full |= 1u << t;
-                    r[t] = rec[iy * rs.nx + ix];
-                } else if (code) {
-                    need |= 1u << t;
-                    const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
-                    r[t].x = v.x;
-                    r[t].z = v.y;
-                }
+    const int32_t q = path / kg.D, d = path - q * kg.D;
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const int N = p.N, W = kg.W;
+    const double2* urow = (kg.utab_lds ? s_u : reinterpret_cast<const double2*>(kg.utab)) +
+                          (int64_t)d * N;
+    const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
+    auto point = [&](int j, double& x0, double& x1) {
+        if (j == 0) {
+            x0 = pr.x, x1 = pr.y;
+        } else if (j == W - 1) {
+            x0 = pr.z, x1 = pr.w;
+        } else {
+            const double2 u = urow[j - 1];
+            arc_point(pr.x, pr.y, pr.z, pr.w, u.x, u.y, x0, x1);
+        }
+    };
+    // this group's share of pass 1, path_pass1's arithmetic: segments p_{j-1} -> p_j for
+    // j in [max(j0, 1), j1) add to L and length; row k (segments k + 1 and k + 2) belongs to
+    // the group of waypoint k + 1
+    double gL = 0.0, glen = 0.0, gk = 0.0;
+    {
+        const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
+        double px, py;
+        if (j0 == 0 && p.quirk_length) {  // get_cost's anchor term (y_0 = anchor, y_1 = p_0)
+            point(0, px, py);
+            const double ax = p.anchor_mode ? p.anchor_x : px;
+            const double ay = p.anchor_mode ? p.anchor_y : py;
+            const double dx = px - ax, dy = py - ay;
+            double s2 = 0.0;
+            s2 = s2 + dx * dx;
+            s2 = s2 + dy * dy;
+            const double n = sqrt(s2);
+            gL = gL + (ls ? n * n : n);
+        }
+        const int ja = max(j0, 1), jb = min(j1, W - 1);
+        point(ja - 1, px, py);
+        double pdx = 0.0, pdy = 0.0, pn = 0.0;
+        for (int j = ja; j <= jb; ++j) {
+            double qx, qy;
+            point(j, qx, qy);
+            const double dx = qx - px, dy = qy - py;
+            double s2 = 0.0;
+            s2 = s2 + dx * dx;
+            s2 = s2 + dy * dy;
+            const double n = sqrt(s2);  // norm_2 = sqrt(dot) (casadi_norm_2)
+            if (j < j1) {
+                glen = glen + n;
+                if (!p.quirk_length || j <= N) gL = gL + (ls ? n * n : n);
             }
+            const double nk = ms ? n * n : n;
+            if (j >= j0 + 1 && j >= 2) {  // row k = j - 2 (problem.py:100-107)
+                double dt = 0.0;
+                dt = dt + pdx * dx;
+                dt = dt + pdy * dy;
+                double c1, c2, c3;
+                kin_row(p, pn, nk, dt, c1, c2, c3);
+                gk = gk + c1;
+                gk = gk + c2;
+                gk = gk + c3;
+            }
+            pdx = dx, pdy = dy, pn = nk, px = qx, py = qy;
         }
     }
-    const double dN = (double)p.N;
+    const double dN = (double)N;
     double gc = 0.0, gn = 0.0;
     float hmax = -INFINITY;
     uint32_t nh = 0, off = 0;
+    for (int jc = j0; jc < j1; jc += CH) {
+        const int je = min(jc + CH, j1);
+        uint4 r[CH];
+        uint32_t inb = 0, need = 0, full = 0;
 #pragma unroll
-    for (int t = 0; t < GL; ++t) {
-        if (j0 + t < j1) {
-            if (!((inb >> t) & 1u)) {
-                ++off;
-                hmax = fmaxf(hmax, 0.0f);  // off-raster counts as sea level
-            } else if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
-                hmax = fmaxf(hmax, 0.0f);
-            } else {
-                gc = gc + (double)__uint_as_float(r[t].x) / dN;
-                float terrain = __uint_as_float(r[t].z);
-                if ((full >> t) & 1u) {
-                    gn = gn + (double)__uint_as_float(r[t].y);
-                    nh += (r[t].w & UAM_FLAG_NFZ) ? 1u : 0u;
-                    if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0f;
+        for (int t = 0; t < CH; ++t) {
+            const int j = jc + t;
+            if (j < je) {
+                double x0, x1;
+                point(j, x0, x1);
+                const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+                const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+                if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
+                    inb |= 1u << t;
+                    const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
+                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                    const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
+                    if (code & 2u) {
+                        need |= 1u << t;
+                        full |= 1u << t;
+                        r[t] = rec[iy * rs.nx + ix];
+                    } else if (code) {
+                        need |= 1u << t;
+                        const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
+                        r[t].x = v.x;
+                        r[t].z = v.y;
+                    }
                 }
-                hmax = fmaxf(hmax, terrain);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            if (jc + t < je) {
+                if (!((inb >> t) & 1u)) {
+                    ++off;
+                    hmax = fmaxf(hmax, 0.0f);  // off-raster counts as sea level
+                } else if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0
+                    hmax = fmaxf(hmax, 0.0f);
+                } else {
+                    gc = gc + (double)__uint_as_float(r[t].x) / dN;
+                    float terrain = __uint_as_float(r[t].z);
+                    if ((full >> t) & 1u) {
+                        gn = gn + (double)__uint_as_float(r[t].y);
+                        nh += (r[t].w & UAM_FLAG_NFZ) ? 1u : 0u;
+                        if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0f;
+                    }
+                    hmax = fmaxf(hmax, terrain);
+                }
             }
         }
     }
-    const int64_t si = (int64_t)path * kg.nseg + s;
     GSlot o;
     o.cost = gc;
+    o.psi = gn;
+    o.L = gL;
+    o.len = glen;
+    o.ksum = gk;
     o.hmax = hmax;
-    o.cnt = nh | (off << 8) | (full ? 1u << 16 : 0u);
-    kg.slot[si] = o;
-    if (full) kg.psi[si] = gn;
+    o.cnt = nh | (off << 8);
+    kg.slot[(int64_t)s * kg.P + path] = o;
 }
 
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout): the partials
-// combined in group order, and the selection over each pair's D paths
+// combined in group order (cost = (N+1) L + the Phi/N partials), and the selection over each
+// pair's D paths
 __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
                                                   int32_t* __restrict__ best_f,
                                                   int32_t* __restrict__ best_l) {
@@ -4716,29 +4830,31 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     const int qi = t / D, di = t - qi * D;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
-        const double4 q1 = kg.p1[gp];
-        double cost = (double)(p.N + 1) * q1.x, nsum = 0.0, hmax = -INFINITY;
+        double L = 0.0, len = 0.0, ksum = 0.0, nsum = 0.0, hmax = -INFINITY;
         int32_t nh = 0, off = 0;
-        const GSlot* sl = kg.slot + gp * kg.nseg;
         for (int s = 0; s < kg.nseg; ++s) {
-            const GSlot g = sl[s];
-            cost = cost + g.cost;
-            if (g.cnt >> 16) nsum = nsum + kg.psi[gp * kg.nseg + s];
+            const GSlot g = kg.slot[(int64_t)s * kg.P + gp];
+            L = L + g.L;
+            len = len + g.len;
+            ksum = ksum + g.ksum;
+            nsum = nsum + g.psi;
             hmax = fmax(hmax, (double)g.hmax);
             nh += (int32_t)(g.cnt & 255u);
             off += (int32_t)((g.cnt >> 8) & 255u);
         }
+        double cost = (double)(p.N + 1) * L;
+        for (int s = 0; s < kg.nseg; ++s) cost = cost + kg.slot[(int64_t)s * kg.P + gp].cost;
         if (out.cost) out.cost[gp] = cost;
-        if (out.length_q) out.length_q[gp] = q1.x;
-        if (out.length) out.length[gp] = q1.y;
-        if (out.kin_sum) out.kin_sum[gp] = q1.z;
+        if (out.length_q) out.length_q[gp] = L;
+        if (out.length) out.length[gp] = len;
+        if (out.kin_sum) out.kin_sum[gp] = ksum;
         if (out.nfz_sum) out.nfz_sum[gp] = nsum;
         if (out.min_clearance) out.min_clearance[gp] = p.altitude - hmax;
         if (out.nfz_hits) out.nfz_hits[gp] = nh;
         if (out.offmap) out.offmap[gp] = off;
         if (out.below_terrain) out.below_terrain[gp] = 0;
         s_cost[di * 64 + qi] = cost;
-        s_len[di * 64 + qi] = q1.y;
+        s_len[di * 64 + qi] = len;
     }
     __syncthreads();
     if (t < 64 && q0 + t < kg.n_pairs) {
@@ -4791,6 +4907,7 @@ struct uam_ctx {
     int k2s_segs = 2;           // K2s segments per path (UAM_OPT_K2S_SEGMENTS: 2..8)
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
+    bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
@@ -4800,7 +4917,14 @@ struct uam_ctx {
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
     int32_t last_group = 0;     // uam_last_group: waypoint-group length of the last call's sums
-    int k2g_group = 8;          // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s)
+    int k2g_group = 21;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
+                                // (profiles/r03/k2g3, tile bits 4, pass 1 beside the gathers):
+                                // 8 0.538, 11 0.496, 16 0.457, 21 0.399, 22 0.405, 28 0.426
+    int k2g_tbits = 4;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
+                                // cfg3 at G = 21: 4 0.399, 5 0.410, 6 0.434 ms)
+    int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
+                                // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR)
+
 };
 
 namespace {
@@ -5404,6 +5528,17 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
         case UAM_OPT_K8_TILED:
             ctx->k8_tiled = value != 0;
             return UAM_OK;
+        case UAM_OPT_K2G_TILE_BITS:
+            if (value < 3 || value > G_TBITS_MAX)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_TILE_BITS %lld outside [3, %d]",
+                            (long long)value, G_TBITS_MAX);
+            ctx->k2g_tbits = (int)value;
+            return UAM_OK;
+        case UAM_OPT_K2G_LDS_FLOOR:
+            if (value < 0 || value > 160 * 1024)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_FLOOR outside [0, 163840]");
+            ctx->k2g_lds = (int)value;
+            return UAM_OK;
         case UAM_OPT_K8_STREAMS:
             if (value < 1 || value > 8)
                 return fail(UAM_E_INVALID, "UAM_OPT_K8_STREAMS %lld outside [1, 8]",
@@ -5428,6 +5563,9 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K3B_POINTS_PER_LANE: *value = ctx->k3b_cpl; return UAM_OK;
         case UAM_OPT_K8_TILED: *value = ctx->k8_tiled ? 1 : 0; return UAM_OK;
         case UAM_OPT_K8_STREAMS: *value = ctx->k8_nstreams; return UAM_OK;
+        case UAM_OPT_K2G_TILE_BITS: *value = ctx->k2g_tbits; return UAM_OK;
+        case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
+
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
     }
 }
@@ -5671,15 +5809,16 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
+    const int tbits = ctx->k2g_tbits;
+    const int bins = (1 << (2 * tbits)) + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const int64_t ncnt = (int64_t)G_BINS * G_NBK;
+    const int64_t ncnt = (int64_t)bins * G_NBK;
     const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
-                 b_slot = al((size_t)n_items * sizeof(GSlot)), b_psi = al((size_t)n_items * 8),
-                 b_p1 = al((size_t)P * 32);
+                 b_slot = al((size_t)n_items * sizeof(GSlot));
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_psi + b_p1, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs;
@@ -5691,13 +5830,15 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.G = G;
     kg.nseg = nseg;
     int tshift = 0;
-    while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << G_TBITS)) ++tshift;
+    while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << tbits)) ++tshift;
     kg.tshift = tshift;
+    kg.tbits = tbits;
+    kg.bins = bins;
+    const size_t ubytes = (size_t)D * ctx->kp.N * 16;
+    kg.utab_lds = ubytes <= (size_t)G_UTAB_LDS ? 1 : 0;
     kg.n_items = n_items;
     size_t o = 0;
     kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first
-    kg.psi = (double*)(w + o), o += b_psi;
-    kg.p1 = (double4*)(w + o), o += b_p1;
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
@@ -5707,28 +5848,34 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     }
+    const size_t lds_need =
+        (size_t)((kr.pwords + 3) & ~3) * 4 + (kg.utab_lds ? ubytes : 0);
+    const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+    if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
+        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<11>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<16>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        ctx->k2g_attrs = true;
+    }
     st = ktime_begin(ctx, s);
     if (st) return st;
-    // pass 1 (f64 ALU) on the side stream, beside the sort and the gathers
-    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-    hipLaunchKernelGGL(k_g_pass1, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, ctx->s2,
-                       ctx->kp, kg);
-    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
-    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(256), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
-    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(256), 0, s, kg);
-    const size_t lds = (size_t)kr.pwords * 4;
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
-    if (G <= 8)
+    // gathers in flight per lane: the whole group up to 16, else chunks (21 -> 11 + 10)
+    const int ch = G <= 8 ? 8 : G <= 11 ? 11 : G <= 16 ? 16 : G <= 22 ? 11 : 16;
+    if (ch == 8)
         hipLaunchKernelGGL(k_g_eval<8>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
-    else if (G <= 12)
-        hipLaunchKernelGGL(k_g_eval<12>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    else if (ch == 11)
+        hipLaunchKernelGGL(k_g_eval<11>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     else
         hipLaunchKernelGGL(k_g_eval<16>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
