@@ -279,7 +279,7 @@ def main():
     if last.startswith("K2g"):
         ktag = last.lower()
         kernel_name = ("K2g sequence (k_g_hist / k_scan / k_g_scatter, k_g_eval over every "
-                       "(path, group) item, k_g_final; k_g_pass1 on the side stream)")
+                       "(path, group) item with its share of pass 1, k_g_final)")
     elif last.startswith("K2s") or last == "K4s":
         ktag = last.lower()
         ev = "k_seg_eval_vol" if last == "K4s" else "k_seg_eval"
@@ -452,10 +452,12 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False):
                            "the no-fly blocks, 16-B records inside them; the algorithmic bytes "
                            "keep SURVEY's 16 B per waypoint, the information each waypoint "
                            "consumes" if packed else "16-B records"),
-         "note": "each 16-B record gather that misses L2 moves one 128-B line (PMC); the "
-                 "measured random-gather ceiling (tools/gather_ceiling.hip) bounds a kernel "
-                 "gathering in random order (K2); K2s's tile-sorted segments pass it through "
-                 "L2 reuse (l2_hit_rate), DESIGN.md §4-5"}
+         "note": "each gathered entry costs one 128-B line request: an L2 hit or a line "
+                 "from the Infinity Cache / HBM (PMC); the measured random-gather ceiling "
+                 "(tools/gather_ceiling.hip) bounds a kernel gathering in random order (K2); "
+                 "the tile-sorted forms (K2g, K2s) pass it through L2 reuse (l2_hit_rate). "
+                 "K2g's evaluation with the whole table in L2 (512^2 raster) takes 254 us of "
+                 "its ~300 us at 4096^2 (profiles/r03/k2g6), DESIGN.md §4-5"}
     return r
 
 

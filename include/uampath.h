@@ -356,7 +356,7 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
 /* Measurement (bench.py's roofline; build-defined).  uam_kernel_timing(ctx, 1) resets and
  * starts timing, 0 stops it: while on, the context records a HIP event pair on the launch
  * stream around every timed path evaluation of uam_eval_generated* -- around the whole launch
- * sequence of K2g and K2s (sorts, evaluation, output launch; K2g's pass 1 on the side stream is
+ * sequence of K2g and K2s (sorts, evaluation, output launch; K2s's side-stream sorts are
  * joined inside it), around the k_eval_pairs / k_eval_wave launch of the other forms (excluding
  * their pair order and selection launches).  uam_kernel_time waits for those events and returns
  * the summed time and the count since the last call (then resets the count).  At most 4096

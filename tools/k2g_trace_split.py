@@ -39,7 +39,7 @@ def main():
             for k, us in ev:
                 d.setdefault(k, []).append(us)
         med = {k: round(statistics.median(v), 1) for k, v in d.items()}
-        tag = {k: st[k] for k in ("group", "tbits", "lds") if k in st}
+        tag = {k: st[k] for k in ("group", "tbits", "lds", "chunk", "minw") if k in st}
         print(json.dumps({**tag, "ms": st["ms"], **med}))
 
 

@@ -2,7 +2,8 @@
 """K2g sweep (GPU box): cfg3 (4096^2 DEM + 70 no-fly shapes, 100k pairs x 5, W = 82) built once,
 then the segment-grouped evaluation timed (uam_kernel_timing: HIP events around the whole
 launch sequence, mean over --reps) for every combination of group length, sort-tile bits and
-evaluation LDS floor given.  Runs with the same group length must give
+evaluation LDS floor given (gathers-in-flight and register-cap settings of
+profiles/r03/k2g7-8 were measured with a build that had those knobs).  Runs with the same group length must give
 identical bits (the other knobs only change which lane does the work); every run is checked
 against the first run of its group length.  One JSON line per setting.
 usage: python tools/probe_k2g.py --groups 8,16 --tbits 4,6 --lds 0,32768"""
@@ -50,7 +51,7 @@ def main():
     for g in ints(a.groups):
         for tb in ints(a.tbits):
             for lds in ints(a.lds):
-                for p1 in (0,):
+                for _ in (0,):
                     e.set_option("group", g)
                     e.set_option("k2g_tile_bits", tb)
                     e.set_option("k2g_lds_floor", lds)
@@ -63,7 +64,7 @@ def main():
                     ms, n = e.kernel_time()
                     e.kernel_timing(False)
                     cost = o["cost"].clone()
-                    row = {"group": g, "tbits": tb, "lds": lds,
+                    row = {"group": g, "tbits": tb, "lds": lds, 
                            "kernel": e.last_kernel(), "ms": round(ms / n, 4),
                            "paths_per_s": round(a.pairs * D / (ms / n * 1e-3), 1)}
                     if g in first:

@@ -4566,7 +4566,7 @@ constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles o
 constexpr int G_BINS_MAX = (1 << (2 * G_TBITS_MAX)) + 1;  // + one bin for off-raster / NaN
 constexpr int G_NBK = 256;                              // partitions of the counting sort
 constexpr int G_MAXLEN = 64;                            // longest group
-constexpr int G_UTAB_LDS = 32 * 1024;                   // unit-arc table in LDS up to this size
+constexpr int G_UTAB_LDS = 48 * 1024;                   // K2g: unit-arc table (in LDS) up to this
 
 struct alignas(16) GSlot {  // 48 B per (path, group), written by one lane
     double cost;     // partial sums from +0.0 in waypoint order: Phi/N,
@@ -4583,7 +4583,7 @@ struct KGrp {
     const double* __restrict__ utab;
     int64_t n_pairs;
     int32_t P, D, W, G, nseg, tshift, tbits, bins;
-    int32_t utab_lds;              // k_g_eval stages utab in LDS (D N 16 <= G_UTAB_LDS)
+    double inv_n;                  // RN(1 / N) for Phi / N (0: divide; N > 4096)
     int64_t n_items;               // P * nseg; item i = path * nseg + group
     uint16_t* __restrict__ key;    // [n_items]
     int32_t* __restrict__ cnt;     // [bins][G_NBK] counts -> offsets
@@ -4674,13 +4674,10 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_map = s_dyn;
     const int mapw = (rs.pwords + 3) & ~3;
-    const double2* s_u = reinterpret_cast<const double2*>(s_dyn + mapw);
+    double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
     for (int i = threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
-    if (kg.utab_lds) {
-        double2* su = reinterpret_cast<double2*>(s_dyn + mapw);
-        const double2* gu = reinterpret_cast<const double2*>(kg.utab);
-        for (int i = threadIdx.x; i < kg.D * p.N; i += 256) su[i] = gu[i];
-    }
+    const double2* gu = reinterpret_cast<const double2*>(kg.utab);
+    for (int i = threadIdx.x; i < kg.D * p.N; i += 256) s_u[i] = gu[i];
     __syncthreads();
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (pos >= kg.n_items) return;
@@ -4690,8 +4687,7 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
     const int32_t q = path / kg.D, d = path - q * kg.D;
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
     const int N = p.N, W = kg.W;
-    const double2* urow = (kg.utab_lds ? s_u : reinterpret_cast<const double2*>(kg.utab)) +
-                          (int64_t)d * N;
+    const double2* urow = s_u + d * N;
     const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
     auto point = [&](int j, double& x0, double& x1) {
         if (j == 0) {
@@ -4703,54 +4699,52 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
             arc_point(pr.x, pr.y, pr.z, pr.w, u.x, u.y, x0, x1);
         }
     };
-    // this group's share of pass 1, path_pass1's arithmetic: segments p_{j-1} -> p_j for
-    // j in [max(j0, 1), j1) add to L and length; row k (segments k + 1 and k + 2) belongs to
-    // the group of waypoint k + 1
+    // this group's share of pass 1 (path_pass1's arithmetic), formed while the waypoints are
+    // generated for the gathers, each point once: segment p_{j-1} -> p_j for j in
+    // [max(j0, 1), j1) adds to L and the length; kinematic row k (segments k + 1 and k + 2)
+    // belongs to the group of waypoint k + 1, so the point after the group closes its last row
+    const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     double gL = 0.0, glen = 0.0, gk = 0.0;
-    {
-        const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
-        double px, py;
-        if (j0 == 0 && p.quirk_length) {  // get_cost's anchor term (y_0 = anchor, y_1 = p_0)
-            point(0, px, py);
-            const double ax = p.anchor_mode ? p.anchor_x : px;
-            const double ay = p.anchor_mode ? p.anchor_y : py;
-            const double dx = px - ax, dy = py - ay;
-            double s2 = 0.0;
-            s2 = s2 + dx * dx;
-            s2 = s2 + dy * dy;
-            const double n = sqrt(s2);
-            gL = gL + (ls ? n * n : n);
-        }
-        const int ja = max(j0, 1), jb = min(j1, W - 1);
-        point(ja - 1, px, py);
-        double pdx = 0.0, pdy = 0.0, pn = 0.0;
-        for (int j = ja; j <= jb; ++j) {
-            double qx, qy;
-            point(j, qx, qy);
-            const double dx = qx - px, dy = qy - py;
-            double s2 = 0.0;
-            s2 = s2 + dx * dx;
-            s2 = s2 + dy * dy;
-            const double n = sqrt(s2);  // norm_2 = sqrt(dot) (casadi_norm_2)
-            if (j < j1) {
-                glen = glen + n;
-                if (!p.quirk_length || j <= N) gL = gL + (ls ? n * n : n);
-            }
-            const double nk = ms ? n * n : n;
-            if (j >= j0 + 1 && j >= 2) {  // row k = j - 2 (problem.py:100-107)
-                double dt = 0.0;
-                dt = dt + pdx * dx;
-                dt = dt + pdy * dy;
-                double c1, c2, c3;
-                kin_row(p, pn, nk, dt, c1, c2, c3);
-                gk = gk + c1;
-                gk = gk + c2;
-                gk = gk + c3;
-            }
-            pdx = dx, pdy = dy, pn = nk, px = qx, py = qy;
-        }
+    double px, py, pdx = 0.0, pdy = 0.0, pn = 0.0;
+    point(j0 == 0 ? 0 : j0 - 1, px, py);
+    if (j0 == 0 && p.quirk_length) {  // get_cost's anchor term (y_0 = anchor, y_1 = p_0)
+        const double ax = p.anchor_mode ? p.anchor_x : px;
+        const double ay = p.anchor_mode ? p.anchor_y : py;
+        const double dx = px - ax, dy = py - ay;
+        const double n = sqrt(dx * dx + dy * dy);  // = (0 + dx dx) + dy dy: dx dx is never -0
+        gL = gL + (ls ? n * n : n);
     }
-    const double dN = (double)N;
+    auto segment = [&](int j, double qx, double qy) {
+        const double dx = qx - px, dy = qy - py;
+        const double n = sqrt(dx * dx + dy * dy);  // norm_2 = sqrt(dot) (casadi_norm_2)
+        if (j < j1) {
+            glen = glen + n;
+            if (!p.quirk_length || j <= N) gL = gL + (ls ? n * n : n);
+        }
+        const double nk = ms ? n * n : n;
+        if (j >= j0 + 1 && j >= 2) {  // row k = j - 2 (problem.py:100-107)
+            double dt = 0.0;
+            dt = dt + pdx * dx;
+            dt = dt + pdy * dy;
+            double c1, c2, c3;
+            kin_row(p, pn, nk, dt, c1, c2, c3);
+            gk = gk + c1;
+            gk = gk + c2;
+            gk = gk + c3;
+        }
+        pdx = dx, pdy = dy, pn = nk, px = qx, py = qy;
+    };
+    // Phi / N: q0 = a (1/N) and one residual step (Markstein), correctly rounded for every
+    // finite float a and 1 <= N <= 4096 (all 2^23 significands checked; the power-of-two
+    // scaling is exact in double: tests/test_host_cpu.py), so bit-equal to the division.
+    // kg.inv_n = 0 (larger N): the division itself.
+    const double dN = (double)N, yN = kg.inv_n;
+    auto over_n = [&](double a) {
+        if (yN == 0.0) return a / dN;
+        const double q0 = a * yN;
+        const double q1 = fma(fma(-q0, dN, a), yN, q0);
+        return __builtin_isinf(a) ? q0 : q1;  // -0 / N comes out +0: both add to gc alike
+    };
     double gc = 0.0, gn = 0.0;
     float hmax = -INFINITY;
     uint32_t nh = 0, off = 0;
@@ -4762,8 +4756,11 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
         for (int t = 0; t < CH; ++t) {
             const int j = jc + t;
             if (j < je) {
-                double x0, x1;
-                point(j, x0, x1);
+                double x0 = px, x1 = py;  // j = 0: p_0, generated above
+                if (j > 0) {
+                    point(j, x0, x1);
+                    segment(j, x0, x1);
+                }
                 const double fx = floor((x0 - rs.x0) * rs.inv_dx);
                 const double fy = floor((rs.y_top - x1) * rs.inv_dy);
                 if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
@@ -4793,7 +4790,7 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                 } else if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0
                     hmax = fmaxf(hmax, 0.0f);
                 } else {
-                    gc = gc + (double)__uint_as_float(r[t].x) / dN;
+                    gc = gc + over_n((double)__uint_as_float(r[t].x));
                     float terrain = __uint_as_float(r[t].z);
                     if ((full >> t) & 1u) {
                         gn = gn + (double)__uint_as_float(r[t].y);
@@ -4804,6 +4801,11 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                 }
             }
         }
+    }
+    if (j1 <= W - 1) {  // the point after the group: its last kinematic row only
+        double x0, x1;
+        point(j1, x0, x1);
+        segment(j1, x0, x1);
     }
     GSlot o;
     o.cost = gc;
@@ -4887,7 +4889,7 @@ struct uam_ctx {
     size_t ktime_n = 0;
     int k1_cpl = 2;             // K1 cells (rows) per lane: 1 = single-cell kernel, 2, 4, 8
                                 // (UAM_OPT_K1_ROWS)
-    hipStream_t s2 = nullptr;   // side stream (K2g / K2s: pass 1 and sorts beside the gathers)
+    hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
@@ -4918,12 +4920,13 @@ struct uam_ctx {
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
     int32_t last_group = 0;     // uam_last_group: waypoint-group length of the last call's sums
     int k2g_group = 21;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
-                                // (profiles/r03/k2g3, tile bits 4, pass 1 beside the gathers):
-                                // 8 0.538, 11 0.496, 16 0.457, 21 0.399, 22 0.405, 28 0.426
+                                // (profiles/r03/k2g7, tile bits 4): 12 0.463, 14 0.435,
+                                // 16 0.442, 18 0.407, 21 0.370, 24 0.395
     int k2g_tbits = 4;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
-                                // cfg3 at G = 21: 4 0.399, 5 0.410, 6 0.434 ms)
+                                // cfg3 at G = 21: 4 0.390, 5 0.381 (k2g7), 6 0.434 ms (k2g3))
     int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
-                                // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR)
+                                // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
+                                // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
 
 };
 
@@ -5806,6 +5809,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (G < 1 || G > G_MAXLEN || !kr.pmap || ko.cells || ko.g_rows || D > 16) return 0;
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
+    const size_t ubytes = (size_t)D * ctx->kp.N * 16;  // the unit-arc rows, staged in LDS
+    if (ubytes > (size_t)G_UTAB_LDS) return 0;
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
@@ -5834,8 +5839,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.tshift = tshift;
     kg.tbits = tbits;
     kg.bins = bins;
-    const size_t ubytes = (size_t)D * ctx->kp.N * 16;
-    kg.utab_lds = ubytes <= (size_t)G_UTAB_LDS ? 1 : 0;
+    kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
     kg.n_items = n_items;
     size_t o = 0;
     kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first
@@ -5843,21 +5847,14 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.key = (uint16_t*)(w + o);
-    if (!ctx->s2) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
-    const size_t lds_need =
-        (size_t)((kr.pwords + 3) & ~3) * 4 + (kg.utab_lds ? ubytes : 0);
+    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes;
     const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+    using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
+    static const EvalFn evals[3] = {k_g_eval<8>, k_g_eval<11>, k_g_eval<16>};
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
-        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<8>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<11>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIP_TRY(hipFuncSetAttribute((const void*)k_g_eval<16>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        for (EvalFn f : evals)
+            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
         ctx->k2g_attrs = true;
     }
     st = ktime_begin(ctx, s);
@@ -5868,14 +5865,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
-    // gathers in flight per lane: the whole group up to 16, else chunks (21 -> 11 + 10)
-    const int ch = G <= 8 ? 8 : G <= 11 ? 11 : G <= 16 ? 16 : G <= 22 ? 11 : 16;
-    if (ch == 8)
-        hipLaunchKernelGGL(k_g_eval<8>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
-    else if (ch == 11)
-        hipLaunchKernelGGL(k_g_eval<11>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
-    else
-        hipLaunchKernelGGL(k_g_eval<16>, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    // gathers in flight per lane (profiles/r03/k2g7: 8 or 11 within 1% at G = 12..24; a
+    // register cap for 5-8 waves per SIMD spills and loses 20-190%, profiles/r03/k2g8)
+    const int ch = G <= 8 ? 0 : G <= 11 ? 1 : G <= 16 ? 0 : G <= 22 ? 1 : 2;
+    hipLaunchKernelGGL(evals[ch], ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
