@@ -69,7 +69,6 @@ def parse():
                     help="threads for the CPU baseline (0: the box's CPU share, "
                          "OMP_NUM_THREADS capped by the affinity mask and 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", type=int, default=0, help="uam_set_tuning kernel variant")
     ap.add_argument("--group", type=int, default=None,
                     help="K2g waypoints per group (uam_set_option UAM_OPT_GROUP; 0 = K2s); "
                          "default: the library's")
@@ -116,7 +115,7 @@ def main():
     from uam_path_planning_amd import distributed as udist
     build.build_library()
     from uam_path_planning_amd.arcs import arc_table
-    from uam_path_planning_amd.engine import CostRaster, Engine, RiskVolume, VolumeGeo
+    from uam_path_planning_amd.engine import CostRaster, Engine, VolumeGeo
     from uam_path_planning_amd.geometry import compile_map
     from uam_path_planning_amd.scenario import (CONFIGS, build_region_map, canonical_params,
                                                 canonical_spec, displacements, layer_weights,
@@ -187,6 +186,22 @@ def main():
             raster = eng.raster_build(geo, dem_dev, summary=False)
             torch.cuda.synchronize()
             setup["raster_build_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+            # K1 alone, warm (a second build into the same records), HIP events on its stream:
+            # 4 B of DEM read + 16 B of record written per cell
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            eng.raster_build(geo, dem_dev, out=raster.rec, summary=False)
+            e1.record()
+            torch.cuda.synchronize()
+            k1_ms = e0.elapsed_time(e1)
+            cells = geo.nx * geo.ny
+            setup["raster_build"] = {
+                "cells": cells, "k1_ms": round(k1_ms, 4),
+                "cells_per_s": round(cells / (k1_ms * 1e-3), 1), "bytes_per_cell": 20,
+                "k1_frac_of_hbm": round(20 * cells / (k1_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)}
+            if "tiles_ingest_s" in setup:
+                setup["raster_build"]["tiles_ingest_plus_k1_ms"] = round(
+                    setup["tiles_ingest_s"] * 1e3 + k1_ms, 3)
             if volume_mode:
                 t2 = time.perf_counter()
                 volume = eng.volume_build(raster, cfg["nz"], cfg["z0"], cfg["dz"],
@@ -199,10 +214,10 @@ def main():
             if volume_mode:
                 vg = VolumeGeo(R, R, cfg["nz"], geo.x0, geo.y_top, geo.dx, geo.dy, cfg["z0"],
                                cfg["dz"])
-                volume = RiskVolume(vg, eng.empty((R, R, cfg["nz"], 4), torch.int32))
+                volume = eng.volume_alloc(vg)
         if world > 1:
             dist.barrier()
-            table = volume.vox if volume_mode else raster.rec
+            table = volume.buf if volume_mode else raster.rec
             secs = udist.broadcast_raster(table, src=0, engine=eng if rccl else None)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = table.numel() * 4
@@ -229,8 +244,6 @@ def main():
     P = Q * D
     outs = eng.outputs(P, W, n_pairs=Q)
     o = outs[0]
-    if args.variant:
-        eng.set_tuning(args.variant)
     if args.group is not None:
         eng.set_option("group", args.group)
 
@@ -264,7 +277,7 @@ def main():
     k_total, k_launches = eng.kernel_time()
     eng.kernel_timing(False)
     step_ev_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    # multi-launch variants (K2b / K2t, variant 1) are not bracketed: their step time stands in
+    # every evaluation form is bracketed once per call; the step time stands in otherwise
     kern_timed = k_launches == args.steps
     kern_ms = k_total / k_launches if kern_timed else step_ev_ms
     if world > 1:
@@ -280,15 +293,12 @@ def main():
         ktag = last.lower()
         kernel_name = ("K2g sequence (k_g_hist / k_scan / k_g_scatter, k_g_eval over every "
                        "(path, group) item with its share of pass 1, k_g_final)")
-    elif last.startswith("K2s") or last == "K4s":
+    elif last.startswith("K2s"):
         ktag = last.lower()
-        ev = "k_seg_eval_vol" if last == "K4s" else "k_seg_eval"
-        kernel_name = (f"{last} sequence (k_seg_hist / k_scan / k_seg_scatter, {ev}<FIRST> "
-                       f"fused with pass 1, {ev}, k_seg_final)")
+        kernel_name = (f"{last} sequence (k_seg_hist / k_scan / k_seg_scatter, k_seg_eval<FIRST> "
+                       f"fused with pass 1, k_seg_eval, k_seg_final)")
     else:
         ktag = "wave" if wave else ("raster+skip" if skip else mode)
-        if raster_mode and not skip and not wave:
-            ktag += f"-v{args.variant or 2}"
         kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
                        f"k_eval_pairs<{ktag}>")
     pkey = f"{args.workload}:{mode}:R{R}:Q{Q}:{ktag}"
@@ -303,12 +313,12 @@ def main():
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
-                                   packed=last in ("K2s+pack", "K2g+pack"))
+                                   packed=last in ("K2s+pack", "K2g+pack"), volume=volume_mode)
     roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
                                     "launch of the kernel (K2g / K2s: around the whole launch "
                                     "sequence), on its launch stream (uam_kernel_timing)"
                                     if kern_timed else
-                                    "torch events around the whole step (multi-launch variant)")
+                                    "torch events around the whole step")
     roofline["library_kernel"] = last
     group = eng.last_group()   # the sum order the library used (0 = sequential)
     roofline["sum_group"] = group
@@ -423,14 +433,15 @@ def main():
         dist.destroy_process_group()
 
 
-def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False):
+def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False):
     """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
-    definition used in SURVEY, DESIGN §4 and here): one 16-B record gather per waypoint + 16 B
-    of outputs per path = 16 W + 16 B/path.  `traffic`: L2->fabric bytes per launch of the same
+    definition used in SURVEY, DESIGN §4 and here): raster, one 16-B record gather per waypoint
+    + 16 B of outputs per path = 16 W + 16 B/path; volume, one 8-B voxel {risk, psi_nfz} + a
+    4-B DEM per waypoint + 16 B of outputs = 12 W + 16.  `traffic`: L2->fabric bytes per launch of the same
     kernel from this build's rocprofv3 PMC passes (tools/pmc_traffic.py ->
     profiles/traffic.json; 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM), which
     include Infinity-Cache hits: they are not proven DRAM bytes."""
-    bytes_per_path = 16 * W + 16
+    bytes_per_path = (12 if volume else 16) * W + 16
     launch_bytes = bytes_per_path * P
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
     traffic = prof.get("l2_fabric_bytes_per_launch")
@@ -441,14 +452,19 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False):
          "traffic_source": prof.get("source"),
          "kernel": kernel_name, "kernel_ms": round(kern_ms, 4),
          "algorithmic_bytes_per_path": bytes_per_path,
-         "algorithmic_bytes_def": "SURVEY.md §8(d): 16 B record gather per waypoint + 16 B "
-                                  "output per path (16 W + 16)",
+         "algorithmic_bytes_def": ("SURVEY.md §8(d), 3-D: 8-B voxel {risk, psi_nfz} + 4-B DEM "
+                                   "per waypoint + 16 B output per path (12 W + 16)" if volume
+                                   else "SURVEY.md §8(d): 16 B record gather per waypoint + "
+                                   "16 B output per path (16 W + 16)"),
          "algorithmic_bytes_per_launch": launch_bytes,
          "traffic_over_algorithmic": round(traffic / launch_bytes, 2) if traffic else None,
          "l2_hit_rate": prof.get("l2_hit_rate"),
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
-         "record_source": ("packed (uam_raster_pack): 8-B {phi, terrain} entries outside "
+         "record_source": ("8-B voxels {risk, psi_nfz} + the 8-B column plane {terrain, "
+                           "flags} (uam_volume_shape): 16 B requested per waypoint, 12 B of "
+                           "them information (the flags word carries the no-fly bit)" if volume
+                           else "packed (uam_raster_pack): 8-B {phi, terrain} entries outside "
                            "the no-fly blocks, 16-B records inside them; the algorithmic bytes "
                            "keep SURVEY's 16 B per waypoint, the information each waypoint "
                            "consumes" if packed else "16-B records"),

@@ -69,8 +69,8 @@ enum {
 enum { UAM_MODE_ANALYTIC = 0, UAM_MODE_RASTER = 1, UAM_MODE_VOLUME = 2 };
 
 /* record flag bits (record = {float phi, float psi_nfz, float dem, uint32 flags}; a volume
- * voxel = {float risk, float psi_nfz, float terrain, uint32 flags}) */
-enum { UAM_FLAG_NFZ = 1u, UAM_FLAG_MASK = 2u, UAM_FLAG_NODATA = 4u, UAM_FLAG_BELOW_TERRAIN = 8u };
+ * column = {float terrain, uint32 flags}) */
+enum { UAM_FLAG_NFZ = 1u, UAM_FLAG_MASK = 2u, UAM_FLAG_NODATA = 4u };
 
 typedef struct uam_ctx uam_ctx;
 typedef void* uam_stream; /* hipStream_t */
@@ -120,9 +120,11 @@ typedef struct {
                               (dem > thr) */
 } uam_raster_desc;
 
-/* 3-D risk volume (BASELINE config 5; no reference counterpart): the raster's x/y grid
- * times nz altitude layers [z0 + iz*dz, z0 + (iz+1)*dz) in metres; voxels [ny][nx][nz]
- * (layer fastest), 16 bytes each; iz = floor((z - z0) * (1/dz)). */
+/* 3-D risk volume (BASELINE config 5; no reference counterpart; SURVEY §8(d)'s layout): the
+ * raster's x/y grid times nz altitude layers [z0 + iz*dz, z0 + (iz+1)*dz) in metres,
+ * iz = floor((z - z0) * (1/dz)).  One device buffer (uam_volume_shape): 8-B voxels
+ * {float risk, float psi_nfz} [ny][nx][nz] (layer fastest), then at col_offset the 8-B column
+ * plane {float terrain (+0 for nodata), uint32 flags} [ny][nx]. */
 typedef struct {
     int32_t nx, ny, nz;
     double x0, y_top, dx, dy;
@@ -190,6 +192,14 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
 int uam_dem_mosaic(uam_ctx* ctx, const float* tiles_dev, int32_t n_tiles, int32_t th,
                    int32_t tw, const int32_t* xoff_dev, const int32_t* yoff_dev, float* dem_dev,
                    int32_t nx, int32_t ny, uam_stream stream);
+/* The mosaic's source tiles (data_manager.py:11-17 over mergeLL.vrt:1-10; build-defined host
+ * reader): n_tiles GeoTIFF files (classic little-endian TIFF, one Float32 band in strips, no
+ * predictor, uncompressed or deflate), each th x tw, read on up to n_threads host threads
+ * (0: the machine's, at most 16) into dst [n_tiles][th][tw] host memory -- page-locked for an
+ * asynchronous copy to uam_dem_mosaic's tiles_dev.  A tile that cannot be read fails the call
+ * (UAM_E_INVALID, its path in uam_last_error). */
+int uam_read_tiles(const char* const* paths, int32_t n_tiles, int32_t th, int32_t tw, float* dst,
+                   int32_t n_threads);
 
 /* K4: pairs_dev [Q][4] (x0,y0,xf,yf), utab_dev [D][N][2] unit-arc table -> wp [Q*D][N+2][2]. */
 int uam_gen_paths(uam_ctx* ctx, const double* pairs_dev, int64_t n_pairs,
@@ -257,13 +267,18 @@ int uam_path_length(uam_ctx* ctx, const double* pts_dev, int64_t n_paths, int32_
 
 int uam_synchronize(uam_ctx* ctx, uam_stream stream);
 
-/* Config 5: build the volume from a 2-D record raster with the same x/y grid (rec2d_dev),
- * risk = phi * layer_w[iz] (layer_w_dev [nz] f64). */
+/* Bytes of the volume buffer (256-B aligned sections) and the column plane's byte offset. */
+int uam_volume_shape(const uam_volume_desc* desc, int64_t* bytes, int64_t* col_offset);
+/* Config 5: build the volume (vol_dev: uam_volume_shape bytes, 256-B aligned) from a 2-D record
+ * raster with the same x/y grid (rec2d_dev): risk = phi * layer_w[iz] (f64 product rounded to
+ * f32; layer_w_dev [nz] f64), psi_nfz of the column; the column plane holds the column's DEM
+ * (+0 for nodata) and its NFZ / MASK / NODATA flags. */
 int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* desc, const void* rec2d_dev,
                      const double* layer_w_dev, void* vol_dev, uam_stream stream);
 /* Config 5 path evaluation: pairs6_dev [Q][6] = (x0, y0, z0, xf, yf, zf) (km, km, m); x/y
  * candidates as uam_eval_generated, altitude z_j = z0 + (zf - z0) * (j / (N+1)); cost =
- * (N+1) L + sum_j risk(voxel_j) / N.  D <= 16. */
+ * (N+1) L + sum_j risk(voxel_j) / N; min_clearance = min_j (z_j - terrain of the column);
+ * below_terrain counts waypoints whose layer centre z0 + (iz + 0.5) dz lies below it.  D <= 16. */
 int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);

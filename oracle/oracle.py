@@ -233,16 +233,19 @@ class Oracle:
 
     # -- volume (config 5) -----------------------------------------------------------------
     def eval_paths3d(self, wp3, vdesc, vol, want_cells=False):
+        """vol = (voxels [ny, nx, nz, 2], columns [ny, nx, 2]) as volume_build returns them."""
         W = self.N + 2
         wp3 = np.ascontiguousarray(wp3, dtype=np.float64).reshape(-1, W, 3)
         P = wp3.shape[0]
-        vol = np.ascontiguousarray(vol, dtype=np.float32)
+        vox = np.ascontiguousarray(vol[0], dtype=np.float32)
+        cols = np.ascontiguousarray(vol[1], dtype=np.float32)
         out = {k: np.zeros(P) for k in ("cost", "lq", "length", "kin", "nfz", "min_clearance")}
         for k in ("nfz_hits", "offmap", "below"):
             out[k] = np.zeros(P, np.int32)
         cells = np.zeros((P, W), np.int32) if want_cells else None
         lib().orc_eval_paths3d(ctypes.byref(self.g), ctypes.byref(self.p), ctypes.byref(vdesc),
-                               _ptr(vol, _f32p), _ptr(wp3, _f64p), ctypes.c_int64(P),
+                               _ptr(vox, _f32p), _ptr(cols, _f32p), _ptr(wp3, _f64p),
+                               ctypes.c_int64(P),
                                _ptr(out["cost"], _f64p), _ptr(out["lq"], _f64p),
                                _ptr(out["length"], _f64p), _ptr(out["kin"], _f64p),
                                _ptr(out["nfz"], _f64p), _ptr(out["nfz_hits"], _i32p),
@@ -318,12 +321,14 @@ def volume_desc(nx, ny, nz, x0, y_top, dx, dy, z0, dz):
 
 
 def volume_build(vdesc, rec2, layer_w):
+    """(voxels [ny, nx, nz, 2] {risk, psi_nfz}, columns [ny, nx, 2] {terrain, flags bits})"""
     rec2 = np.ascontiguousarray(rec2, dtype=np.float32)
     lw = np.ascontiguousarray(layer_w, dtype=np.float64)
-    vol = np.zeros((vdesc.ny, vdesc.nx, vdesc.nz, 4), dtype=np.float32)
+    vox = np.zeros((vdesc.ny, vdesc.nx, vdesc.nz, 2), dtype=np.float32)
+    cols = np.zeros((vdesc.ny, vdesc.nx, 2), dtype=np.float32)
     lib().orc_volume_build(ctypes.byref(vdesc), _ptr(rec2, _f32p), _ptr(lw, _f64p),
-                           _ptr(vol, _f32p))
-    return vol
+                           _ptr(vox, _f32p), _ptr(cols, _f32p))
+    return vox, cols
 
 
 def gen_paths3d(pairs6, utab):

@@ -466,28 +466,28 @@ int orc_argmin(const double* v, int64_t groups, int32_t G, int32_t take_sqrt, in
 
 /* ---- volume mode (BASELINE config 5; no reference counterpart) --------------------------
  * Restates the build's own definition (include/uampath.h uam_volume_build /
- * uam_eval_generated3d): voxel [ny][nx][nz] {risk, psi_nfz, terrain, flags}. */
-#define ORC_FLAG_BELOW 8u
+ * uam_eval_generated3d): voxels [ny][nx][nz] {risk, psi_nfz}, columns [ny][nx]
+ * {terrain (0 on nodata), flags}; a waypoint is below the terrain when its layer centre
+ * z0 + (iz + 0.5) dz is. */
 
 typedef struct {
     int32_t nx, ny, nz;
     double x0, y_top, dx, dy, z0, dz;
 } orc_volume;
 
-int orc_volume_build(const orc_volume* v, const float* rec2, const double* layer_w, float* vol) {
+int orc_volume_build(const orc_volume* v, const float* rec2, const double* layer_w, float* vox,
+                     float* cols) {
     for (int64_t col = 0; col < (int64_t)v->nx * v->ny; ++col) {
         uint32_t f2;
         memcpy(&f2, &rec2[4 * col + 3], 4);
         float terrain = (f2 & ORC_FLAG_NODATA) ? 0.0f : rec2[4 * col + 2];
+        uint32_t fl = f2 & (ORC_FLAG_NFZ | ORC_FLAG_MASK | ORC_FLAG_NODATA);
+        cols[2 * col] = terrain;
+        memcpy(&cols[2 * col + 1], &fl, 4);
         for (int iz = 0; iz < v->nz; ++iz) {
-            int64_t o = (col * v->nz + iz) * 4;
-            double hc = v->z0 + ((double)iz + 0.5) * v->dz;
-            uint32_t fl = f2 & (ORC_FLAG_NFZ | ORC_FLAG_MASK | ORC_FLAG_NODATA);
-            if (hc < (double)terrain) fl |= ORC_FLAG_BELOW;
-            vol[o + 0] = (float)((double)rec2[4 * col] * layer_w[iz]);
-            vol[o + 1] = rec2[4 * col + 1];
-            vol[o + 2] = terrain;
-            memcpy(&vol[o + 3], &fl, 4);
+            int64_t o = (col * v->nz + iz) * 2;
+            vox[o + 0] = (float)((double)rec2[4 * col] * layer_w[iz]);
+            vox[o + 1] = rec2[4 * col + 1];
         }
     }
     return 0;
@@ -524,7 +524,8 @@ int orc_gen_paths3d(const double* pairs6, int64_t Q, const double* utab, int32_t
 }
 
 int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v,
-                     const float* vol, const double* wp3, int64_t P, double* cost, double* lq,
+                     const float* vox, const float* cols, const double* wp3, int64_t P,
+                     double* cost, double* lq,
                      double* length, double* kin, double* nfz, int32_t* hits, double* minclr,
                      int32_t* offmap, int32_t* below, int32_t* cells) {
     const int N = p->N, W = N + 2;
@@ -559,16 +560,18 @@ int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v
                 if (cells) cells[pi * W + j] = -1;
                 continue;
             }
-            int64_t vi = ((int64_t)fy * v->nx + (int64_t)fx) * v->nz + (int64_t)fz;
+            int64_t ci = (int64_t)fy * v->nx + (int64_t)fx;
+            int64_t vi = ci * v->nz + (int64_t)fz;
             if (cells) cells[pi * W + j] = (int32_t)vi;
-            const float* r = vol + 4 * vi;
+            const float* r = vox + 2 * vi;
+            const float terrain = cols[2 * ci];
             uint32_t fl;
-            memcpy(&fl, &r[3], 4);
+            memcpy(&fl, &cols[2 * ci + 1], 4);
             c = c + (double)r[0] / (double)N;
             ns = ns + (double)r[1];
             nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
-            bel += (fl & ORC_FLAG_BELOW) ? 1 : 0;
-            cm = fmin(cm, z[3 * j + 2] - (double)r[2]);
+            bel += (v->z0 + (fz + 0.5) * v->dz < (double)terrain) ? 1 : 0;
+            cm = fmin(cm, z[3 * j + 2] - (double)terrain);
         }
         if (cost) cost[pi] = c;
         if (lq) lq[pi] = lq2;

@@ -148,8 +148,8 @@ def test_cfg5_volume_1024x1024x64(eng, oracle_mod):
                                 cfg["dz"])
     rec2 = _np(r2.rec).view(np.float32)
     ref_vol = oracle_mod.volume_build(vd, rec2, lw)
-    vox = _np(vol.vox)
-    np.testing.assert_array_equal(vox, ref_vol.view(np.int32))      # all 67M voxels
+    np.testing.assert_array_equal(_np(vol.vox), ref_vol[0].view(np.int32))  # all 67M voxels
+    np.testing.assert_array_equal(_np(vol.cols), ref_vol[1].view(np.int32))
     pairs = random_pairs3d(Q, seed=0)
     ut = arc_table(N, displacements(D))
 

@@ -512,7 +512,17 @@ def test_volume_mode_vs_oracle(eng, oracle_mod):
     vol = eng.volume_build(r2, nz, z0, dz, lw)
     vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, z0, dz)
     ref_vol = oracle_mod.volume_build(vd, _np(r2.rec).view(np.float32), lw)
-    np.testing.assert_array_equal(_np(vol.vox), ref_vol.view(np.int32))
+    np.testing.assert_array_equal(_np(vol.vox), ref_vol[0].view(np.int32))
+    np.testing.assert_array_equal(_np(vol.cols), ref_vol[1].view(np.int32))
+    # the column bitmap: 8 x 8-column blocks at 256^2, set iff a column has terrain bits != 0
+    # or the no-fly flag
+    c = ref_vol[1].view(np.uint32)
+    need = ((c[..., 0] != 0) | ((c[..., 1] & 1) != 0)).reshape(R // 8, 8, R // 8, 8)
+    need = need.any(axis=(1, 3)).reshape(-1)
+    bits = np.unpackbits(_np(vol.cbits)[: need.size // 32].view(np.uint8),
+                         bitorder="little").astype(bool)
+    np.testing.assert_array_equal(bits, need)
+    assert 0 < need.sum() < need.size
     pairs = random_pairs3d(300, seed=4, zmin=-50.0, zmax=700.0)   # some outside [0, 640)
     ut = arc_table(40, displacements(5))
     ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, ref_vol)

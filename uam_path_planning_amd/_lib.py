@@ -24,7 +24,7 @@ OPTIONS = {"group": 1, "sorted_min_paths": 2, "k2s_segments": 3, "wave_max_paths
            "k8_tiled": 9, "k8_streams": 10, "k2g_tile_bits": 11, "k2g_lds_floor": 12}
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
 MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
-FLAG_NFZ, FLAG_MASK, FLAG_NODATA, FLAG_BELOW_TERRAIN = 1, 2, 4, 8
+FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _f64p = ctypes.POINTER(ctypes.c_double)
@@ -140,6 +140,10 @@ SIGNATURES = {
     "uam_last_group": (ctypes.c_int32, [_vp]),
     "uam_set_option": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.c_int64]),
     "uam_get_option": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+    "uam_read_tiles": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32]),
+    "uam_volume_shape": (ctypes.c_int, [ctypes.POINTER(VolumeDesc), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
     "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,

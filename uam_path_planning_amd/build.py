@@ -7,7 +7,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "uampath.hip")
-SRCS = [SRC, os.path.join(HERE, "csrc", "polyproc.cpp")]
+SRCS = [SRC, os.path.join(HERE, "csrc", "polyproc.cpp"), os.path.join(HERE, "csrc", "tiles.cpp")]
 DEPS = SRCS + [os.path.join(HERE, "csrc", "polyproc.h"), os.path.join(HERE, "csrc", "ccl_tile.inc")]
 HEADER = os.path.join(ROOT, "include", "uampath.h")
 OUT = os.path.join(HERE, "lib", "libuampath.so")
@@ -40,7 +40,7 @@ def build_library(force=False, verbose=False):
     tmp = OUT + ".tmp"
     # UAM_HIPCC_EXTRA: extra flags for tuning experiments (e.g. "-DUAM_RF_WAVES=3")
     extra = os.environ.get("UAM_HIPCC_EXTRA", "").split()
-    cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", tmp, *SRCS]
+    cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", tmp, *SRCS, "-lz"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

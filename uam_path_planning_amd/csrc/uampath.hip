@@ -139,9 +139,17 @@ struct KRaster {
     int32_t pwords, phb, pwb, pnbx;
 };
 
+// volume (config 5): 8-B voxels {risk, psi_nfz} [ny][nx][nz], the 8-B column plane
+// {terrain (+0 on nodata), flags} [ny][nx] and the column bitmap (one bit per 2^cshift-square
+// block of columns: set unless every column reads {+0.0f, no NFZ}) of one buffer
+// (uam_volume_shape)
 struct KVolume {
     int32_t nx, ny, nz;
-    double x0, y_top, z0, inv_dx, inv_dy, inv_dz;
+    double x0, y_top, z0, dz, inv_dx, inv_dy, inv_dz;
+    const uint2* __restrict__ vox;
+    const uint2* __restrict__ col;
+    const uint32_t* __restrict__ cbits;
+    int32_t cshift, cnbx, cwords;
 };
 
 struct KOut {
@@ -368,26 +376,82 @@ __global__ __launch_bounds__(256) void k_dem_mosaic(const float* __restrict__ ti
 }
 
 // Volume build (config 5): voxel (ix, iy, iz), iz fastest, from the 2-D record of its column:
-// risk = Φ(column) * w[iz] (f64 product rounded to f32), psi_nfz and flags of the column,
-// terrain = column DEM (0 for nodata = sea), BELOW_TERRAIN when the layer centre
-// z0 + (iz + 0.5) dz lies below the terrain.
+// risk = Φ(column) * w[iz] (f64 product rounded to f32) and the column's psi_nfz; the layer's
+// lane 0 also writes the column plane entry {terrain = column DEM (+0 for nodata = sea),
+// NFZ | MASK | NODATA flags}.  BELOW_TERRAIN is not stored: the evaluation derives it from the
+// layer centre z0 + (iz + 0.5) dz and the column's terrain.
 __global__ __launch_bounds__(256) void k_volume_build(const uint4* __restrict__ rec2, int nx,
-                                                      int ny, int nz, double z0, double dz,
+                                                      int ny, int nz,
                                                       const double* __restrict__ layer_w,
-                                                      uint4* __restrict__ vol) {
+                                                      uint2* __restrict__ vox,
+                                                      uint2* __restrict__ col) {
     const int64_t total = (int64_t)nx * ny * nz;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total;
          v += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t col = v / nz;
-        const int iz = (int)(v - col * nz);
-        const uint4 r = rec2[col];
-        const float terrain = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
-        const double hc = z0 + ((double)iz + 0.5) * dz;
-        uint32_t fl = r.w & (UAM_FLAG_NFZ | UAM_FLAG_MASK | UAM_FLAG_NODATA);
-        if (hc < (double)terrain) fl |= UAM_FLAG_BELOW_TERRAIN;
+        const int64_t c = v / nz;
+        const int iz = (int)(v - c * nz);
+        const uint4 r = rec2[c];
         const float risk = (float)((double)__uint_as_float(r.x) * layer_w[iz]);
-        vol[v] = make_uint4(__float_as_uint(risk), r.y, __float_as_uint(terrain), fl);
+        vox[v] = make_uint2(__float_as_uint(risk), r.y);
+        if (iz == 0) {
+            const uint32_t terrain = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
+            col[c] = make_uint2(terrain, r.w & (UAM_FLAG_NFZ | UAM_FLAG_MASK | UAM_FLAG_NODATA));
+        }
     }
+}
+
+// a volume waypoint's voxel and column (in: inside the volume); r = {risk, psi, terrain, flags}.
+// With the column bitmap (sbits, in LDS) a column of a clear block is not read: it is
+// {+0.0f, 0} by the bitmap's definition, so every output is the same.
+__device__ __forceinline__ uint4 vol_fetch(const KVolume& vs, const uint32_t* sbits, double x0,
+                                           double x1, double z, bool& in, int64_t& v) {
+    const double fx = floor((x0 - vs.x0) * vs.inv_dx);
+    const double fy = floor((vs.y_top - x1) * vs.inv_dy);
+    const double fz = floor((z - vs.z0) * vs.inv_dz);
+    in = (fx >= 0.0) && (fx < (double)vs.nx) && (fy >= 0.0) && (fy < (double)vs.ny) &&
+         (fz >= 0.0) && (fz < (double)vs.nz);
+    const int32_t ix = in ? (int32_t)fx : 0, iy = in ? (int32_t)fy : 0;
+    const int64_t c = (int64_t)iy * vs.nx + ix;
+    v = c * vs.nz + (in ? (int64_t)fz : (int64_t)0);
+    const uint2 a = vs.vox[v];
+    uint2 b = make_uint2(0u, 0u);
+    const int32_t blk = (iy >> vs.cshift) * vs.cnbx + (ix >> vs.cshift);
+    if (!sbits || ((sbits[blk >> 5] >> (blk & 31)) & 1u)) b = vs.col[c];
+    return make_uint4(a.x, a.y, b.x, b.y);
+}
+
+// the column bitmap: one lane per block of 2^shift x 2^shift columns, set when a column of it
+// has terrain bits != +0.0f or the no-fly flag; the wave's ballot gives two words
+__global__ __launch_bounds__(256) void k_volume_colbits(const uint2* __restrict__ col, int nx,
+                                                        int ny, int shift, int nbx, int n_blocks,
+                                                        int n_words, uint32_t* __restrict__ out) {
+    const int32_t blk = blockIdx.x * blockDim.x + threadIdx.x;
+    bool need = false;
+    if (blk < n_blocks) {
+        const int bx = blk % nbx, by = blk / nbx;
+        const int x0 = bx << shift, y0 = by << shift;
+        const int x1 = min(x0 + (1 << shift), nx), y1 = min(y0 + (1 << shift), ny);
+        for (int iy = y0; iy < y1 && !need; ++iy)
+            for (int ix = x0; ix < x1; ++ix) {
+                const uint2 c = col[(int64_t)iy * nx + ix];
+                if (c.x != 0u || (c.y & UAM_FLAG_NFZ)) {
+                    need = true;
+                    break;
+                }
+            }
+    }
+    const uint64_t m = __ballot(need);
+    const int lane = threadIdx.x & 63;
+    const int32_t w0 = (blk - lane) >> 5;  // the wave's first block is a multiple of 64
+    if (lane == 0 && w0 < n_words) out[w0] = (uint32_t)m;
+    if (lane == 32 && w0 + 1 < n_words) out[w0 + 1] = (uint32_t)(m >> 32);
+}
+
+// below the column's terrain: the layer centre z0 + (iz + 0.5) dz of altitude z
+__device__ __forceinline__ bool vol_below(const KVolume& vs, double z, uint32_t terrain_bits) {
+    const double fz = floor((z - vs.z0) * vs.inv_dz);
+    const double hc = vs.z0 + (fz + 0.5) * vs.dz;
+    return hc < (double)__uint_as_float(terrain_bits);
 }
 
 // candidate point k (1..N) of pair pr: solver.py:121-136 restated as
@@ -671,10 +735,10 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
 constexpr int MODE_RASTER_SKIP = 4;
 
 // Volume mode (BASELINE config 5, no reference counterpart): the waypoint's voxel
-// (ix, iy as in raster mode, iz = floor((z - z0) / dz)) holds {risk f32, psi_nfz f32,
-// terrain f32, flags}; risk already carries the altitude-layer weight.
+// (ix, iy as in raster mode, iz = floor((z - z0) / dz)) holds {risk f32, psi_nfz f32} (risk
+// already carries the altitude-layer weight) and its column {terrain f32, flags}.
 template <bool GEN, int C>
-__device__ __forceinline__ void issue_chunk_vol(const KVolume& vs, const uint4* __restrict__ vol,
+__device__ __forceinline__ void issue_chunk_vol(const KVolume& vs, const uint32_t* sbits,
                                                 const PathSrc<GEN>& src, int j0, int W,
                                                 int32_t* cells, Chunk<C>& ch) {
 #pragma unroll
@@ -685,24 +749,19 @@ __device__ __forceinline__ void issue_chunk_vol(const KVolume& vs, const uint4* 
         if (j < W) {
             double x0, x1;
             src.at(j, x0, x1);
-            const double z = src.alt(j);
-            const double fx = floor((x0 - vs.x0) * vs.inv_dx);
-            const double fy = floor((vs.y_top - x1) * vs.inv_dy);
-            const double fz = floor((z - vs.z0) * vs.inv_dz);
-            const bool in = (fx >= 0.0) && (fx < (double)vs.nx) && (fy >= 0.0) &&
-                            (fy < (double)vs.ny) && (fz >= 0.0) && (fz < (double)vs.nz);
-            const int64_t v =
-                in ? ((int64_t)fy * vs.nx + (int64_t)fx) * vs.nz + (int64_t)fz : (int64_t)0;
+            bool in;
+            int64_t v;
+            ch.r[t] = vol_fetch(vs, sbits, x0, x1, src.alt(j), in, v);
             ch.in[t] = in;
-            ch.r[t] = vol[v];
             if (cells) cells[j] = in ? (int32_t)v : -1;
         }
     }
 }
 
 template <bool GEN, int C>
-__device__ __forceinline__ void consume_chunk_vol(const Chunk<C>& ch, const PathSrc<GEN>& src,
-                                                  int j0, int W, double dN, PathAcc& a) {
+__device__ __forceinline__ void consume_chunk_vol(const KVolume& vs, const Chunk<C>& ch,
+                                                  const PathSrc<GEN>& src, int j0, int W,
+                                                  double dN, PathAcc& a) {
 #pragma unroll
     for (int t = 0; t < C; ++t) {
         const int j = j0 + t;
@@ -714,8 +773,9 @@ __device__ __forceinline__ void consume_chunk_vol(const Chunk<C>& ch, const Path
         a.cost = a.cost + (double)__uint_as_float(ch.r[t].x) / dN;
         a.nsum = a.nsum + (double)__uint_as_float(ch.r[t].y);
         a.nh += (ch.r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
-        a.below += (ch.r[t].w & UAM_FLAG_BELOW_TERRAIN) ? 1 : 0;
-        a.cmin = fmin(a.cmin, src.alt(j) - (double)__uint_as_float(ch.r[t].z));
+        const double z = src.alt(j);
+        a.below += vol_below(vs, z, ch.r[t].z) ? 1 : 0;
+        a.cmin = fmin(a.cmin, z - (double)__uint_as_float(ch.r[t].z));
     }
 }
 
@@ -832,8 +892,8 @@ __device__ __forceinline__ PathAcc eval_path(const KGeom& g, const KParams& p, c
         int32_t* cells = out.cells ? out.cells + path * W : nullptr;
         for (int j0 = 0; j0 < W; j0 += C) {
             Chunk<C> ch;
-            issue_chunk_vol<GEN, C>(vs, rec, src, j0, W, cells, ch);
-            consume_chunk_vol<GEN, C>(ch, src, j0, W, dN, a);
+            issue_chunk_vol<GEN, C>(vs, sbits, src, j0, W, cells, ch);
+            consume_chunk_vol<GEN, C>(vs, ch, src, j0, W, dN, a);
         }
     } else if (MODE == UAM_MODE_ANALYTIC) {
         for (int j = 0; j < W; ++j) {
@@ -992,6 +1052,9 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
     uint32_t* s_bits = reinterpret_cast<uint32_t*>(s_bel + BP);  // gather-skip bitmap
     if (MODE == MODE_RASTER_SKIP) {
         for (int i = threadIdx.x; i < rs.swords; i += blockDim.x) s_bits[i] = rs.sum[i];
+        __syncthreads();
+    } else if (MODE == UAM_MODE_VOLUME) {  // the column bitmap
+        for (int i = threadIdx.x; i < vs.cwords; i += blockDim.x) s_bits[i] = vs.cbits[i];
         __syncthreads();
     }
 
@@ -3178,13 +3241,7 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             int64_t cell;
             if (MODE == UAM_MODE_VOLUME) {
                 const double z = src.alt(j);
-                const double fx = floor((x - vs.x0) * vs.inv_dx);
-                const double fy = floor((vs.y_top - y) * vs.inv_dy);
-                const double fz = floor((z - vs.z0) * vs.inv_dz);
-                in[t] = (fx >= 0.0) && (fx < (double)vs.nx) && (fy >= 0.0) &&
-                        (fy < (double)vs.ny) && (fz >= 0.0) && (fz < (double)vs.nz);
-                cell = in[t] ? ((int64_t)fy * vs.nx + (int64_t)fx) * vs.nz + (int64_t)fz
-                             : (int64_t)0;
+                r[t] = vol_fetch(vs, nullptr, x, y, z, in[t], cell);
                 zz[t] = z;
             } else {
                 const double fx = floor((x - rs.x0) * rs.inv_dx);
@@ -3192,8 +3249,8 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
                 in[t] = (fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) &&
                         (fy < (double)rs.ny);
                 cell = in[t] ? (int64_t)fy * rs.nx + (int64_t)fx : (int64_t)0;
+                r[t] = rec[cell];
             }
-            r[t] = rec[cell];
             if (cells) cells[j] = in[t] ? (int32_t)cell : -1;
         }
     };
@@ -3204,7 +3261,7 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             if (j >= W) continue;
             if (MODE == UAM_MODE_VOLUME) {
                 if (in[t]) {
-                    below += (r[t].w & UAM_FLAG_BELOW_TERRAIN) ? 1 : 0;
+                    below += vol_below(vs, zz[t], r[t].z) ? 1 : 0;
                     cmin = fmin(cmin, zz[t] - (double)__uint_as_float(r[t].z));
                 }
             } else {
@@ -6204,11 +6261,43 @@ int make_kvolume(const uam_volume_desc* d, KVolume* k) {
     if (!(d->dx > 0.0) || !(d->dy > 0.0) || !(d->dz > 0.0))
         return fail(UAM_E_INVALID, "dx, dy, dz must be > 0");
     k->nx = d->nx, k->ny = d->ny, k->nz = d->nz;
-    k->x0 = d->x0, k->y_top = d->y_top, k->z0 = d->z0;
+    k->x0 = d->x0, k->y_top = d->y_top, k->z0 = d->z0, k->dz = d->dz;
     k->inv_dx = 1.0 / d->dx, k->inv_dy = 1.0 / d->dy, k->inv_dz = 1.0 / d->dz;
+    k->vox = nullptr, k->col = nullptr;
     return UAM_OK;
 }
+
+// the volume buffer: voxels [ny][nx][nz] 8 B, then (256-B aligned) the column plane 8 B, then
+// (256-B aligned) the column bitmap, blocks of 8 x 8 columns doubled until it fits 8 KiB
+constexpr int VOL_CBITS_MAX = 8 * 1024 * 8;
+int64_t al256(int64_t v) { return (v + 255) & ~(int64_t)255; }
+int64_t vol_col_offset(const uam_volume_desc* d) {
+    return al256((int64_t)d->nx * d->ny * d->nz * 8);
+}
+int64_t vol_bits_offset(const uam_volume_desc* d) {
+    return vol_col_offset(d) + al256((int64_t)d->nx * d->ny * 8);
+}
+void vol_bits_dims(const uam_volume_desc* d, KVolume* k) {
+    int sh = 3;
+    auto nb = [&](int s) {
+        return (int64_t)((d->nx + (1 << s) - 1) >> s) * ((d->ny + (1 << s) - 1) >> s);
+    };
+    while (nb(sh) > VOL_CBITS_MAX) ++sh;
+    k->cshift = sh;
+    k->cnbx = (d->nx + (1 << sh) - 1) >> sh;
+    k->cwords = (int32_t)((nb(sh) + 63) / 64 * 2);  // whole waves of the bitmap kernel
+}
 }  // namespace
+
+int uam_volume_shape(const uam_volume_desc* vd, int64_t* bytes, int64_t* col_offset) {
+    KVolume kv;
+    int st = make_kvolume(vd, &kv);
+    if (st) return st;
+    vol_bits_dims(vd, &kv);
+    if (bytes) *bytes = vol_bits_offset(vd) + al256((int64_t)kv.cwords * 4);
+    if (col_offset) *col_offset = vol_col_offset(vd);
+    return UAM_OK;
+}
 
 int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
                      const double* layer_w, void* vol, uam_stream stream) {
@@ -6218,10 +6307,18 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
     if (st) return st;
     if (!rec2d || !layer_w || !vol) return fail(UAM_E_INVALID, "volume build pointer is NULL");
     DeviceGuard dg(ctx->device);
+    if ((uintptr_t)vol & 255) return fail(UAM_E_INVALID, "volume buffer not 256-B aligned");
     const int64_t total = (int64_t)vd->nx * vd->ny * vd->nz;
     hipLaunchKernelGGL(k_volume_build, dim3(grid_for(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, (const uint4*)rec2d, vd->nx, vd->ny, vd->nz, vd->z0,
-                       vd->dz, layer_w, (uint4*)vol);
+                       (hipStream_t)stream, (const uint4*)rec2d, vd->nx, vd->ny, vd->nz,
+                       layer_w, (uint2*)vol, (uint2*)((char*)vol + vol_col_offset(vd)));
+    vol_bits_dims(vd, &kv);
+    const int nblk = kv.cwords * 32;  // whole waves; blocks past the last one are clear
+    const int nreal = kv.cnbx * ((vd->ny + (1 << kv.cshift) - 1) >> kv.cshift);
+    hipLaunchKernelGGL(k_volume_colbits, dim3(grid_for(nblk, 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint2*)((char*)vol + vol_col_offset(vd)),
+                       vd->nx, vd->ny, kv.cshift, kv.cnbx, nreal, kv.cwords,
+                       (uint32_t*)((char*)vol + vol_bits_offset(vd)));
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
@@ -6238,6 +6335,11 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     st = make_kvolume(vd, &kv);
     if (st) return st;
     if (!vol || !pairs6 || !utab) return fail(UAM_E_INVALID, "pointer is NULL");
+    if ((uintptr_t)vol & 255) return fail(UAM_E_INVALID, "volume buffer not 256-B aligned");
+    kv.vox = (const uint2*)vol;
+    kv.col = (const uint2*)((const char*)vol + vol_col_offset(vd));
+    kv.cbits = (const uint32_t*)((const char*)vol + vol_bits_offset(vd));
+    vol_bits_dims(vd, &kv);
     const KOut ko = make_kout(out);
     int32_t* best_f = out ? out->best_fval_idx : nullptr;
     int32_t* best_l = out ? out->best_length_idx : nullptr;
@@ -6247,14 +6349,15 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     ctx->last_group = 0;
     if (want_wave(ctx, n_pairs * D)) {
         ctx->last_kernel = "K4w";
-        st = launch_wave(ctx, UAM_MODE_VOLUME, true, kr, kv, vol, nullptr, pairs6, utab, D,
+        st = launch_wave(ctx, UAM_MODE_VOLUME, true, kr, kv, nullptr, nullptr, pairs6, utab, D,
                          n_pairs * D, ko, best_f, best_l, (hipStream_t)stream);
         if (st < 0) return st;
         if (st == 1) return UAM_OK;
     }
     const int64_t blocks = (n_pairs + 63) / 64;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "batch too large");
-    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t));
+    const size_t lds = (size_t)64 * D * (6 * sizeof(double) + 3 * sizeof(int32_t)) +
+                       (size_t)kv.cwords * 4;
     // the raster pair order over the volume's x/y extent (results do not depend on it)
     const int32_t* order = nullptr;
     if (ctx->pair_order && n_pairs >= 4096 && n_pairs < INT32_MAX) {
@@ -6268,7 +6371,7 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
     if (st) return st;
     hipLaunchKernelGGL((k_eval_pairs<UAM_MODE_VOLUME, 1>), dim3((unsigned)blocks),
                        dim3(64 * D), lds, (hipStream_t)stream, ctx->kg, ctx->kp, kr, kv,
-                       (const uint4*)vol, pairs6, n_pairs, utab, D, ko, best_f, best_l, order);
+                       nullptr, pairs6, n_pairs, utab, D, ko, best_f, best_l, order);
     HIP_TRY(hipGetLastError());
     st = ktime_end(ctx, (hipStream_t)stream);
     if (st) return st;

@@ -6,6 +6,7 @@ visible GPU or without libuampath.so, constructing an Engine raises.
 """
 import collections
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -114,7 +115,10 @@ class VolumeGeo:
 @dataclass
 class RiskVolume:
     geo: VolumeGeo
-    vox: object = field(repr=False)     # [ny, nx, nz, 4] int32 view of 16-B voxels
+    buf: object = field(repr=False)     # the device buffer (uam_volume_shape bytes)
+    vox: object = field(repr=False)     # [ny, nx, nz, 2] int32 view: 8-B voxels {risk, psi}
+    cols: object = field(repr=False)    # [ny, nx, 2] int32 view: columns {terrain, flags}
+    cbits: object = field(repr=False, default=None)  # int32 view: the column bitmap words
 
 
 def _ptr(t):
@@ -262,6 +266,17 @@ class Engine:
             raster.packed = pk
         return raster
 
+    def read_tiles(self, paths, th, tw, n_threads=0, pinned=False):
+        """GeoTIFF tiles -> host float32 [T, th, tw] (uam_read_tiles: parallel native reader;
+        pinned=True reads into page-locked memory)."""
+        torch = _torch()
+        out = torch.empty((len(paths), th, tw), dtype=torch.float32, pin_memory=bool(pinned))
+        arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(str(p)) for p in paths])
+        _lib.check(self.lib.uam_read_tiles(arr, len(paths), int(th), int(tw),
+                                           ctypes.c_void_p(out.data_ptr()), int(n_threads)),
+                   "uam_read_tiles")
+        return out
+
     def dem_mosaic(self, tiles, xoff, yoff, nx, ny, fill=-9999.0, dem=None):
         torch = _torch()
         t = self.tensor(tiles, torch.float32)
@@ -387,6 +402,21 @@ class Engine:
         return o
 
     # -- volume (config 5) -------------------------------------------------------------
+    def volume_alloc(self, vg):
+        """An uninitialised volume buffer of VolumeGeo vg (uam_volume_shape), e.g. for a rank
+        that receives it by broadcast."""
+        torch = _torch()
+        nbytes, off = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.uam_volume_shape(ctypes.byref(vg.as_struct()), ctypes.byref(nbytes),
+                                             ctypes.byref(off)), "uam_volume_shape")
+        buf = self.empty((nbytes.value // 4,), torch.int32)   # caching allocator: 512-B aligned
+        nv = vg.nx * vg.ny * vg.nz * 2
+        vox = buf[:nv].view(vg.ny, vg.nx, vg.nz, 2)
+        nc = vg.nx * vg.ny * 2
+        cols = buf[off.value // 4: off.value // 4 + nc].view(vg.ny, vg.nx, 2)
+        bits0 = off.value // 4 + (nc * 4 + 255) // 256 * 64
+        return RiskVolume(vg, buf, vox, cols, buf[bits0:])
+
     def volume_build(self, raster, nz, z0, dz, layer_w):
         torch = _torch()
         g = raster.geo
@@ -394,11 +424,11 @@ class Engine:
         lw = self.tensor(layer_w, torch.float64).reshape(-1)
         if lw.numel() != nz:
             raise ValueError(f"layer_w has {lw.numel()} entries, nz = {nz}")
-        vox = self.empty((g.ny, g.nx, int(nz), 4), torch.int32)
+        vol = self.volume_alloc(vg)
         _lib.check(self.lib.uam_volume_build(self._ctx, ctypes.byref(vg.as_struct()),
-                                             _ptr(raster.rec), _ptr(lw), _ptr(vox),
+                                             _ptr(raster.rec), _ptr(lw), _ptr(vol.buf),
                                              self.stream), "uam_volume_build")
-        return RiskVolume(vg, vox)
+        return vol
 
     def eval_generated3d(self, pairs6, utab, volume, outputs=None):
         """pairs6 [Q, 6] = (x0, y0, z0, xf, yf, zf) (km, km, m); path p = q*D + d."""
@@ -416,7 +446,7 @@ class Engine:
             o, s = self._outputs(Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False,
                                  n_pairs=Q)
         _lib.check(self.lib.uam_eval_generated3d(
-            self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.vox), _ptr(pr), Q,
+            self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.buf), _ptr(pr), Q,
             _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated3d")
         return o
 

@@ -60,6 +60,24 @@ def read_vrt(path):
     return Vrt(w, h, gt, nodata, srcs)
 
 
+def tile_layout(vrt):
+    """-> (paths, th, tw, xoff [T] int32, yoff [T] int32) after the checks load_tiles makes on
+    the VRT (equal-sized tiles, each whole source tile placed 1:1 at its DstRect)."""
+    paths, xo, yo, shape = [], [], [], None
+    for s in vrt.sources:
+        if s.src[2:] != s.dst[2:] or s.src[:2] != (0, 0):
+            raise ValueError(f"{s.filename}: resampling / partial SrcRect not supported")
+        if shape is None:
+            shape = (s.src[3], s.src[2])
+        elif (s.src[3], s.src[2]) != shape:
+            raise ValueError("tiles of different sizes")
+        paths.append(s.filename)
+        xo.append(s.dst[0])
+        yo.append(s.dst[1])
+    th, tw = shape if shape else (1, 1)
+    return paths, th, tw, np.asarray(xo, np.int32), np.asarray(yo, np.int32)
+
+
 def load_tiles(vrt):
     """-> tiles [T][th][tw] float32, xoff [T] int32, yoff [T] int32 (tiles equal-sized, whole
     source tile placed 1:1 at its DstRect -- the layout of the reference mosaic)."""
