@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""cfg4's DEM ingest, split by phase (GPU box): the 8192^2 synthetic DEM written as 2 035
+GeoTIFF tiles + VRT (mergeLL.vrt layout), then read back as DataManager.load_dem does --
+VRT parse, native tile read (uam_read_tiles) with 1-16 threads into pageable or page-locked
+host memory, host-to-device copy, device mosaic (uam_dem_mosaic) -- and K1 on the result.
+One JSON line per setting; the files stay in the page cache between settings (as in bench.py,
+which reads the tiles it has just written).
+usage: python tools/probe_ingest.py [--R 8192] [--threads 1,4,8,16]"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--R", type=int, default=8192)
+    ap.add_argument("--threads", default="1,4,8,16")
+    a = ap.parse_args()
+    import torch
+
+    from uam_path_planning_amd.engine import Engine
+    from uam_path_planning_amd.map_generation import write_tiled_dem
+    from uam_path_planning_amd.map_generation.vrt import read_vrt, tile_layout
+    from uam_path_planning_amd.scenario import raster_geo
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    eng = Engine(0)
+    geo = raster_geo(a.R)
+    dem = synthetic_dem(a.R)
+    tdir = tempfile.mkdtemp(prefix="uam_tiles_")
+    try:
+        vrt = write_tiled_dem(dem, (geo.x0, geo.dx, 0.0, geo.y_top, 0.0, -geo.dy), tdir)
+        ref = torch.as_tensor(dem, device=eng.torch_device)
+        for pinned in (False, True):
+            for nt in [int(x) for x in a.threads.split(",")]:
+                for rep in range(2):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    v = read_vrt(vrt)
+                    paths, th, tw, xo, yo = tile_layout(v)
+                    t1 = time.perf_counter()
+                    tiles = eng.read_tiles(paths, th, tw, n_threads=nt, pinned=pinned)
+                    t2 = time.perf_counter()
+                    tdev = tiles.to(eng.torch_device)
+                    torch.cuda.synchronize()
+                    t3 = time.perf_counter()
+                    d = eng.dem_mosaic(tdev, xo, yo, v.width, v.height, fill=-9999.0)
+                    torch.cuda.synchronize()
+                    t4 = time.perf_counter()
+                    ok = bool(torch.equal(d.view(torch.int32), ref.view(torch.int32)))
+                    print(json.dumps({"pinned": pinned, "threads": nt, "rep": rep,
+                                      "tiles": len(paths), "vrt_parse_ms": round((t1 - t0) * 1e3, 2),
+                                      "read_ms": round((t2 - t1) * 1e3, 2),
+                                      "h2d_ms": round((t3 - t2) * 1e3, 2),
+                                      "mosaic_ms": round((t4 - t3) * 1e3, 2),
+                                      "total_ms": round((t4 - t0) * 1e3, 2), "identical": ok}),
+                          flush=True)
+                    del tiles, tdev, d
+    finally:
+        shutil.rmtree(tdir, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
