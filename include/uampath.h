@@ -200,6 +200,12 @@ int uam_dem_mosaic(uam_ctx* ctx, const float* tiles_dev, int32_t n_tiles, int32_
  * (UAM_E_INVALID, its path in uam_last_error). */
 int uam_read_tiles(const char* const* paths, int32_t n_tiles, int32_t th, int32_t tw, float* dst,
                    int32_t n_threads);
+/* The same tiles straight into device memory tiles_dev [n_tiles][th][tw] (uam_dem_mosaic's
+ * input): read on the thread pool in ~32 MiB chunks into two page-locked buffers the context
+ * keeps, each chunk copied on stream while the next one is read.  Returns once the last copy
+ * is enqueued (the buffers are reused after their copies complete). */
+int uam_load_tiles(uam_ctx* ctx, const char* const* paths, int32_t n_tiles, int32_t th,
+                   int32_t tw, float* tiles_dev, int32_t n_threads, uam_stream stream);
 
 /* K4: pairs_dev [Q][4] (x0,y0,xf,yf), utab_dev [D][N][2] unit-arc table -> wp [Q*D][N+2][2]. */
 int uam_gen_paths(uam_ctx* ctx, const double* pairs_dev, int64_t n_pairs,

@@ -493,6 +493,29 @@ def test_vrt_ingest_and_dem_mask(eng, oracle_mod, tmp_path, thr):
     np.testing.assert_array_equal(mask, (dem == -9999) if thr == -9999 else (dem > thr))
 
 
+def test_load_tiles_chunked(eng, tmp_path):
+    """uam_load_tiles (parallel native reader, ~32 MiB chunks through two page-locked buffers,
+    each copied while the next is read): 544 tiles of 225 x 150 = three chunks, the last one
+    partial, twice through the same context; the device tiles equal the Python reader's bit for
+    bit.  A missing tile fails loudly with its path."""
+    import os
+
+    from uam_path_planning_amd.map_generation.vrt import (load_tiles, read_vrt, tile_layout,
+                                                          write_tiled_dem)
+
+    dem = np.random.default_rng(11).standard_normal((150 * 17, 225 * 32)).astype(np.float32)
+    v = read_vrt(write_tiled_dem(dem, (0.0, 1.0, 0.0, 0.0, 0.0, -1.0), str(tmp_path)))
+    paths, th, tw, xo, yo = tile_layout(v)
+    assert len(paths) == 544
+    ref, _, _ = load_tiles(v)
+    for _ in range(2):
+        got = eng.load_tiles(paths, th, tw, n_threads=8)
+        np.testing.assert_array_equal(_np(got).view(np.int32), ref.view(np.int32))
+    os.remove(paths[300])
+    with pytest.raises(Exception, match=os.path.basename(paths[300])):
+        eng.load_tiles(paths, th, tw)
+
+
 def test_volume_mode_vs_oracle(eng, oracle_mod):
     """Config 5 (3-D risk volume, build-defined semantics): volume build and the volume path
     kernel bit-exact vs the oracle, incl. waypoints below/above the layer range."""

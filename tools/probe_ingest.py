@@ -38,6 +38,26 @@ def main():
     try:
         vrt = write_tiled_dem(dem, (geo.x0, geo.dx, 0.0, geo.y_top, 0.0, -geo.dy), tdir)
         ref = torch.as_tensor(dem, device=eng.torch_device)
+        for rep in range(3):   # uam_load_tiles: chunks through the context's page-locked ring
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            v = read_vrt(vrt)
+            paths, th, tw, xo, yo = tile_layout(v)
+            t1 = time.perf_counter()
+            tdev = eng.load_tiles(paths, th, tw)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            d = eng.dem_mosaic(tdev, xo, yo, v.width, v.height, fill=-9999.0)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            ok = bool(torch.equal(d.view(torch.int32), ref.view(torch.int32)))
+            print(json.dumps({"load_tiles": True, "rep": rep, "tiles": len(paths),
+                              "vrt_parse_ms": round((t1 - t0) * 1e3, 2),
+                              "read_and_copy_ms": round((t2 - t1) * 1e3, 2),
+                              "mosaic_ms": round((t3 - t2) * 1e3, 2),
+                              "total_ms": round((t3 - t0) * 1e3, 2), "identical": ok}),
+                  flush=True)
+            del tdev, d
         for pinned in (False, True):
             for nt in [int(x) for x in a.threads.split(",")]:
                 for rep in range(2):

@@ -142,6 +142,8 @@ SIGNATURES = {
     "uam_get_option": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "uam_read_tiles": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32]),
+    "uam_load_tiles": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32, _vp]),
     "uam_volume_shape": (ctypes.c_int, [ctypes.POINTER(VolumeDesc), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),

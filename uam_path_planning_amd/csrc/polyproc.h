@@ -4,8 +4,18 @@
 #include <cstdint>
 #include <vector>
 
+#include <functional>
+
 // thread-local uam_last_error() text (defined in uampath.hip); returns code
 int uam_fail_(int code, const char* fmt, ...);
+
+// tiles.cpp: read GeoTIFF tiles [0, n_tiles) in chunks of per_chunk on a thread pool: for chunk
+// c, slot(c) gives its destination [per_chunk][th][tw] (nullptr: fail UAM_E_HIP), then
+// filled(c, i0, i1) is called once tiles [i0, i1) are in (non-zero: stop with that code)
+int tiles_stream(const char* const* paths, int32_t n_tiles, int32_t th, int32_t tw,
+                 int32_t n_threads, int32_t per_chunk,
+                 const std::function<float*(int32_t chunk)>& slot,
+                 const std::function<int(int32_t chunk, int32_t i0, int32_t i1)>& filled);
 
 namespace uampoly {
 

@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -159,6 +161,95 @@ const char* read_tile(const char* path, int32_t th, int32_t tw, float* dst,
     return nullptr;
 }
 
+// A pool of reader threads over one call: read(i0, i1, dst) reads tiles [i0, i1) into
+// dst [i1 - i0][th][tw] with every thread of the pool, and returns once all are in.
+class TileReaderPool {
+   public:
+    TileReaderPool(const char* const* paths, int32_t th, int32_t tw, int nt)
+        : paths_(paths), th_(th), tw_(tw) {
+        for (int k = 1; k < nt; ++k) pool_.emplace_back([this] { loop(); });
+    }
+    ~TileReaderPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : pool_) t.join();
+    }
+    // false on a failed tile (first one in tile order: error())
+    bool read(int32_t i0, int32_t i1, float* dst) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            i0_ = i0, i1_ = i1, dst_ = dst;
+            next_.store(i0);
+            busy_ = (int)pool_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return busy_ == 0; });
+        return err_tile_ < 0;
+    }
+    const std::string& error() const { return err_; }
+
+   private:
+    void work() {
+        std::vector<uint8_t>& buf = tl_buf();
+        for (;;) {
+            const int32_t i = next_.fetch_add(1);
+            if (i >= i1_) return;
+            const char* e =
+                read_tile(paths_[i], th_, tw_, dst_ + (size_t)(i - i0_) * th_ * tw_, &buf);
+            if (e) {
+                std::lock_guard<std::mutex> g(emu_);
+                if (err_tile_ < 0 || i < err_tile_) {
+                    err_tile_ = i;
+                    err_ = std::string(paths_[i]) + ": " + e;
+                }
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0) done_cv_.notify_all();
+        }
+    }
+    static std::vector<uint8_t>& tl_buf() {
+        thread_local std::vector<uint8_t> b;
+        return b;
+    }
+    const char* const* paths_;
+    int32_t th_, tw_;
+    std::vector<std::thread> pool_;
+    std::mutex mu_, emu_;
+    std::condition_variable cv_, done_cv_;
+    bool quit_ = false;
+    uint64_t gen_ = 0;
+    int busy_ = 0;
+    int32_t i0_ = 0, i1_ = 0;
+    float* dst_ = nullptr;
+    std::atomic<int32_t> next_{0};
+    int32_t err_tile_ = -1;
+    std::string err_;
+};
+
+int pool_threads(int32_t n_threads, int32_t n_tiles) {
+    // default: the machine's threads up to 16 (a GPU box's CPU share)
+    int nt = n_threads > 0 ? n_threads : std::min(16, (int)std::thread::hardware_concurrency());
+    return std::max(1, std::min({nt, 64, (int)n_tiles}));
+}
+
 }  // namespace
 
 extern "C" int uam_read_tiles(const char* const* paths, int32_t n_tiles, int32_t th, int32_t tw,
@@ -166,32 +257,24 @@ extern "C" int uam_read_tiles(const char* const* paths, int32_t n_tiles, int32_t
     if (n_tiles < 0 || th <= 0 || tw <= 0 || (n_tiles > 0 && (!paths || !dst)))
         return uam_fail_(UAM_E_INVALID, "uam_read_tiles: bad arguments");
     if (n_tiles == 0) return UAM_OK;
-    // default: the machine's threads up to 16 (a GPU box's CPU share)
-    int nt = n_threads > 0 ? n_threads : std::min(16, (int)std::thread::hardware_concurrency());
-    nt = std::max(1, std::min({nt, 64, (int)n_tiles}));
-    std::atomic<int32_t> next{0};
-    std::mutex mu;
-    std::string first_err;
-    int32_t err_tile = -1;
-    auto work = [&]() {
-        std::vector<uint8_t> buf;
-        for (;;) {
-            const int32_t i = next.fetch_add(1);
-            if (i >= n_tiles) return;
-            const char* e = read_tile(paths[i], th, tw, dst + (size_t)i * th * tw, &buf);
-            if (e) {
-                std::lock_guard<std::mutex> g(mu);
-                if (err_tile < 0 || i < err_tile) {
-                    err_tile = i;
-                    first_err = std::string(paths[i]) + ": " + e;
-                }
-            }
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int k = 1; k < nt; ++k) pool.emplace_back(work);
-    work();
-    for (auto& th_ : pool) th_.join();
-    if (err_tile >= 0) return uam_fail_(UAM_E_INVALID, "%s", first_err.c_str());
+    TileReaderPool pool(paths, th, tw, pool_threads(n_threads, n_tiles));
+    if (!pool.read(0, n_tiles, dst)) return uam_fail_(UAM_E_INVALID, "%s", pool.error().c_str());
+    return UAM_OK;
+}
+
+// uam_load_tiles (uampath.hip) streams chunks through its page-locked ring with this
+int tiles_stream(const char* const* paths, int32_t n_tiles, int32_t th, int32_t tw,
+                 int32_t n_threads, int32_t per_chunk,
+                 const std::function<float*(int32_t chunk)>& slot,
+                 const std::function<int(int32_t chunk, int32_t i0, int32_t i1)>& filled) {
+    TileReaderPool pool(paths, th, tw, pool_threads(n_threads, n_tiles));
+    for (int32_t c = 0, i0 = 0; i0 < n_tiles; ++c, i0 += per_chunk) {
+        const int32_t i1 = std::min(n_tiles, i0 + per_chunk);
+        float* dst = slot(c);
+        if (!dst) return UAM_E_HIP;
+        if (!pool.read(i0, i1, dst)) return uam_fail_(UAM_E_INVALID, "%s", pool.error().c_str());
+        const int st = filled(c, i0, i1);
+        if (st) return st;
+    }
     return UAM_OK;
 }

@@ -4949,6 +4949,11 @@ struct uam_ctx {
     hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
+    // uam_load_tiles: two page-locked chunk buffers, each reused once its copy has completed
+    char* tring[2] = {nullptr, nullptr};
+    size_t tring_bytes = 0;
+    hipEvent_t tring_ev[2] = {nullptr, nullptr};
+    bool tring_used[2] = {false, false};
     void* devarena = nullptr;   // K8 device scratch arena (DevArena), created on first use
     double* d_tmtab = nullptr;  // K7 reprojection row / column tables (grow-only)
     size_t tmtab_n = 0;
@@ -5119,6 +5124,13 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     for (hipStream_t k : ctx->k8s)
         if (k) (void)hipStreamDestroy(k);
     if (ctx->pinned) pinned_arena_free(ctx->pinned);
+    for (int b = 0; b < 2; ++b) {
+        if (ctx->tring_ev[b]) {
+            (void)hipEventSynchronize(ctx->tring_ev[b]);
+            (void)hipEventDestroy(ctx->tring_ev[b]);
+        }
+        if (ctx->tring[b]) (void)hipHostFree(ctx->tring[b]);
+    }
     if (ctx->devarena) dev_arena_free(ctx->devarena);
     if (ctx->d_tmtab) (void)hipFree(ctx->d_tmtab);
     delete ctx;
@@ -5421,6 +5433,56 @@ int uam_dem_mosaic(uam_ctx* ctx, const float* tiles, int32_t n_tiles, int32_t th
                        (hipStream_t)stream, tiles, n_tiles, th, tw, xoff, yoff, dem, nx, ny);
     HIP_TRY(hipGetLastError());
     return UAM_OK;
+}
+
+int uam_load_tiles(uam_ctx* ctx, const char* const* paths, int32_t n_tiles, int32_t th,
+                   int32_t tw, float* tiles_dev, int32_t n_threads, uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    if (n_tiles < 0 || th <= 0 || tw <= 0 || (n_tiles > 0 && (!paths || !tiles_dev)))
+        return fail(UAM_E_INVALID, "uam_load_tiles: bad arguments");
+    if (n_tiles == 0) return UAM_OK;
+    DeviceGuard dg(ctx->device);
+    const size_t tile_bytes = (size_t)th * tw * 4;
+    constexpr size_t CHUNK = (size_t)32 << 20;  // per buffer: ~230 of mergeLL.vrt's tiles
+    const int32_t per = (int32_t)std::max<size_t>(1, CHUNK / tile_bytes);
+    const size_t need = (size_t)per * tile_bytes;
+    if (ctx->tring_bytes < need) {  // grow: wait for the old buffers' copies, then replace
+        for (int b = 0; b < 2; ++b) {
+            if (ctx->tring_used[b]) HIP_TRY(hipEventSynchronize(ctx->tring_ev[b]));
+            ctx->tring_used[b] = false;
+            if (ctx->tring[b]) HIP_TRY(hipHostFree(ctx->tring[b]));
+            ctx->tring[b] = nullptr;
+        }
+        ctx->tring_bytes = 0;
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(hipHostMalloc((void**)&ctx->tring[b], need));
+            if (!ctx->tring_ev[b])
+                HIP_TRY(hipEventCreateWithFlags(&ctx->tring_ev[b], hipEventDisableTiming));
+        }
+        ctx->tring_bytes = need;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    // chunk c is read into buffer c % 2 while chunk c - 1's copy runs
+    return tiles_stream(
+        paths, n_tiles, th, tw, n_threads, per,
+        [&](int32_t c) -> float* {
+            const int b = c & 1;
+            if (ctx->tring_used[b] && hipEventSynchronize(ctx->tring_ev[b]) != hipSuccess) {
+                fail(UAM_E_HIP, "uam_load_tiles: chunk copy failed");
+                return nullptr;
+            }
+            ctx->tring_used[b] = false;
+            return reinterpret_cast<float*>(ctx->tring[b]);
+        },
+        [&](int32_t c, int32_t i0, int32_t i1) -> int {
+            const int b = c & 1;
+            HIP_TRY(hipMemcpyAsync(reinterpret_cast<char*>(tiles_dev) + (size_t)i0 * tile_bytes,
+                                   ctx->tring[b], (size_t)(i1 - i0) * tile_bytes,
+                                   hipMemcpyHostToDevice, s));
+            HIP_TRY(hipEventRecord(ctx->tring_ev[b], s));
+            ctx->tring_used[b] = true;
+            return UAM_OK;
+        });
 }
 
 int uam_gen_paths(uam_ctx* ctx, const double* pairs, int64_t n_pairs, const double* utab,

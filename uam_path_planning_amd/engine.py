@@ -277,6 +277,18 @@ class Engine:
                    "uam_read_tiles")
         return out
 
+    def load_tiles(self, paths, th, tw, n_threads=0):
+        """GeoTIFF tiles -> device float32 [T, th, tw] (uam_load_tiles: the parallel reader
+        streaming ~32 MiB chunks through the context's page-locked buffers, each copied while
+        the next is read)."""
+        torch = _torch()
+        out = self.empty((len(paths), th, tw), torch.float32)
+        arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(str(p)) for p in paths])
+        _lib.check(self.lib.uam_load_tiles(self._ctx, arr, len(paths), int(th), int(tw),
+                                           _ptr(out), int(n_threads), self.stream),
+                   "uam_load_tiles")
+        return out
+
     def dem_mosaic(self, tiles, xoff, yoff, nx, ny, fill=-9999.0, dem=None):
         torch = _torch()
         t = self.tensor(tiles, torch.float32)

@@ -5,6 +5,7 @@ read_vrt() parses the XML; load_tiles() reads every source tile (geotiff.read_ge
 [T][th][tw] stack with per-tile destination offsets, which the device mosaic kernel
 (uam_dem_mosaic) places into the DEM plane.  write_tiled_dem() writes a DEM as such a tile set
 + VRT (used for the synthetic stand-in of the absent real tiles)."""
+import gc
 import os
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass, field
@@ -32,6 +33,18 @@ class Vrt:
 
 
 def read_vrt(path):
+    # a mosaic VRT holds thousands of sources: the cyclic collector adds 50 ms at random
+    # points of the parse (profiles/r03/ingest), so it is paused for it
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        return _read_vrt(path)
+    finally:
+        if gc_was:
+            gc.enable()
+
+
+def _read_vrt(path):
     root = ET.parse(path).getroot()
     w, h = int(root.get("rasterXSize")), int(root.get("rasterYSize"))
     gt_el = root.find("GeoTransform")
