@@ -162,6 +162,12 @@ typedef struct {
 typedef struct {
     int32_t n_outer, n_inner, max_backtrack, memory;
     double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
+    int32_t n_restart;       /* restarts of a path ending with sqrt(sum g^2) > delta (0: none):
+                                the obstacle holding most interior waypoints has them moved
+                                along the start-goal chord's normal to restart_margin km past
+                                its boundary, multipliers and penalty reset; the attempt with
+                                the smallest sum g^2 is returned (oracle refine_restart) */
+    double restart_margin;
 } uam_refine_params;
 
 int uam_abi_version(void);

@@ -58,14 +58,15 @@ class _RefineParams(ctypes.Structure):
                 ("c0", ctypes.c_double), ("rho", ctypes.c_double), ("c_max", ctypes.c_double),
                 ("alpha0", ctypes.c_double), ("armijo", ctypes.c_double),
                 ("theta", ctypes.c_double), ("max_step", ctypes.c_double),
-                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double)]
+                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double),
+                ("n_restart", ctypes.c_int32), ("restart_margin", ctypes.c_double)]
 
 
 def refine_params(n_outer=15, n_inner=50, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
                   alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5, memory=8, inner_tol=1e-3,
-                  delta=1e-4):
+                  delta=1e-4, n_restart=0, restart_margin=0.05):
     return _RefineParams(n_outer, n_inner, max_backtrack, memory, c0, rho, c_max, alpha0,
-                         armijo, theta, max_step, inner_tol, delta)
+                         armijo, theta, max_step, inner_tol, delta, n_restart, restart_margin)
 
 
 class _TM(ctypes.Structure):

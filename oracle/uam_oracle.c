@@ -598,6 +598,8 @@ int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v
 typedef struct {
     int32_t n_outer, n_inner, max_backtrack, memory;
     double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
+    int32_t n_restart;      /* restarts of a path that ends with sqrt(sum g^2) > delta */
+    double restart_margin;  /* km past the obstacle's boundary a restart moves waypoints */
 } orc_refine_params;
 #define RF_MAXM 8
 
@@ -960,6 +962,81 @@ static void lbfgs_dir(const double* gr, double* dr, const double* hs, const doub
     }
 }
 
+/* distance along the unit direction (ux, uy) from (x0, x1), inside shape s (every h_i < 0),
+ * to its boundary: the smallest positive root over the inequalities (each h_i linear in t,
+ * or the ellipse's quadratic) */
+static double exit_dist(const orc_geom* g, int s, double x0, double x1, double ux, double uy) {
+    double t = INFINITY;
+    for (int i = g->shape_first[s]; i < g->shape_first[s] + g->shape_count[s]; ++i) {
+        const double* q = g->ineq_par + 6 * (int64_t)i;
+        const double h = ineq_h(g, i, x0, x1);
+        double ti = INFINITY;
+        if (g->ineq_kind[i] == ORC_ELLIPSE) {
+            const double a0 = (x0 - q[0]) / q[2], b0 = (x1 - q[1]) / q[3];
+            const double da = ux / q[2], db = uy / q[3];
+            double qa = 0.0, qb = 0.0;
+            qa = qa + da * da;
+            qa = qa + db * db;
+            qb = qb + a0 * da;
+            qb = qb + b0 * db;
+            qb = 2.0 * qb;
+            const double disc = qb * qb - (4.0 * qa) * h;
+            if (qa > 0.0 && disc >= 0.0) ti = (sqrt(disc) - qb) / (2.0 * qa);
+        } else {
+            double gx, gy;
+            ineq_grad(g, i, x0, x1, &gx, &gy);
+            double rate = 0.0;
+            rate = rate + gx * ux;
+            rate = rate + gy * uy;
+            if (rate > 0.0) ti = -h / rate;
+        }
+        if (ti >= 0.0 && ti < t) t = ti;
+    }
+    return t;
+}
+
+/* Restart of a stalled path (build-defined): the obstacle holding the most interior waypoints
+ * (ties: the lowest index) has those waypoints moved across the start-goal chord's normal to
+ * restart_margin past its boundary, all to the side their mean offset from the obstacle's
+ * centre already leans to (+normal on a tie).  Returns 0 when no interior waypoint lies
+ * inside an obstacle (nothing to restart from). */
+static int refine_restart(const orc_geom* g, const orc_params* p, double* z, double margin,
+                          double* tmp) {
+    const int N = p->N, W = N + 2;
+    int best = -1, bestn = 0;
+    for (int s = 0; s < g->n_obstacles; ++s) {
+        int n = 0;
+        for (int j = 1; j <= N; ++j) n += psi(g, s, z[2 * j], z[2 * j + 1], 1, 0.0) > 0.0;
+        if (n > bestn) best = s, bestn = n;
+    }
+    if (best < 0) return 0;
+    const double cx = z[2 * (W - 1)] - z[0], cy = z[2 * (W - 1) + 1] - z[1];
+    double l2 = 0.0;
+    l2 = l2 + cx * cx;
+    l2 = l2 + cy * cy;
+    const double len = sqrt(l2);
+    if (!(len > 0.0)) return 0;
+    const double nx = -cy / len, ny = cx / len;
+    double ox = g->shape_center[2 * best], oy = g->shape_center[2 * best + 1];
+    if (isnan(ox) || isnan(oy)) ox = 0.5 * (z[0] + z[2 * (W - 1)]), oy = 0.5 * (z[1] + z[2 * (W - 1) + 1]);
+    for (int j = 0; j < W; ++j) {
+        tmp[j] = 0.0;
+        if (j >= 1 && j <= N && psi(g, best, z[2 * j], z[2 * j + 1], 1, 0.0) > 0.0)
+            tmp[j] = (z[2 * j] - ox) * nx + (z[2 * j + 1] - oy) * ny;
+    }
+    const double lean = wsum(tmp, W);
+    const double sx = lean < 0.0 ? -nx : nx, sy = lean < 0.0 ? -ny : ny;
+    for (int j = 1; j <= N; ++j) {
+        if (!(psi(g, best, z[2 * j], z[2 * j + 1], 1, 0.0) > 0.0)) continue;
+        const double t = exit_dist(g, best, z[2 * j], z[2 * j + 1], sx, sy);
+        if (!(t < INFINITY)) continue;
+        const double step = t + margin;
+        z[2 * j] = z[2 * j] + step * sx;
+        z[2 * j + 1] = z[2 * j + 1] + step * sy;
+    }
+    return 1;
+}
+
 int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* rp, double* wp,
                int64_t P, double* cost, double* infeas, int32_t* iters) {
     const int N = p->N, W = N + 2;
@@ -972,13 +1049,18 @@ int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* 
     double* hs = (double*)calloc((size_t)(m > 0 ? m : 1) * 2 * W, sizeof(double));
     double* hy = (double*)calloc((size_t)(m > 0 ? m : 1) * 2 * W, sizeof(double));
     double* tmp = (double*)malloc(sizeof(double) * W);
+    double* zbest = (double*)malloc(sizeof(double) * 2 * W);
     for (int64_t pi = 0; pi < P; ++pi) {
         double* z = wp + pi * (int64_t)W * 2;
         double *yk = y, *yo = y + 3 * N;
+        double best_inf = INFINITY, f = 0.0, inf = 0.0;
+        int32_t used = 0;
+        for (int rs = 0; rs <= (rp->n_restart > 0 ? rp->n_restart : 0); ++rs) {
+        if (rs > 0 && !refine_restart(g, p, z, rp->restart_margin, tmp)) break;
         for (int64_t i = 0; i < R; ++i) y[i] = 0.0;
         for (int k = 0; k < 2 * W; ++k) gr[k] = dr[k] = 0.0;
-        double c = rp->c0, alpha = rp->alpha0, prev = INFINITY, inf = 0.0, f = 0.0;
-        int32_t used = 0;
+        double c = rp->c0, alpha = rp->alpha0, prev = INFINITY;
+        inf = 0.0;
         for (int o = 0; o < rp->n_outer; ++o) {
             int cnt = 0, head = 0;
             double rho[RF_MAXM], gamma = 1.0, gn2 = 0.0;
@@ -1052,7 +1134,15 @@ int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* 
             prev = inf;
             if (sqrt(inf) <= rp->delta) break;
         }
-        refine_L(g, p, z, dr, 0.0, NULL, yk, yo, c, 0, &f, NULL);
+        if (rs == 0 || inf < best_inf) {  /* the best attempt by sum g^2 (first on ties) */
+            best_inf = inf;
+            memcpy(zbest, z, sizeof(double) * 2 * W);
+        }
+        if (sqrt(inf) <= rp->delta) break;
+        }
+        memcpy(z, zbest, sizeof(double) * 2 * W);
+        inf = best_inf;
+        refine_L(g, p, z, dr, 0.0, NULL, yk, yo, rp->c0, 0, &f, NULL);
         if (cost) cost[pi] = f;
         if (infeas) infeas[pi] = inf;
         if (iters) iters[pi] = used;
@@ -1063,6 +1153,7 @@ int orc_refine(const orc_geom* g, const orc_params* p, const orc_refine_params* 
     free(hs);
     free(hy);
     free(tmp);
+    free(zbest);
     return 0;
 }
 

@@ -193,3 +193,27 @@ def test_refine_mask_widths_and_region_list_walk(eng, oracle_mod):
                  big["enlargement"], big["weights"], tuple(big["x_start"]))
     wp = oracle_mod.gen_paths(random_pairs(8, seed=14), arc_table(40, displacements(5)))
     _check(eng, orc, oracle_mod, wp, n_outer=3, n_inner=8)
+
+
+def test_refine_restart_bit_exact(eng, oracle_mod):
+    """n_restart > 0 (oracle refine_restart): a path that ends above delta is restarted with
+    the waypoints inside the obstacle that holds most of them moved along the chord normal past
+    its boundary; GPU == oracle bit for bit on the cfg3 map (70 no-fly shapes: polygons and
+    balls, so both exit-distance forms run), and no path ends worse than without restarts (the
+    first attempt is the no-restart run, the best attempt is kept)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    spec = canonical_spec(nfz_polygons=64)
+    N = 40
+    orc = _setup(eng, oracle_mod, spec, N, spec["options"], spec["maxratio"], spec["maxalpha"],
+                 spec["enlargement"], spec["weights"], tuple(spec["x_start"]))
+    pairs = random_pairs(24, seed=5)
+    wp = oracle_mod.gen_paths(pairs, arc_table(N, displacements(5))).reshape(-1, N + 2, 2)
+    base = orc.refine(wp, oracle_mod.refine_params(n_outer=4, n_inner=12))
+    gpu, ref = _check(eng, orc, oracle_mod, wp, n_outer=4, n_inner=12, n_restart=2,
+                      restart_margin=0.05)
+    assert (ref["infeas"] <= base["infeas"]).all()
+    assert (ref["iters"] > base["iters"]).any()          # some paths were restarted
+    assert (ref["infeas"] < base["infeas"]).any()        # and some came out better

@@ -67,3 +67,26 @@ def test_refine_lbfgs_beats_steepest_descent(oracle_mod):
     sd = orc.refine(wp, oracle_mod.refine_params(n_outer=10, n_inner=20, memory=0))
     lb = orc.refine(wp, oracle_mod.refine_params(n_outer=10, n_inner=20, memory=8))
     assert np.sqrt(lb["infeas"]).sum() < 0.5 * np.sqrt(sd["infeas"]).sum()
+
+
+def test_refine_restart_never_worse(oracle_mod):
+    """oracle refine_restart: attempt 0 is the plain run and the best attempt by sum g^2 is
+    kept, so no path ends worse with restarts; n_restart = 0 is the plain run bit for bit."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    spec = canonical_spec(nfz_polygons=16)
+    N = 24
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                            spec["maxalpha"], spec["enlargement"], spec["weights"],
+                            anchor=tuple(spec["x_start"]))
+    wp = oracle_mod.gen_paths(random_pairs(6, seed=8),
+                              arc_table(N, displacements(5))).reshape(-1, N + 2, 2)
+    a = orc.refine(wp, oracle_mod.refine_params(n_outer=3, n_inner=8))
+    b = orc.refine(wp, oracle_mod.refine_params(n_outer=3, n_inner=8, n_restart=0,
+                                                restart_margin=0.3))
+    np.testing.assert_array_equal(a["wp"], b["wp"])
+    c = orc.refine(wp, oracle_mod.refine_params(n_outer=3, n_inner=8, n_restart=2))
+    assert (c["infeas"] <= a["infeas"]).all()
+    assert (c["iters"] >= a["iters"]).all()

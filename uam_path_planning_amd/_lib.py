@@ -75,7 +75,8 @@ class RefineParams(ctypes.Structure):
                 ("c0", ctypes.c_double), ("rho", ctypes.c_double), ("c_max", ctypes.c_double),
                 ("alpha0", ctypes.c_double), ("armijo", ctypes.c_double),
                 ("theta", ctypes.c_double), ("max_step", ctypes.c_double),
-                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double)]
+                ("inner_tol", ctypes.c_double), ("delta", ctypes.c_double),
+                ("n_restart", ctypes.c_int32), ("restart_margin", ctypes.c_double)]
 
 
 class TmParams(ctypes.Structure):

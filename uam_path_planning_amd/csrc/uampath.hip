@@ -1131,6 +1131,8 @@ __global__ __launch_bounds__(1024, MINW) void k_eval_pairs(KGeom g, KParams p, K
 struct KRefine {
     int32_t n_outer, n_inner, max_backtrack, memory;
     double c0, rho, c_max, alpha0, armijo, theta, max_step, inner_tol, delta;
+    int32_t n_restart;
+    double restart_margin;
 };
 constexpr int RF_MAXM = 8;  // L-BFGS memory bound (uam_refine_params.memory)
 
@@ -2220,6 +2222,132 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
             for (int w = 0; w < 2; ++w) any0[w] |= mk0[k][w], any1[w] |= mk1[k][w] | mk2[k][w];
         const uint64_t u00 = wave_or_u64(any0[0]), u01 = mw0 > 1 ? wave_or_u64(any0[1]) : 0ull;
         const uint64_t u10 = wave_or_u64(any1[0]), u11 = mw1 > 1 ? wave_or_u64(any1[1]) : 0ull;
+#ifdef UAM_K3B_FUSED_WALKS
+        // (measurement build, tools/r03_k3b.sh: slower than the sequential walks below,
+        // profiles/r03/k3b) The two walks interleaved: each step takes the next region shape and the next
+        // obstacle shape, issues both records' scalar loads together, then their inequalities
+        // two of each at a time, so one walk's load latency overlaps the other's loads and f64
+        // work (the sequential form paid the two walks' round trips one after the other).
+        // Each walk keeps its own shape order and each shape its inequality order, so every
+        // sum is formed exactly as body0 / body1 form it.
+        uint64_t ra[2] = {u00, u01}, ob[2] = {u10, u11};
+        int wa = 0, wb = 0;
+        for (;;) {
+            while (wa < 2 && !ra[wa]) ++wa;
+            while (wb < 2 && !ob[wb]) ++wb;
+            if (wa >= 2 && wb >= 2) break;
+            const bool hA = wa < 2, hB = wb < 2;
+            int sA = 0, sB = 0;
+            uint32_t mine = 0, m1 = 0, m2 = 0;
+            if (hA) {
+                const int bit = __builtin_ctzll(ra[wa]);
+                ra[wa] &= ra[wa] - 1;
+                sA = gr.mbase[0] + 64 * wa + bit;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k)
+                    mine |= (uint32_t)(((wa ? mk0[k][1] : mk0[k][0]) >> bit) & 1ull) << k;
+            }
+            if (hB) {
+                const int bit = __builtin_ctzll(ob[wb]);
+                ob[wb] &= ob[wb] - 1;
+                sB = gr.mbase[1] + 64 * wb + bit;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    m1 |= (uint32_t)(((wb ? mk1[k][1] : mk1[k][0]) >> bit) & 1ull) << k;
+                    m2 |= (uint32_t)(((wb ? mk2[k][1] : mk2[k][0]) >> bit) & 1ull) << k;
+                }
+            }
+            const DevShape shA = uload(g.shape, sA);  // shape 0 stands in for an absent one
+            const DevShape shB = uload(g.shape, sB);
+#ifdef UAM_K3B_DIAG
+            if (hA) dg[0] += 1, dg[1] += __builtin_popcount(mine);
+            if (hB) dg[2] += 1, dg[3] += __builtin_popcount(m1 | m2);
+#endif
+            // body0's prologue: region switch and culling
+            uint32_t needA = 0;
+            if (hA) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    if (!((mine >> k) & 1u)) continue;
+                    if (shA.region != rc[k]) {
+                        if (rc[k] >= 0) R.pen[k] = R.pen[k] + wc[k] * t[k];
+                        rc[k] = shA.region;
+                        wc[k] = shA.wreg;
+                        t[k] = 0.0;
+                    }
+                    if (!((shA.flags & SHAPE_CULL_PEN) && outside(shA.box_pen, x[k], y[k])))
+                        needA |= 1u << k;
+                }
+            }
+            // body1's prologue: culling of the psi and contains terms
+            uint32_t n1 = 0, n2 = 0;
+            if (hB) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const bool out = outside(shB.box_obs, x[k], y[k]);
+                    if (((m1 >> k) & 1u) && !((shB.flags & SHAPE_CULL_PSI) && out)) n1 |= 1u << k;
+                    if (((m2 >> k) & 1u) && !((shB.flags & SHAPE_CULL_HIT) && out)) n2 |= 1u << k;
+                }
+            }
+            const int cA = (hA && __ballot(needA != 0u)) ? shA.count : 0;
+            const int cB = (hB && __ballot((n1 | n2) != 0u)) ? shB.count : 0;
+            double rA[CPL], rB[CPL];
+            bool inB[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) rA[k] = 1.0, rB[k] = 1.0, inB[k] = true;
+            auto fA = [&](const DevIneq& q) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const double h = ineq_h(&q, x[k], y[k]);
+                    if (pen_smooth) {
+                        const double m = fmin(h - p.enlargement, 0.0);
+                        rA[k] = rA[k] * (m * m);
+                    } else {
+                        rA[k] = rA[k] * fmin(p.enlargement - h, 0.0);
+                    }
+                }
+            };
+            auto fB = [&](const DevIneq& q) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const double h = ineq_h(&q, x[k], y[k]);
+                    if (obs_smooth) {
+                        const double m = fmin(h - 0.0, 0.0);
+                        rB[k] = rB[k] * (m * m);
+                    } else {
+                        rB[k] = rB[k] * fmin(0.0 - h, 0.0);
+                    }
+                    inB[k] = inB[k] && !(h > 1e-14);
+                }
+            };
+            const int cm = max(cA, cB);
+            for (int i = 0; i < cm; ++i) {
+                // always-valid indices (inequality 0 for a finished shape), so the two scalar
+                // loads issue back to back
+                const DevIneq qa0 = uload(g.ineq, i < cA ? shA.first + i : 0);
+                const DevIneq qb0 = uload(g.ineq, i < cB ? shB.first + i : 0);
+                if (i < cA) fA(qa0);
+                if (i < cB) fB(qb0);
+            }
+            if (cA) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k)
+                    if ((needA >> k) & 1u)
+                        t[k] = shA.has_center ? t[k] + rA[k] / shA.norm_pen : t[k] + rA[k];
+            }
+            if (cB) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    if (((n1 >> k) & 1u) && !(rB[k] == 0.0)) add_term(k, rB[k]);
+                    if ((n2 >> k) & 1u) R.hit[k] = R.hit[k] || inB[k];
+                }
+            }
+        }
+        k3b_finish_pen();
+#ifdef UAM_K3B_DIAG
+        e1 = __builtin_amdgcn_s_memtime();
+#endif
+#else
 #pragma unroll
         for (int w = 0; w < 2; ++w)
             for (uint64_t bb = w ? u01 : u00; bb; bb &= bb - 1) {
@@ -2245,6 +2373,7 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
                 }
                 body1(gr.mbase[1] + 64 * w + bit, a1, a2);
             }
+#endif
     } else {
         wave_walk_cells<0, CPL>(g, slot0, body0);
         k3b_finish_pen();
@@ -2883,13 +3012,137 @@ __device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const do
 #ifndef UAM_RF_WAVES
 #define UAM_RF_WAVES 4
 #endif
+// distance along the unit direction (ux, uy) from a point inside shape sh (every h_i < 0) to
+// its boundary: the smallest positive root over its inequalities (oracle exit_dist, op for op)
+__device__ double rf_exit_dist(const KGeom& g, const DevShape& sh, double x0, double x1,
+                               double ux, double uy) {
+    double t = INFINITY;
+    for (int i = sh.first; i < sh.first + sh.count; ++i) {
+        const DevIneq& q = g.ineq[i];
+        const double h = ineq_h(&q, x0, x1);
+        double ti = INFINITY;
+        if (q.kind == UAM_INEQ_ELLIPSE) {
+            const double a0 = (x0 - q.p[0]) / q.p[2], b0 = (x1 - q.p[1]) / q.p[3];
+            const double da = ux / q.p[2], db = uy / q.p[3];
+            double qa = 0.0, qb = 0.0;
+            qa = qa + da * da;
+            qa = qa + db * db;
+            qb = qb + a0 * da;
+            qb = qb + b0 * db;
+            qb = 2.0 * qb;
+            const double disc = qb * qb - (4.0 * qa) * h;
+            if (qa > 0.0 && disc >= 0.0) ti = (sqrt(disc) - qb) / (2.0 * qa);
+        } else {
+            double gx, gy;
+            ineq_grad(&q, x0, x1, gx, gy);
+            double rate = 0.0;
+            rate = rate + gx * ux;
+            rate = rate + gy * uy;
+            if (rate > 0.0) ti = -h / rate;
+        }
+        if (ti >= 0.0 && ti < t) t = ti;
+    }
+    return t;
+}
+
+// Restart of a stalled path (oracle refine_restart): the obstacle holding the most interior
+// waypoints (ties: the lowest index) has them moved along the start-goal chord's normal to
+// margin past its boundary, to the side their mean offset from its centre leans to.  Returns
+// false (wave-uniform) when no interior waypoint lies inside an obstacle.
+__device__ bool rf_restart(const KGeom& g, double* z, int N, int lane, double margin) {
+    const int W = N + 2, S = g.n_obstacles;
+    auto inside = [&](const DevShape& sh, double x, double y) {
+        if ((sh.flags & SHAPE_CULL_PSI) && outside(sh.box_obs, x, y)) return false;  // psi +0
+        return psi(g, sh, x, y, true, 0.0) > 0.0;
+    };
+    int best = -1, bestn = 0;
+    for (int s = 0; s < S; ++s) {
+        const DevShape& sh = g.shape[s];
+        int n = 0;
+        for (int j = lane; j < W; j += 64)
+            if (j >= 1 && j <= N && inside(sh, z[2 * j], z[2 * j + 1])) ++n;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) n += __shfl_xor(n, off, 64);
+        if (n > bestn) best = s, bestn = n;
+    }
+    if (best < 0) return false;
+    const double cx = z[2 * (W - 1)] - z[0], cy = z[2 * (W - 1) + 1] - z[1];
+    double l2 = 0.0;
+    l2 = l2 + cx * cx;
+    l2 = l2 + cy * cy;
+    const double len = sqrt(l2);
+    if (!(len > 0.0)) return false;
+    const double nx = -cy / len, ny = cx / len;
+    const DevShape& sh = g.shape[best];
+    double ox = sh.cx, oy = sh.cy;
+    if (isnan(ox) || isnan(oy))
+        ox = 0.5 * (z[0] + z[2 * (W - 1)]), oy = 0.5 * (z[1] + z[2 * (W - 1) + 1]);
+    double part = 0.0;
+    bool mine[8];  // j = lane + 64 k, k < 8 (W <= 512 for the refinement)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int j = lane + 64 * k;
+        mine[k] = j >= 1 && j <= N && inside(sh, z[2 * j], z[2 * j + 1]);
+        if (j < W) part = part + (mine[k] ? (z[2 * j] - ox) * nx + (z[2 * j + 1] - oy) * ny : 0.0);
+    }
+    const double lean = wave_sum(part);
+    const double sx = lean < 0.0 ? -nx : nx, sy = lean < 0.0 ? -ny : ny;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int j = lane + 64 * k;
+        if (!mine[k]) continue;
+        const double t = rf_exit_dist(g, sh, z[2 * j], z[2 * j + 1], sx, sy);
+        if (!(t < INFINITY)) continue;
+        const double step = t + margin;
+        z[2 * j] = z[2 * j] + step * sx;
+        z[2 * j + 1] = z[2 * j + 1] + step * sy;
+    }
+    wave_sync();
+    return true;
+}
+
+// Restarts (n_restart > 0, uam_refine): attempt 0 is k_refine<false> (it also saves each path's
+// final waypoints to zlast); then per restart k_rf_push moves zlast of every path still above
+// delta and k_refine<true> runs the ALM again from it, keeping the better attempt (sum g^2,
+// first on ties) in wp / cost / infeas -- oracle orc_refine's restart loop, one launch per
+// step, so the plain refinement keeps its register budget.
+__global__ __launch_bounds__(256) void k_rf_push(KGeom g, KParams p, KRefine rf, int64_t P,
+                                                 double* __restrict__ zlast,
+                                                 const double* __restrict__ infeas,
+                                                 int32_t* __restrict__ active) {
+    extern __shared__ double rp_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int64_t path = (int64_t)blockIdx.x * wpb + wave;
+    if (path >= P) return;  // whole wave
+    if (!active[path]) return;
+    const int N = p.N, W = N + 2;
+    if (sqrt(infeas[path]) <= rf.delta) {  // converged: no further attempts
+        if (lane == 0) active[path] = 0;
+        return;
+    }
+    double* z = rp_lds + (int64_t)wave * 2 * W;
+    double* zg = zlast + path * (int64_t)W * 2;
+    for (int k = lane; k < 2 * W; k += 64) z[k] = zg[k];
+    wave_sync();
+    const bool ok = rf_restart(g, z, N, lane, rf.restart_margin);
+    if (!ok) {
+        if (lane == 0) active[path] = 0;
+        return;
+    }
+    for (int k = lane; k < 2 * W; k += 64) zg[k] = z[k];
+}
+
+template <bool RESTART>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVES))) void k_refine(
     KGeom g, KParams p, KRefine rf, double* __restrict__ wp, int64_t P, double* __restrict__ ws,
-    double* __restrict__ cost, double* __restrict__ infeas, int32_t* __restrict__ iters) {
+    double* __restrict__ cost, double* __restrict__ infeas, int32_t* __restrict__ iters,
+    double* __restrict__ zlast, const int32_t* __restrict__ active) {
     extern __shared__ double rf_lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int64_t path = (int64_t)blockIdx.x * wpb + wave;
     if (path >= P) return;  // whole wave
+    if (RESTART && !active[path]) return;
     const int N = p.N, W = N + 2, S = g.n_obstacles;
     const int m = rf.memory < 0 ? 0 : (rf.memory > RF_MAXM ? RF_MAXM : rf.memory);
     const int nmw = rf_mask_words(S);
@@ -2904,8 +3157,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVE
     double* yo = ws + path * ((int64_t)S * W + (int64_t)m * 4 * W);
     double* hs = yo + (int64_t)S * W;
     double* hy = hs + (int64_t)m * 2 * W;
+    double* zl = zlast ? zlast + path * (int64_t)W * 2 : nullptr;
     for (int k = lane; k < 2 * W; k += 64) {
-        z[k] = zg[k];
+        z[k] = RESTART ? zl[k] : zg[k];
         gr[k] = 0.0;
         dr[k] = 0.0;
     }
@@ -3044,6 +3298,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UAM_RF_WAVE
         if (inf > rf.theta * prev) c = fmin(c * rf.rho, rf.c_max);
         prev = inf;
         if (sqrt(inf) <= rf.delta) break;
+    }
+    if (zl && !RESTART)
+        for (int k = lane; k < 2 * W; k += 64) zl[k] = z[k];
+    if (RESTART) {
+        for (int k = lane; k < 2 * W; k += 64) zl[k] = z[k];  // the next restart starts here
+        const double best = infeas[path];                    // same value in every lane
+        const int32_t before = iters[path];
+        wave_sync();
+        if (!(inf < best)) {  // the earlier attempt stays
+            if (lane == 0) iters[path] = before + used;
+            return;
+        }
+        used += before;
     }
     rf_L(g, p, rp, lane, 0.0, c, false, &f, nullptr);
     for (int k = lane; k < 2 * W; k += 64) zg[k] = z[k];
@@ -6449,7 +6716,10 @@ int64_t uam_refine_workspace_bytes(uam_ctx* ctx, int64_t n_paths,
                                    const uam_refine_params* params) {
     if (!ctx || !ctx->have_params || n_paths < 0 || !params) return -1;
     const int64_t W = ctx->kp.N + 2, m = refine_memory(params);
-    return ((int64_t)ctx->kg.n_obstacles * W + m * 4 * W) * n_paths * (int64_t)sizeof(double);
+    // restarts: each path's last waypoints (2W f64) and its still-active flag
+    const int64_t rs = params->n_restart > 0 ? 2 * W * (int64_t)sizeof(double) + 4 : 0;
+    return ((int64_t)ctx->kg.n_obstacles * W + m * 4 * W) * n_paths * (int64_t)sizeof(double) +
+           rs * n_paths;
 }
 
 int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_params* rp,
@@ -6465,6 +6735,8 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
         !(rp->max_step > 0.0) || rp->memory < 0 || rp->memory > RF_MAXM)
         return fail(UAM_E_INVALID, "bad refine params (memory must be 0..%d)", RF_MAXM);
     const int64_t N = ctx->kp.N, W = N + 2;
+    if (rp->n_restart < 0 || (rp->n_restart > 0 && (W > 512 || !(rp->restart_margin >= 0.0))))
+        return fail(UAM_E_INVALID, "bad restart settings (n_restart >= 0, margin >= 0, W <= 512)");
     const int64_t per_wave =
         (6 * W + 3 * N + 2 * RF_MAXM + rf_mask_words(ctx->kg.n_obstacles) * W) *
         (int64_t)sizeof(double);
@@ -6479,14 +6751,38 @@ int uam_refine(uam_ctx* ctx, double* wp, int64_t n_paths, const uam_refine_param
     const int wpb = (int)std::min<int64_t>(4, 65536 / per_wave);
     const int64_t blocks = (n_paths + wpb - 1) / wpb;
     if (blocks > INT32_MAX) return fail(UAM_E_INVALID, "too many paths");
-    KRefine kr{rp->n_outer, rp->n_inner, rp->max_backtrack, rp->memory, rp->c0,
-               rp->rho,     rp->c_max,   rp->alpha0,        rp->armijo, rp->theta,
-               rp->max_step, rp->inner_tol, rp->delta};
+    KRefine kr{rp->n_outer,  rp->n_inner,   rp->max_backtrack, rp->memory,    rp->c0,
+               rp->rho,      rp->c_max,     rp->alpha0,        rp->armijo,    rp->theta,
+               rp->max_step, rp->inner_tol, rp->delta,         rp->n_restart, rp->restart_margin};
     DeviceGuard dg(ctx->device);
-    hipLaunchKernelGGL(k_refine, dim3((unsigned)blocks), dim3(64 * wpb),
-                       (size_t)(wpb * per_wave), (hipStream_t)stream, ctx->kg, ctx->kp, kr, wp,
-                       n_paths, (double*)workspace, cost, infeas, iters);
+    const hipStream_t s = (hipStream_t)stream;
+    double* zlast = nullptr;
+    int32_t* active = nullptr;
+    double* cbuf = cost;
+    double* ibuf = infeas;
+    int32_t* tbuf = iters;
+    if (rp->n_restart > 0) {  // restart scratch after the multipliers / L-BFGS rings
+        const int64_t base = ((int64_t)ctx->kg.n_obstacles * W + refine_memory(rp) * 4 * W) *
+                             n_paths;
+        zlast = (double*)workspace + base;
+        active = (int32_t*)(zlast + 2 * W * n_paths);
+        if (!cbuf || !ibuf || !tbuf)
+            return fail(UAM_E_INVALID, "n_restart > 0 needs the cost, infeas and iters outputs");
+        HIP_TRY(hipMemsetAsync(active, 0xff, (size_t)n_paths * 4, s));  // all active (-1)
+    }
+    hipLaunchKernelGGL(k_refine<false>, dim3((unsigned)blocks), dim3(64 * wpb),
+                       (size_t)(wpb * per_wave), s, ctx->kg, ctx->kp, kr, wp, n_paths,
+                       (double*)workspace, cbuf, ibuf, tbuf, zlast, (const int32_t*)nullptr);
     HIP_TRY(hipGetLastError());
+    for (int r = 0; r < rp->n_restart; ++r) {
+        hipLaunchKernelGGL(k_rf_push, dim3((unsigned)blocks), dim3(64 * wpb),
+                           (size_t)wpb * 2 * W * sizeof(double), s, ctx->kg, ctx->kp, kr,
+                           n_paths, zlast, (const double*)ibuf, active);
+        hipLaunchKernelGGL(k_refine<true>, dim3((unsigned)blocks), dim3(64 * wpb),
+                           (size_t)(wpb * per_wave), s, ctx->kg, ctx->kp, kr, wp, n_paths,
+                           (double*)workspace, cbuf, ibuf, tbuf, zlast, (const int32_t*)active);
+        HIP_TRY(hipGetLastError());
+    }
     return UAM_OK;
 }
 

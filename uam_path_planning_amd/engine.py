@@ -140,7 +140,7 @@ def _check_outputs(o, P, Q, W):
 # refinement defaults (same as oracle.refine_params)
 REFINE_DEFAULTS = dict(n_outer=15, n_inner=50, max_backtrack=30, c0=10.0, rho=5.0, c_max=1e8,
                        alpha0=1e-4, armijo=1e-4, theta=0.25, max_step=0.5, memory=8,
-                       inner_tol=1e-3, delta=1e-4)
+                       inner_tol=1e-3, delta=1e-4, n_restart=0, restart_margin=0.05)
 
 
 class Engine:
@@ -521,7 +521,8 @@ class Engine:
                                int(rp["memory"]), float(rp["c0"]), float(rp["rho"]),
                                float(rp["c_max"]), float(rp["alpha0"]), float(rp["armijo"]),
                                float(rp["theta"]), float(rp["max_step"]),
-                               float(rp["inner_tol"]), float(rp["delta"]))
+                               float(rp["inner_tol"]), float(rp["delta"]),
+                               int(rp["n_restart"]), float(rp["restart_margin"]))
         nbytes = self.lib.uam_refine_workspace_bytes(self._ctx, P, ctypes.byref(st))
         if nbytes < 0:
             raise _lib.UamError("uam_refine_workspace_bytes: set geometry and params first")
