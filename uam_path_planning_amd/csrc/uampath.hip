@@ -2222,132 +2222,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
             for (int w = 0; w < 2; ++w) any0[w] |= mk0[k][w], any1[w] |= mk1[k][w] | mk2[k][w];
         const uint64_t u00 = wave_or_u64(any0[0]), u01 = mw0 > 1 ? wave_or_u64(any0[1]) : 0ull;
         const uint64_t u10 = wave_or_u64(any1[0]), u11 = mw1 > 1 ? wave_or_u64(any1[1]) : 0ull;
-#ifdef UAM_K3B_FUSED_WALKS
-        // (measurement build, tools/r03_k3b.sh: slower than the sequential walks below,
-        // profiles/r03/k3b) The two walks interleaved: each step takes the next region shape and the next
-        // obstacle shape, issues both records' scalar loads together, then their inequalities
-        // two of each at a time, so one walk's load latency overlaps the other's loads and f64
-        // work (the sequential form paid the two walks' round trips one after the other).
-        // Each walk keeps its own shape order and each shape its inequality order, so every
-        // sum is formed exactly as body0 / body1 form it.
-        uint64_t ra[2] = {u00, u01}, ob[2] = {u10, u11};
-        int wa = 0, wb = 0;
-        for (;;) {
-            while (wa < 2 && !ra[wa]) ++wa;
-            while (wb < 2 && !ob[wb]) ++wb;
-            if (wa >= 2 && wb >= 2) break;
-            const bool hA = wa < 2, hB = wb < 2;
-            int sA = 0, sB = 0;
-            uint32_t mine = 0, m1 = 0, m2 = 0;
-            if (hA) {
-                const int bit = __builtin_ctzll(ra[wa]);
-                ra[wa] &= ra[wa] - 1;
-                sA = gr.mbase[0] + 64 * wa + bit;
-#pragma unroll
-                for (int k = 0; k < CPL; ++k)
-                    mine |= (uint32_t)(((wa ? mk0[k][1] : mk0[k][0]) >> bit) & 1ull) << k;
-            }
-            if (hB) {
-                const int bit = __builtin_ctzll(ob[wb]);
-                ob[wb] &= ob[wb] - 1;
-                sB = gr.mbase[1] + 64 * wb + bit;
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    m1 |= (uint32_t)(((wb ? mk1[k][1] : mk1[k][0]) >> bit) & 1ull) << k;
-                    m2 |= (uint32_t)(((wb ? mk2[k][1] : mk2[k][0]) >> bit) & 1ull) << k;
-                }
-            }
-            const DevShape shA = uload(g.shape, sA);  // shape 0 stands in for an absent one
-            const DevShape shB = uload(g.shape, sB);
-#ifdef UAM_K3B_DIAG
-            if (hA) dg[0] += 1, dg[1] += __builtin_popcount(mine);
-            if (hB) dg[2] += 1, dg[3] += __builtin_popcount(m1 | m2);
-#endif
-            // body0's prologue: region switch and culling
-            uint32_t needA = 0;
-            if (hA) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    if (!((mine >> k) & 1u)) continue;
-                    if (shA.region != rc[k]) {
-                        if (rc[k] >= 0) R.pen[k] = R.pen[k] + wc[k] * t[k];
-                        rc[k] = shA.region;
-                        wc[k] = shA.wreg;
-                        t[k] = 0.0;
-                    }
-                    if (!((shA.flags & SHAPE_CULL_PEN) && outside(shA.box_pen, x[k], y[k])))
-                        needA |= 1u << k;
-                }
-            }
-            // body1's prologue: culling of the psi and contains terms
-            uint32_t n1 = 0, n2 = 0;
-            if (hB) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const bool out = outside(shB.box_obs, x[k], y[k]);
-                    if (((m1 >> k) & 1u) && !((shB.flags & SHAPE_CULL_PSI) && out)) n1 |= 1u << k;
-                    if (((m2 >> k) & 1u) && !((shB.flags & SHAPE_CULL_HIT) && out)) n2 |= 1u << k;
-                }
-            }
-            const int cA = (hA && __ballot(needA != 0u)) ? shA.count : 0;
-            const int cB = (hB && __ballot((n1 | n2) != 0u)) ? shB.count : 0;
-            double rA[CPL], rB[CPL];
-            bool inB[CPL];
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) rA[k] = 1.0, rB[k] = 1.0, inB[k] = true;
-            auto fA = [&](const DevIneq& q) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const double h = ineq_h(&q, x[k], y[k]);
-                    if (pen_smooth) {
-                        const double m = fmin(h - p.enlargement, 0.0);
-                        rA[k] = rA[k] * (m * m);
-                    } else {
-                        rA[k] = rA[k] * fmin(p.enlargement - h, 0.0);
-                    }
-                }
-            };
-            auto fB = [&](const DevIneq& q) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const double h = ineq_h(&q, x[k], y[k]);
-                    if (obs_smooth) {
-                        const double m = fmin(h - 0.0, 0.0);
-                        rB[k] = rB[k] * (m * m);
-                    } else {
-                        rB[k] = rB[k] * fmin(0.0 - h, 0.0);
-                    }
-                    inB[k] = inB[k] && !(h > 1e-14);
-                }
-            };
-            const int cm = max(cA, cB);
-            for (int i = 0; i < cm; ++i) {
-                // always-valid indices (inequality 0 for a finished shape), so the two scalar
-                // loads issue back to back
-                const DevIneq qa0 = uload(g.ineq, i < cA ? shA.first + i : 0);
-                const DevIneq qb0 = uload(g.ineq, i < cB ? shB.first + i : 0);
-                if (i < cA) fA(qa0);
-                if (i < cB) fB(qb0);
-            }
-            if (cA) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k)
-                    if ((needA >> k) & 1u)
-                        t[k] = shA.has_center ? t[k] + rA[k] / shA.norm_pen : t[k] + rA[k];
-            }
-            if (cB) {
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    if (((n1 >> k) & 1u) && !(rB[k] == 0.0)) add_term(k, rB[k]);
-                    if ((n2 >> k) & 1u) R.hit[k] = R.hit[k] || inB[k];
-                }
-            }
-        }
-        k3b_finish_pen();
-#ifdef UAM_K3B_DIAG
-        e1 = __builtin_amdgcn_s_memtime();
-#endif
-#else
 #pragma unroll
         for (int w = 0; w < 2; ++w)
             for (uint64_t bb = w ? u01 : u00; bb; bb &= bb - 1) {
@@ -2373,7 +2247,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
                 }
                 body1(gr.mbase[1] + 64 * w + bit, a1, a2);
             }
-#endif
     } else {
         wave_walk_cells<0, CPL>(g, slot0, body0);
         k3b_finish_pen();
