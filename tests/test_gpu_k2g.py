@@ -197,12 +197,41 @@ def test_k2g_options(oracle_mod):
 
     build.build_library()
     e = Engine(0)
-    assert e.get_option("group") == 21
+    assert e.get_option("group") == 24
     for bad in (-1, 65):
         with pytest.raises(ValueError):
             e.set_option("group", bad)
     e.set_option("group", 12)
     assert e.get_option("group") == 12
+    assert e.get_option("k2g_chunk") == 0
+    for bad in (-1, 5, 7, 10, 12, 16):
+        with pytest.raises(ValueError):
+            e.set_option("k2g_chunk", bad)
+    e.set_option("k2g_chunk", 11)
+    assert e.get_option("k2g_chunk") == 11
+
+
+@pytest.mark.parametrize("chunk,group", [(6, 24), (8, 21), (8, 26), (11, 21), (11, 5), (6, 64)])
+def test_k2g_chunk_lengths(oracle_mod, chunk, group):
+    """The gathers in flight per lane (UAM_OPT_K2G_CHUNK) only change how a group's waypoints
+    are cut into load batches (full and partial chunks, groups shorter than a chunk): every
+    output equals the grouped oracle's."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    e, orc, raster, rd, rec = _case(oracle_mod, group, 80, maxalpha=0.015)
+    e.set_option("k2g_chunk", chunk)
+    e.raster_summary(raster, 0, packed=True)
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = random_pairs(2000, seed=9)
+    pairs[5] = np.nan
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec,
+                         group=group)
+    gpu = e.eval_generated(pairs, ut, raster=raster)
+    assert e.last_kernel() == "K2g+pack" and e.last_group() == group
+    _check(gpu, ref, oracle_mod, D)
 
 
 @pytest.mark.parametrize("tbits,lds", [(6, 0), (4, 49152), (3, 0)])

@@ -6,7 +6,7 @@ evaluation LDS floor given (gathers-in-flight and register-cap settings of
 profiles/r03/k2g7-8 were measured with a build that had those knobs).  Runs with the same group length must give
 identical bits (the other knobs only change which lane does the work); every run is checked
 against the first run of its group length.  One JSON line per setting.
-usage: python tools/probe_k2g.py --groups 8,16 --tbits 4,6 --lds 0,32768"""
+usage: python tools/probe_k2g.py --groups 8,16 --tbits 4,6 --lds 0,32768 --chunks 0,8"""
 import argparse
 import json
 import os
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--groups", default="8,12,16,21")
     ap.add_argument("--tbits", default="6")
     ap.add_argument("--lds", default="0")
+    ap.add_argument("--chunks", default="0")
     ap.add_argument("--pairs", type=int, default=100000)
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
@@ -51,7 +52,8 @@ def main():
     for g in ints(a.groups):
         for tb in ints(a.tbits):
             for lds in ints(a.lds):
-                for _ in (0,):
+                for chk in ints(a.chunks):
+                    e.set_option("k2g_chunk", chk)
                     e.set_option("group", g)
                     e.set_option("k2g_tile_bits", tb)
                     e.set_option("k2g_lds_floor", lds)
@@ -64,7 +66,7 @@ def main():
                     ms, n = e.kernel_time()
                     e.kernel_timing(False)
                     cost = o["cost"].clone()
-                    row = {"group": g, "tbits": tb, "lds": lds, 
+                    row = {"group": g, "tbits": tb, "lds": lds, "chunk": chk,
                            "kernel": e.last_kernel(), "ms": round(ms / n, 4),
                            "paths_per_s": round(a.pairs * D / (ms / n * 1e-3), 1)}
                     if g in first:

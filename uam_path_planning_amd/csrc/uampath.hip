@@ -4760,7 +4760,8 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
 // sums differ by rounding only (<= 1e-12 relative, tests/test_oracle_golden.py); against the
 // grouped oracle they are bit-exact.
 constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles over the raster
-constexpr int G_BINS_MAX = (1 << (2 * G_TBITS_MAX)) + 1;  // + one bin for off-raster / NaN
+// tile bins twice over (a ragged last group's items have their own) + one for off-raster / NaN
+constexpr int G_BINS_MAX = (2 << (2 * G_TBITS_MAX)) + 1;
 constexpr int G_NBK = 256;                              // partitions of the counting sort
 constexpr int G_MAXLEN = 64;                            // longest group
 constexpr int G_UTAB_LDS = 48 * 1024;                   // K2g: unit-arc table (in LDS) up to this
@@ -4780,6 +4781,9 @@ struct KGrp {
     const double* __restrict__ utab;
     int64_t n_pairs;
     int32_t P, D, W, G, nseg, tshift, tbits, bins;
+    int32_t last_bin;              // key offset of the last group's items (0: groups all G long)
+    uint64_t m_nseg, m_d;          // div_magic multipliers and shifts for / nseg and / D
+    int32_t sh_nseg, sh_d;
     double inv_n;                  // RN(1 / N) for Phi / N (0: divide; N > 4096)
     int64_t n_items;               // P * nseg; item i = path * nseg + group
     uint16_t* __restrict__ key;    // [n_items]
@@ -4835,7 +4839,10 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
         const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
         double x0, x1;
         src.at((j0 + j1 - 1) >> 1, x0, x1);
-        const uint32_t k = grp_key(kg, rs, x0, x1);
+        uint32_t k = grp_key(kg, rs, x0, x1);
+        // a ragged last group's items in their own bins: the waves then rarely mix group
+        // lengths, so k_g_eval's straight-line chunks stay wave-uniform
+        if (s == kg.nseg - 1 && k != (uint32_t)kg.bins - 1) k += kg.last_bin;
         kg.key[i] = (uint16_t)k;
         atomicAdd(&h[k], 1);
     }
@@ -4858,6 +4865,28 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
         kg.order[atomicAdd(&cur[kg.key[i]], 1)] = (int32_t)i;
 }
 
+// sqrt(x) for x in [2^-767, 2^1000]: the gfx9 lowering of sqrt(double) (rsq, then two
+// Goldschmidt / Newton corrections) without its scaling and special-value steps, which are
+// identities in that range -- so bit-equal to sqrt() there.  Callers check the range.
+__device__ __forceinline__ double sqrt_mid(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    const double d0 = fma(-g, g, x);
+    g = fma(d0, h, g);
+    const double d1 = fma(-g, g, x);
+    return fma(d1, h, g);
+}
+
+// a / D for a < 2^31 by one 64-bit multiply (Granlund-Montgomery): sh = 32 + ceil(log2 D),
+// m = ceil(2^sh / D) <= 2^33, so a m < 2^64 and the error a (m D - 2^sh) / (D 2^sh) < a / 2^sh
+// stays below 1 / D (host: magic_div)
+__device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
+    return (uint32_t)(((uint64_t)a * m) >> sh);
+}
+
 // every (path, group) item in sorted order (workgroup b takes the sorted chunk xcd_chunk(b));
 // the group's waypoints from the packed raster exactly as seg_pass2_pack reads them (block
 // codes in LDS), CH gathers issued before the first of them is consumed; the unit-arc rows in
@@ -4865,8 +4894,18 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
 // partials go to the item's slot.  Dynamic LDS: the block codes, the unit-arc table, padded
 // to a floor that caps the workgroups per CU (UAM_OPT_K2G_LDS) so an XCD's resident items
 // cover a narrow range of the sorted order.
-template <int CH>
-__global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
+// LS / MS: get_cost's length term and the ratio rows on squared norms (length_smooth,
+// maxratio_smooth), compile-time so the waypoint loop carries no select for them.
+// The group's waypoints go through in chunks of CH.  A chunk in which every lane of the wave
+// has CH waypoints, none of them the goal p_{W-1} (the key puts a ragged last group's items in
+// their own bins, so waves rarely mix group lengths), runs the straight-line form: each point
+// generated by the arc formula, every segment term and kinematic row added (the first chunk
+// only skips the rows that belong to the previous group), the segment norm through sqrt_mid
+// when the whole wave's squared norms are in its range.  Any other chunk runs the general form
+// with the endpoint, range and row tests per waypoint.  Both add exactly the same terms in the
+// same order.
+template <int CH, bool LS, bool MS>
+__global__ __launch_bounds__(256, 4) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                                                 const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_map = s_dyn;
@@ -4879,28 +4918,35 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (pos >= kg.n_items) return;
     const int32_t item = kg.order[pos];
-    const int32_t path = item / kg.nseg;
+    const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int s = item - path * kg.nseg;
-    const int32_t q = path / kg.D, d = path - q * kg.D;
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
     const int N = p.N, W = kg.W;
     const double2* urow = s_u + d * N;
     const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
+    // arc_point's arithmetic with the pair's terms hoisted (the same operations in the same
+    // order: v = x0 - xf, C = (xf + x0) / 2, p = C + 0.5 (R(v) u))
+    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
+    auto arc = [&](int j, double& x0, double& x1) {  // 1 <= j <= N
+        const double2 u = urow[j - 1];
+        x0 = cx + 0.5 * (vx * u.x - vy * u.y);
+        x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+    };
     auto point = [&](int j, double& x0, double& x1) {
         if (j == 0) {
             x0 = pr.x, x1 = pr.y;
         } else if (j == W - 1) {
             x0 = pr.z, x1 = pr.w;
         } else {
-            const double2 u = urow[j - 1];
-            arc_point(pr.x, pr.y, pr.z, pr.w, u.x, u.y, x0, x1);
+            arc(j, x0, x1);
         }
     };
     // this group's share of pass 1 (path_pass1's arithmetic), formed while the waypoints are
     // generated for the gathers, each point once: segment p_{j-1} -> p_j for j in
     // [max(j0, 1), j1) adds to L and the length; kinematic row k (segments k + 1 and k + 2)
     // belongs to the group of waypoint k + 1, so the point after the group closes its last row
-    const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     double gL = 0.0, glen = 0.0, gk = 0.0;
     double px, py, pdx = 0.0, pdy = 0.0, pn = 0.0;
     point(j0 == 0 ? 0 : j0 - 1, px, py);
@@ -4909,26 +4955,49 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
         const double ay = p.anchor_mode ? p.anchor_y : py;
         const double dx = px - ax, dy = py - ay;
         const double n = sqrt(dx * dx + dy * dy);  // = (0 + dx dx) + dy dy: dx dx is never -0
-        gL = gL + (ls ? n * n : n);
+        gL = gL + (LS ? n * n : n);
     }
+    auto row = [&](double nk, double dx, double dy) {  // kinematic row: segments (pd, d)
+        double dt = 0.0;
+        dt = dt + pdx * dx;
+        dt = dt + pdy * dy;
+        double c1, c2, c3;
+        kin_row(p, pn, nk, dt, c1, c2, c3);
+        gk = gk + c1;
+        gk = gk + c2;
+        gk = gk + c3;
+    };
+    // general form: segment p_{j-1} -> (qx, qy) = p_j with every test of the reference's loop
     auto segment = [&](int j, double qx, double qy) {
         const double dx = qx - px, dy = qy - py;
         const double n = sqrt(dx * dx + dy * dy);  // norm_2 = sqrt(dot) (casadi_norm_2)
         if (j < j1) {
             glen = glen + n;
-            if (!p.quirk_length || j <= N) gL = gL + (ls ? n * n : n);
+            if (!p.quirk_length || j <= N) gL = gL + (LS ? n * n : n);
         }
-        const double nk = ms ? n * n : n;
-        if (j >= j0 + 1 && j >= 2) {  // row k = j - 2 (problem.py:100-107)
-            double dt = 0.0;
-            dt = dt + pdx * dx;
-            dt = dt + pdy * dy;
-            double c1, c2, c3;
-            kin_row(p, pn, nk, dt, c1, c2, c3);
-            gk = gk + c1;
-            gk = gk + c2;
-            gk = gk + c3;
+        const double nk = MS ? n * n : n;
+        if (j >= j0 + 1 && j >= 2) row(nk, dx, dy);  // row k = j - 2 (problem.py:100-107)
+        pdx = dx, pdy = dy, pn = nk, px = qx, py = qy;
+    };
+    // straight-line form: j0 < j < j1, 2 <= j <= N (RV: the row is added; false only for the
+    // first chunk's waypoints j0 and, in group 0, j0 + 1 -- decided per lane)
+    // The empty asm statements pin the running sums to their waypoint: without them the
+    // scheduler defers the dependent adds to the chunk's end and keeps every waypoint's terms
+    // live (the kernel then spills at 4 waves per SIMD).
+    auto pin = [](double& v) { asm volatile("" : "+v"(v)); };
+    auto segment_fast = [&](double qx, double qy, bool rv) {
+        const double dx = qx - px, dy = qy - py;
+        const double ss = dx * dx + dy * dy;
+        double n = sqrt_mid(ss);
+        const bool ok = (ss >= 0x1p-767) && (ss <= 0x1p1000);  // NaN: not ok
+        if (__builtin_expect(__any(!ok), 0)) {  // wave-uniform: sqrt() where out of range
+            if (!ok) n = sqrt(ss);
         }
+        glen = glen + n;
+        gL = gL + (LS ? n * n : n);
+        const double nk = MS ? n * n : n;
+        if (rv) row(nk, dx, dy);
+        pin(glen), pin(gL), pin(gk);
         pdx = dx, pdy = dy, pn = nk, px = qx, py = qy;
     };
     // Phi / N: q0 = a (1/N) and one residual step (Markstein), correctly rounded for every
@@ -4942,60 +5011,95 @@ __global__ __launch_bounds__(256) void k_g_eval(KParams p, KRaster rs, KGrp kg,
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;  // -0 / N comes out +0: both add to gc alike
     };
+    // the gather of point (x0, x1): one 16-B load per waypoint, issued outside every branch so
+    // the compiler's wait counts stay exact and CH gathers are really in flight.  A code-3
+    // waypoint reads its record from rec; a code-1 waypoint the aligned pair of 8-B plane-A
+    // entries holding its cell (both cells of a pair share a 128-B line, so the request is the
+    // same); a waypoint with nothing to gather (code 0, off the raster, past the group's end)
+    // reads the plane's first pair, one line per wave, and its value is not used.
+    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
+    auto locate = [&](double x0, double x1, int t, uint32_t& inb, uint32_t& need,
+                      uint32_t& full, uint32_t& odd) -> const uint4* {
+        // the cell: floor(t) in [0, n) <=> t in [0, n) for integer n, and the truncating
+        // conversion equals floor for t >= 0 (NaN fails both tests)
+        const double tx = (x0 - rs.x0) * rs.inv_dx;
+        const double ty = (rs.y_top - x1) * rs.inv_dy;
+        const uint4* ptr = dummy;
+        if ((tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny)) {
+            inb |= 1u << t;
+            const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
+            const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+            const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
+            if (code & 2u) {
+                need |= 1u << t;
+                full |= 1u << t;
+                ptr = rec + (iy * rs.nx + ix);
+            } else if (code) {
+                need |= 1u << t;
+                const int32_t a = pk_addr(rs, ix, iy);
+                odd |= (uint32_t)(a & 1) << t;
+                ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
+            }
+        }
+        return ptr;
+    };
+    // the consume step, branch-free: a lane with nothing gathered adds +0.0 (an exact no-op on
+    // accumulators that are never -0) and takes fmax(hmax, +0.0), exactly what the branches of
+    // raster_pass2_skip do
     double gc = 0.0, gn = 0.0;
     float hmax = -INFINITY;
     uint32_t nh = 0, off = 0;
-    for (int jc = j0; jc < j1; jc += CH) {
+    auto consume1 = [&](const uint4& r, bool in, bool nd, bool fl, bool od) {
+        const uint32_t phi = nd ? (od ? r.z : r.x) : 0u;
+        uint32_t ter = nd ? (fl ? r.z : od ? r.w : r.y) : 0u;
+        const uint32_t psi = fl ? r.y : 0u;
+        if (fl && (r.w & UAM_FLAG_NODATA)) ter = 0u;
+        nh += (fl && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+        off += in ? 0u : 1u;
+        gc = gc + over_n((double)__uint_as_float(phi));
+        gn = gn + (double)__uint_as_float(psi);
+        hmax = fmaxf(hmax, __uint_as_float(ter));
+    };
+    for (int jc = j0, it = 0; jc < j1; jc += CH, ++it) {
         const int je = min(jc + CH, j1);
-        uint4 r[CH];
-        uint32_t inb = 0, need = 0, full = 0;
+        if (__all(je - jc == CH && je < W)) {  // wave-uniform: the straight-line form
+            const bool first = it == 0;
+            uint4 r[CH];
+            uint32_t inb = 0, need = 0, full = 0, odd = 0;
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int j = jc + t;
-            if (j < je) {
+            for (int t = 0; t < CH; ++t) {
+                const int j = jc + t;
+                double x0, x1;
+                if (t == 0 && first && __any(j == 0)) {
+                    point(j, x0, x1);
+                } else {
+                    arc(j, x0, x1);
+                }
+                // the rows of waypoints j0 and (group 0) j0 + 1 belong elsewhere / do not exist
+                const bool rv = !(first && (t == 0 || (t == 1 && j0 == 0)));
+                if (t == 0 && first && j == 0) {
+                    // p_0 of group 0: no segment ends here (the anchor term stands for it)
+                    px = x0, py = x1;
+                } else {
+                    segment_fast(x0, x1, rv);
+                }
+                r[t] = *locate(x0, x1, t, inb, need, full, odd);
+            }
+#pragma unroll
+            for (int t = 0; t < CH; ++t)
+                consume1(r[t], (inb >> t) & 1u, (need >> t) & 1u, (full >> t) & 1u,
+                         (odd >> t) & 1u);
+        } else {  // the general form, one waypoint at a time (the ragged and last chunks)
+#pragma unroll 1
+            for (int j = jc; j < je; ++j) {
                 double x0 = px, x1 = py;  // j = 0: p_0, generated above
                 if (j > 0) {
                     point(j, x0, x1);
                     segment(j, x0, x1);
                 }
-                const double fx = floor((x0 - rs.x0) * rs.inv_dx);
-                const double fy = floor((rs.y_top - x1) * rs.inv_dy);
-                if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
-                    inb |= 1u << t;
-                    const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
-                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                    const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
-                    if (code & 2u) {
-                        need |= 1u << t;
-                        full |= 1u << t;
-                        r[t] = rec[iy * rs.nx + ix];
-                    } else if (code) {
-                        need |= 1u << t;
-                        const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
-                        r[t].x = v.x;
-                        r[t].z = v.y;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            if (jc + t < je) {
-                if (!((inb >> t) & 1u)) {
-                    ++off;
-                    hmax = fmaxf(hmax, 0.0f);  // off-raster counts as sea level
-                } else if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0
-                    hmax = fmaxf(hmax, 0.0f);
-                } else {
-                    gc = gc + over_n((double)__uint_as_float(r[t].x));
-                    float terrain = __uint_as_float(r[t].z);
-                    if ((full >> t) & 1u) {
-                        gn = gn + (double)__uint_as_float(r[t].y);
-                        nh += (r[t].w & UAM_FLAG_NFZ) ? 1u : 0u;
-                        if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0f;
-                    }
-                    hmax = fmaxf(hmax, terrain);
-                }
+                uint32_t inb = 0, need = 0, full = 0, odd = 0;
+                const uint4 r = *locate(x0, x1, 0, inb, need, full, odd);
+                consume1(r, inb & 1u, need & 1u, full & 1u, odd & 1u);
             }
         }
     }
@@ -5121,14 +5225,17 @@ struct uam_ctx {
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
     int32_t last_group = 0;     // uam_last_group: waypoint-group length of the last call's sums
-    int k2g_group = 21;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
-                                // (profiles/r03/k2g7, tile bits 4): 12 0.463, 14 0.435,
-                                // 16 0.442, 18 0.407, 21 0.370, 24 0.395
+    int k2g_group = 24;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
+                                // (profiles/r03/k2g9, tile bits 4, 8 gathers in flight): 12
+                                // 0.433, 16 0.404, 18 0.359, 21 0.337, 24 0.333, 28 0.333,
+                                // 32 0.349
     int k2g_tbits = 4;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
                                 // cfg3 at G = 21: 4 0.390, 5 0.381 (k2g7), 6 0.434 ms (k2g3))
     int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
+    int k2g_chunk = 0;          // K2g gathers in flight per lane (UAM_OPT_K2G_CHUNK: 6, 8, 11;
+                                // 0 = 8)
 
 };
 
@@ -5801,6 +5908,12 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                 return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_FLOOR outside [0, 163840]");
             ctx->k2g_lds = (int)value;
             return UAM_OK;
+        case UAM_OPT_K2G_CHUNK:
+            if (value != 0 && value != 6 && value != 8 && value != 11)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 8 or 11",
+                            (long long)value);
+            ctx->k2g_chunk = (int)value;
+            return UAM_OK;
         case UAM_OPT_K8_STREAMS:
             if (value < 1 || value > 8)
                 return fail(UAM_E_INVALID, "UAM_OPT_K8_STREAMS %lld outside [1, 8]",
@@ -5827,6 +5940,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K8_STREAMS: *value = ctx->k8_nstreams; return UAM_OK;
         case UAM_OPT_K2G_TILE_BITS: *value = ctx->k2g_tbits; return UAM_OK;
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
+        case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
 
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
     }
@@ -6058,6 +6172,15 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     return st ? st : 1;
 }
 
+// div_magic's multiplier and shift for divisor D >= 1: sh = 32 + ceil(log2 D), m = ceil(2^sh / D)
+static void magic_div(uint32_t D, uint64_t* m, int32_t* sh) {
+    int k = 0;
+    while ((1u << k) < D) ++k;
+    *sh = 32 + k;
+    const unsigned __int128 one = 1;
+    *m = (uint64_t)(((one << *sh) + D - 1) / D);
+}
+
 // K2g launch (segment-grouped raster evaluation); returns 1 if launched, 0 if the batch is not
 // one it takes (the caller runs K2s / K2).  Needs the packed raster.  Scratch: the pair-order
 // scratch (order_scratch), so two streams sharing the context serialise on it.
@@ -6074,7 +6197,13 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
     const int tbits = ctx->k2g_tbits;
-    const int bins = (1 << (2 * tbits)) + 1;
+    const int tiles = 1 << (2 * tbits);
+#ifndef UAM_K2G_NO_LASTBIN  // (measurement builds: mixed group lengths in one key space)
+    const int last_bin = (W % G) ? tiles : 0;  // a ragged last group gets its own bins
+#else
+    const int last_bin = 0;
+#endif
+    const int bins = tiles + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)bins * G_NBK;
     const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
@@ -6098,6 +6227,9 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.tshift = tshift;
     kg.tbits = tbits;
     kg.bins = bins;
+    kg.last_bin = last_bin;
+    magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
+    magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
     kg.n_items = n_items;
     size_t o = 0;
@@ -6109,7 +6241,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes;
     const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
-    static const EvalFn evals[3] = {k_g_eval<8>, k_g_eval<11>, k_g_eval<16>};
+#define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
+                        k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
+    static const EvalFn evals[12] = {UAM_G_EVALS(6), UAM_G_EVALS(8), UAM_G_EVALS(11)};
+#undef UAM_G_EVALS
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
         for (EvalFn f : evals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -6124,9 +6259,11 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
-    // gathers in flight per lane (profiles/r03/k2g7: 8 or 11 within 1% at G = 12..24; a
-    // register cap for 5-8 waves per SIMD spills and loses 20-190%, profiles/r03/k2g8)
-    const int ch = G <= 8 ? 0 : G <= 11 ? 1 : G <= 16 ? 0 : G <= 22 ? 1 : 2;
+    // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
+    // 10 0.369, 6 0.351)
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 8;
+    const int ch = (chl == 6 ? 0 : chl == 8 ? 1 : 2) * 4 + (ctx->kp.length_smooth ? 2 : 0) +
+                   (ctx->kp.maxratio_smooth ? 1 : 0);
     hipLaunchKernelGGL(evals[ch], ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
