@@ -407,7 +407,7 @@ int32_t uam_last_group(const uam_ctx* ctx);
 
 /* Context options: which kernel form runs (results never depend on them, except for the sum
  * order UAM_OPT_GROUP selects, which uam_last_group reports).  Read by the calls that follow.
- *   UAM_OPT_GROUP                K2g waypoints per group, 1..64 (default 24); 0 = no K2g (the
+ *   UAM_OPT_GROUP                K2g waypoints per group, 1..64 (default 21); 0 = no K2g (the
  *                                raster batches it takes run K2s: the reference's sum order)
  *   UAM_OPT_SORTED_MIN_PATHS     smallest raster batch (paths) the sorted forms K2g / K2s take
  *                                (default 65536; smaller batches run K2 / K2w)
@@ -425,8 +425,9 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6 (4)
  *   UAM_OPT_K2G_LDS_FLOOR        K2g evaluation: dynamic-LDS floor per workgroup in bytes, which
  *                                caps the workgroups resident per CU (default 0)
- *   UAM_OPT_K2G_CHUNK            K2g evaluation: gathers in flight per lane, 6/8/11; 0 (default)
- *                                = 8 */
+ *   UAM_OPT_K2G_CHUNK            K2g evaluation: gathers in flight per lane, 6/8/11/16 (16 runs
+ *                                two waves per SIMD); 0 (default) = 8
+ *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -440,7 +441,8 @@ enum {
     UAM_OPT_K8_STREAMS = 10,
     UAM_OPT_K2G_TILE_BITS = 11,
     UAM_OPT_K2G_LDS_FLOOR = 12,
-    UAM_OPT_K2G_CHUNK = 13
+    UAM_OPT_K2G_CHUNK = 13,
+    UAM_OPT_K2G_CURVE = 14
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

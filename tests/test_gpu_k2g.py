@@ -197,21 +197,24 @@ def test_k2g_options(oracle_mod):
 
     build.build_library()
     e = Engine(0)
-    assert e.get_option("group") == 24
+    assert e.get_option("group") == 21
     for bad in (-1, 65):
         with pytest.raises(ValueError):
             e.set_option("group", bad)
     e.set_option("group", 12)
     assert e.get_option("group") == 12
     assert e.get_option("k2g_chunk") == 0
-    for bad in (-1, 5, 7, 10, 12, 16):
+    for bad in (-1, 5, 7, 10, 12, 17):
         with pytest.raises(ValueError):
             e.set_option("k2g_chunk", bad)
     e.set_option("k2g_chunk", 11)
     assert e.get_option("k2g_chunk") == 11
+    assert e.get_option("k2g_curve") == 1
+    with pytest.raises(ValueError):
+        e.set_option("k2g_curve", 2)
 
 
-@pytest.mark.parametrize("chunk,group", [(6, 24), (8, 21), (8, 26), (11, 21), (11, 5), (6, 64)])
+@pytest.mark.parametrize("chunk,group", [(6, 24), (8, 21), (8, 26), (11, 21), (11, 5), (6, 64), (16, 21), (16, 40)])
 def test_k2g_chunk_lengths(oracle_mod, chunk, group):
     """The gathers in flight per lane (UAM_OPT_K2G_CHUNK) only change how a group's waypoints
     are cut into load batches (full and partial chunks, groups shorter than a chunk): every
@@ -234,8 +237,9 @@ def test_k2g_chunk_lengths(oracle_mod, chunk, group):
     _check(gpu, ref, oracle_mod, D)
 
 
-@pytest.mark.parametrize("tbits,lds", [(6, 0), (4, 49152), (3, 0)])
-def test_k2g_tuning_knobs(oracle_mod, tbits, lds):
+@pytest.mark.parametrize("tbits,lds,curve", [(6, 0, 1), (4, 49152, 1), (3, 0, 1), (4, 0, 0),
+                                             (5, 0, 0)])
+def test_k2g_tuning_knobs(oracle_mod, tbits, lds, curve):
     """The knobs that only move work between lanes -- the sort key's tile grid
     (UAM_OPT_K2G_TILE_BITS) and the evaluation's LDS floor (UAM_OPT_K2G_LDS_FLOOR) -- leave
     every output equal to the grouped oracle's; groups of 21 take two gather chunks; a
@@ -248,6 +252,7 @@ def test_k2g_tuning_knobs(oracle_mod, tbits, lds):
     e, orc, raster, rd, rec = _case(oracle_mod, 21, 80, maxalpha=0.015)
     e.set_option("k2g_tile_bits", tbits)
     e.set_option("k2g_lds_floor", lds)
+    e.set_option("k2g_curve", curve)
     e.raster_summary(raster, 0, packed=True)
     D = 5
     ut = arc_table(80, displacements(D))

@@ -421,7 +421,7 @@ def test_raster_kernels_bit_identical(eng, oracle_mod, D):
     finally:
         eng.set_option("wave_max_paths", 16384)
         eng.set_option("sorted_min_paths", 65536)
-        eng.set_option("group", 24)
+        eng.set_option("group", 21)
     assert seen == ({"K2w", "K2d"} if D > 16 else {"K2w", "K2+skip", "K2s+pack", "K2g+pack"})
     with pytest.raises(ValueError):
         eng.set_option("wave_max_paths", -1)

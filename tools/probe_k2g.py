@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--tbits", default="6")
     ap.add_argument("--lds", default="0")
     ap.add_argument("--chunks", default="0")
+    ap.add_argument("--curves", default="1")
     ap.add_argument("--pairs", type=int, default=100000)
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
@@ -52,8 +53,9 @@ def main():
     for g in ints(a.groups):
         for tb in ints(a.tbits):
             for lds in ints(a.lds):
-                for chk in ints(a.chunks):
+                for chk, cv in [(c, v) for c in ints(a.chunks) for v in ints(a.curves)]:
                     e.set_option("k2g_chunk", chk)
+                    e.set_option("k2g_curve", cv)
                     e.set_option("group", g)
                     e.set_option("k2g_tile_bits", tb)
                     e.set_option("k2g_lds_floor", lds)
@@ -66,7 +68,7 @@ def main():
                     ms, n = e.kernel_time()
                     e.kernel_timing(False)
                     cost = o["cost"].clone()
-                    row = {"group": g, "tbits": tb, "lds": lds, "chunk": chk,
+                    row = {"group": g, "tbits": tb, "lds": lds, "chunk": chk, "curve": cv,
                            "kernel": e.last_kernel(), "ms": round(ms / n, 4),
                            "paths_per_s": round(a.pairs * D / (ms / n * 1e-3), 1)}
                     if g in first:

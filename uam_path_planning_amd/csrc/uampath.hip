@@ -4782,6 +4782,7 @@ struct KGrp {
     int64_t n_pairs;
     int32_t P, D, W, G, nseg, tshift, tbits, bins;
     int32_t last_bin;              // key offset of the last group's items (0: groups all G long)
+    const uint16_t* __restrict__ tkey;  // [2^tbits][2^tbits] tile -> position on the curve
     uint64_t m_nseg, m_d;          // div_magic multipliers and shifts for / nseg and / D
     int32_t sh_nseg, sh_d;
     double inv_n;                  // RN(1 / N) for Phi / N (0: divide; N > 4096)
@@ -4806,7 +4807,8 @@ __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t 
     return src;
 }
 
-// sort key of a point: Morton code of its 2^tbits x 2^tbits-grid tile, bins - 1 off the raster
+// sort key of a point: the position of its tile of the 2^tbits x 2^tbits grid on the tile curve
+// (Hilbert by default: consecutive tiles always adjacent), bins - 1 off the raster
 __device__ __forceinline__ uint32_t grp_key(const KGrp& kg, const KRaster& rs, double x0,
                                             double x1) {
     const double fx = floor((x0 - rs.x0) * rs.inv_dx);
@@ -4814,10 +4816,7 @@ __device__ __forceinline__ uint32_t grp_key(const KGrp& kg, const KRaster& rs, d
     if (!((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)))
         return kg.bins - 1;
     const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
-    uint32_t k = 0;
-    for (int bit = kg.tbits - 1; bit >= 0; --bit)
-        k = (k << 2) | (((ty >> bit) & 1u) << 1) | ((tx >> bit) & 1u);
-    return k;
+    return kg.tkey[(ty << kg.tbits) | tx];
 }
 
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
@@ -4905,15 +4904,36 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
 // with the endpoint, range and row tests per waypoint.  Both add exactly the same terms in the
 // same order.
 template <int CH, bool LS, bool MS>
-__global__ __launch_bounds__(256, 4) void k_g_eval(KParams p, KRaster rs, KGrp kg,
+__global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                                                 const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_map = s_dyn;
     const int mapw = (rs.pwords + 3) & ~3;
     double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
-    for (int i = threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
-    const double2* gu = reinterpret_cast<const double2*>(kg.utab);
-    for (int i = threadIdx.x; i < kg.D * p.N; i += 256) s_u[i] = gu[i];
+    // staging: every load of a thread issued before its first LDS store (one round trip per
+    // workgroup instead of one per 256 words)
+    {
+        constexpr int U = 4;
+        const int nv = rs.pwords >> 2, nu = kg.D * p.N;
+        const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
+        uint4* dst = reinterpret_cast<uint4*>(s_map);
+        const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
+        uint4* du = reinterpret_cast<uint4*>(s_u);
+        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += 256 * U) {
+            uint4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {  // unconditional loads (past the end: the first word)
+                const int i = i0 + k * 256;
+                v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {  // unconditional stores (past the end: a junk slot)
+                const int i = i0 + k * 256;
+                *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
+            }
+        }
+        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
+    }
     __syncthreads();
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (pos >= kg.n_items) return;
@@ -5217,6 +5237,8 @@ struct uam_ctx {
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
+    uint16_t* d_tkey = nullptr; // K2g: sort key of each tile (curve order), for tkey_bits/curve
+    int tkey_bits = -1, tkey_curve = -1;
     size_t ord_bytes = 0;
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
                                   // another stream waits for it before rewriting the scratch
@@ -5225,15 +5247,15 @@ struct uam_ctx {
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
     int32_t last_group = 0;     // uam_last_group: waypoint-group length of the last call's sums
-    int k2g_group = 24;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
-                                // (profiles/r03/k2g9, tile bits 4, 8 gathers in flight): 12
-                                // 0.433, 16 0.404, 18 0.359, 21 0.337, 24 0.333, 28 0.333,
-                                // 32 0.349
+    int k2g_group = 21;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
+                                // (profiles/r03/k2g13, tile bits 4, Hilbert, 8 in flight): 14
+                                // 0.387, 16 0.405, 18 0.365, 21 0.329, 24 0.356
     int k2g_tbits = 4;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
                                 // cfg3 at G = 21: 4 0.390, 5 0.381 (k2g7), 6 0.434 ms (k2g3))
     int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
+    int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
     int k2g_chunk = 0;          // K2g gathers in flight per lane (UAM_OPT_K2G_CHUNK: 6, 8, 11;
                                 // 0 = 8)
 
@@ -5359,6 +5381,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
     if (ctx->ev_ord) (void)hipEventSynchronize(ctx->ev_ord);
     if (ctx->d_ord) (void)hipFree(ctx->d_ord);
+    if (ctx->d_tkey) (void)hipFree(ctx->d_tkey);
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -5908,9 +5931,14 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                 return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_FLOOR outside [0, 163840]");
             ctx->k2g_lds = (int)value;
             return UAM_OK;
+        case UAM_OPT_K2G_CURVE:
+            if (value != 0 && value != 1)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CURVE %lld not 0 or 1", (long long)value);
+            ctx->k2g_curve = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2G_CHUNK:
-            if (value != 0 && value != 6 && value != 8 && value != 11)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 8 or 11",
+            if (value != 0 && value != 6 && value != 8 && value != 11 && value != 16)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 8, 11 or 16",
                             (long long)value);
             ctx->k2g_chunk = (int)value;
             return UAM_OK;
@@ -5941,6 +5969,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_TILE_BITS: *value = ctx->k2g_tbits; return UAM_OK;
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
+        case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
     }
@@ -6172,6 +6201,54 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
     return st ? st : 1;
 }
 
+// position of tile (x, y) on the Hilbert curve of a 2^bits x 2^bits grid
+static uint32_t hilbert_d(int bits, uint32_t x, uint32_t y) {
+    uint32_t d = 0;
+    for (uint32_t s = 1u << (bits - 1); s > 0; s >>= 1) {
+        const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
+        d += s * s * ((3u * rx) ^ ry);
+        if (ry == 0) {
+            if (rx == 1) {
+                x = s - 1 - x;
+                y = s - 1 - y;
+            }
+            const uint32_t t = x;
+            x = y;
+            y = t;
+        }
+    }
+    return d;
+}
+
+// the K2g tile-key table for (bits, curve), uploaded once per setting
+static int tile_keys(uam_ctx* ctx, int bits, int curve, hipStream_t s) {
+    if (ctx->d_tkey && ctx->tkey_bits == bits && ctx->tkey_curve == curve) return UAM_OK;
+    const uint32_t n = 1u << bits;
+    std::vector<uint16_t> h((size_t)n * n);
+    for (uint32_t y = 0; y < n; ++y)
+        for (uint32_t x = 0; x < n; ++x) {
+            uint32_t k = 0;
+            if (curve) {
+                k = hilbert_d(bits, x, y);
+            } else {
+                for (int b = bits - 1; b >= 0; --b)
+                    k = (k << 2) | (((y >> b) & 1u) << 1) | ((x >> b) & 1u);
+            }
+            h[(size_t)y * n + x] = (uint16_t)k;
+        }
+    if (!ctx->d_tkey) {
+        const size_t cap = sizeof(uint16_t) << (2 * G_TBITS_MAX);
+        if (hipMalloc(&ctx->d_tkey, cap) != hipSuccess) return fail(UAM_E_NOMEM, "tile keys");
+    }
+    // stream-ordered: the launches that read the table follow on s
+    HIP_TRY(hipMemcpyAsync(ctx->d_tkey, h.data(), h.size() * sizeof(uint16_t),
+                           hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // h is freed on return
+    ctx->tkey_bits = bits;
+    ctx->tkey_curve = curve;
+    return UAM_OK;
+}
+
 // div_magic's multiplier and shift for divisor D >= 1: sh = 32 + ceil(log2 D), m = ceil(2^sh / D)
 static void magic_div(uint32_t D, uint64_t* m, int32_t* sh) {
     int k = 0;
@@ -6228,6 +6305,9 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.tbits = tbits;
     kg.bins = bins;
     kg.last_bin = last_bin;
+    st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
+    if (st) return st;
+    kg.tkey = ctx->d_tkey;
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
@@ -6238,12 +6318,13 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.key = (uint16_t*)(w + o);
-    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes;
+    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16;  // + junk slot
     const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
                         k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
-    static const EvalFn evals[12] = {UAM_G_EVALS(6), UAM_G_EVALS(8), UAM_G_EVALS(11)};
+    static const EvalFn evals[16] = {UAM_G_EVALS(6), UAM_G_EVALS(8), UAM_G_EVALS(11),
+                                     UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
         for (EvalFn f : evals)
@@ -6262,7 +6343,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 8;
-    const int ch = (chl == 6 ? 0 : chl == 8 ? 1 : 2) * 4 + (ctx->kp.length_smooth ? 2 : 0) +
+    const int ch = (chl == 6 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
+                   (ctx->kp.length_smooth ? 2 : 0) +
                    (ctx->kp.maxratio_smooth ? 1 : 0);
     hipLaunchKernelGGL(evals[ch], ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
