@@ -422,7 +422,8 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K3B_POINTS_PER_LANE  analytic K3b evaluation phase: 1 (default) or 2
  *   UAM_OPT_K8_TILED             DEM polygons: 1 (default) tile labelling in LDS, 0 cell-parallel
  *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4)
- *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6 (4)
+ *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6; 0
+ *                                (default) = tiles of ~256 x 256 cells
  *   UAM_OPT_K2G_LDS_FLOOR        K2g evaluation: dynamic-LDS floor per workgroup in bytes, which
  *                                caps the workgroups resident per CU (default 0)
  *   UAM_OPT_K2G_CHUNK            K2g evaluation: gathers in flight per lane, 6/8/11/16 (16 runs

@@ -210,6 +210,10 @@ def test_k2g_options(oracle_mod):
     e.set_option("k2g_chunk", 11)
     assert e.get_option("k2g_chunk") == 11
     assert e.get_option("k2g_curve") == 1
+    assert e.get_option("k2g_tile_bits") == 0  # automatic: tiles of ~256^2 cells
+    for bad in (-1, 1, 2, 7):
+        with pytest.raises(ValueError):
+            e.set_option("k2g_tile_bits", bad)
     with pytest.raises(ValueError):
         e.set_option("k2g_curve", 2)
 
@@ -238,7 +242,7 @@ def test_k2g_chunk_lengths(oracle_mod, chunk, group):
 
 
 @pytest.mark.parametrize("tbits,lds,curve", [(6, 0, 1), (4, 49152, 1), (3, 0, 1), (4, 0, 0),
-                                             (5, 0, 0)])
+                                             (5, 0, 0), (0, 0, 1)])
 def test_k2g_tuning_knobs(oracle_mod, tbits, lds, curve):
     """The knobs that only move work between lanes -- the sort key's tile grid
     (UAM_OPT_K2G_TILE_BITS) and the evaluation's LDS floor (UAM_OPT_K2G_LDS_FLOOR) -- leave

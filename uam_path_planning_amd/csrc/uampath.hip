@@ -5250,8 +5250,10 @@ struct uam_ctx {
     int k2g_group = 21;         // K2g waypoints per group (UAM_OPT_GROUP; 0 = K2s).  cfg3 ms
                                 // (profiles/r03/k2g13, tile bits 4, Hilbert, 8 in flight): 14
                                 // 0.387, 16 0.405, 18 0.365, 21 0.329, 24 0.356
-    int k2g_tbits = 4;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
-                                // cfg3 at G = 21: 4 0.390, 5 0.381 (k2g7), 6 0.434 ms (k2g3))
+    int k2g_tbits = 0;          // K2g sort key: 2^tbits x 2^tbits tiles (UAM_OPT_K2G_TILE_BITS;
+                                // 0 = tiles of ~256^2 cells: cfg3 (4096^2) Hilbert 4 0.329,
+                                // 5 0.343, 6 0.381 ms (k2g13); cfg4 (8192^2) 4 1.062, 5 0.996,
+                                // 6 1.043 ms (cfg4_tbits))
     int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
@@ -5921,8 +5923,8 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
             ctx->k8_tiled = value != 0;
             return UAM_OK;
         case UAM_OPT_K2G_TILE_BITS:
-            if (value < 3 || value > G_TBITS_MAX)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_TILE_BITS %lld outside [3, %d]",
+            if (value != 0 && (value < 3 || value > G_TBITS_MAX))
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_TILE_BITS %lld not 0 or in [3, %d]",
                             (long long)value, G_TBITS_MAX);
             ctx->k2g_tbits = (int)value;
             return UAM_OK;
@@ -6273,7 +6275,11 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
-    const int tbits = ctx->k2g_tbits;
+    int tbits = ctx->k2g_tbits;
+    if (tbits == 0) {  // tiles of ~256 x 256 cells
+        tbits = 3;
+        while (tbits < G_TBITS_MAX && (std::max(kr.nx, kr.ny) >> tbits) > 256) ++tbits;
+    }
     const int tiles = 1 << (2 * tbits);
 #ifndef UAM_K2G_NO_LASTBIN  // (measurement builds: mixed group lengths in one key space)
     const int last_bin = (W % G) ? tiles : 0;  // a ragged last group gets its own bins
