@@ -4807,16 +4807,11 @@ __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t 
     return src;
 }
 
-// sort key of a point: the position of its tile of the 2^tbits x 2^tbits grid on the tile curve
-// (Hilbert by default: consecutive tiles always adjacent), bins - 1 off the raster
-__device__ __forceinline__ uint32_t grp_key(const KGrp& kg, const KRaster& rs, double x0,
-                                            double x1) {
-    const double fx = floor((x0 - rs.x0) * rs.inv_dx);
-    const double fy = floor((rs.y_top - x1) * rs.inv_dy);
-    if (!((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)))
-        return kg.bins - 1;
-    const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
-    return kg.tkey[(ty << kg.tbits) | tx];
+// a / D for a < 2^31 by one 64-bit multiply (Granlund-Montgomery): sh = 32 + ceil(log2 D),
+// m = ceil(2^sh / D) <= 2^33, so a m < 2^64 and the error a (m D - 2^sh) / (D 2^sh) < a / 2^sh
+// stays below 1 / D (host: magic_div)
+__device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
+    return (uint32_t)(((uint64_t)a * m) >> sh);
 }
 
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
@@ -4824,32 +4819,69 @@ __device__ __forceinline__ uint32_t grp_key(const KGrp& kg, const KRaster& rs, d
 // bin-major so the scan yields each (bin, partition)'s offset
 __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
     __shared__ int32_t h[G_BINS_MAX];
+    __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
     const int t = threadIdx.x, b = blockIdx.x;
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
+    for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
     // thread = item (consecutive threads: the groups of one path, then the next path's), so
-    // the key stores are coalesced and a path's pair is one broadcast load
+    // the key stores are coalesced and a path's pair is one broadcast load; U items per thread
+    // with all their loads issued first (indices clamped into the partition)
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
-    for (int64_t i = lo + t; i < hi; i += 1024) {
-        const int32_t path = (int32_t)(i / kg.nseg);
-        const int s = (int)(i - (int64_t)path * kg.nseg);
-        const PathSrc<true> src = grp_src(kg, p.N, path);
-        const int j0 = s * kg.G, j1 = min(j0 + kg.G, kg.W);
-        double x0, x1;
-        src.at((j0 + j1 - 1) >> 1, x0, x1);
-        uint32_t k = grp_key(kg, rs, x0, x1);
-        // a ragged last group's items in their own bins: the waves then rarely mix group
-        // lengths, so k_g_eval's straight-line chunks stay wave-uniform
-        if (s == kg.nseg - 1 && k != (uint32_t)kg.bins - 1) k += kg.last_bin;
-        kg.key[i] = (uint16_t)k;
-        atomicAdd(&h[k], 1);
+    const int N = p.N, W = kg.W;
+    constexpr int U = 4;
+    for (int64_t i0 = lo + t; i0 < hi; i0 += 1024 * U) {
+        double4 pr[U];
+        double2 u[U];
+        int jm[U], sg[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = (int32_t)min(i0 + k * 1024, hi - 1);
+            const int32_t path = (int32_t)div_magic((uint32_t)i, kg.m_nseg, kg.sh_nseg);
+            sg[k] = i - path * kg.nseg;
+            const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+            const int32_t d = path - q * kg.D;
+            const int j0 = sg[k] * kg.G, j1 = min(j0 + kg.G, W);
+            jm[k] = (j0 + j1 - 1) >> 1;  // the group's middle waypoint
+            pr[k] = reinterpret_cast<const double4*>(kg.pairs)[q];
+            u[k] = reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(jm[k] - 1, 0), N - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t i = i0 + k * 1024;
+            if (i >= hi) break;
+            double x0, x1;  // PathSrc::at's point
+            if (jm[k] == 0) {
+                x0 = pr[k].x, x1 = pr[k].y;
+            } else if (jm[k] == W - 1) {
+                x0 = pr[k].z, x1 = pr[k].w;
+            } else {
+                arc_point(pr[k].x, pr[k].y, pr[k].z, pr[k].w, u[k].x, u[k].y, x0, x1);
+            }
+            // the key: the position of the point's tile of the 2^tbits x 2^tbits grid on the
+            // tile curve (Hilbert by default: consecutive tiles always adjacent), bins - 1 off
+            // the raster or NaN
+            const double fx = floor((x0 - rs.x0) * rs.inv_dx);
+            const double fy = floor((rs.y_top - x1) * rs.inv_dy);
+            uint32_t key = kg.bins - 1;
+            if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
+                const uint32_t tx = (uint32_t)fx >> kg.tshift, ty = (uint32_t)fy >> kg.tshift;
+                key = tk[(ty << kg.tbits) | tx];
+                // a ragged last group's items in their own bins: the waves then rarely mix
+                // group lengths, so k_g_eval's straight-line chunks stay wave-uniform
+                if (sg[k] == kg.nseg - 1) key += kg.last_bin;
+            }
+            kg.key[i] = (uint16_t)key;
+            atomicAdd(&h[key], 1);
+        }
     }
     __syncthreads();
     for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
-// launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered
+// launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered; U keys
+// per thread loaded before the first cursor update
 __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
     __shared__ int32_t cur[G_BINS_MAX];
     const int t = threadIdx.x, b = blockIdx.x;
@@ -4860,8 +4892,17 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
-    for (int64_t i = lo + t; i < hi; i += 1024)
-        kg.order[atomicAdd(&cur[kg.key[i]], 1)] = (int32_t)i;
+    constexpr int U = 8;
+    for (int64_t i0 = lo + t; i0 < hi; i0 += 1024 * U) {
+        uint16_t kk[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) kk[k] = kg.key[min(i0 + k * 1024, hi - 1)];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t i = i0 + k * 1024;
+            if (i < hi) kg.order[atomicAdd(&cur[kk[k]], 1)] = (int32_t)i;
+        }
+    }
 }
 
 // sqrt(x) for x in [2^-767, 2^1000]: the gfx9 lowering of sqrt(double) (rsq, then two
@@ -4877,13 +4918,6 @@ __device__ __forceinline__ double sqrt_mid(double x) {
     g = fma(d0, h, g);
     const double d1 = fma(-g, g, x);
     return fma(d1, h, g);
-}
-
-// a / D for a < 2^31 by one 64-bit multiply (Granlund-Montgomery): sh = 32 + ceil(log2 D),
-// m = ceil(2^sh / D) <= 2^33, so a m < 2^64 and the error a (m D - 2^sh) / (D 2^sh) < a / 2^sh
-// stays below 1 / D (host: magic_div)
-__device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
-    return (uint32_t)(((uint64_t)a * m) >> sh);
 }
 
 // every (path, group) item in sorted order (workgroup b takes the sorted chunk xcd_chunk(b));
