@@ -5176,6 +5176,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout): the partials
 // combined in group order (cost = (N+1) L + the Phi/N partials), and the selection over each
 // pair's D paths
+template <int NR>  // slots per path held in registers (0: a loop for long paths)
 __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
                                                   int32_t* __restrict__ best_f,
                                                   int32_t* __restrict__ best_l) {
@@ -5189,18 +5190,45 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
         const int64_t gp = (q0 + qi) * D + di;
         double L = 0.0, len = 0.0, ksum = 0.0, nsum = 0.0, hmax = -INFINITY;
         int32_t nh = 0, off = 0;
-        for (int s = 0; s < kg.nseg; ++s) {
-            const GSlot g = kg.slot[(int64_t)s * kg.P + gp];
-            L = L + g.L;
-            len = len + g.len;
-            ksum = ksum + g.ksum;
-            nsum = nsum + g.psi;
-            hmax = fmax(hmax, (double)g.hmax);
-            nh += (int32_t)(g.cnt & 255u);
-            off += (int32_t)((g.cnt >> 8) & 255u);
+        double cost;
+        if (NR > 0) {
+            // every slot loaded before the first is used (clamped indices: unconditional
+            // loads, one round trip); the Phi/N partials wait in registers for L
+            GSlot g[NR > 0 ? NR : 1];
+#pragma unroll
+            for (int s = 0; s < NR; ++s)
+                g[s] = kg.slot[(int64_t)min(s, kg.nseg - 1) * kg.P + gp];
+#pragma unroll
+            for (int s = 0; s < NR; ++s) {
+                if (s >= kg.nseg) break;
+                L = L + g[s].L;
+                len = len + g[s].len;
+                ksum = ksum + g[s].ksum;
+                nsum = nsum + g[s].psi;
+                hmax = fmax(hmax, (double)g[s].hmax);
+                nh += (int32_t)(g[s].cnt & 255u);
+                off += (int32_t)((g[s].cnt >> 8) & 255u);
+            }
+            cost = (double)(p.N + 1) * L;
+#pragma unroll
+            for (int s = 0; s < NR; ++s) {
+                if (s >= kg.nseg) break;
+                cost = cost + g[s].cost;
+            }
+        } else {
+            for (int s = 0; s < kg.nseg; ++s) {
+                const GSlot g = kg.slot[(int64_t)s * kg.P + gp];
+                L = L + g.L;
+                len = len + g.len;
+                ksum = ksum + g.ksum;
+                nsum = nsum + g.psi;
+                hmax = fmax(hmax, (double)g.hmax);
+                nh += (int32_t)(g.cnt & 255u);
+                off += (int32_t)((g.cnt >> 8) & 255u);
+            }
+            cost = (double)(p.N + 1) * L;
+            for (int s = 0; s < kg.nseg; ++s) cost = cost + kg.slot[(int64_t)s * kg.P + gp].cost;
         }
-        double cost = (double)(p.N + 1) * L;
-        for (int s = 0; s < kg.nseg; ++s) cost = cost + kg.slot[(int64_t)s * kg.P + gp].cost;
         if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = L;
         if (out.length) out.length[gp] = len;
@@ -6387,7 +6415,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                    (ctx->kp.length_smooth ? 2 : 0) +
                    (ctx->kp.maxratio_smooth ? 1 : 0);
     hipLaunchKernelGGL(evals[ch], ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
-    hipLaunchKernelGGL(k_g_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
+    // the output launch holds a path's slots in registers up to 8 groups
+    using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
+    const FinalFn fin = nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
+    hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
     st = ktime_end(ctx, s);
