@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU box, round 3: sorted pairs written beside the order (no dependent pair load in the evaluation) against the previous
+# build (lib/prev.so), same box; kernel trace.
+cd "$GRAFT_REPO_ROOT"
+o=r03/k2g20
+mkdir -p gpurun_out/$o
+export TMPDIR=/tmp
+L=uam_path_planning_amd/lib
+P3="python -u tools/probe_k2g.py --groups 21 --chunks 8 --tbits 0 --reps 20"
+tools/gpu_session.sh \
+  "300|$o/k2g_tests|python -u -m pytest tests/test_gpu_k2g.py -x -q --timeout 120 --timeout-method thread" \
+  "120|$o/new_a|$P3" "120|$o/prev_a|UAM_LIB_PATH=$L/prev.so $P3" \
+  "120|$o/new_b|$P3" "120|$o/prev_b|UAM_LIB_PATH=$L/prev.so $P3" \
+  "120|$o/grp|python -u tools/probe_k2g.py --groups 8,12,16 --chunks 8 --tbits 0 --reps 10" \
+  "120|$o/trace|rocprofv3 --kernel-trace --stats -d gpurun_out/$o/trace -o run --output-format csv -- python3 tools/probe_k2g.py --groups 21 --chunks 8 --tbits 0 --reps 5"
