@@ -5305,6 +5305,7 @@ struct uam_ctx {
     hipEvent_t ev_ord = nullptr;  // recorded after the last launch that read d_ord: a call on
                                   // another stream waits for it before rewriting the scratch
     bool ord_pending = false;
+    hipStream_t ord_stream = nullptr;  // the stream of the last launch that read the scratch
     hipStream_t k8s[7] = {};    // K8 side streams (created on first use)
     void* comm = nullptr;       // RCCL communicator of uam_comm_init / uam_bcast_raster_group
     const char* last_kernel = "";  // uam_last_kernel: the path evaluation the last call ran
@@ -6062,7 +6063,9 @@ int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
 // other's order; the caller records ctx->ev_ord after the launch that reads the order.
 static int order_scratch(uam_ctx* ctx, size_t need, hipStream_t s, char** w) {
     if (!ctx->ev_ord) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_ord, hipEventDisableTiming));
-    if (ctx->ord_pending) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_ord, 0));
+    // another stream's launches that read the scratch must finish first (the caller's own
+    // stream is ordered already: no wait packet on the common path)
+    if (ctx->ord_pending && ctx->ord_stream != s) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_ord, 0));
     if (need > ctx->ord_bytes) {
         if (ctx->d_ord) {
             HIP_TRY(hipEventSynchronize(ctx->ev_ord));
@@ -6080,6 +6083,7 @@ static int order_scratch(uam_ctx* ctx, size_t need, hipStream_t s, char** w) {
 static int order_done(uam_ctx* ctx, hipStream_t s) {
     HIP_TRY(hipEventRecord(ctx->ev_ord, s));
     ctx->ord_pending = true;
+    ctx->ord_stream = s;
     return UAM_OK;
 }
 
