@@ -472,8 +472,9 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
                  "from the Infinity Cache / HBM (PMC); the measured random-gather ceiling "
                  "(tools/gather_ceiling.hip) bounds a kernel gathering in random order (K2); "
                  "the tile-sorted forms (K2g, K2s) pass it through L2 reuse (l2_hit_rate). "
-                 "K2g's evaluation with the whole table in L2 (512^2 raster) takes 254 us of "
-                 "its ~300 us at 4096^2 (profiles/r03/k2g6), DESIGN.md §4-5"}
+                 "K2g at cfg3: 13.5M of its ~49M L2 requests per step miss and come from the "
+                 "Infinity Cache / HBM at <= 55-59 G lines/s; its evaluation launch is ~283 us "
+                 "of the ~0.34 ms step (profiles/r03/k2g_v9), DESIGN.md §4-5"}
     return r
 
 
