@@ -4594,11 +4594,16 @@ template <int CH>
 __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* __restrict__ rec,
                                                const uint32_t* map, const PathSrc<true>& src,
                                                int j0, int j1, double dN, PathAcc& a) {
+    // one 16-B load per waypoint outside every branch (as k_g_eval: the branchy form made the
+    // compiler wait for each gather): the record in a code-3 block, the aligned pair of
+    // plane-A entries in a code-1 block, the plane's first pair otherwise (value unused)
+    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
     for (int jc = j0; jc < j1; jc += CH) {
         uint4 r[CH];
-        uint32_t inb = 0, need = 0, full = 0;
+        uint32_t inb = 0, need = 0, full = 0, odd = 0;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
+            const uint4* ptr = dummy;
             if (jc + t < j1) {
                 double x0, x1;
                 src.at(jc + t, x0, x1);
@@ -4612,15 +4617,16 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
                     if (code & 2u) {
                         need |= 1u << t;
                         full |= 1u << t;
-                        r[t] = rec[iy * rs.nx + ix];
+                        ptr = rec + (iy * rs.nx + ix);
                     } else if (code) {
                         need |= 1u << t;
-                        const uint2 v = rs.pa[pk_addr(rs, ix, iy)];
-                        r[t].x = v.x;
-                        r[t].z = v.y;
+                        const int32_t pa = pk_addr(rs, ix, iy);
+                        odd |= (uint32_t)(pa & 1) << t;
+                        ptr = reinterpret_cast<const uint4*>(rs.pa + (pa & ~1));
                     }
                 }
             }
+            r[t] = *ptr;
         }
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
@@ -4633,6 +4639,12 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
             if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
                 a.hmax = fmax(a.hmax, 0.0);
                 continue;
+            }
+            if (!((full >> t) & 1u) && ((odd >> t) & 1u)) {  // the pair's second cell
+                r[t].x = r[t].z;
+                r[t].z = r[t].w;
+            } else if (!((full >> t) & 1u)) {
+                r[t].z = r[t].y;
             }
             a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
             double terrain = (double)__uint_as_float(r[t].z);
