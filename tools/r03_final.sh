@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box, round 3 final tree: full GPU suite, smoke, cfg3 bench line.
 cd "$GRAFT_REPO_ROOT"
-o=r03/final
+o=${OUT:-r03/final}
 mkdir -p gpurun_out/$o
 tools/gpu_session.sh \
   "600|$o/gpu_tests|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
