@@ -78,6 +78,10 @@ def parse():
                     help="K2s gathers the 16-B records instead of the packed copy "
                          "(uam_raster_pack: 8-B phi/terrain plane outside the no-fly blocks; "
                          "A/B, results are identical)")
+    ap.add_argument("--cells", action="store_true",
+                    help="also return every waypoint's raster cell index (outputs cells "
+                         "[P, W] int32, the reference's returned waypoints); priced at "
+                         "16 W + 16 + 4 W B/path (SURVEY §8(d))")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -242,47 +246,47 @@ def main():
     pairs = eng.tensor(pairs_host, torch.float64)
     ut = eng.tensor(ut_host, torch.float64)
     P = Q * D
-    outs = eng.outputs(P, W, n_pairs=Q)
+    outs = eng.outputs(P, W, n_pairs=Q, want_cells=args.cells and not volume_mode)
     o = outs[0]
     if args.group is not None:
         eng.set_option("group", args.group)
 
-    def step(ev=None):
-        # one launch: pair order + arc generation + gather + cost reduction + selection
-        if ev is not None:
-            ev[0].record()
+    def step():
+        # one call: sort + arc generation + gather + cost reduction + selection
         if volume_mode:
             eng.eval_generated3d(pairs, ut, volume, outputs=outs)
         else:
             eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
-        if ev is not None:
-            ev[1].record()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # the timed region: ONE HIP event pair on the launch stream (libuampath enqueues on torch's
+    # current stream) around all K steps, so no per-step marker perturbs the launches
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.kernel_timing(True)    # HIP events around the dominant kernel, on its launch stream
     t0 = time.perf_counter()
+    ev0.record()
     for i in range(args.steps):
-        step(events[i])
+        step()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    # cross-check after the timed region: the library's own HIP-event pair around each call's
+    # launch sequence (uam_kernel_timing), same steps
+    eng.kernel_timing(True)
+    for i in range(args.steps):
+        step()
     k_total, k_launches = eng.kernel_time()
     eng.kernel_timing(False)
-    step_ev_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    # every evaluation form is bracketed once per call; the step time stands in otherwise
-    kern_timed = k_launches == args.steps
-    kern_ms = k_total / k_launches if kern_timed else step_ev_ms
+    seq_ms = k_total / k_launches if k_launches == args.steps else None
     if world > 1:
-        elapsed, kern_ms, step_ev_ms = udist.max_over_ranks([elapsed, kern_ms, step_ev_ms],
-                                                            device=eng.torch_device)
+        elapsed, kern_ms = udist.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
 
     total_paths = Q_total * D * args.steps
     value = total_paths / elapsed
@@ -313,16 +317,16 @@ def main():
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
-                                   packed=last in ("K2s+pack", "K2g+pack"), volume=volume_mode)
-    roofline["kernel_ms_source"] = ("HIP events recorded by libuampath around each timed "
-                                    "launch of the kernel (K2g / K2s: around the whole launch "
-                                    "sequence), on its launch stream (uam_kernel_timing)"
-                                    if kern_timed else
-                                    "torch events around the whole step")
+                                   packed=last in ("K2s+pack", "K2g+pack"), volume=volume_mode,
+                                   cells=args.cells and not volume_mode)
+    roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "
+                                    "stream) around the K timed steps / K: the whole launch "
+                                    "sequence of every step (sorts, evaluation, output "
+                                    "launch) and the GPU's gaps between steps")
+    roofline["sequence_ms_library_events"] = (round(seq_ms, 4) if seq_ms is not None else None)
     roofline["library_kernel"] = last
     group = eng.last_group()   # the sum order the library used (0 = sequential)
     roofline["sum_group"] = group
-    roofline["step_event_ms"] = round(step_ev_ms, 4)
     roofline["profile_key"] = pkey
     result = {
         "metric": METRIC,
@@ -377,20 +381,20 @@ def main():
         rd, rec, vd, vox = oracle_inputs(O, geo, raster, volume, mode)
         gpu_cost = o["cost"].cpu().numpy()
         gpu_best = o["best_fval_idx"].cpu().numpy()
+        gpu_cells = o["cells"].cpu().numpy() if "cells" in o else None
         chunk = 50 if mode == "analytic" else 2000
-        done, t_cpu, mism, bmis = 0, 0.0, 0, 0
-        seq_rel = None
+        done, t_cpu, mism, bmis, cmis = 0, 0.0, 0, 0, 0
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
-            r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, group)
+            r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, group,
+                            want_cells=gpu_cells is not None)
             t_cpu += time.perf_counter() - ts
-            if group and seq_rel is None:   # grouped vs the reference's sequential order
-                rs = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, 0)
-                seq_rel = float(np.max(np.abs(r["cost"] - rs["cost"]) /
-                                       np.maximum(np.abs(rs["cost"]), 1e-300)))
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
+            if gpu_cells is not None:
+                cmis += int(np.sum(r["cells"].reshape(-1, W) !=
+                                   gpu_cells[done * D:(done + len(sl)) * D]))
             done += len(sl)
         one_core = done * D / t_cpu
         # the same sample over `threads` contiguous pair shards (ctypes drops the GIL inside
@@ -411,6 +415,20 @@ def main():
                 list(ex.map(lambda k: shard(bounds[k], bounds[k + 1]), range(threads)))
                 wall += time.perf_counter() - ts
                 passes += 1
+            seq = None
+            if group and mode == "raster":
+                # every pair of the batch through the reference's sequential order (threads
+                # over pair shards): how far the grouped sums move the costs and whether they
+                # move either selection
+                sb = np.linspace(0, Q, threads + 1).astype(int)
+
+                def seq_shard(k):
+                    return oracle_eval(O, orc, pairs_host[sb[k]:sb[k + 1]], ut_host, mode, rd,
+                                       rec, vd, vox, 0)
+
+                parts = list(ex.map(seq_shard, range(threads)))
+                seq = {key: np.concatenate([pp[key] for pp in parts])
+                       for key in ("cost", "length")}
         result["cpu_baseline"] = {
             "value": round(passes * done * D / wall, 1), "unit": "candidate-paths/s",
             "cores": threads, "kind": "port", "single_core_value": round(one_core, 1),
@@ -422,9 +440,26 @@ def main():
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
                             "best_index_mismatches": bmis,
                             "rule": f"bit-exact float64 vs CPU oracle (sum order: "
-                                    f"{order_name(group)})"}
-        if seq_rel is not None:
-            result["parity"]["max_rel_cost_vs_sequential_order"] = seq_rel
+                                    f"{order_name(group)}) on the cpu_baseline sample"}
+        if gpu_cells is not None:
+            result["parity"]["cell_index_mismatches"] = cmis
+        if seq is not None:
+            ok = np.isfinite(seq["cost"])
+            rel = np.abs(gpu_cost[ok] - seq["cost"][ok]) / np.maximum(np.abs(seq["cost"][ok]),
+                                                                      1e-300)
+            glen = o["length"].cpu().numpy()
+            result["parity"]["vs_sequential_order"] = {
+                "paths": int(Q * D),
+                "max_rel_cost": float(rel.max()) if rel.size else 0.0,
+                "max_rel_length": float(np.max(np.abs(glen[ok] - seq["length"][ok]) /
+                                               np.maximum(seq["length"][ok], 1e-300))),
+                "best_fval_idx_disagreements": int(np.sum(
+                    O.argmin(seq["cost"], D, True) != gpu_best)),
+                "best_length_idx_disagreements": int(np.sum(
+                    O.argmin(seq["length"], D, False) != o["best_length_idx"].cpu().numpy())),
+                "rule": "the whole batch through the reference's sequential sums "
+                        "(problem.py:38-44, 130-146) against the GPU's grouped sums; "
+                        "north_star tolerance 1e-5 relative on cost"}
             result["parity"]["tolerance_vs_reference"] = 1e-5
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -433,7 +468,7 @@ def main():
         dist.destroy_process_group()
 
 
-def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False):
+def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False, cells=False):
     """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
     definition used in SURVEY, DESIGN §4 and here): raster, one 16-B record gather per waypoint
     + 16 B of outputs per path = 16 W + 16 B/path; volume, one 8-B voxel {risk, psi_nfz} + a
@@ -441,7 +476,7 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
     kernel from this build's rocprofv3 PMC passes (tools/pmc_traffic.py ->
     profiles/traffic.json; 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM), which
     include Infinity-Cache hits: they are not proven DRAM bytes."""
-    bytes_per_path = (12 if volume else 16) * W + 16
+    bytes_per_path = (12 if volume else 16) * W + 16 + (4 * W if cells else 0)
     launch_bytes = bytes_per_path * P
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
     traffic = prof.get("l2_fabric_bytes_per_launch")
@@ -454,6 +489,9 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
          "algorithmic_bytes_per_path": bytes_per_path,
          "algorithmic_bytes_def": ("SURVEY.md §8(d), 3-D: 8-B voxel {risk, psi_nfz} + 4-B DEM "
                                    "per waypoint + 16 B output per path (12 W + 16)" if volume
+                                   else "SURVEY.md §8(d): 16 B record gather per waypoint + "
+                                   "16 B output per path + 4 B waypoint index per waypoint "
+                                   "(16 W + 16 + 4 W)" if cells
                                    else "SURVEY.md §8(d): 16 B record gather per waypoint + "
                                    "16 B output per path (16 W + 16)"),
          "algorithmic_bytes_per_launch": launch_bytes,
@@ -510,11 +548,11 @@ def oracle_inputs(O, geo, raster, volume, mode):
     return rd, rec, vd, vox
 
 
-def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0):
+def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_cells=False):
     if mode == "volume":
         return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
     return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec,
-                          group=group)
+                          group=group, want_cells=want_cells)
 
 
 def order_name(group):

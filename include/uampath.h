@@ -386,8 +386,9 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * sequence of K2g and K2s (sorts, evaluation, output launch; K2s's side-stream sorts are
  * joined inside it), around the k_eval_pairs / k_eval_wave launch of the other forms (excluding
  * their pair order and selection launches).  uam_kernel_time waits for those events and returns
- * the summed time and the count since the last call (then resets the count).  At most 4096
- * events pairs are pending: query at least that often (further timed calls fail UAM_E_STATE). */
+ * the summed time and the count since the last call (then resets both).  Every 4096 timed
+ * calls the pending pairs are folded into a running total (the timed call waits for the last
+ * of them once), so any number of calls may pass between queries. */
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable);
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
 /* The path evaluation the last uam_eval_generated* call on ctx ran: "K2g+pack" (segment-grouped

@@ -41,6 +41,37 @@ def _worker(rank, world, port, q):
         secs = D.broadcast_raster(rec, src=0)
         res["rec_checksum"] = int(rec.to(torch.int64).sum())
         res["bcast_s"] = secs
+
+        # a CostRaster whose derived copies (skip bitmap, packed copy) were built from the
+        # receiver's OLD records: after the broadcast they must not survive (distributed.py
+        # broadcast_raster) -- dropped with no engine, rebuilt from the new records with one
+        from uam_path_planning_amd.engine import CostRaster
+        from uam_path_planning_amd.scenario import raster_geo
+
+        def stale_raster(seed):
+            g = torch.Generator().manual_seed(seed)
+            r = torch.randint(-2**31, 2**31 - 1, (32, 48, 4), dtype=torch.int32, generator=g)
+            return CostRaster(raster_geo(32), r, summary=torch.full((8,), 7 + rank),
+                              block=8, packed=torch.full((16,), 9 + rank))
+
+        cr = stale_raster(123 if rank == 0 else 999)
+        D.broadcast_raster(cr, src=0)
+        res["dropped"] = (cr.summary is None, cr.packed is None,
+                          int(cr.rec.to(torch.int64).sum()))
+
+        class _Rebuild:
+            calls = []
+
+            def raster_summary(self, raster, block, packed=False):
+                # the stub "rebuilds" from the records it is handed: their checksum
+                self.calls.append((block, packed))
+                raster.summary = int(raster.rec.to(torch.int64).sum())
+                raster.packed = raster.summary if packed else None
+
+        cr = stale_raster(123 if rank == 0 else 999)
+        rb = _Rebuild()
+        D.broadcast_raster(cr, src=0, rebuild=rb)
+        res["rebuilt"] = (rb.calls, cr.summary, cr.packed)
         res["max"] = D.max_over_ranks([float(rank), 10.0 - rank])
 
         # the RCCL communicator setup of uam_comm_init: rank 0 draws the id, every rank joins
@@ -87,6 +118,10 @@ def test_gloo_world2():
     assert out[1]["shard_first"] == allp[1000].tolist()
     assert out[0]["shard_sum"] + out[1]["shard_sum"] == pytest.approx(float(allp.sum()))
     assert out[0]["rec_checksum"] == out[1]["rec_checksum"] != 0
+    # stale derived copies: dropped without an engine, rebuilt from the broadcast records
+    ck = out[0]["dropped"][2]
+    assert out[0]["dropped"] == out[1]["dropped"] == (True, True, ck)
+    assert out[0]["rebuilt"] == out[1]["rebuilt"] == ([(8, True)], ck, ck)
     assert out[0]["max"] == out[1]["max"] == [1.0, 10.0]
     assert out[0]["comm"] == (True, 2, 0) and out[1]["comm"] == (True, 2, 1)
     assert out[0]["best"] == out[1]["best"] == (0.5, 57)

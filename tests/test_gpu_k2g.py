@@ -268,3 +268,36 @@ def test_k2g_tuning_knobs(oracle_mod, tbits, lds, curve):
     gpu = e.eval_generated(pairs, ut, raster=raster)
     assert e.last_kernel() == "K2g+pack" and e.last_group() == 21
     _check(gpu, ref, oracle_mod, D)
+
+
+@pytest.mark.parametrize("group,chunk", [(21, 0), (8, 0), (5, 11), (64, 16)])
+def test_k2g_waypoint_cells(oracle_mod, group, chunk):
+    """K2g with waypoint indices requested (the reference's returned waypoints, solver.py:49,
+    main.py:186-190, as raster cells): cfg3's geometry (4096^2, 70 no-fly shapes, N = 80) on a
+    2k-pair subsample, paths leaving the raster and NaN pairs included.  Every cell index
+    (-1 off the raster) equals the oracle's bit for bit, and the other outputs stay those of
+    the grouped oracle (the cell-writing form takes CH = 8 whatever the chunk option)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    e, orc, raster, rd, rec = _case(oracle_mod, group, 80, R=4096, nfz=64)
+    e.set_option("k2g_chunk", chunk)
+    e.raster_summary(raster, 0, packed=True)
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = random_pairs(2000, seed=21)
+    pairs[::53, 2] -= 80.0
+    pairs[7] = np.nan
+    ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec,
+                         group=group, want_cells=True)
+    assert (ref["cells"] == -1).any() and (ref["cells"] >= 0).mean() > 0.5
+    gpu = e.eval_generated(pairs, ut, raster=raster, want_cells=True)
+    assert e.last_kernel() == "K2g+pack" and e.last_group() == group
+    np.testing.assert_array_equal(gpu["cells"].cpu().numpy().reshape(ref["cells"].shape),
+                                  ref["cells"])
+    _check(gpu, ref, oracle_mod, D)
+    # the same batch without cells: identical outputs
+    gpu2 = e.eval_generated(pairs, ut, raster=raster)
+    for gk, _ in KEYS:
+        assert torch.equal(gpu[gk], gpu2[gk]), gk

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -56,11 +57,15 @@ bool values(const std::vector<uint8_t>& b, uint16_t typ, uint32_t count, size_t 
     const size_t sz = typ == 3 ? 2 : typ == 4 ? 4 : 0;
     if (!sz) return false;
     size_t off = entry + 8;
+    // a malformed count (up to 2^32) must fail here, not in resize: the values have to lie
+    // inside the file
+    if ((uint64_t)sz * count > (uint64_t)b.size()) return false;
     if ((uint64_t)sz * count > 4) {
         uint32_t o;
         if (!rd32(b, off, &o)) return false;
         off = o;
     }
+    if ((uint64_t)off + (uint64_t)sz * count > (uint64_t)b.size()) return false;
     out->resize(count);
     for (uint32_t i = 0; i < count; ++i) {
         if (sz == 2) {
@@ -142,6 +147,9 @@ const char* read_tile(const char* path, int32_t th, int32_t tw, float* dst,
     if ((int64_t)t.width != tw || (int64_t)t.length != th)
         return "tile size differs from the mosaic's SrcRect";
     const size_t row = (size_t)tw * 4;
+    // the strips must cover every row: dst is a reused ring buffer, so an uncovered row would
+    // silently keep a previous chunk's pixels
+    if ((uint64_t)t.offsets.size() * t.rps < (uint64_t)th) return "strips do not cover the tile";
     for (size_t s = 0; s < t.offsets.size(); ++s) {
         const uint64_t r0 = (uint64_t)s * t.rps;
         if (r0 >= (uint64_t)th) break;
@@ -200,8 +208,14 @@ class TileReaderPool {
         for (;;) {
             const int32_t i = next_.fetch_add(1);
             if (i >= i1_) return;
-            const char* e =
-                read_tile(paths_[i], th_, tw_, dst_ + (size_t)(i - i0_) * th_ * tw_, &buf);
+            // no exception may leave a pool thread (std::terminate would end the process):
+            // allocation failures become the tile's error
+            const char* e;
+            try {
+                e = read_tile(paths_[i], th_, tw_, dst_ + (size_t)(i - i0_) * th_ * tw_, &buf);
+            } catch (const std::exception&) {
+                e = "out of memory reading the tile";
+            }
             if (e) {
                 std::lock_guard<std::mutex> g(emu_);
                 if (err_tile_ < 0 || i < err_tile_) {

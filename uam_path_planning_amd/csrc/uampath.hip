@@ -4805,6 +4805,7 @@ struct KGrp {
     int32_t* __restrict__ order;   // [n_items] item of each sorted position
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
+    int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
 };
 
 __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
@@ -4949,7 +4950,10 @@ __device__ __forceinline__ double sqrt_mid(double x) {
 // when the whole wave's squared norms are in its range.  Any other chunk runs the general form
 // with the endpoint, range and row tests per waypoint.  Both add exactly the same terms in the
 // same order.
-template <int CH, bool LS, bool MS>
+// CELLS: also write every waypoint's raster cell index (iy nx + ix, -1 off the raster) to
+// kg.cells[path][j], the reference's returned waypoints as raster cells (solver.py:49,
+// main.py:186-190); a compile-time flag, so the form without it is unchanged.
+template <int CH, bool LS, bool MS, bool CELLS = false>
 __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                                                 const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -5085,7 +5089,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
     // reads the plane's first pair, one line per wave, and its value is not used.
     const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
     auto locate = [&](double x0, double x1, int t, uint32_t& inb, uint32_t& need,
-                      uint32_t& full, uint32_t& odd) -> const uint4* {
+                      uint32_t& full, uint32_t& odd, int32_t& cell) -> const uint4* {
         // the cell: floor(t) in [0, n) <=> t in [0, n) for integer n, and the truncating
         // conversion equals floor for t >= 0 (NaN fails both tests)
         const double tx = (x0 - rs.x0) * rs.inv_dx;
@@ -5094,6 +5098,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
         if ((tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny)) {
             inb |= 1u << t;
             const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
+            if (CELLS) cell = iy * rs.nx + ix;
             const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
             const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
             if (code & 2u) {
@@ -5107,6 +5112,9 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
             }
         }
+#ifdef UAM_K2G_DIAG_NOGATHER  // measurement build: every load reads the plane's first pair
+        ptr = dummy;
+#endif
         return ptr;
     };
     // the consume step, branch-free: a lane with nothing gathered adds +0.0 (an exact no-op on
@@ -5131,6 +5139,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
         if (__all(je - jc == CH && je < W)) {  // wave-uniform: the straight-line form
             const bool first = it == 0;
             uint4 r[CH];
+            int32_t cl[CH];
             uint32_t inb = 0, need = 0, full = 0, odd = 0;
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
@@ -5143,33 +5152,52 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 }
                 // the rows of waypoints j0 and (group 0) j0 + 1 belong elsewhere / do not exist
                 const bool rv = !(first && (t == 0 || (t == 1 && j0 == 0)));
+#ifdef UAM_K2G_DIAG_NOGEO  // measurement build: no segment / kinematic work
+                (void)rv;
+                px = x0, py = x1;
+#else
                 if (t == 0 && first && j == 0) {
                     // p_0 of group 0: no segment ends here (the anchor term stands for it)
                     px = x0, py = x1;
                 } else {
                     segment_fast(x0, x1, rv);
                 }
-                r[t] = *locate(x0, x1, t, inb, need, full, odd);
+#endif
+                cl[t] = -1;
+                r[t] = *locate(x0, x1, t, inb, need, full, odd, cl[t]);
             }
 #pragma unroll
             for (int t = 0; t < CH; ++t)
                 consume1(r[t], (inb >> t) & 1u, (need >> t) & 1u, (full >> t) & 1u,
                          (odd >> t) & 1u);
+            if (CELLS) {
+                int32_t* dst = kg.cells + (int64_t)path * W + jc;
+#pragma unroll
+                for (int t = 0; t < CH; ++t) dst[t] = cl[t];
+            }
         } else {  // the general form, one waypoint at a time (the ragged and last chunks)
 #pragma unroll 1
             for (int j = jc; j < je; ++j) {
                 double x0 = px, x1 = py;  // j = 0: p_0, generated above
                 if (j > 0) {
                     point(j, x0, x1);
+#ifndef UAM_K2G_DIAG_NOGEO
                     segment(j, x0, x1);
+#endif
                 }
                 uint32_t inb = 0, need = 0, full = 0, odd = 0;
-                const uint4 r = *locate(x0, x1, 0, inb, need, full, odd);
+                int32_t cl = -1;
+                const uint4 r = *locate(x0, x1, 0, inb, need, full, odd, cl);
                 consume1(r, inb & 1u, need & 1u, full & 1u, odd & 1u);
+                if (CELLS) kg.cells[(int64_t)path * W + j] = cl;
             }
         }
     }
+#ifdef UAM_K2G_DIAG_NOGEO
+    if (false) {
+#else
     if (j1 <= W - 1) {  // the point after the group: its last kinematic row only
+#endif
         double x0, x1;
         point(j1, x0, x1);
         segment(j1, x0, x1);
@@ -5182,7 +5210,20 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
     o.ksum = gk;
     o.hmax = hmax;
     o.cnt = nh | (off << 8);
+#if defined(UAM_K2G_DIAG_NOSLOT)  // measurement build: slots written only when a NaN shows up
+    if (!(gc == gc) || !(gL == gL)) kg.slot[(int64_t)s * kg.P + path] = o;
+#elif defined(UAM_K2G_SLOT_NT)
+    GSlot* dst = kg.slot + (int64_t)s * kg.P + path;
+    __builtin_nontemporal_store(o.cost, &dst->cost);
+    __builtin_nontemporal_store(o.psi, &dst->psi);
+    __builtin_nontemporal_store(o.L, &dst->L);
+    __builtin_nontemporal_store(o.len, &dst->len);
+    __builtin_nontemporal_store(o.ksum, &dst->ksum);
+    __builtin_nontemporal_store(o.hmax, &dst->hmax);
+    __builtin_nontemporal_store(o.cnt, &dst->cnt);
+#else
     kg.slot[(int64_t)s * kg.P + path] = o;
+#endif
 }
 
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout): the partials
@@ -5282,6 +5323,8 @@ struct uam_ctx {
     bool ktime_on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ktime_ev;
     size_t ktime_n = 0;
+    double ktime_acc_ms = 0.0;  // folded pairs (uam_kernel_time reports these + the pending)
+    int64_t ktime_acc_n = 0;
     int k1_cpl = 2;             // K1 cells (rows) per lane: 1 = single-cell kernel, 2, 4, 8
                                 // (UAM_OPT_K1_ROWS)
     hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
@@ -5309,6 +5352,7 @@ struct uam_ctx {
     int k2s_segs = 2;           // K2s segments per path (UAM_OPT_K2S_SEGMENTS: 2..8)
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
+    bool k2g_attrs_cells = false;  // the same for the cell-writing K2g forms
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     uint16_t* d_tkey = nullptr; // K2g: sort key of each tile (curve order), for tkey_bits/curve
@@ -5350,10 +5394,25 @@ int check_ctx(uam_ctx* ctx, bool need_params) {
 
 // Kernel timing (uam_kernel_timing): an event pair recorded on the launch stream around the
 // dominant path kernel; pairs are pooled and reused after uam_kernel_time / a reset.
+// the pending event pairs' times added to the running total (waits for the last of them)
+int ktime_fold(uam_ctx* ctx) {
+    for (size_t i = 0; i < ctx->ktime_n; ++i) {
+        HIP_TRY(hipEventSynchronize(ctx->ktime_ev[i].second));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, ctx->ktime_ev[i].first, ctx->ktime_ev[i].second));
+        ctx->ktime_acc_ms += ms;
+    }
+    ctx->ktime_acc_n += (int64_t)ctx->ktime_n;
+    ctx->ktime_n = 0;
+    return UAM_OK;
+}
+
 int ktime_begin(uam_ctx* ctx, hipStream_t s) {
     if (!ctx->ktime_on) return UAM_OK;
-    if (ctx->ktime_n >= 4096)
-        return fail(UAM_E_STATE, "kernel timing: 4096 event pairs pending, call uam_kernel_time");
+    if (ctx->ktime_n >= 4096) {  // fold the pending pairs into the running total (one wait)
+        const int st = ktime_fold(ctx);
+        if (st) return st;
+    }
     if (ctx->ktime_n == ctx->ktime_ev.size()) {
         hipEvent_t a, b;
         HIP_TRY(hipEventCreate(&a));
@@ -5943,6 +6002,8 @@ int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
     ctx->ktime_on = enable != 0;
     ctx->ktime_n = 0;
+    ctx->ktime_acc_ms = 0.0;
+    ctx->ktime_acc_n = 0;
     return UAM_OK;
 }
 
@@ -6055,16 +6116,12 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
     if (!ctx || !ms_total || !launches) return fail(UAM_E_INVALID, "NULL argument");
     DeviceGuard dg(ctx->device);
-    double tot = 0.0;
-    for (size_t i = 0; i < ctx->ktime_n; ++i) {
-        HIP_TRY(hipEventSynchronize(ctx->ktime_ev[i].second));
-        float ms = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&ms, ctx->ktime_ev[i].first, ctx->ktime_ev[i].second));
-        tot += ms;
-    }
-    *ms_total = tot;
-    *launches = (int64_t)ctx->ktime_n;
-    ctx->ktime_n = 0;
+    const int st = ktime_fold(ctx);
+    if (st) return st;
+    *ms_total = ctx->ktime_acc_ms;
+    *launches = ctx->ktime_acc_n;
+    ctx->ktime_acc_ms = 0.0;
+    ctx->ktime_acc_n = 0;
     return UAM_OK;
 }
 
@@ -6345,7 +6402,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                           int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
                           int32_t* best_f, int32_t* best_l, hipStream_t s) {
     const int G = ctx->k2g_group;
-    if (G < 1 || G > G_MAXLEN || !kr.pmap || ko.cells || ko.g_rows || D > 16) return 0;
+    if (G < 1 || G > G_MAXLEN || !kr.pmap || ko.g_rows || D > 16) return 0;
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
     const size_t ubytes = (size_t)D * ctx->kp.N * 16;  // the unit-arc rows, staged in LDS
@@ -6407,7 +6464,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
                         k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
-    static const EvalFn evals[16] = {UAM_G_EVALS(6), UAM_G_EVALS(8), UAM_G_EVALS(11),
+    #ifndef UAM_K2G_CH6
+#define UAM_K2G_CH6 6
+#endif
+    static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8), UAM_G_EVALS(11),
                                      UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
@@ -6430,7 +6490,20 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int ch = (chl == 6 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                    (ctx->kp.length_smooth ? 2 : 0) +
                    (ctx->kp.maxratio_smooth ? 1 : 0);
-    hipLaunchKernelGGL(evals[ch], ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    // with waypoint cells requested: the CH = 8 form that also writes them
+    static const EvalFn evals_cells[4] = {k_g_eval<8, false, false, true>,
+                                          k_g_eval<8, false, true, true>,
+                                          k_g_eval<8, true, false, true>,
+                                          k_g_eval<8, true, true, true>};
+    kg.cells = ko.cells;
+    const EvalFn ev = ko.cells ? evals_cells[ch & 3] : evals[ch];
+    if (lds > 64 * 1024 && !ctx->k2g_attrs_cells && ko.cells) {
+        for (EvalFn f : evals_cells)
+            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+        ctx->k2g_attrs_cells = true;
+    }
+    hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
