@@ -293,7 +293,12 @@ def main():
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    if last.startswith("K2g"):
+    if last.startswith("K2h"):
+        ktag = last.lower()
+        kernel_name = ("K2h sequence (k_g_hist (+ the unit-arc sums) / k_scan / k_g_scatter, "
+                       "k_h_eval over every (path, group) item: points, cells, records; "
+                       "k_h_final: the similarity-form geometry, grouped sums, selection)")
+    elif last.startswith("K2g"):
         ktag = last.lower()
         kernel_name = ("K2g sequence (k_g_hist / k_scan / k_g_scatter, k_g_eval over every "
                        "(path, group) item with its share of pass 1, k_g_final)")
@@ -317,7 +322,8 @@ def main():
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
-                                   packed=last in ("K2s+pack", "K2g+pack"), volume=volume_mode,
+                                   packed=last in ("K2s+pack", "K2g+pack", "K2h+pack"),
+                                   volume=volume_mode,
                                    cells=args.cells and not volume_mode)
     roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "
                                     "stream) around the K timed steps / K: the whole launch "
@@ -368,7 +374,7 @@ def main():
         result["parity"] = {"paths_checked": m[0], "cost_mismatches": m[1],
                             "best_index_mismatches": m[2], "ranks": world,
                             "rule": f"bit-exact float64 vs CPU oracle (sum order: "
-                                    f"{order_name(group)}), first "
+                                    f"{order_name(group, last)}), first "
                                     f"{PARITY_PAIRS_PER_RANK} pairs of every rank's shard"}
 
     # ---- CPU baseline + parity sample (rank 0, N=1 only) ----------------------------------
@@ -388,7 +394,7 @@ def main():
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
             r = oracle_eval(O, orc, sl, ut_host, mode, rd, rec, vd, vox, group,
-                            want_cells=gpu_cells is not None)
+                            want_cells=gpu_cells is not None, kernel=last)
             t_cpu += time.perf_counter() - ts
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
@@ -405,7 +411,7 @@ def main():
         def shard(lo, hi):
             for c0 in range(lo, hi, chunk):
                 oracle_eval(O, orc, sample[c0:min(hi, c0 + chunk)], ut_host, mode, rd, rec, vd,
-                            vox)
+                            vox, group, kernel=last)
 
         bounds = np.linspace(0, done, threads + 1).astype(int)
         passes, wall = 0, 0.0
@@ -440,7 +446,7 @@ def main():
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
                             "best_index_mismatches": bmis,
                             "rule": f"bit-exact float64 vs CPU oracle (sum order: "
-                                    f"{order_name(group)}) on the cpu_baseline sample"}
+                                    f"{order_name(group, last)}) on the cpu_baseline sample"}
         if gpu_cells is not None:
             result["parity"]["cell_index_mismatches"] = cmis
         if seq is not None:
@@ -548,14 +554,26 @@ def oracle_inputs(O, geo, raster, volume, mode):
     return rd, rec, vd, vox
 
 
-def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_cells=False):
+def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_cells=False,
+                kernel=None):
+    """The oracle's statement of what `kernel` (uam_last_kernel) computes: K2h -> the
+    similarity form with grouped raster sums (orc_eval_generated_h), K2g -> the grouped order
+    (orc_eval_paths_g), otherwise / kernel=None with group 0 -> the reference's sequential
+    order."""
     if mode == "volume":
         return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
+    if kernel == "K2h+pack":
+        return orc.eval_generated_h(pairs, ut_host, rdesc=rd, rec=rec, group=group,
+                                    want_cells=want_cells)
     return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec,
                           group=group, want_cells=want_cells)
 
 
-def order_name(group):
+def order_name(group, kernel=None):
+    if kernel == "K2h+pack":
+        return (f"raster sums as per-path partial sums over groups of {group} waypoints, added "
+                f"in group order; the geometry terms in the similarity form (oracle "
+                f"orc_eval_generated_h)")
     return (f"per-path partial sums over groups of {group} waypoints, added in group order "
             f"(oracle orc_eval_paths_g)" if group else "sequential, the reference's")
 
@@ -571,7 +589,8 @@ def rank_parity(eng, spec, params, mode, geo, raster, volume, pairs_host, ut_hos
                    altitude=params.altitude)
     n = min(PARITY_PAIRS_PER_RANK, len(pairs_host))
     rd, rec, vd, vox = oracle_inputs(O, geo, raster, volume, mode)
-    r = oracle_eval(O, orc, pairs_host[:n], ut_host, mode, rd, rec, vd, vox, group)
+    r = oracle_eval(O, orc, pairs_host[:n], ut_host, mode, rd, rec, vd, vox, group,
+                    kernel=eng.last_kernel())
     cost = o["cost"][:n * D].cpu().numpy()
     best = o["best_fval_idx"][:n].cpu().numpy()
     return [float(n * D), float(np.sum(r["cost"] != cost)),

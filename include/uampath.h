@@ -427,9 +427,15 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                (default) = tiles of ~256 x 256 cells
  *   UAM_OPT_K2G_LDS_FLOOR        K2g evaluation: dynamic-LDS floor per workgroup in bytes, which
  *                                caps the workgroups resident per CU (default 0)
- *   UAM_OPT_K2G_CHUNK            K2g evaluation: gathers in flight per lane, 6/8/11/16 (16 runs
- *                                two waves per SIMD); 0 (default) = 8
- *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order */
+ *   UAM_OPT_K2G_CHUNK            K2g / K2h evaluation: gathers in flight per lane, 6/7/8/11/16
+ *                                (K2g: 7 runs as 6, 16 at two waves per SIMD); 0 (default) = 8
+ *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order
+ *   UAM_OPT_K2G_SIM              1 (default): generated raster batches take K2h, K2g's sort and
+ *                                grouped raster sums with the geometry terms (L, length,
+ *                                kinematic rows) in the similarity form -- the unit arc's sums
+ *                                scaled by |x0 - xf| / 2 (oracle orc_eval_generated_h; needs
+ *                                maxratio_smooth = 0); 0: K2g, the geometry per waypoint
+ *                                segment in the grouped order (orc_eval_paths_g) */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -444,7 +450,8 @@ enum {
     UAM_OPT_K2G_TILE_BITS = 11,
     UAM_OPT_K2G_LDS_FLOOR = 12,
     UAM_OPT_K2G_CHUNK = 13,
-    UAM_OPT_K2G_CURVE = 14
+    UAM_OPT_K2G_CURVE = 14,
+    UAM_OPT_K2G_SIM = 15
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

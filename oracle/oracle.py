@@ -256,6 +256,47 @@ class Oracle:
             out["cells"] = cells
         return out
 
+    # -- generated candidates, similarity form (K2h / K4h) ---------------------------------
+    def eval_generated_h(self, pairs, utab, mode="raster", rdesc=None, rec=None, vdesc=None,
+                         vol=None, group=0, want_cells=False):
+        """Candidates of pairs ([Q, 4], or [Q, 6] with altitudes in volume mode) x the rows of
+        utab [D, N, 2], path q*D + d: the geometry terms in the similarity form (the unit
+        polyline's sums scaled by h = |x0 - xf| / 2), the raster / volume terms per generated
+        waypoint with their sums grouped by `group` (0: sequential) -- uam_oracle.c
+        orc_eval_generated_h, the definition K2h / K4h reproduce."""
+        W = self.N + 2
+        ut = np.ascontiguousarray(utab, dtype=np.float64)
+        D = ut.shape[0]
+        m = 1 if mode == "raster" else 2
+        pr = np.ascontiguousarray(pairs, dtype=np.float64).reshape(-1, 4 if m == 1 else 6)
+        Q = pr.shape[0]
+        P = Q * D
+        out = {k: np.zeros(P) for k in ("cost", "lq", "length", "kin", "nfz", "min_clearance")}
+        for k in ("nfz_hits", "offmap", "below"):
+            out[k] = np.zeros(P, np.int32)
+        cells = np.zeros((P, W), np.int32) if want_cells else None
+        vox = cols = None
+        if m == 1:
+            rec = np.ascontiguousarray(rec, dtype=np.float32)
+        else:
+            vox = np.ascontiguousarray(vol[0], dtype=np.float32)
+            cols = np.ascontiguousarray(vol[1], dtype=np.float32)
+        st = lib().orc_eval_generated_h(
+            ctypes.byref(self.g), ctypes.byref(self.p), ctypes.c_int32(m),
+            None if rdesc is None else ctypes.byref(rdesc), _ptr(rec if m == 1 else None, _f32p),
+            None if vdesc is None else ctypes.byref(vdesc), _ptr(vox, _f32p),
+            _ptr(cols, _f32p), _ptr(pr, _f64p), ctypes.c_int64(Q), _ptr(ut, _f64p),
+            ctypes.c_int32(D), ctypes.c_int32(int(group)), _ptr(out["cost"], _f64p),
+            _ptr(out["lq"], _f64p), _ptr(out["length"], _f64p), _ptr(out["kin"], _f64p),
+            _ptr(out["nfz"], _f64p), _ptr(out["nfz_hits"], _i32p),
+            _ptr(out["min_clearance"], _f64p), _ptr(out["offmap"], _i32p),
+            _ptr(out["below"], _i32p), _ptr(cells, _i32p))
+        if st != 0:
+            raise ValueError("the similarity form needs maxratio_smooth = False")
+        if want_cells:
+            out["cells"] = cells
+        return out
+
     # -- points ----------------------------------------------------------------------------
     def eval_points(self, pts):
         pts = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 2)

@@ -587,6 +587,179 @@ int orc_eval_paths3d(const orc_geom* g, const orc_params* p, const orc_volume* v
     return 0;
 }
 
+/* ---- generated candidates in the similarity form (K2h / K4h) ----------------
+ * The candidates of solver.py:103-136 are circular arcs from x0 to xf; restated through the
+ * unit-arc table (orc_gen_paths) they are p_k = C + (1/2) R(v) u_k with v = x0 - xf,
+ * R(v) = [[vx, -vy], [vy, vx]], u_1..u_N the table row of displacement d and u_0 = (1, 0),
+ * u_{N+1} = (-1, 0) (then p_0 = x0, p_{N+1} = xf).  The path is the unit polyline u under a
+ * similarity of scale h = |v| / 2: every chord is h times the unit chord b_k = |u_k - u_{k-1}|
+ * and every turn angle is the unit polyline's.  The path terms that depend on the geometry
+ * only are therefore per-displacement constants scaled by h (maxratio_smooth = 0):
+ *   length_of (problem.py:130-146)   sum_k nrm(p_k - p_{k-1}) = h S1 (nrm = norm_2) or
+ *                                    h^2 S2 (smooth: norm_2(.)**2), over k = 1..N (get_cost's
+ *                                    L with the quirk, plus its anchor term nrm(p_0 - anchor))
+ *                                    or k = 1..N+1 (the true length, solver.py:49)
+ *   get_nonlincon rows (problem.py:100-107)  c1 + c2 = h max(0, b_{k+2} - r b_{k+1})
+ *                                    + h max(0, b_{k+1}/r - b_{k+2}), c3 = max(0, mincos - cos of
+ *                                    the unit turn), summed: h E12 + E3 (0 for h = 0, NaN, inf:
+ *                                    the reference's rows are max(0, NaN) = 0 there)
+ * Exact in real arithmetic; in float64 these differ from the per-segment sums of the
+ * waypoints by rounding only (bench.py's parity.vs_sequential_order measures it on the whole
+ * cfg3 batch).  The raster / volume terms are evaluated per waypoint exactly as in
+ * orc_eval_paths_g / orc_eval_paths3d at the generated points (gen_point), their sums in the
+ * grouped order of `group` (0: sequential).  Build-defined: the definition the GPU's K2h / K4h
+ * reproduce bit for bit. */
+typedef struct {
+    double s1n, s2n, s1a, s2a, e12, e3;
+} orc_unit_geo;
+
+/* the unit polyline's sums for one table row u [N][2] (every order below is the definition) */
+static void unit_geo(const orc_params* p, const double* u, orc_unit_geo* t) {
+    const int N = p->N;
+    const double mincos = cos(p->maxalpha), r = p->maxratio;
+    double s1n = 0.0, s2n = 0.0, s1a = 0.0, s2a = 0.0, e12 = 0.0, e3 = 0.0;
+    double qx = 1.0, qy = 0.0, pdx = 0.0, pdy = 0.0, pb = 0.0;
+    for (int k = 1; k <= N + 1; ++k) {
+        const double cx = (k <= N) ? u[2 * (k - 1)] : -1.0;
+        const double cy = (k <= N) ? u[2 * (k - 1) + 1] : 0.0;
+        const double dx = cx - qx, dy = cy - qy;
+        const double b = sqrt(dx * dx + dy * dy);
+        if (k <= N) {
+            s1n = s1n + b;
+            s2n = s2n + b * b;
+        }
+        s1a = s1a + b;
+        s2a = s2a + b * b;
+        if (k >= 2) { /* row k - 2: chords k - 1 and k */
+            e12 = e12 + fmax(0.0, b - r * pb);
+            e12 = e12 + fmax(0.0, pb / r - b);
+            const double dt = pdx * dx + pdy * dy;
+            e3 = e3 + fmax(0.0, mincos - dt / (pb * b));
+        }
+        qx = cx, qy = cy, pdx = dx, pdy = dy, pb = b;
+    }
+    t->s1n = s1n, t->s2n = s2n, t->s1a = s1a, t->s2a = s2a, t->e12 = e12, t->e3 = e3;
+}
+
+/* the geometry terms of one candidate: pair (x0, y0, xf, yf), the row's unit sums */
+static void sim_geo(const orc_params* p, const orc_unit_geo* t, double x0, double y0, double xf,
+                    double yf, double* L, double* len, double* ksum) {
+    const double vx = x0 - xf, vy = y0 - yf;
+    const double s = vx * vx + vy * vy;
+    const double h = sqrt(s) * 0.5, h2 = s * 0.25;
+    const int ls = p->length_smooth != 0;
+    if (p->quirk_length) {
+        const double ax = p->anchor_mode ? p->anchor_x : x0;
+        const double ay = p->anchor_mode ? p->anchor_y : y0;
+        const double dx = x0 - ax, dy = y0 - ay;
+        const double a = nrm_of(dx * dx + dy * dy, ls);
+        *L = a + (ls ? h2 * t->s2n : h * t->s1n);
+    } else {
+        *L = ls ? h2 * t->s2a : h * t->s1a;
+    }
+    *len = h * t->s1a;
+    *ksum = (h > 0.0 && h < INFINITY) ? h * t->e12 + t->e3 : 0.0;
+}
+
+/* mode 1: raster (rs, rec; pairs [Q][4]); mode 2: volume (v, vox [ny][nx][nz][2],
+ * cols [ny][nx][2]; pairs [Q][6] = (x0, y0, z0, xf, yf, zf)).  Path q D + d.  below: volume
+ * only.  Returns -1 for maxratio_smooth (its turn rows are not scale-free). */
+int orc_eval_generated_h(const orc_geom* g, const orc_params* p, int32_t mode,
+                         const orc_raster* rs, const float* rec, const orc_volume* v,
+                         const float* vox, const float* cols, const double* pairs, int64_t Q,
+                         const double* utab, int32_t D, int32_t group, double* cost, double* lq,
+                         double* length, double* kin, double* nfz, int32_t* hits,
+                         double* minclr, int32_t* offmap, int32_t* below, int32_t* cells) {
+    if (p->maxratio_smooth || (mode != 1 && mode != 2)) return -1;
+    const int N = p->N, W = N + 2;
+    const int G = group > 0 ? group : 0;
+    orc_unit_geo* ug = (orc_unit_geo*)malloc(sizeof(orc_unit_geo) * (size_t)D);
+    for (int d = 0; d < D; ++d) unit_geo(p, utab + (int64_t)d * N * 2, &ug[d]);
+    const int stride = mode == 1 ? 4 : 6;
+    const double idx = mode == 1 ? 1.0 / rs->dx : 1.0 / v->dx;
+    const double idy = mode == 1 ? 1.0 / rs->dy : 1.0 / v->dy;
+    const double idz = mode == 2 ? 1.0 / v->dz : 0.0;
+    for (int64_t q = 0; q < Q; ++q) {
+        const double* pr6 = pairs + stride * q;
+        const double pr[4] = {pr6[0], pr6[1], pr6[stride == 4 ? 2 : 3], pr6[stride == 4 ? 3 : 4]};
+        for (int d = 0; d < D; ++d) {
+            const int64_t pi = q * D + d;
+            double L, len, ks;
+            sim_geo(p, &ug[d], pr[0], pr[1], pr[2], pr[3], &L, &len, &ks);
+            gacc ac, an;
+            gacc_init(&ac, (double)(N + 1) * L, G);
+            gacc_init(&an, 0.0, G);
+            double hmax = -INFINITY, cm = INFINITY;
+            int32_t nh = 0, off = 0, bel = 0;
+            for (int j = 0; j < W; ++j) {
+                double x0, x1;
+                if (j == 0) {
+                    x0 = pr[0], x1 = pr[1];
+                } else if (j == W - 1) {
+                    x0 = pr[2], x1 = pr[3];
+                } else {
+                    gen_point(pr, utab + ((int64_t)d * N + (j - 1)) * 2, &x0, &x1);
+                }
+                if (mode == 1) {
+                    const double fx = floor((x0 - rs->x0) * idx);
+                    const double fy = floor((rs->y_top - x1) * idy);
+                    if (!((fx >= 0.0) && (fx < (double)rs->nx) && (fy >= 0.0) &&
+                          (fy < (double)rs->ny))) {
+                        ++off;
+                        if (cells) cells[pi * W + j] = -1;
+                        if (0.0 > hmax) hmax = 0.0; /* off-raster counts as sea level */
+                        continue;
+                    }
+                    const int64_t cell = (int64_t)fy * rs->nx + (int64_t)fx;
+                    if (cells) cells[pi * W + j] = (int32_t)cell;
+                    const float* rc = rec + 4 * cell;
+                    uint32_t fl;
+                    memcpy(&fl, &rc[3], 4);
+                    gacc_add(&ac, j, (double)rc[0] / (double)N);
+                    gacc_add(&an, j, (double)rc[1]);
+                    nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
+                    const double terrain = (fl & ORC_FLAG_NODATA) ? 0.0 : (double)rc[2];
+                    if (terrain > hmax) hmax = terrain;
+                } else {
+                    const double z = pr6[2] + (pr6[5] - pr6[2]) * ((double)j / (double)(W - 1));
+                    const double fx = floor((x0 - v->x0) * idx);
+                    const double fy = floor((v->y_top - x1) * idy);
+                    const double fz = floor((z - v->z0) * idz);
+                    if (!(fx >= 0.0 && fx < (double)v->nx && fy >= 0.0 && fy < (double)v->ny &&
+                          fz >= 0.0 && fz < (double)v->nz)) {
+                        ++off;
+                        if (cells) cells[pi * W + j] = -1;
+                        continue;
+                    }
+                    const int64_t ci = (int64_t)fy * v->nx + (int64_t)fx;
+                    const int64_t vi = ci * v->nz + (int64_t)fz;
+                    if (cells) cells[pi * W + j] = (int32_t)vi;
+                    const float* r = vox + 2 * vi;
+                    const float terrain = cols[2 * ci];
+                    uint32_t fl;
+                    memcpy(&fl, &cols[2 * ci + 1], 4);
+                    gacc_add(&ac, j, (double)r[0] / (double)N);
+                    gacc_add(&an, j, (double)r[1]);
+                    nh += (fl & ORC_FLAG_NFZ) ? 1 : 0;
+                    bel += (v->z0 + (fz + 0.5) * v->dz < (double)terrain) ? 1 : 0;
+                    cm = fmin(cm, z - (double)terrain);
+                }
+            }
+            if (cost) cost[pi] = gacc_done(&ac);
+            if (lq) lq[pi] = L;
+            if (length) length[pi] = len;
+            if (kin) kin[pi] = ks;
+            if (nfz) nfz[pi] = gacc_done(&an);
+            if (hits) hits[pi] = nh;
+            if (offmap) offmap[pi] = off;
+            if (minclr) minclr[pi] = mode == 1 ? p->altitude - hmax : cm;
+            if (below) below[pi] = bel;
+        }
+    }
+    free(ug);
+    return 0;
+}
+
 /* ---- batched refinement (no pinned reference output) ----------------
  * Restates the build's ALM refinement (include/uampath.h uam_refine): the reference solves
  *   min get_cost(z)  s.t.  get_nonlincon(z) in {0}            (solver.py:82-93)

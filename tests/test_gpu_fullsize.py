@@ -15,6 +15,8 @@ north_star bar is 1e-5 relative on cost, bit-exact on indices)."""
 import numpy as np
 import pytest
 
+import kernel_ref
+
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
@@ -118,8 +120,8 @@ def test_cfg4_geotiff_tiles_8192(eng, oracle_mod, tmp_path):
     sub = np.sort(np.random.default_rng(7).choice(len(pairs), 2000, replace=False))
     rd = oracle_mod.Oracle.raster_desc(g.nx, g.ny, g.x0, g.y_top, g.dx, g.dy, g.nodata,
                                        g.dem_threshold)
-    ref = orc.eval_paths(oracle_mod.gen_paths(pairs[sub], ut), mode="raster", rdesc=rd,
-                         rec=rec.view(np.float32), group=eng.last_group())
+    ref = kernel_ref.raster_ref(oracle_mod, orc, eng.last_kernel(), eng.last_group(),
+                                pairs[sub], ut, rd, rec.view(np.float32))
     _check_subsample(oracle_mod, gpu, ref, sub, D)
     assert (ref["nfz_hits"] > 0).any()
     _check_properties(eng, oracle_mod, launch, pairs, gpu, D)

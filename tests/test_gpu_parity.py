@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import golden_io as G
+import kernel_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -324,19 +325,21 @@ def test_full_size_cfg3_properties(eng, oracle_mod):
     oracle on a 2k-pair subsample (bit-exact), size-independent properties on the rest."""
     orc, raster, rd, rec, pairs, ut = _raster_case(eng, oracle_mod, 4096, 100_000, 80, nfz=64)
     gpu = eng.eval_generated(pairs, ut, raster=raster)
-    assert eng.last_kernel() == "K2g+pack"     # the default for this batch size
+    assert eng.last_kernel() == "K2h+pack"     # the default for this batch size
     group = eng.last_group()
     assert group > 0
     sub = np.random.default_rng(7).choice(len(pairs), 2000, replace=False)
     sub.sort()
     wp = oracle_mod.gen_paths(pairs[sub], ut)
-    ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, group=group)
+    ref = kernel_ref.raster_ref(oracle_mod, orc, eng.last_kernel(), group, pairs[sub], ut, rd,
+                                rec)
     idx = (sub[:, None] * 5 + np.arange(5)).reshape(-1)
     for gk, ok in PATH_KEYS:
         np.testing.assert_array_equal(_np(gpu[gk])[idx], ref[ok], err_msg=gk)
-    # the grouped sums against the reference's sequential order: rounding only (bar 1e-5)
+    # against the reference's per-segment sequential sums: rounding only (bar 1e-5)
     seq = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
     np.testing.assert_allclose(_np(gpu["cost"])[idx], seq["cost"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(_np(gpu["length"])[idx], seq["length"], rtol=1e-12, atol=0)
     cost, lq = _np(gpu["cost"]), _np(gpu["length_q"])
     assert np.isfinite(cost).all()
     assert (cost >= 81 * lq - 1e-9).all()                 # penalties are non-negative
@@ -402,14 +405,16 @@ def test_raster_kernels_bit_identical(eng, oracle_mod, D):
     ref = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
     seen = set()
     try:
-        for wmax, smin, group in ((1 << 40, 65536, 8), (0, 65536, 8), (0, 0, 0), (0, 0, 8)):
+        for wmax, smin, group, sim in ((1 << 40, 65536, 8, 1), (0, 65536, 8, 1), (0, 0, 0, 1),
+                                       (0, 0, 8, 1), (0, 0, 8, 0)):
             eng.set_option("wave_max_paths", wmax)
             eng.set_option("sorted_min_paths", smin)
             eng.set_option("group", group)
+            eng.set_option("k2g_sim", sim)
             gpu = eng.eval_generated(pairs, ut, raster=raster)
             seen.add(eng.last_kernel())
-            r = ref if eng.last_group() == 0 else orc.eval_paths(
-                wp, mode="raster", rdesc=rd, rec=rec, group=eng.last_group())
+            r = ref if eng.last_group() == 0 else kernel_ref.raster_ref(
+                oracle_mod, orc, eng.last_kernel(), eng.last_group(), pairs, ut, rd, rec)
             _assert_paths_equal(gpu, r, raster=True)
             np.testing.assert_array_equal(_np(gpu["best_fval_idx"]),
                                           oracle_mod.argmin(r["cost"], D, True))
@@ -422,7 +427,9 @@ def test_raster_kernels_bit_identical(eng, oracle_mod, D):
         eng.set_option("wave_max_paths", 16384)
         eng.set_option("sorted_min_paths", 65536)
         eng.set_option("group", 21)
-    assert seen == ({"K2w", "K2d"} if D > 16 else {"K2w", "K2+skip", "K2s+pack", "K2g+pack"})
+        eng.set_option("k2g_sim", 1)
+    assert seen == ({"K2w", "K2d"} if D > 16 else
+                    {"K2w", "K2+skip", "K2s+pack", "K2h+pack", "K2g+pack"})
     with pytest.raises(ValueError):
         eng.set_option("wave_max_paths", -1)
 

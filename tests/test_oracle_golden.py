@@ -235,3 +235,106 @@ def test_grouped_sum_order(oracle_mod, group):
     for k in ("cost", "lq", "length", "kin", "nfz"):
         np.testing.assert_allclose(grp[k], seq[k], rtol=1e-12, atol=1e-300, err_msg=k)
     assert (seq["offmap"] > 0).any() and (seq["nfz"] > 0).any() and (seq["kin"] > 0).any()
+
+
+def _similarity_restatement(pairs, ut, N, p):
+    """Pure-Python statement of the similarity form (independent of uam_oracle.c): per
+    displacement row the unit polyline u_0 = (1, 0), u_1..u_N = the table row, u_{N+1} =
+    (-1, 0), its chord sums and row sums; per candidate h = |x0 - xf| / 2 scales them.
+    Returns per path (L, length, kinematic sum)."""
+    import math
+    mincos, r = math.cos(p["maxalpha"]), p["maxratio"]
+    ug = []
+    for row in ut:
+        pts = [(1.0, 0.0)] + [tuple(x) for x in row] + [(-1.0, 0.0)]
+        s1n = s2n = s1a = s2a = e12 = e3 = 0.0
+        pb = pdx = pdy = 0.0
+        for k in range(1, N + 2):
+            dx, dy = pts[k][0] - pts[k - 1][0], pts[k][1] - pts[k - 1][1]
+            b = math.sqrt(dx * dx + dy * dy)
+            if k <= N:
+                s1n, s2n = s1n + b, s2n + b * b
+            s1a, s2a = s1a + b, s2a + b * b
+            if k >= 2:
+                e12 = e12 + max(0.0, b - r * pb)
+                e12 = e12 + max(0.0, pb / r - b)
+                e3 = e3 + max(0.0, mincos - (pdx * dx + pdy * dy) / (pb * b))
+            pb, pdx, pdy = b, dx, dy
+        ug.append((s1n, s2n, s1a, s2a, e12, e3))
+    out = []
+    for x0, y0, xf, yf in pairs:
+        vx, vy = x0 - xf, y0 - yf
+        s = vx * vx + vy * vy
+        h, h2 = math.sqrt(s) * 0.5, s * 0.25
+        for s1n, s2n, s1a, s2a, e12, e3 in ug:
+            L = 0.0 + (h2 * s2n if p["length_smooth"] else h * s1n)   # anchor = p_0: 0
+            ks = h * e12 + e3 if (h > 0.0 and h < math.inf) else 0.0
+            out.append((L, h * s1a, ks))
+    return out
+
+
+@pytest.mark.parametrize("maxalpha", [np.pi / 80, 0.015])
+def test_similarity_form(oracle_mod, maxalpha):
+    """K2h's definition (orc_eval_generated_h): the geometry terms from the unit arc's sums
+    scaled by h = |x0 - xf| / 2 equal a pure-Python statement bit for bit, and the reference's
+    per-segment sums (problem.py:100-107, 130-146; orc_eval_paths) within rounding; the raster
+    terms are the grouped order's (orc_eval_paths_g) bit for bit: no-fly sums, hits, off-raster
+    counts, clearance, waypoint cells."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements, raster_geo
+    from uam_path_planning_amd.synthetic import random_pairs, synthetic_dem
+
+    spec = canonical_spec(nfz_polygons=8)
+    N = 80
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                            maxalpha, spec["enlargement"], spec["weights"], altitude=320.0)
+    geo = raster_geo(256)
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                       geo.nodata, geo.dem_threshold)
+    rec = orc.raster_build(rd, synthetic_dem(256))
+    pairs = random_pairs(80, seed=14)
+    pairs[::7, 0] += 40.0
+    pairs[5, :2] = pairs[5, 2:] + [0.7, -0.4]
+    pairs[9, 2:] = pairs[9, :2]          # start == goal
+    ut = arc_table(N, displacements(5))
+    wp = oracle_mod.gen_paths(pairs, ut)
+    seq = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, want_cells=True)
+    for G in (0, 21):
+        h = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=G, want_cells=True)
+        grp = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec, group=G)
+        opts = dict(spec["options"], maxratio=spec["maxratio"], maxalpha=maxalpha)
+        py = _similarity_restatement(pairs, ut, N, opts)
+        for i, (L, ln, ks) in enumerate(py):
+            assert (L, ln, ks) == (h["lq"][i], h["length"][i], h["kin"][i]), i
+        for k in ("nfz_hits", "offmap", "min_clearance", "cells"):
+            np.testing.assert_array_equal(h[k], seq[k], err_msg=k)
+        np.testing.assert_array_equal(h["nfz"], grp["nfz"])
+        ok = seq["length"] > 0
+        for k in ("cost", "lq", "length"):
+            np.testing.assert_allclose(h[k][ok], seq[k][ok], rtol=1e-12, err_msg=k)
+        np.testing.assert_allclose(h["kin"], seq["kin"], rtol=1e-11, atol=1e-13)
+        assert (h["kin"] > 0).any() == (maxalpha < 0.02)
+
+
+def test_similarity_form_canonical_goldens(oracle_mod):
+    """The similarity form on the reference's own canonical scenario (main.py: N = 80, the 5
+    displacements of main.py:160): L, the length and the kinematic rows' sum agree with the
+    reference's recorded values (create_x_init's transcendental waypoints, per-segment sums)
+    within 1e-12 -- the geometry does not depend on the raster, a small one serves."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import raster_geo
+
+    meta, arr = G.canonical()
+    orc = _oracle(oracle_mod, meta)
+    geo = raster_geo(64)
+    rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
+                                       geo.nodata, geo.dem_threshold)
+    rec = np.zeros((64, 64, 4), np.float32)
+    xs, xg = meta["map"]["x_start"], meta["map"]["x_goal"]
+    pair = np.array([[xs[0], xs[1], xg[0], xg[1]]])
+    h = orc.eval_generated_h(pair, arc_table(meta["N"], meta["displacements"]), rdesc=rd,
+                             rec=rec, group=21)
+    np.testing.assert_allclose(h["lq"], arr["lq"], rtol=1e-12)
+    np.testing.assert_allclose(h["length"], arr["length"], rtol=1e-12)
+    N = meta["N"]
+    np.testing.assert_allclose(h["kin"], arr["g"][:, :3 * N].sum(1), rtol=1e-12, atol=1e-12)

@@ -4788,6 +4788,42 @@ struct alignas(16) GSlot {  // 48 B per (path, group), written by one lane
     uint32_t cnt;    // nfz hits | off-raster << 8
 };
 
+// K2h: the unit polyline's sums of one displacement row (oracle orc_unit_geo)
+struct UGeo {
+    double s1n, s2n, s1a, s2a, e12, e3;
+};
+
+// the unit polyline's sums of one table row u[N] (oracle unit_geo: the same operations)
+__device__ void unit_geo_row(const KParams& p, const double2* __restrict__ u, UGeo* out) {
+    const int N = p.N;
+    const double mincos = p.mincos, r = p.r_eff;
+    double s1n = 0.0, s2n = 0.0, s1a = 0.0, s2a = 0.0, e12 = 0.0, e3 = 0.0;
+    double qx = 1.0, qy = 0.0, pdx = 0.0, pdy = 0.0, pb = 0.0;
+    for (int k = 1; k <= N + 1; ++k) {
+        double cx = -1.0, cy = 0.0;
+        if (k <= N) {
+            const double2 c = u[k - 1];
+            cx = c.x, cy = c.y;
+        }
+        const double dx = cx - qx, dy = cy - qy;
+        const double b = sqrt(dx * dx + dy * dy);
+        if (k <= N) {
+            s1n = s1n + b;
+            s2n = s2n + b * b;
+        }
+        s1a = s1a + b;
+        s2a = s2a + b * b;
+        if (k >= 2) {  // row k - 2: chords k - 1 and k
+            e12 = e12 + fmax(0.0, b - r * pb);
+            e12 = e12 + fmax(0.0, pb / r - b);
+            const double dt = pdx * dx + pdy * dy;
+            e3 = e3 + fmax(0.0, mincos - dt / (pb * b));
+        }
+        qx = cx, qy = cy, pdx = dx, pdy = dy, pb = b;
+    }
+    out->s1n = s1n, out->s2n = s2n, out->s1a = s1a, out->s2a = s2a, out->e12 = e12, out->e3 = e3;
+}
+
 struct KGrp {
     const double* __restrict__ pairs;
     const double* __restrict__ utab;
@@ -4806,6 +4842,7 @@ struct KGrp {
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
+    UGeo* __restrict__ ugeo;       // K2h: [D] unit sums, formed by k_g_hist's extra block
 };
 
 __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
@@ -4830,10 +4867,18 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
 // groups (the tile under the group's middle waypoint) and the partition's histogram, stored
 // bin-major so the scan yields each (bin, partition)'s offset
+// K2h launches one block more: it forms the D rows' unit sums (unit_geo_row) beside the
+// histogram blocks, so the step has no launch for them
 __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
     __shared__ int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
     const int t = threadIdx.x, b = blockIdx.x;
+    if (b == G_NBK) {
+        if (kg.ugeo && t < kg.D)
+            unit_geo_row(p, reinterpret_cast<const double2*>(kg.utab) + (int64_t)t * p.N,
+                         kg.ugeo + t);
+        return;
+    }
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
@@ -5301,6 +5346,259 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     }
 }
 
+// ---- K2h: generated candidates in the similarity form (oracle orc_eval_generated_h) --------
+// The candidate arcs are p_k = C + (1/2) R(v) u_k (u_0 = (1, 0), u_{N+1} = (-1, 0)): the unit
+// polyline of the displacement's table row under a similarity of scale h = |v| / 2.  Every
+// term that depends on the geometry only -- get_cost's L (problem.py:130-146, with the quirk's
+// anchor term), the true length (solver.py:49), the kinematic rows (problem.py:100-107, their
+// ratio rows scale with h, their turn rows are the unit polyline's) -- is a per-displacement
+// sum of the unit polyline times h (maxratio_smooth = 0), formed once per launch (UGeo) and
+// scaled per path in the output launch.  What stays per waypoint is what the raster decides:
+// the point, its cell and its record (Phi / N, psi, terrain, no-fly hit), with K2g's sort,
+// staging and grouped partial sums; so an item carries no f64 geometry (no segment norms, no
+// square roots, no kinematic rows) and its slot is 24 B.  Exact in real arithmetic; in float64
+// the geometry terms differ from per-segment sums by rounding only (bench.py
+// parity.vs_sequential_order on the whole cfg3 batch).
+
+struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
+    double cost;   // Phi / N of the group's waypoints, from +0.0 in waypoint order
+    double psi;    // the no-fly psi, likewise
+    float hmax;    // max terrain of the group's waypoints as consume reads it
+    uint32_t cnt;  // nfz hits | off-raster << 8
+};
+
+// every (path, group) item in K2g's sorted order: the group's points, cells and records only.
+// Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the arc
+// formula), CH unconditional 16-B loads (a slot past the group's end reads the plane's first
+// pair and is masked off in the consume step), then the branch-free consume.
+template <int CH, bool CELLS>
+__global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp kg,
+                                                   const uint4* __restrict__ rec) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint32_t* s_map = s_dyn;
+    const int mapw = (rs.pwords + 3) & ~3;
+    double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
+    // CELLS: each wave's [CH][64] staging slice of waypoint cells, after the unit-arc rows and
+    // their junk slot
+    int32_t* s_cells = reinterpret_cast<int32_t*>(s_u + kg.D * p.N + 1);
+    {  // staging as k_g_eval: every load of a thread issued before its first LDS store
+        constexpr int U = 4;
+        const int nv = rs.pwords >> 2, nu = kg.D * p.N;
+        const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
+        uint4* dst = reinterpret_cast<uint4*>(s_map);
+        const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
+        uint4* du = reinterpret_cast<uint4*>(s_u);
+        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += 256 * U) {
+            uint4 v[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * 256;
+                v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * 256;
+                *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
+            }
+        }
+        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
+    }
+    __syncthreads();
+    // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
+    // last item evaluates nothing and writes nothing
+    const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    const bool live = pos < kg.n_items;
+    const int32_t item = live ? kg.order[pos] : 0;
+    const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
+    const int s = item - path * kg.nseg;
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const int N = p.N, W = kg.W;
+    const double2* urow = s_u + d * N;
+    const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
+    // chunks: the wave's most, so the loop is wave-uniform
+    int nch = (j1 - j0 + CH - 1) / CH;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nch = max(nch, __shfl_xor(nch, o));
+    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
+    const double dN = (double)N, yN = kg.inv_n;
+    auto over_n = [&](double a) {  // Phi / N exactly as k_g_eval forms it
+        if (yN == 0.0) return a / dN;
+        const double q0 = a * yN;
+        const double q1 = fma(fma(-q0, dN, a), yN, q0);
+        return __builtin_isinf(a) ? q0 : q1;
+    };
+    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
+    double gc = 0.0, gn = 0.0;
+    float hmax = -INFINITY;
+    uint32_t nh = 0, off = 0;
+    for (int c = 0; c < nch; ++c) {
+        const int jc = j0 + c * CH;
+        uint4 r[CH];
+        int32_t cl[CH];
+        uint32_t inb = 0, need = 0, full = 0, odd = 0;
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int j = jc + t;
+            const double2 u = urow[min(max(j - 1, 0), N - 1)];
+            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
+            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+            x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
+            x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
+            const double tx = (x0 - rs.x0) * rs.inv_dx;
+            const double ty = (rs.y_top - x1) * rs.inv_dy;
+            const uint4* ptr = dummy;
+            cl[t] = -1;
+            if ((j < j1) && (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) &&
+                (ty < (double)rs.ny)) {
+                inb |= 1u << t;
+                const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
+                if (CELLS) cl[t] = iy * rs.nx + ix;
+                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
+                if (code & 2u) {
+                    need |= 1u << t;
+                    full |= 1u << t;
+                    ptr = rec + (iy * rs.nx + ix);
+                } else if (code) {
+                    need |= 1u << t;
+                    const int32_t a = pk_addr(rs, ix, iy);
+                    odd |= (uint32_t)(a & 1) << t;
+                    ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
+                }
+            }
+            r[t] = *ptr;
+        }
+        const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const bool vl = t < nv;
+            const bool in = (inb >> t) & 1u, nd = (need >> t) & 1u, fl = (full >> t) & 1u,
+                       od = (odd >> t) & 1u;
+            const uint4 rt = r[t];
+            const uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
+            uint32_t ter = nd ? (fl ? rt.z : od ? rt.w : rt.y) : 0u;
+            const uint32_t psi = fl ? rt.y : 0u;
+            if (fl && (rt.w & UAM_FLAG_NODATA)) ter = 0u;
+            nh += (fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            off += (vl && !in) ? 1u : 0u;
+            gc = gc + over_n((double)__uint_as_float(phi));
+            gn = gn + (double)__uint_as_float(psi);
+            hmax = fmaxf(hmax, vl ? __uint_as_float(ter) : -INFINITY);
+        }
+        if (CELLS) {
+            // through the wave's LDS slice: lane l stages its CH cells, then each store
+            // instruction writes 64 / CH items' runs of CH consecutive cells (runs of
+            // cells[path][jc..jc+nv)), instead of 64 scattered 4-B stores per waypoint
+            int32_t* sw = s_cells + (threadIdx.x >> 6) * (CH * 64);
+            const int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int t = 0; t < CH; ++t) sw[t * 64 + lane] = cl[t];
+            __builtin_amdgcn_wave_barrier();
+            const int64_t base = (int64_t)path * W + jc;  // this lane's run
+            constexpr int IPS = 64 / CH;                 // items per store instruction
+#pragma unroll
+            for (int k = 0; k < (64 + IPS - 1) / IPS; ++k) {
+                const int it = k * IPS + lane / CH, t = lane % CH;
+                const int src = it < 64 ? it : 63;
+                const int64_t b_it = __shfl(base, src);
+                const int nv_it = __shfl(nv, src);
+                if (lane < IPS * CH && it < 64 && t < nv_it) kg.cells[b_it + t] = sw[t * 64 + it];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    HSlot o;
+    o.cost = gc;
+    o.psi = gn;
+    o.hmax = hmax;
+    o.cnt = nh | (off << 8);
+    if (live) reinterpret_cast<HSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
+}
+
+// outputs of every path (block = 64 pairs x D, k_g_final's layout): the geometry terms from
+// the pair's scale and the displacement's unit sums (oracle sim_geo), cost = (N+1) L + the
+// Phi / N partials in group order, and the main.py:175-180 selection
+template <int NR>  // slots per path held in registers (0: a loop for long paths)
+__global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
+                                                  int32_t* __restrict__ best_f,
+                                                  int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int D = kg.D, t = threadIdx.x;
+    double* s_cost = smem;
+    double* s_len = smem + 64 * D;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int qi = t / D, di = t - qi * D;
+    const HSlot* slot = reinterpret_cast<const HSlot*>(kg.slot);
+    if (q0 + qi < kg.n_pairs) {
+        const int64_t gp = (q0 + qi) * D + di;
+        HSlot g[NR > 0 ? NR : 1];
+        if (NR > 0) {
+#pragma unroll
+            for (int s = 0; s < NR; ++s) g[s] = slot[(int64_t)min(s, kg.nseg - 1) * kg.P + gp];
+        }
+        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q0 + qi];
+        const UGeo u = kg.ugeo[di];
+        // sim_geo (oracle): h = |v| / 2, h^2 = |v|^2 / 4
+        const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+        const double sv = vx * vx + vy * vy;
+        const double h = sqrt(sv) * 0.5, h2 = sv * 0.25;
+        const bool ls = p.length_smooth != 0;
+        double L;
+        if (p.quirk_length) {
+            const double ax = p.anchor_mode ? p.anchor_x : pr.x;
+            const double ay = p.anchor_mode ? p.anchor_y : pr.y;
+            const double dx = pr.x - ax, dy = pr.y - ay;
+            const double n = sqrt(dx * dx + dy * dy);
+            L = (ls ? n * n : n) + (ls ? h2 * u.s2n : h * u.s1n);
+        } else {
+            L = ls ? h2 * u.s2a : h * u.s1a;
+        }
+        const double len = h * u.s1a;
+        const double ksum = (h > 0.0 && h < INFINITY) ? h * u.e12 + u.e3 : 0.0;
+        double nsum = 0.0, hmax = -INFINITY;
+        int32_t nh = 0, off = 0;
+        double cost = (double)(p.N + 1) * L;
+        if (NR > 0) {
+#pragma unroll
+            for (int s = 0; s < NR; ++s) {
+                if (s >= kg.nseg) break;
+                cost = cost + g[s].cost;
+                nsum = nsum + g[s].psi;
+                hmax = fmax(hmax, (double)g[s].hmax);
+                nh += (int32_t)(g[s].cnt & 255u);
+                off += (int32_t)((g[s].cnt >> 8) & 255u);
+            }
+        } else {
+            for (int s = 0; s < kg.nseg; ++s) {
+                const HSlot gs = slot[(int64_t)s * kg.P + gp];
+                cost = cost + gs.cost;
+                nsum = nsum + gs.psi;
+                hmax = fmax(hmax, (double)gs.hmax);
+                nh += (int32_t)(gs.cnt & 255u);
+                off += (int32_t)((gs.cnt >> 8) & 255u);
+            }
+        }
+        if (out.cost) out.cost[gp] = cost;
+        if (out.length_q) out.length_q[gp] = L;
+        if (out.length) out.length[gp] = len;
+        if (out.kin_sum) out.kin_sum[gp] = ksum;
+        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
+        if (out.min_clearance) out.min_clearance[gp] = p.altitude - hmax;
+        if (out.nfz_hits) out.nfz_hits[gp] = nh;
+        if (out.offmap) out.offmap[gp] = off;
+        if (out.below_terrain) out.below_terrain[gp] = 0;
+        s_cost[di * 64 + qi] = cost;
+        s_len[di * 64 + qi] = len;
+    }
+    __syncthreads();
+    if (t < 64 && q0 + t < kg.n_pairs) {
+        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -5377,6 +5675,8 @@ struct uam_ctx {
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
+    int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
+                                // geometry, K2g proper; maxratio_smooth always runs K2g)
     int k2g_chunk = 0;          // K2g gathers in flight per lane (UAM_OPT_K2G_CHUNK: 6, 8, 11;
                                 // 0 = 8)
 
@@ -6075,10 +6375,15 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
             ctx->k2g_curve = (int)value;
             return UAM_OK;
         case UAM_OPT_K2G_CHUNK:
-            if (value != 0 && value != 6 && value != 8 && value != 11 && value != 16)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 8, 11 or 16",
+            if (value != 0 && value != 6 && value != 7 && value != 8 && value != 11 && value != 16)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 7, 8, 11 or 16",
                             (long long)value);
             ctx->k2g_chunk = (int)value;
+            return UAM_OK;
+        case UAM_OPT_K2G_SIM:
+            if (value != 0 && value != 1)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_SIM %lld not 0 or 1", (long long)value);
+            ctx->k2g_sim = (int)value;
             return UAM_OK;
         case UAM_OPT_K8_STREAMS:
             if (value < 1 || value > 8)
@@ -6107,6 +6412,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_TILE_BITS: *value = ctx->k2g_tbits; return UAM_OK;
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
+        case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
@@ -6425,11 +6731,15 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)bins * G_NBK;
     const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    // K2h (the similarity form) unless disabled or maxratio_smooth (its turn rows are not
+    // scale-free): 24-B slots, the geometry in the output launch
+    const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth;
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
-                 b_slot = al((size_t)n_items * sizeof(GSlot));
+                 b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot))),
+                 b_ug = al((size_t)D * sizeof(UGeo));
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs;
@@ -6454,12 +6764,14 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
     kg.n_items = n_items;
     size_t o = 0;
-    kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first
+    kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first (HSlot for K2h)
+    kg.ugeo = sim ? (UGeo*)(w + o) : nullptr, o += b_ug;
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.key = (uint16_t*)(w + o);
-    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16;  // + junk slot
+    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +  // + junk slot
+                            (sim && ko.cells ? (size_t)4 * 8 * 64 * 4 : 0);    // K2h cells
     const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
@@ -6470,15 +6782,23 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8), UAM_G_EVALS(11),
                                      UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
+    static const EvalFn hevals[5] = {k_h_eval<6, false>, k_h_eval<7, false>, k_h_eval<8, false>,
+                                     k_h_eval<11, false>, k_h_eval<16, false>};
+    static const EvalFn hevals_cells[1] = {k_h_eval<8, true>};
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
         for (EvalFn f : evals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
+        for (EvalFn f : hevals)
+            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+        HIP_TRY(hipFuncSetAttribute((const void*)hevals_cells[0],
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         ctx->k2g_attrs = true;
     }
     st = ktime_begin(ctx, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK + (sim ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
@@ -6487,7 +6807,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 8;
-    const int ch = (chl == 6 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
+    const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : 4;
+    const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                    (ctx->kp.length_smooth ? 2 : 0) +
                    (ctx->kp.maxratio_smooth ? 1 : 0);
     // with waypoint cells requested: the CH = 8 form that also writes them
@@ -6496,7 +6817,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                                           k_g_eval<8, true, false, true>,
                                           k_g_eval<8, true, true, true>};
     kg.cells = ko.cells;
-    const EvalFn ev = ko.cells ? evals_cells[ch & 3] : evals[ch];
+    const EvalFn ev = sim ? (ko.cells ? hevals_cells[0] : hevals[hch])
+                          : ko.cells ? evals_cells[ch & 3] : evals[ch];
     if (lds > 64 * 1024 && !ctx->k2g_attrs_cells && ko.cells) {
         for (EvalFn f : evals_cells)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -6506,13 +6828,15 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
-    const FinalFn fin = nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
+    const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
+                            : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
     hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
+    ctx->last_kernel = sim ? "K2h+pack" : "K2g+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -6629,10 +6953,7 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
     if (mode == UAM_MODE_RASTER && ctx->k2g_group > 0) {
         st = launch_grouped(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
         if (st < 0) return st;
-        if (st == 1) {
-            ctx->last_kernel = "K2g+pack";
-            return UAM_OK;
-        }
+        if (st == 1) return UAM_OK;  // last_kernel: "K2h+pack" / "K2g+pack"
     }
     if (mode == UAM_MODE_RASTER) {
         st = launch_segmented(ctx, kr, rec, pairs, n_pairs, utab, D, ko, best_f, best_l, s);
