@@ -225,6 +225,12 @@ def main():
             secs = udist.broadcast_raster(table, src=0, engine=eng if rccl else None)
             setup["raster_bcast_ms"] = round(secs * 1e3, 3)
             setup["raster_bytes"] = table.numel() * 4
+        if volume_mode and not args.no_pack:
+            t1 = time.perf_counter()
+            # every rank derives K4h's packed copy (16-B voxels in 4 x 2-cell blocks) locally
+            eng.volume_pack(volume)
+            torch.cuda.synchronize()
+            setup["volume_pack_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
         if raster_mode and not args.no_skip:
             t1 = time.perf_counter()
             # every rank derives the skip bitmap (and K2s's packed copy) locally
@@ -293,7 +299,13 @@ def main():
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    if last.startswith("K2h"):
+    if last.startswith("K4h"):
+        ktag = last.lower()
+        kernel_name = ("K4h sequence (k_v_hist (+ the unit-arc sums) / k_g_scatter, k_v_eval "
+                       "over every (path, group) item: points, one 16-B packed voxel per "
+                       "waypoint; k_v_final: the similarity-form geometry, grouped sums, "
+                       "selection)")
+    elif last.startswith("K2h"):
         ktag = last.lower()
         kernel_name = ("K2h sequence (k_g_hist (+ the unit-arc sums) / k_scan / k_g_scatter, "
                        "k_h_eval over every (path, group) item: points, cells, records; "
@@ -388,8 +400,9 @@ def main():
         gpu_cost = o["cost"].cpu().numpy()
         gpu_best = o["best_fval_idx"].cpu().numpy()
         gpu_cells = o["cells"].cpu().numpy() if "cells" in o else None
+        gpu_other = {k: o[k].cpu().numpy() for k in ("min_clearance", "nfz_hits", "length")}
         chunk = 50 if mode == "analytic" else 2000
-        done, t_cpu, mism, bmis, cmis = 0, 0.0, 0, 0, 0
+        done, t_cpu, mism, bmis, cmis, omis = 0, 0.0, 0, 0, 0, 0
         while done < Q and t_cpu < args.cpu_seconds:
             sl = pairs_host[done:done + chunk]
             ts = time.perf_counter()
@@ -397,6 +410,10 @@ def main():
                             want_cells=gpu_cells is not None, kernel=last)
             t_cpu += time.perf_counter() - ts
             mism += int(np.sum(r["cost"] != gpu_cost[done * D:(done + len(sl)) * D]))
+            for gk, rk in (("min_clearance", "min_clearance"), ("nfz_hits", "nfz_hits"),
+                           ("length", "length")):
+                g_o = gpu_other[gk][done * D:(done + len(sl)) * D]
+                omis += int(np.sum(~((r[rk] == g_o) | (np.isnan(r[rk]) & np.isnan(g_o)))))
             bmis += int(np.sum(O.argmin(r["cost"], D, True) != gpu_best[done:done + len(sl)]))
             if gpu_cells is not None:
                 cmis += int(np.sum(r["cells"].reshape(-1, W) !=
@@ -445,6 +462,7 @@ def main():
                       f"shards, {passes} pass(es) in {wall:.2f} s; 1 thread: {t_cpu:.1f} s"}
         result["parity"] = {"paths_checked": done * D, "cost_mismatches": mism,
                             "best_index_mismatches": bmis,
+                            "clearance_hits_length_mismatches": omis,
                             "rule": f"bit-exact float64 vs CPU oracle (sum order: "
                                     f"{order_name(group, last)}) on the cpu_baseline sample"}
         if gpu_cells is not None:
@@ -550,7 +568,8 @@ def oracle_inputs(O, geo, raster, volume, mode):
     if mode == "volume":
         g3 = volume.geo
         vd = O.volume_desc(g3.nx, g3.ny, g3.nz, g3.x0, g3.y_top, g3.dx, g3.dy, g3.z0, g3.dz)
-        vox = volume.vox.cpu().numpy().view(np.float32)
+        vox = (volume.vox.cpu().numpy().view(np.float32),
+               volume.cols.cpu().numpy().view(np.float32))
     return rd, rec, vd, vox
 
 
@@ -561,6 +580,9 @@ def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_ce
     (orc_eval_paths_g), otherwise / kernel=None with group 0 -> the reference's sequential
     order."""
     if mode == "volume":
+        if kernel == "K4h+pack":
+            return orc.eval_generated_h(pairs, ut_host, mode="volume", vdesc=vd, vol=vox,
+                                        group=group)
         return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
     if kernel == "K2h+pack":
         return orc.eval_generated_h(pairs, ut_host, rdesc=rd, rec=rec, group=group,

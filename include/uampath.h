@@ -294,6 +294,24 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* desc, const void* rec2
 int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);
+/* The packed volume (K4h): one 16-B voxel {float risk, float psi_nfz, float terrain, uint32
+ * flags} per (ix, iy, iz) -- the column's terrain and flags beside the layer's pair, so a
+ * waypoint is one request -- in blocks of 4 x 2 cells of one layer (one 128-B line),
+ * layer-major planes, padded to whole blocks.  uam_volume_pack derives it from a built volume
+ * (vol_dev); packed_dev holds uam_volume_packed_bytes bytes, 256-B aligned. */
+int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);
+int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
+                    void* packed_dev, uam_stream stream);
+/* uam_eval_generated3d with the packed copy: batches of >= UAM_OPT_SORTED_MIN_PATHS paths
+ * (maxratio_smooth off, no cells) run K4h -- the (path, group) items sorted on the altitude
+ * band and x/y tile of their middle waypoint, grouped partial sums (UAM_OPT_GROUP), the
+ * geometry terms in the similarity form (oracle orc_eval_generated_h mode 2; uam_last_kernel
+ * "K4h+pack"); every other batch runs uam_eval_generated3d on vol_dev.  packed_dev NULL: the
+ * same as uam_eval_generated3d. */
+int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
+                           const void* packed_dev, const double* pairs6_dev, int64_t n_pairs,
+                           const double* utab_dev, int32_t D, const uam_path_outputs* out,
+                           uam_stream stream);
 
 /* ---- Raster broadcast over RCCL / xGMI (the reference has no
  * collective at all -- its only IPC is the solver's TCP socket, path_generation/solver.py:26-38).
@@ -435,7 +453,11 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                kinematic rows) in the similarity form -- the unit arc's sums
  *                                scaled by |x0 - xf| / 2 (oracle orc_eval_generated_h; needs
  *                                maxratio_smooth = 0); 0: K2g, the geometry per waypoint
- *                                segment in the grouped order (orc_eval_paths_g) */
+ *                                segment in the grouped order (orc_eval_paths_g)
+ *   UAM_OPT_K2G_LDS_WINDOW       K2h experiment (not faster): 0 (default), or
+ *                                96 / 128: 1024-item workgroups that stage a window of that
+ *                                many cells square of the packed plane in LDS and serve the
+ *                                code-1 waypoints inside it from there.  Same outputs. */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -451,7 +473,8 @@ enum {
     UAM_OPT_K2G_LDS_FLOOR = 12,
     UAM_OPT_K2G_CHUNK = 13,
     UAM_OPT_K2G_CURVE = 14,
-    UAM_OPT_K2G_SIM = 15
+    UAM_OPT_K2G_SIM = 15,
+    UAM_OPT_K2G_LDS_WINDOW = 16
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

@@ -165,3 +165,18 @@ def test_cfg5_volume_1024x1024x64(eng, oracle_mod):
     idx = (sub[:, None] * D + np.arange(D)).reshape(-1)
     np.testing.assert_array_equal(_np(gpu["below_terrain"])[idx], ref["below"])
     _check_properties(eng, oracle_mod, launch, pairs, gpu, D)
+    # K4h: the packed copy (one 16-B voxel per waypoint), the sorted grouped evaluation with
+    # the similarity-form geometry -- bit-exact against its oracle statement on the subsample,
+    # the reference's sequential per-segment sums within rounding
+    eng.volume_pack(vol)
+    gh = launch(pairs)
+    assert eng.last_kernel() == "K4h+pack"
+    refh = orc.eval_generated_h(pairs[sub], ut, mode="volume", vdesc=vd, vol=ref_vol,
+                                group=eng.last_group())
+    _check_subsample(oracle_mod, gh, refh, sub, D)
+    np.testing.assert_array_equal(_np(gh["below_terrain"])[idx], refh["below"])
+    for k in ("min_clearance", "nfz_hits", "offmap", "below_terrain"):
+        np.testing.assert_array_equal(_np(gh[k]), _np(gpu[k]), err_msg=k)
+    for k in ("cost", "length", "length_q", "nfz_sum"):
+        np.testing.assert_allclose(_np(gh[k]), _np(gpu[k]), rtol=1e-12, err_msg=k)
+    _check_properties(eng, oracle_mod, launch, pairs, gh, D)

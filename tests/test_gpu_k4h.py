@@ -1,0 +1,136 @@
+"""K4h -- the volume (BASELINE config 5) in K2h's form: the packed copy (uam_volume_pack: one
+16-B voxel {risk, psi_nfz, terrain, flags} per cell and layer, 4 x 2-cell blocks per layer),
+the (path, group) items sorted on the altitude band and x/y tile of their middle waypoint,
+grouped partial sums, the geometry terms in the similarity form.  Against the oracle's
+statement of it (orc_eval_generated_h, mode 2) bit for bit; against the sequential
+lane-per-path K4 (orc_eval_paths3d) within rounding for the sums and exactly for the order-free
+outputs (hits, off-volume counts, min clearance, below-terrain counts).  Reference rules as
+K2h (no reference counterpart for the altitude terms)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+KEYS = (("cost", "cost"), ("length_q", "lq"), ("length", "length"), ("kin_sum", "kin"),
+        ("nfz_sum", "nfz"), ("nfz_hits", "nfz_hits"), ("offmap", "offmap"),
+        ("min_clearance", "min_clearance"), ("below_terrain", "below"))
+
+
+def _case(oracle_mod, R, nz, N, group, maxalpha=None):
+    from uam_path_planning_amd import build
+    from uam_path_planning_amd.engine import Engine, PathParams
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import (build_region_map, canonical_spec, layer_weights,
+                                                raster_geo)
+    from uam_path_planning_amd.synthetic import synthetic_dem
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    build.build_library()
+    e = Engine(0)
+    e.set_option("group", group)
+    e.set_option("sorted_min_paths", 0)
+    e.set_option("wave_max_paths", 0)
+    spec = canonical_spec(nfz_polygons=16)
+    ma = spec["maxalpha"] if maxalpha is None else maxalpha
+    e.set_geometry(compile_map(build_region_map(spec)))
+    e.set_params(PathParams(N=N, **spec["options"], maxratio=spec["maxratio"], maxalpha=ma,
+                            enlargement=spec["enlargement"], weights=tuple(spec["weights"]),
+                            altitude=320.0))
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, spec["options"],
+                            spec["maxratio"], ma, spec["enlargement"], spec["weights"],
+                            altitude=320.0)
+    geo = raster_geo(R)
+    r2 = e.raster_build(geo, synthetic_dem(R))
+    lw = layer_weights(nz)
+    vol = e.volume_build(r2, nz, 0.0, 640.0 / nz, lw)
+    e.volume_pack(vol)
+    vd = oracle_mod.volume_desc(R, R, nz, geo.x0, geo.y_top, geo.dx, geo.dy, 0.0, 640.0 / nz)
+    host = (vol.vox.cpu().numpy().view(np.float32), vol.cols.cpu().numpy().view(np.float32))
+    return e, orc, vol, vd, host
+
+
+def _pairs3d(n, seed):
+    from uam_path_planning_amd.synthetic import random_pairs3d
+
+    pr = random_pairs3d(n, seed=seed)
+    pr[::41, 2] = -50.0          # climbs in from below the volume
+    pr[::43, 5] = 900.0          # leaves it at the top
+    pr[::97, 0] += 70.0          # off the x/y grid
+    pr[5, 1] = np.nan
+    pr[11, 3:5] = pr[11, 0:2]    # start == goal (h = 0)
+    return pr
+
+
+def _check(gpu, ref, oracle_mod, D):
+    for gk, ok in KEYS:
+        np.testing.assert_array_equal(gpu[gk].cpu().numpy(), ref[ok], err_msg=gk)
+    np.testing.assert_array_equal(gpu["best_fval_idx"].cpu().numpy(),
+                                  oracle_mod.argmin(ref["cost"], D, True))
+    np.testing.assert_array_equal(gpu["best_length_idx"].cpu().numpy(),
+                                  oracle_mod.argmin(ref["length"], D, False))
+
+
+@pytest.mark.parametrize("R,nz,group", [(256, 16, 21), (256, 64, 8), (512, 7, 21),
+                                        (300, 33, 64), (256, 16, 1)])
+def test_k4h_vs_oracle(oracle_mod, R, nz, group):
+    """Volumes with nx not a multiple of the block width (300), odd layer counts (7, 33: the
+    altitude bands' last band partial), groups of 1-64; every output equals orc_eval_generated_h
+    bit for bit; against the sequential K4 form: exact for the order-free outputs, rounding
+    for the sums."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, R, nz, 80, group)
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs3d(3000, 17)
+    ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=group)
+    assert (ref["offmap"] > 0).any() and (ref["below"] > 0).any()
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack" and e.last_group() == group
+    _check(gpu, ref, oracle_mod, D)
+    seq = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, host)
+    for k in ("nfz_hits", "offmap", "min_clearance", "below"):
+        np.testing.assert_array_equal(ref[k], seq[k], err_msg=k)
+    ok = np.isfinite(seq["cost"]) & (seq["length"] > 0)
+    np.testing.assert_allclose(ref["cost"][ok], seq["cost"][ok], rtol=1e-12)
+
+
+@pytest.mark.parametrize("chunk", [6, 7, 11])
+def test_k4h_chunks(oracle_mod, chunk):
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21, maxalpha=0.015)
+    e.set_option("k2g_chunk", chunk)
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs3d(2000, 23)
+    ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=21)
+    assert (ref["kin"] > 0).any()
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack"
+    _check(gpu, ref, oracle_mod, D)
+
+
+def test_k4h_pack_layout(oracle_mod):
+    """uam_volume_pack against its definition: voxel (ix, iy, iz) at
+    ((iz nby2 + iy/2) nbx4 + ix/4) 8 + (iy%2) 4 + ix%4, {risk, psi} of the voxel, {terrain,
+    flags} of the column, zero padding."""
+    e, orc, vol, vd, host = _case(oracle_mod, 300, 7, 10, 21)
+    pk = vol.packed.cpu().numpy().reshape(-1, 4)
+    ny, nx, nz = 300, 300, 7
+    nbx4, nby2 = (nx + 3) // 4, (ny + 1) // 2
+    iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    idx = (((iz * nby2 + iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
+    vox = vol.vox.cpu().numpy()            # [ny, nx, nz, 2]
+    cols = vol.cols.cpu().numpy()          # [ny, nx, 2]
+    want = np.concatenate([vox.transpose(2, 0, 1, 3).reshape(-1, 2),
+                           np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)], axis=1)
+    np.testing.assert_array_equal(pk[idx], want)
+    mask = np.ones(len(pk), bool)
+    mask[idx] = False
+    assert (pk[mask] == 0).all()

@@ -70,3 +70,40 @@ def test_volume_build_and_eval_vs_python(oracle_mod):
         assert ref["min_clearance"][p] == cm, p
         assert ref["length"][p] == geo2["length"][p] and ref["kin"][p] == geo2["kin"][p]
     assert ref["offmap"].any() and ref["below"].any() and ref["nfz_hits"].any()
+
+
+def test_volume_similarity_form_vs_sequential(oracle_mod):
+    """orc_eval_generated_h in volume mode (K4h's definition): the order-free outputs (hits,
+    off-volume and below-terrain counts, min clearance) equal orc_eval_paths3d's exactly; cost,
+    L, length and the no-fly sum differ by rounding only (grouped raster sums, similarity-form
+    geometry)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import canonical_spec, displacements, layer_weights
+    from uam_path_planning_amd.synthetic import random_pairs3d
+
+    nx, ny, nz, z0, dz = 64, 48, 16, 0.0, 40.0
+    x0, y_top, dx, dy = 0.0, 20.0, 60.0 / 64, 60.0 / 64
+    rng = np.random.default_rng(5)
+    rec2 = np.zeros((ny, nx, 4), np.float32)
+    rec2[..., 0] = rng.uniform(0.0, 5.0, (ny, nx))
+    rec2[..., 1] = np.where(rng.random((ny, nx)) < 0.3, rng.uniform(0.0, 2.0, (ny, nx)), 0.0)
+    rec2[..., 2] = rng.uniform(-15.0, 400.0, (ny, nx))
+    rec2[..., 3] = ((rng.random((ny, nx)) < 0.2).astype(np.uint32)).view(np.float32)
+    vd = oracle_mod.volume_desc(nx, ny, nz, x0, y_top, dx, dy, z0, dz)
+    vol = oracle_mod.volume_build(vd, rec2, layer_weights(nz))
+    spec = canonical_spec(nfz_polygons=0)
+    N = 40
+    orc = oracle_mod.Oracle(oracle_mod.compile_spec(spec), N, spec["options"], spec["maxratio"],
+                            spec["maxalpha"], spec["enlargement"], spec["weights"])
+    ut = arc_table(N, displacements(5))
+    pairs = random_pairs3d(300, seed=8)
+    pairs[::17, 2] = -30.0
+    seq = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, vol, want_cells=True)
+    for G in (0, 7, 21):
+        h = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=vol, group=G,
+                                 want_cells=True)
+        for k in ("nfz_hits", "offmap", "below", "min_clearance", "cells"):
+            np.testing.assert_array_equal(h[k], seq[k], err_msg=k)
+        for k in ("cost", "lq", "length", "nfz"):
+            np.testing.assert_allclose(h[k], seq[k], rtol=1e-12, atol=1e-300, err_msg=k)
+    assert (seq["offmap"] > 0).any() and (seq["below"] > 0).any() and (seq["nfz"] > 0).any()

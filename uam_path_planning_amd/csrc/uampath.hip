@@ -4843,7 +4843,25 @@ struct KGrp {
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
     UGeo* __restrict__ ugeo;       // K2h: [D] unit sums, formed by k_g_hist's extra block
+    int32_t* __restrict__ gcnt;    // [bins] items per bin, zero on entry (k_g_hist adds its
+                                   // partitions' counts, the output launch re-zeroes it)
 };
+
+// K2h / K4h: the D rows' unit sums by one block: the table staged in LDS by every thread with
+// one round trip of loads (the sums then read LDS: a row's 81 steps would otherwise each wait
+// for a global load), then one thread per row
+// (su: the calling kernel's histogram LDS, cap entries; a larger table is read from global)
+__device__ __forceinline__ void unit_geo_block(const KParams& p, const KGrp& kg, double2* su,
+                                               int cap) {
+    const int n = kg.D * p.N;
+    const double2* u = reinterpret_cast<const double2*>(kg.utab);
+    if (n <= cap) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) su[i] = u[i];
+        __syncthreads();
+        u = su;
+    }
+    if ((int)threadIdx.x < kg.D) unit_geo_row(p, u + threadIdx.x * p.N, kg.ugeo + threadIdx.x);
+}
 
 __device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
     const int32_t q = path / kg.D, d = path - q * kg.D;
@@ -4870,13 +4888,12 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
 // K2h launches one block more: it forms the D rows' unit sums (unit_geo_row) beside the
 // histogram blocks, so the step has no launch for them
 __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
-    __shared__ int32_t h[G_BINS_MAX];
+    __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
     const int t = threadIdx.x, b = blockIdx.x;
-    if (b == G_NBK) {
-        if (kg.ugeo && t < kg.D)
-            unit_geo_row(p, reinterpret_cast<const double2*>(kg.utab) + (int64_t)t * p.N,
-                         kg.ugeo + t);
+    if (b == G_NBK) {  // the unit rows through LDS (the histogram's; one round trip)
+        if (kg.ugeo)
+            unit_geo_block(p, kg, reinterpret_cast<double2*>(h), (int)(sizeof(h) / 16));
         return;
     }
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
@@ -4935,17 +4952,44 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
         }
     }
     __syncthreads();
-    for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
+    // the partition's place in each bin: its count added to the bin's total (the order of
+    // the partitions inside a bin follows the atomics -- it only decides which lane evaluates
+    // an item, never what the item computes); k_g_scatter scans the totals itself
+    for (int k = t; k < kg.bins; k += 1024)
+        if (h[k]) kg.cnt[(int64_t)k * G_NBK + b] = atomicAdd(&kg.gcnt[k], h[k]);
 }
 
-// launch 3 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered; U keys
+// launch 2: every block scans the bin totals in LDS (exclusive; bins <= G_BINS_MAX), its
+// cursors = bin start + the partition's place in the bin (k_g_hist), items scattered; U keys
 // per thread loaded before the first cursor update
 __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
     __shared__ int32_t cur[G_BINS_MAX];
+    __shared__ int32_t wsum[16];
     const int t = threadIdx.x, b = blockIdx.x;
-    for (int k = t; k < kg.bins; k += 1024) {
-        const int64_t c = (int64_t)k * G_NBK + b;
-        cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
+    const int per = (kg.bins + 1023) / 1024;  // bins per thread, consecutive
+    int run = 0;
+    for (int k = 0; k < per; ++k) {
+        const int i = t * per + k;
+        const int v = i < kg.bins ? kg.gcnt[i] : 0;
+        if (i < kg.bins) cur[i] = run;  // exclusive within the thread's run
+        run += v;
+    }
+    // exclusive scan of the 1024 thread totals: within the wave, then over the 16 waves
+    const int lane = t & 63, wv = t >> 6;
+    int inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wv; ++w) woff += wsum[w];
+    const int excl = woff + inc - run;
+    for (int k = 0; k < per; ++k) {
+        const int i = t * per + k;
+        if (i < kg.bins) cur[i] += excl + kg.cnt[(int64_t)i * G_NBK + b];
     }
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
@@ -4958,7 +5002,10 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int64_t i = i0 + k * 1024;
-            if (i < hi) kg.order[atomicAdd(&cur[kk[k]], 1)] = (int32_t)i;
+            if (i < hi) {
+                const int32_t at = atomicAdd(&cur[kk[k]], 1);
+                if ((uint32_t)at < (uint32_t)kg.n_items) kg.order[at] = (int32_t)i;  // (bound)
+            }
         }
     }
 }
@@ -5284,6 +5331,8 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     double* s_len = smem + 64 * D;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
+    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
+        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         double L = 0.0, len = 0.0, ksum = 0.0, nsum = 0.0, hmax = -INFINITY;
@@ -5371,9 +5420,14 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the arc
 // formula), CH unconditional 16-B loads (a slot past the group's end reads the plane's first
 // pair and is masked off in the consume step), then the branch-free consume.
-template <int CH, bool CELLS>
-__global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp kg,
-                                                   const uint4* __restrict__ rec) {
+// BS, WIN (UAM_OPT_K2G_LDS_WINDOW; measured, not the default -- DESIGN.md §4 K2h): workgroups
+// of BS items, and a WIN x WIN-cell window of the packed plane staged in LDS around the
+// workgroup's middle item (its middle waypoint's cell): a code-1 waypoint inside it reads LDS,
+// its global load is the dummy line.  The window's staging reads each of its lines once.
+template <int CH, bool CELLS, int BS = 256, int WIN = 0>
+__global__ __launch_bounds__(BS, BS == 256 ? 4 : 1) void k_h_eval(KParams p, KRaster rs,
+                                                                  KGrp kg,
+                                                                  const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_map = s_dyn;
     const int mapw = (rs.pwords + 3) & ~3;
@@ -5381,6 +5435,9 @@ __global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp k
     // CELLS: each wave's [CH][64] staging slice of waypoint cells, after the unit-arc rows and
     // their junk slot
     int32_t* s_cells = reinterpret_cast<int32_t*>(s_u + kg.D * p.N + 1);
+    // WIN: the window (plane-A layout: 4 x 4-cell blocks of 8-B entries) after the cells slice
+    uint2* s_win = reinterpret_cast<uint2*>(s_cells + (CELLS ? (BS / 64) * CH * 64 : 0));
+    __shared__ int32_t s_org[2];
     {  // staging as k_g_eval: every load of a thread issued before its first LDS store
         constexpr int U = 4;
         const int nv = rs.pwords >> 2, nu = kg.D * p.N;
@@ -5388,25 +5445,60 @@ __global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp k
         uint4* dst = reinterpret_cast<uint4*>(s_map);
         const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
         uint4* du = reinterpret_cast<uint4*>(s_u);
-        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += 256 * U) {
+        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += BS * U) {
             uint4 v[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * 256;
+                const int i = i0 + k * BS;
                 v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * 256;
+                const int i = i0 + k * BS;
                 *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
             }
         }
-        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += 256) s_map[i] = rs.pmap[i];
+        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += BS) s_map[i] = rs.pmap[i];
+    }
+    const int64_t pos0 = xcd_chunk(blockIdx.x, gridDim.x) * BS;
+    if (WIN > 0) {
+        if (threadIdx.x == 0) {  // the window around the middle item's middle waypoint
+            const int64_t pm = min(pos0 + BS / 2, kg.n_items - 1);
+            const int32_t it = kg.order[pm];
+            const int32_t pth = (int32_t)div_magic((uint32_t)it, kg.m_nseg, kg.sh_nseg);
+            const int sg = it - pth * kg.nseg;
+            const int32_t qq = (int32_t)div_magic((uint32_t)pth, kg.m_d, kg.sh_d);
+            const int32_t dd = pth - qq * kg.D;
+            const double4 pm4 = reinterpret_cast<const double4*>(kg.pairs)[qq];
+            const int jj0 = sg * kg.G, jj1 = min(jj0 + kg.G, kg.W);
+            const int jm = min(max((jj0 + jj1 - 1) >> 1, 1), p.N);
+            const double2 um = reinterpret_cast<const double2*>(kg.utab)[dd * p.N + jm - 1];
+            double mx, my;
+            arc_point(pm4.x, pm4.y, pm4.z, pm4.w, um.x, um.y, mx, my);
+            const double tx = (mx - rs.x0) * rs.inv_dx, ty = (rs.y_top - my) * rs.inv_dy;
+            const int32_t cx0 = (tx >= 0.0 && tx < (double)rs.nx) ? (int32_t)tx : 0;
+            const int32_t cy0 = (ty >= 0.0 && ty < (double)rs.ny) ? (int32_t)ty : 0;
+            s_org[0] = max(0, min(cx0 - WIN / 2, rs.nx - WIN)) & ~3;
+            s_org[1] = max(0, min(cy0 - WIN / 2, rs.ny - WIN)) & ~3;
+        }
+        __syncthreads();
+        const int ox = s_org[0], oy = s_org[1];
+        constexpr int WB = WIN / 4;  // window blocks per side; a block = 16 entries = 8 x uint4
+        uint4* dw = reinterpret_cast<uint4*>(s_win);
+        for (int i = threadIdx.x; i < WB * WB * 8; i += BS) {
+            const int blk = i >> 3, part = i & 7;
+            const int by = blk / WB, bx = blk - by * WB;
+            const int gy = (oy >> 2) + by, gx = (ox >> 2) + bx;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (gx * 4 < rs.nx && gy * 4 < rs.ny)
+                v = reinterpret_cast<const uint4*>(rs.pa + (((int64_t)gy * rs.pnbx + gx) << 4))[part];
+            dw[i] = v;
+        }
     }
     __syncthreads();
     // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
     // last item evaluates nothing and writes nothing
-    const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    const int64_t pos = pos0 + threadIdx.x;
     const bool live = pos < kg.n_items;
     const int32_t item = live ? kg.order[pos] : 0;
     const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
@@ -5436,8 +5528,9 @@ __global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp k
     for (int c = 0; c < nch; ++c) {
         const int jc = j0 + c * CH;
         uint4 r[CH];
+        uint2 lv[WIN > 0 ? CH : 1];
         int32_t cl[CH];
-        uint32_t inb = 0, need = 0, full = 0, odd = 0;
+        uint32_t inb = 0, need = 0, full = 0, odd = 0, inw = 0;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int j = jc + t;
@@ -5466,9 +5559,21 @@ __global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp k
                     const int32_t a = pk_addr(rs, ix, iy);
                     odd |= (uint32_t)(a & 1) << t;
                     ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
+                    if (WIN > 0) {
+                        const int wx = ix - s_org[0], wy = iy - s_org[1];
+                        if ((uint32_t)wx < (uint32_t)WIN && (uint32_t)wy < (uint32_t)WIN) {
+                            inw |= 1u << t;
+                            ptr = dummy;
+                        }
+                    }
                 }
             }
             r[t] = *ptr;
+            if (WIN > 0) {  // the window's entry (index 0 when unused)
+                const int wx = ((inw >> t) & 1u) ? ((int32_t)((x0 - rs.x0) * rs.inv_dx) - s_org[0]) : 0;
+                const int wy = ((inw >> t) & 1u) ? ((int32_t)((rs.y_top - x1) * rs.inv_dy) - s_org[1]) : 0;
+                lv[t] = s_win[(((wy >> 2) * (WIN / 4) + (wx >> 2)) << 4) | ((wy & 3) << 2) | (wx & 3)];
+            }
         }
         const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
 #pragma unroll
@@ -5477,8 +5582,9 @@ __global__ __launch_bounds__(256, 4) void k_h_eval(KParams p, KRaster rs, KGrp k
             const bool in = (inb >> t) & 1u, nd = (need >> t) & 1u, fl = (full >> t) & 1u,
                        od = (odd >> t) & 1u;
             const uint4 rt = r[t];
-            const uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
+            uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
             uint32_t ter = nd ? (fl ? rt.z : od ? rt.w : rt.y) : 0u;
+            if (WIN > 0 && ((inw >> t) & 1u)) phi = lv[t].x, ter = lv[t].y;
             const uint32_t psi = fl ? rt.y : 0u;
             if (fl && (rt.w & UAM_FLAG_NODATA)) ter = 0u;
             nh += (fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
@@ -5531,6 +5637,8 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
     const HSlot* slot = reinterpret_cast<const HSlot*>(kg.slot);
+    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
+        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         HSlot g[NR > 0 ? NR : 1];
@@ -5599,6 +5707,271 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
     }
 }
 
+// ---- K4h: the volume (config 5) in K2h's form -------------------------------------------------
+// The packed volume (uam_volume_pack): one 16-B voxel {risk, psi_nfz, terrain, flags} per
+// (ix, iy, iz) -- the column's terrain / flags beside the layer's pair, so a waypoint is ONE
+// request -- in blocks of 4 x 2 cells of one layer (one 128-B line), layer-major planes.  The
+// (path, group) items are sorted on the altitude band and the Hilbert tile of the middle
+// waypoint (band-major, so the items an XCD runs together share a band's lines), evaluated
+// with K2h's grouped partial sums, and the output launch adds the similarity-form geometry.
+// Definition: oracle orc_eval_generated_h, mode 2.
+__device__ __forceinline__ int64_t vpk_index(int32_t nbx4, int32_t nby2, int32_t ix, int32_t iy,
+                                             int32_t iz) {
+    return ((((int64_t)iz * nby2 + (iy >> 1)) * nbx4 + (ix >> 2)) << 3) | ((iy & 1) << 2) |
+           (ix & 3);
+}
+
+// one thread per packed voxel (padding cells: zero)
+__global__ __launch_bounds__(256) void k_volume_pack(const uint2* __restrict__ vox,
+                                                     const uint2* __restrict__ col, int nx,
+                                                     int ny, int nz, int nbx4, int nby2,
+                                                     uint4* __restrict__ out) {
+    const int64_t total = (int64_t)nbx4 * nby2 * 8 * nz;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t w = (int32_t)(i & 7);
+        const int64_t blk = i >> 3;
+        const int32_t bx = (int32_t)(blk % nbx4);
+        const int64_t r = blk / nbx4;
+        const int32_t by = (int32_t)(r % nby2), iz = (int32_t)(r / nby2);
+        const int32_t ix = bx * 4 + (w & 3), iy = by * 2 + (w >> 2);
+        uint4 o = make_uint4(0u, 0u, 0u, 0u);
+        if (ix < nx && iy < ny) {
+            const int64_t c = (int64_t)iy * nx + ix;
+            const uint2 a = vox[c * nz + iz], b = col[c];
+            o = make_uint4(a.x, a.y, b.x, b.y);
+        }
+        out[i] = o;
+    }
+}
+
+struct alignas(16) VSlot {  // 32 B per (path, group)
+    double cost;   // risk / N of the group's waypoints, from +0.0 in waypoint order
+    double psi;    // psi_nfz likewise
+    double cm;     // min over the group's waypoints of z_j - terrain (+inf: none)
+    uint32_t cnt;  // nfz hits | off-volume << 8 | below-terrain << 16
+    uint32_t pad;
+};
+
+struct KVol4 {  // the packed volume as K4h reads it
+    int32_t nx, ny, nz, nbx4, nby2;
+    double x0, y_top, z0, dz, inv_dx, inv_dy, inv_dz;
+    const uint4* __restrict__ vp;
+    int32_t zshift, nbands;
+};
+
+// the altitude of waypoint j (uam_eval_generated3d: z0 + (zf - z0) (j / (N+1)))
+__device__ __forceinline__ double vz_at(double za, double zb, double jw) {
+    return za + (zb - za) * jw;
+}
+
+// sort, launch 1 (K4h): keys on (altitude band, tile) of each item's middle waypoint; block
+// G_NBK forms the unit sums (k_g_hist's K2h block)
+__global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
+    __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
+    __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];
+    const int t = threadIdx.x, b = blockIdx.x;
+    if (b == G_NBK) {  // the unit rows through LDS (the histogram's; one round trip)
+        if (kg.ugeo)
+            unit_geo_block(p, kg, reinterpret_cast<double2*>(h), (int)(sizeof(h) / 16));
+        return;
+    }
+    for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
+    for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
+    __syncthreads();
+    const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
+    const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
+    const int N = p.N, W = kg.W;
+    const int tiles = 1 << (2 * kg.tbits);
+    for (int64_t i = lo + t; i < hi; i += 1024) {
+        const int32_t path = (int32_t)div_magic((uint32_t)i, kg.m_nseg, kg.sh_nseg);
+        const int sg = (int)(i - (int64_t)path * kg.nseg);
+        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+        const int32_t d = path - q * kg.D;
+        const int j0 = sg * kg.G, j1 = min(j0 + kg.G, W);
+        const int jm = (j0 + j1 - 1) >> 1;
+        const double* pr = kg.pairs + (int64_t)q * 6;
+        double x0, x1;
+        if (jm == 0) {
+            x0 = pr[0], x1 = pr[1];
+        } else if (jm == W - 1) {
+            x0 = pr[3], x1 = pr[4];
+        } else {
+            const double2 u = reinterpret_cast<const double2*>(kg.utab)[d * N + jm - 1];
+            arc_point(pr[0], pr[1], pr[3], pr[4], u.x, u.y, x0, x1);
+        }
+        const double z = vz_at(pr[2], pr[5], (double)jm / (double)(W - 1));
+        const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
+        const double tz = (z - vs.z0) * vs.inv_dz;
+        uint32_t key = kg.bins - 1;
+        if ((tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) && (ty < (double)vs.ny) &&
+            (tz >= 0.0) && (tz < (double)vs.nz)) {
+            const uint32_t cx = (uint32_t)tx >> kg.tshift, cy = (uint32_t)ty >> kg.tshift;
+            key = ((uint32_t)tz >> vs.zshift) * tiles + tk[(cy << kg.tbits) | cx];
+            if (sg == kg.nseg - 1) key += kg.last_bin;
+        }
+        kg.key[i] = (uint16_t)key;
+        atomicAdd(&h[key], 1);
+    }
+    __syncthreads();
+    for (int k = t; k < kg.bins; k += 1024)
+        if (h[k]) kg.cnt[(int64_t)k * G_NBK + b] = atomicAdd(&kg.gcnt[k], h[k]);
+}
+
+// every (path, group) item in sorted order: points (x, y by the arc formula, z on the linear
+// climb), ONE 16-B load per waypoint from the packed volume (a slot outside the volume or past
+// the group's end reads the first voxel line and is masked off), the branch-free consume
+template <int CH>
+__global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg) {
+    extern __shared__ __attribute__((aligned(16))) double2 s_u[];  // unit-arc rows, then j / (W-1)
+    const int N = p.N, W = kg.W;
+    const int nu = kg.D * N;
+    double* s_jw = reinterpret_cast<double*>(s_u + nu);
+    for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
+    for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
+    __syncthreads();
+    const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    if (pos >= kg.n_items) return;
+    const int32_t item = kg.order[pos];
+    const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
+    const int s = item - path * kg.nseg;
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
+    const double* prp = kg.pairs + (int64_t)q * 6;
+    const double2 pa = *reinterpret_cast<const double2*>(prp);
+    const double2 pb = *reinterpret_cast<const double2*>(prp + 2);
+    const double2 pc = *reinterpret_cast<const double2*>(prp + 4);
+    const double ax = pa.x, ay = pa.y, za = pb.x, bx = pb.y, by = pc.x, zb = pc.y;
+    const double2* urow = s_u + d * N;
+    const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
+    const double vx = ax - bx, vy = ay - by;
+    const double cx = (bx + ax) * 0.5, cy = (by + ay) * 0.5;
+    const double dN = (double)N, yN = kg.inv_n;
+    auto over_n = [&](double a) {
+        if (yN == 0.0) return a / dN;
+        const double q0 = a * yN;
+        const double q1 = fma(fma(-q0, dN, a), yN, q0);
+        return __builtin_isinf(a) ? q0 : q1;
+    };
+    const uint4* const dummy = vs.vp;
+    double gc = 0.0, gn = 0.0, cm = INFINITY;
+    uint32_t nh = 0, off = 0, bel = 0;
+    for (int jc = j0; jc < j1; jc += CH) {
+        uint4 r[CH];
+        double zt[CH];
+        int32_t izt[CH];
+        uint32_t inb = 0;
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int j = jc + t;
+            const double2 u = urow[min(max(j - 1, 0), N - 1)];
+            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
+            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+            x0 = j == 0 ? ax : j == W - 1 ? bx : x0;
+            x1 = j == 0 ? ay : j == W - 1 ? by : x1;
+            const double z = vz_at(za, zb, s_jw[min(j, W - 1)]);
+            zt[t] = z;
+            const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
+            const double tz = (z - vs.z0) * vs.inv_dz;
+            const uint4* ptr = dummy;
+            izt[t] = 0;
+            if ((j < j1) && (tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) &&
+                (ty < (double)vs.ny) && (tz >= 0.0) && (tz < (double)vs.nz)) {
+                inb |= 1u << t;
+                const int32_t ix = (int32_t)tx, iy = (int32_t)ty, iz = (int32_t)tz;
+                izt[t] = iz;
+                ptr = vs.vp + vpk_index(vs.nbx4, vs.nby2, ix, iy, iz);
+            }
+            r[t] = *ptr;
+        }
+        const int nv = min(CH, j1 - jc);
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const bool vl = t < nv, in = (inb >> t) & 1u;
+            const uint4 rt = r[t];
+            const float ter = __uint_as_float(rt.z);
+            gc = gc + over_n(in ? (double)__uint_as_float(rt.x) : 0.0);
+            gn = gn + (in ? (double)__uint_as_float(rt.y) : 0.0);
+            nh += (in && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            off += (vl && !in) ? 1u : 0u;
+            bel += (in && (vs.z0 + ((double)izt[t] + 0.5) * vs.dz < (double)ter)) ? 1u : 0u;
+            cm = in ? fmin(cm, zt[t] - (double)ter) : cm;
+        }
+    }
+    VSlot o;
+    o.cost = gc;
+    o.psi = gn;
+    o.cm = cm;
+    o.cnt = nh | (off << 8) | (bel << 16);
+    o.pad = 0;
+    reinterpret_cast<VSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
+}
+
+// outputs of every path (block = 64 pairs x D): the similarity-form geometry (oracle sim_geo on
+// the pair's x/y), cost = (N+1) L + the risk / N partials in group order, min clearance, the
+// counts, and the main.py:175-180 selection
+__global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
+                                                  int32_t* __restrict__ best_f,
+                                                  int32_t* __restrict__ best_l) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int D = kg.D, t = threadIdx.x;
+    double* s_cost = smem;
+    double* s_len = smem + 64 * D;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int qi = t / D, di = t - qi * D;
+    const VSlot* slot = reinterpret_cast<const VSlot*>(kg.slot);
+    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
+        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
+    if (q0 + qi < kg.n_pairs) {
+        const int64_t gp = (q0 + qi) * D + di;
+        const double* pr = kg.pairs + (q0 + qi) * 6;
+        const double x0 = pr[0], y0 = pr[1], xf = pr[3], yf = pr[4];
+        const UGeo u = kg.ugeo[di];
+        const double vx = x0 - xf, vy = y0 - yf;
+        const double sv = vx * vx + vy * vy;
+        const double h = sqrt(sv) * 0.5, h2 = sv * 0.25;
+        const bool ls = p.length_smooth != 0;
+        double L;
+        if (p.quirk_length) {
+            const double axx = p.anchor_mode ? p.anchor_x : x0;
+            const double ayy = p.anchor_mode ? p.anchor_y : y0;
+            const double dx = x0 - axx, dy = y0 - ayy;
+            const double n = sqrt(dx * dx + dy * dy);
+            L = (ls ? n * n : n) + (ls ? h2 * u.s2n : h * u.s1n);
+        } else {
+            L = ls ? h2 * u.s2a : h * u.s1a;
+        }
+        const double len = h * u.s1a;
+        const double ksum = (h > 0.0 && h < INFINITY) ? h * u.e12 + u.e3 : 0.0;
+        double cost = (double)(p.N + 1) * L, nsum = 0.0, cm = INFINITY;
+        int32_t nh = 0, off = 0, bel = 0;
+        for (int s = 0; s < kg.nseg; ++s) {
+            const VSlot g = slot[(int64_t)s * kg.P + gp];
+            cost = cost + g.cost;
+            nsum = nsum + g.psi;
+            cm = fmin(cm, g.cm);
+            nh += (int32_t)(g.cnt & 255u);
+            off += (int32_t)((g.cnt >> 8) & 255u);
+            bel += (int32_t)((g.cnt >> 16) & 255u);
+        }
+        if (out.cost) out.cost[gp] = cost;
+        if (out.length_q) out.length_q[gp] = L;
+        if (out.length) out.length[gp] = len;
+        if (out.kin_sum) out.kin_sum[gp] = ksum;
+        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
+        if (out.min_clearance) out.min_clearance[gp] = cm;
+        if (out.nfz_hits) out.nfz_hits[gp] = nh;
+        if (out.offmap) out.offmap[gp] = off;
+        if (out.below_terrain) out.below_terrain[gp] = bel;
+        s_cost[di * 64 + qi] = cost;
+        s_len[di * 64 + qi] = len;
+    }
+    __syncthreads();
+    if (t < 64 && q0 + t < kg.n_pairs) {
+        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -5651,6 +6024,8 @@ struct uam_ctx {
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     bool k2g_attrs_cells = false;  // the same for the cell-writing K2g forms
+    int32_t* d_gcnt = nullptr;  // K2g / K2h sort: bin totals (zero between calls)
+    bool gcnt_dirty = false;    // re-zero them before the next sort
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     uint16_t* d_tkey = nullptr; // K2g: sort key of each tile (curve order), for tkey_bits/curve
@@ -5675,6 +6050,7 @@ struct uam_ctx {
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
+    int k2g_lwin = 0;           // K2h LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW: 0, 96, 128)
     int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
     int k2g_chunk = 0;          // K2g gathers in flight per lane (UAM_OPT_K2G_CHUNK: 6, 8, 11;
@@ -5818,6 +6194,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventSynchronize(ctx->ev_ord);
     if (ctx->d_ord) (void)hipFree(ctx->d_ord);
     if (ctx->d_tkey) (void)hipFree(ctx->d_tkey);
+    if (ctx->d_gcnt) (void)hipFree(ctx->d_gcnt);
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -6380,6 +6757,12 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             (long long)value);
             ctx->k2g_chunk = (int)value;
             return UAM_OK;
+        case UAM_OPT_K2G_LDS_WINDOW:
+            if (value != 0 && value != 96 && value != 128)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_WINDOW %lld not 0, 96 or 128",
+                            (long long)value);
+            ctx->k2g_lwin = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2G_SIM:
             if (value != 0 && value != 1)
                 return fail(UAM_E_INVALID, "UAM_OPT_K2G_SIM %lld not 0 or 1", (long long)value);
@@ -6413,6 +6796,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
+        case UAM_OPT_K2G_LDS_WINDOW: *value = ctx->k2g_lwin; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
@@ -6730,7 +7114,6 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int bins = tiles + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)bins * G_NBK;
-    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
     // K2h (the similarity form) unless disabled or maxratio_smooth (its turn rows are not
     // scale-free): 24-B slots, the geometry in the output launch
     const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth;
@@ -6759,6 +7142,16 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
     if (st) return st;
     kg.tkey = ctx->d_tkey;
+    if (!ctx->d_gcnt) {  // the bin totals: zeroed here, left zero by every output launch
+        if (hipMalloc(&ctx->d_gcnt, sizeof(int32_t) * G_BINS_MAX) != hipSuccess)
+            return fail(UAM_E_NOMEM, "K2g bin totals");
+        ctx->gcnt_dirty = true;
+    }
+    if (ctx->gcnt_dirty) {  // first use, or a sequence that did not reach its output launch
+        HIP_TRY(hipMemsetAsync(ctx->d_gcnt, 0, sizeof(int32_t) * G_BINS_MAX, s));
+        ctx->gcnt_dirty = false;
+    }
+    kg.gcnt = ctx->d_gcnt;
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
@@ -6799,9 +7192,6 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = ktime_begin(ctx, s);
     if (st) return st;
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK + (sim ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kr, kg);
-    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
-                       kg.tot);
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
@@ -6817,26 +7207,134 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                                           k_g_eval<8, true, false, true>,
                                           k_g_eval<8, true, true, true>};
     kg.cells = ko.cells;
-    const EvalFn ev = sim ? (ko.cells ? hevals_cells[0] : hevals[hch])
-                          : ko.cells ? evals_cells[ch & 3] : evals[ch];
+    EvalFn ev = sim ? (ko.cells ? hevals_cells[0] : hevals[hch])
+                    : ko.cells ? evals_cells[ch & 3] : evals[ch];
+    // the LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW, K2h without cells): 1024-item
+    // workgroups, one per CU, a WIN x WIN window (WIN = 96: 72 KiB; 128: 128 KiB)
+    int bs = 256;
+    size_t lds_run = lds;
+    if (sim && !ko.cells && ctx->k2g_lwin) {
+        ev = ctx->k2g_lwin == 96 ? k_h_eval<8, false, 1024, 96> : k_h_eval<8, false, 1024, 128>;
+        bs = 1024;
+        lds_run = lds_need + (size_t)ctx->k2g_lwin * ctx->k2g_lwin * 8;
+        if (lds_run > 160 * 1024) return fail(UAM_E_INVALID, "LDS window too large");
+        HIP_TRY(hipFuncSetAttribute((const void*)ev, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+    }
     if (lds > 64 * 1024 && !ctx->k2g_attrs_cells && ko.cells) {
         for (EvalFn f : evals_cells)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
         ctx->k2g_attrs_cells = true;
     }
-    hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kr, kg, (const uint4*)rec);
+    hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds_run, s,
+                       ctx->kp, kr, kg, (const uint4*)rec);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
                             : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
     hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
-    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
+    if (hipGetLastError() != hipSuccess) {
+        ctx->gcnt_dirty = true;
+        return fail(UAM_E_HIP, "grouped evaluation launch");
+    }
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
     ctx->last_kernel = sim ? "K2h+pack" : "K2g+pack";
+    st = order_done(ctx, s);
+    return st ? st : 1;
+}
+
+// K4h launch (the packed volume in K2h's form); returns 1 if launched, 0 if the batch is not
+// one it takes (the caller runs K4).  Scratch: the pair-order scratch (order_scratch).
+static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6, int64_t n_pairs,
+                            const double* utab, int32_t D, const KOut& ko, int32_t* best_f,
+                            int32_t* best_l, hipStream_t s) {
+    const int G = ctx->k2g_group;
+    if (G < 1 || G > G_MAXLEN || ko.cells || ko.g_rows || D > 16 || ctx->kp.maxratio_smooth ||
+        !ctx->k2g_sim)
+        return 0;
+    const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
+    if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
+    if ((size_t)D * ctx->kp.N * 16 > (size_t)G_UTAB_LDS) return 0;
+    const size_t lds = (size_t)D * ctx->kp.N * 16 + (size_t)W * 8;
+    const int nseg = (int)((W + G - 1) / G);
+    const int64_t n_items = P * nseg;
+    if (n_items >= INT32_MAX) return 0;
+    const int tbits = ctx->k2g_tbits ? std::min(ctx->k2g_tbits, 4) : 4;
+    const int tiles = 1 << (2 * tbits);
+    if (tiles * kv.nbands * 2 + 1 > G_BINS_MAX) return 0;
+    const int last_bin = (W % G) ? tiles * kv.nbands : 0;
+    const int bins = tiles * kv.nbands + last_bin + 1;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const int64_t ncnt = (int64_t)bins * G_NBK;
+    const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
+                 b_ord = al((size_t)n_items * 4), b_slot = al((size_t)n_items * sizeof(VSlot)),
+                 b_ug = al((size_t)D * sizeof(UGeo));
+    char* w = nullptr;
+    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug, s, &w);
+    if (st) return st;
+    KGrp kg{};
+    kg.pairs = pairs6;
+    kg.utab = utab;
+    kg.n_pairs = n_pairs;
+    kg.P = (int32_t)P;
+    kg.D = D;
+    kg.W = (int32_t)W;
+    kg.G = G;
+    kg.nseg = nseg;
+    int tshift = 0;
+    while (((std::max(kv.nx, kv.ny) - 1) >> tshift) >= (1 << tbits)) ++tshift;
+    kg.tshift = tshift;
+    kg.tbits = tbits;
+    kg.bins = bins;
+    kg.last_bin = last_bin;
+    st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
+    if (st) return st;
+    kg.tkey = ctx->d_tkey;
+    if (!ctx->d_gcnt) {
+        if (hipMalloc(&ctx->d_gcnt, sizeof(int32_t) * G_BINS_MAX) != hipSuccess)
+            return fail(UAM_E_NOMEM, "K2g bin totals");
+        ctx->gcnt_dirty = true;
+    }
+    if (ctx->gcnt_dirty) {
+        HIP_TRY(hipMemsetAsync(ctx->d_gcnt, 0, sizeof(int32_t) * G_BINS_MAX, s));
+        ctx->gcnt_dirty = false;
+    }
+    kg.gcnt = ctx->d_gcnt;
+    magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
+    magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
+    kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
+    kg.n_items = n_items;
+    size_t o = 0;
+    kg.slot = (GSlot*)(w + o), o += b_slot;  // VSlot
+    kg.ugeo = (UGeo*)(w + o), o += b_ug;
+    kg.order = (int32_t*)(w + o), o += b_ord;
+    kg.cnt = (int32_t*)(w + o), o += b_cnt;
+    kg.key = (uint16_t*)(w + o);
+    st = ktime_begin(ctx, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_v_hist, dim3(G_NBK + 1), dim3(1024), 0, s, ctx->kp, kv, kg);
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
+    const dim3 ge((unsigned)((n_items + 255) / 256));
+    using VEvalFn = void (*)(KParams, KVol4, KGrp);
+    // gathers in flight per lane: 6 by default (k_v_eval<8> spills at 4 waves per SIMD)
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 6;
+    const VEvalFn ev = chl <= 6 ? k_v_eval<6> : chl == 7 ? k_v_eval<7> : chl <= 8 ? k_v_eval<8>
+                                                                        : k_v_eval<11>;
+    hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kv, kg);
+    hipLaunchKernelGGL(k_v_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
+                       (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
+    if (hipGetLastError() != hipSuccess) {
+        ctx->gcnt_dirty = true;
+        return fail(UAM_E_HIP, "grouped volume evaluation launch");
+    }
+    st = ktime_end(ctx, s);
+    if (st) return st;
+    ctx->last_group = G;
+    ctx->last_kernel = "K4h+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -7223,6 +7721,85 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
                        (uint32_t*)((char*)vol + vol_bits_offset(vd)));
     HIP_TRY(hipGetLastError());
     return UAM_OK;
+}
+
+namespace {
+// the packed volume's dimensions (uam_volume_pack): 4 x 2-cell blocks, nz layer planes
+void vpk_dims(const uam_volume_desc* d, int32_t* nbx4, int32_t* nby2, int64_t* bytes) {
+    *nbx4 = (d->nx + 3) >> 2;
+    *nby2 = (d->ny + 1) >> 1;
+    *bytes = (int64_t)*nbx4 * *nby2 * 8 * d->nz * 16;
+}
+}  // namespace
+
+int uam_volume_packed_bytes(const uam_volume_desc* vd, int64_t* bytes) {
+    KVolume kv;
+    int st = make_kvolume(vd, &kv);
+    if (st) return st;
+    if (!bytes) return fail(UAM_E_INVALID, "bytes is NULL");
+    int32_t a, b;
+    vpk_dims(vd, &a, &b, bytes);
+    return UAM_OK;
+}
+
+int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, void* packed,
+                    uam_stream stream) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    KVolume kv;
+    int st = make_kvolume(vd, &kv);
+    if (st) return st;
+    if (!vol || !packed) return fail(UAM_E_INVALID, "volume pack pointer is NULL");
+    if (((uintptr_t)vol & 255) || ((uintptr_t)packed & 255))
+        return fail(UAM_E_INVALID, "volume buffers not 256-B aligned");
+    DeviceGuard dg(ctx->device);
+    int32_t nbx4, nby2;
+    int64_t bytes;
+    vpk_dims(vd, &nbx4, &nby2, &bytes);
+    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for(bytes / 16, 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint2*)vol,
+                       (const uint2*)((const char*)vol + vol_col_offset(vd)), vd->nx, vd->ny,
+                       vd->nz, nbx4, nby2, (uint4*)packed);
+    HIP_TRY(hipGetLastError());
+    return UAM_OK;
+}
+
+int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
+                           const void* packed, const double* pairs6, int64_t n_pairs,
+                           const double* utab, int32_t D, const uam_path_outputs* out,
+                           uam_stream stream) {
+    if (packed) {
+        int st = check_ctx(ctx, true);
+        if (st) return st;
+        if (n_pairs < 0 || D < 1 || D > 16)
+            return fail(UAM_E_INVALID, "n_pairs < 0 or D outside [1, 16]");
+        if (n_pairs == 0) return UAM_OK;
+        KVolume kv0;
+        st = make_kvolume(vd, &kv0);
+        if (st) return st;
+        if (!pairs6 || !utab) return fail(UAM_E_INVALID, "pointer is NULL");
+        if ((uintptr_t)packed & 255) return fail(UAM_E_INVALID, "packed volume not 256-B aligned");
+        KVol4 kv{};
+        kv.nx = vd->nx, kv.ny = vd->ny, kv.nz = vd->nz;
+        int64_t bytes;
+        vpk_dims(vd, &kv.nbx4, &kv.nby2, &bytes);
+        kv.x0 = vd->x0, kv.y_top = vd->y_top, kv.z0 = vd->z0, kv.dz = vd->dz;
+        kv.inv_dx = 1.0 / vd->dx, kv.inv_dy = 1.0 / vd->dy, kv.inv_dz = 1.0 / vd->dz;
+        kv.vp = (const uint4*)packed;
+        int zs = 0;  // altitude bands: at most 16
+        while ((vd->nz - 1) >> zs >= 16) ++zs;
+        kv.zshift = zs;
+        kv.nbands = ((vd->nz - 1) >> zs) + 1;
+        const KOut ko = make_kout(out);
+        DeviceGuard dg(ctx->device);
+        if (!want_wave(ctx, n_pairs * D)) {
+            st = launch_grouped3d(ctx, kv, pairs6, n_pairs, utab, D, ko,
+                                  out ? out->best_fval_idx : nullptr,
+                                  out ? out->best_length_idx : nullptr, (hipStream_t)stream);
+            if (st < 0) return st;
+            if (st == 1) return UAM_OK;
+        }
+    }
+    return uam_eval_generated3d(ctx, vd, vol, pairs6, n_pairs, utab, D, out, stream);
 }
 
 int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,

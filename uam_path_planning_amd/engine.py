@@ -119,6 +119,9 @@ class RiskVolume:
     vox: object = field(repr=False)     # [ny, nx, nz, 2] int32 view: 8-B voxels {risk, psi}
     cols: object = field(repr=False)    # [ny, nx, 2] int32 view: columns {terrain, flags}
     cbits: object = field(repr=False, default=None)  # int32 view: the column bitmap words
+    # the packed copy K4h reads (Engine.volume_pack: 16-B voxels {risk, psi, terrain, flags} in
+    # 4 x 2-cell blocks per layer), or None; rebuild it after buf changes
+    packed: object = field(repr=False, default=None)
 
 
 def _ptr(t):
@@ -442,6 +445,19 @@ class Engine:
                                              self.stream), "uam_volume_build")
         return vol
 
+    def volume_pack(self, volume):
+        """Derive the packed copy K4h evaluates (uam_volume_pack) into volume.packed."""
+        torch = _torch()
+        nb = ctypes.c_int64()
+        _lib.check(self.lib.uam_volume_packed_bytes(ctypes.byref(volume.geo.as_struct()),
+                                                    ctypes.byref(nb)), "uam_volume_packed_bytes")
+        packed = self.empty((nb.value // 4,), torch.int32)
+        _lib.check(self.lib.uam_volume_pack(self._ctx, ctypes.byref(volume.geo.as_struct()),
+                                            _ptr(volume.buf), _ptr(packed), self.stream),
+                   "uam_volume_pack")
+        volume.packed = packed
+        return packed
+
     def eval_generated3d(self, pairs6, utab, volume, outputs=None):
         """pairs6 [Q, 6] = (x0, y0, z0, xf, yf, zf) (km, km, m); path p = q*D + d."""
         torch = _torch()
@@ -457,9 +473,10 @@ class Engine:
         else:
             o, s = self._outputs(Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False,
                                  n_pairs=Q)
-        _lib.check(self.lib.uam_eval_generated3d(
-            self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.buf), _ptr(pr), Q,
-            _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated3d")
+        _lib.check(self.lib.uam_eval_generated3d_p(
+            self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.buf),
+            _ptr(volume.packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
+            "uam_eval_generated3d_p")
         return o
 
     def gen_paths(self, pairs, utab):
