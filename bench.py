@@ -592,6 +592,10 @@ def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_ce
 
 
 def order_name(group, kernel=None):
+    if kernel == "K4h+pack":
+        return (f"volume sums as per-path partial sums over groups of {group} waypoints, added "
+                f"in group order; the geometry terms in the similarity form (oracle "
+                f"orc_eval_generated_h, volume mode)")
     if kernel == "K2h+pack":
         return (f"raster sums as per-path partial sums over groups of {group} waypoints, added "
                 f"in group order; the geometry terms in the similarity form (oracle "

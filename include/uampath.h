@@ -409,8 +409,10 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem_dev, const uam_raster_desc* 
  * of them once), so any number of calls may pass between queries. */
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable);
 int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
-/* The path evaluation the last uam_eval_generated* call on ctx ran: "K2g+pack" (segment-grouped
- * raster, the default for packed rasters and batches >= UAM_OPT_SORTED_MIN_PATHS paths),
+/* The path evaluation the last uam_eval_generated* call on ctx ran: "K2h+pack" (segment-grouped
+ * raster with the similarity-form geometry, the default for packed rasters and batches >=
+ * UAM_OPT_SORTED_MIN_PATHS paths), "K2g+pack" (the same with per-segment geometry:
+ * UAM_OPT_K2G_SIM = 0 or maxratio_smooth), "K4h+pack" (the packed volume, K2h's form),
  * "K2s+pack" / "K2s+skip" / "K2s" (segment-sorted raster, sequential sums), "K2+skip" / "K2"
  * (lane per path), "K2w" (wave per path), "K2d" (D > 16), "K3b", "K3", "K3d", "K4", "K4w";
  * "" before the first call.  The string is static (never freed).  For benchmarks and tests:
@@ -418,10 +420,18 @@ int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches);
 const char* uam_last_kernel(const uam_ctx* ctx);
 
 /* Waypoint-group length of the per-path sums of the last uam_eval_generated* call on ctx: G > 0
- * when the segment-grouped raster evaluation K2g ran (cost, length_q, length, kin_sum and
- * nfz_sum formed as per-group partial sums, each term attached to a waypoint of the group
- * [kG, (k+1)G), added in group order; oracle/uam_oracle.c orc_eval_paths_g), 0 for the
- * reference's sequential order (problem.py:38-44, 84-114, 130-146). */
+ * when a segment-grouped evaluation ran -- K2g: cost, length_q, length, kin_sum and nfz_sum
+ * formed as per-group partial sums, each term attached to a waypoint of the group
+ * [kG, (k+1)G), added in group order (oracle/uam_oracle.c orc_eval_paths_g); K2h / K4h: the
+ * raster (volume) terms of cost and nfz_sum so, length_q / length / kin_sum in the similarity
+ * form (orc_eval_generated_h) -- 0 for the reference's sequential order (problem.py:38-44,
+ * 84-114, 130-146).
+ * Tolerance against the sequential order: rounding only.  Measured: <= 8.2e-14 relative on
+ * cost and 4.4e-14 on length over the whole cfg3 batch (500k paths), <= 1e-12 on every test
+ * map, against the north_star's 1e-5; the selections (best_fval_idx, best_length_idx) agreed
+ * on all 100k cfg3 pairs (bench.py parity.vs_sequential_order) -- they can differ only where
+ * two candidates of a pair are within that rounding of each other.  A caller that needs the
+ * sequential bits sets UAM_OPT_GROUP = 0 (K2s / K4). */
 int32_t uam_last_group(const uam_ctx* ctx);
 
 /* Context options: which kernel form runs (results never depend on them, except for the sum
@@ -457,7 +467,11 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K2G_LDS_WINDOW       K2h experiment (not faster): 0 (default), or
  *                                96 / 128: 1024-item workgroups that stage a window of that
  *                                many cells square of the packed plane in LDS and serve the
- *                                code-1 waypoints inside it from there.  Same outputs. */
+ *                                code-1 waypoints inside it from there.  Same outputs.
+ *   UAM_OPT_K4H_BAND             K4h sort key: altitude layers per band, a power of two
+ *                                (default 0: the fewest giving at most 16 bands); tiles from
+ *                                UAM_OPT_K2G_TILE_BITS (default 4: 16 x 16 tiles), at most
+ *                                4096 (tile, band) bins */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -474,7 +488,8 @@ enum {
     UAM_OPT_K2G_CHUNK = 13,
     UAM_OPT_K2G_CURVE = 14,
     UAM_OPT_K2G_SIM = 15,
-    UAM_OPT_K2G_LDS_WINDOW = 16
+    UAM_OPT_K2G_LDS_WINDOW = 16,
+    UAM_OPT_K4H_BAND = 17
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

@@ -117,20 +117,45 @@ def test_k4h_chunks(oracle_mod, chunk):
 
 
 def test_k4h_pack_layout(oracle_mod):
-    """uam_volume_pack against its definition: voxel (ix, iy, iz) at
-    ((iz nby2 + iy/2) nbx4 + ix/4) 8 + (iy%2) 4 + ix%4, {risk, psi} of the voxel, {terrain,
-    flags} of the column, zero padding."""
+    """uam_volume_pack against its definition: the 16-B table (voxel (ix, iy, iz) at
+    ((iz nby2 + iy/2) nbx4 + ix/4) 8 + (iy%2) 4 + ix%4: {risk, psi} of the voxel, {terrain,
+    flags} of the column), the 8-B table ({risk, terrain} at ((iz nby4 + iy/4) nbx4 + ix/4) 16
+    + (iy%4) 4 + ix%4), zero padding, and the 2-bit code per 8 x 8 columns (3 where a column
+    has psi != +-0 or the no-fly flag, else 1), 256-B aligned sections."""
     e, orc, vol, vd, host = _case(oracle_mod, 300, 7, 10, 21)
-    pk = vol.packed.cpu().numpy().reshape(-1, 4)
+    raw = vol.packed.cpu().numpy()
     ny, nx, nz = 300, 300, 7
-    nbx4, nby2 = (nx + 3) // 4, (ny + 1) // 2
+    al = lambda v: (v + 255) // 256 * 256
+    nbx4, nby2, nby4 = (nx + 3) // 4, (ny + 1) // 2, (ny + 3) // 4
+    n16 = nbx4 * nby2 * 8 * nz
+    off8 = al(n16 * 16)
+    n8 = nbx4 * nby4 * 16 * nz
+    offc = off8 + al(n8 * 8)
+    cnbx = cnby = (nx + 7) // 8
+    cw = (cnbx * cnby + 15) // 16
+    assert raw.nbytes == offc + al(cw * 4)
+    b = raw.view(np.uint8)
+    t16 = b[:n16 * 16].view(np.int32).reshape(-1, 4)
+    t8 = b[off8:off8 + n8 * 8].view(np.int32).reshape(-1, 2)
+    cm = b[offc:offc + cw * 4].view(np.uint32)
     iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
-    idx = (((iz * nby2 + iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
     vox = vol.vox.cpu().numpy()            # [ny, nx, nz, 2]
     cols = vol.cols.cpu().numpy()          # [ny, nx, 2]
-    want = np.concatenate([vox.transpose(2, 0, 1, 3).reshape(-1, 2),
-                           np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)], axis=1)
-    np.testing.assert_array_equal(pk[idx], want)
-    mask = np.ones(len(pk), bool)
-    mask[idx] = False
-    assert (pk[mask] == 0).all()
+    vz = vox.transpose(2, 0, 1, 3).reshape(-1, 2)
+    cz = np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)
+    i16 = (((iz * nby2 + iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
+    np.testing.assert_array_equal(t16[i16], np.concatenate([vz, cz], axis=1))
+    i8 = (((iz * nby4 + iy // 4) * nbx4 + ix // 4) * 16 + (iy % 4) * 4 + ix % 4).reshape(-1)
+    np.testing.assert_array_equal(t8[i8], np.stack([vz[:, 0], cz[:, 0]], axis=1))
+    for t, idx in ((t16, i16), (t8, i8)):
+        mask = np.ones(len(t), bool)
+        mask[idx] = False
+        assert (t[mask] == 0).all()
+    psi = vox[:, :, 0, 1].view(np.uint32) & 0x7fffffff
+    nfz = cols[:, :, 1].view(np.uint32) & 1
+    hot = np.zeros((cnby * 8, cnbx * 8), bool)
+    hot[:ny, :nx] = (psi != 0) | (nfz != 0)
+    want = np.where(hot.reshape(cnby, 8, cnbx, 8).any(axis=(1, 3)), 3, 1).reshape(-1)
+    got = ((cm[:, None] >> (2 * np.arange(16))) & 3).reshape(-1)[:cnbx * cnby]
+    np.testing.assert_array_equal(got, want)
+    assert (want == 3).any() and (want == 1).any()

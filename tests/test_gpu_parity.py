@@ -340,6 +340,24 @@ def test_full_size_cfg3_properties(eng, oracle_mod):
     seq = orc.eval_paths(wp, mode="raster", rdesc=rd, rec=rec)
     np.testing.assert_allclose(_np(gpu["cost"])[idx], seq["cost"], rtol=1e-12, atol=0)
     np.testing.assert_allclose(_np(gpu["length"])[idx], seq["length"], rtol=1e-12, atol=0)
+    # the whole batch through the sequential order (threads over pair shards; the C oracle
+    # drops the GIL): the grouped sums move no selection on this batch (the
+    # selection of the reference order, pinned at cfg3 size) and no cost by more than 1e-12
+    import concurrent.futures
+    bounds = np.linspace(0, len(pairs), 9).astype(int)
+
+    def seq_part(k):
+        sl = pairs[bounds[k]:bounds[k + 1]]
+        r = orc.eval_paths(oracle_mod.gen_paths(sl, ut), mode="raster", rdesc=rd, rec=rec)
+        return r["cost"], r["length"]
+
+    with concurrent.futures.ThreadPoolExecutor(8) as ex:
+        parts = list(ex.map(seq_part, range(8)))
+    sc = np.concatenate([p_[0] for p_ in parts])
+    sl_ = np.concatenate([p_[1] for p_ in parts])
+    np.testing.assert_allclose(_np(gpu["cost"]), sc, rtol=1e-12, atol=0)
+    assert (oracle_mod.argmin(sc, 5, True) != _np(gpu["best_fval_idx"])).sum() == 0
+    assert (oracle_mod.argmin(sl_, 5, False) != _np(gpu["best_length_idx"])).sum() == 0
     cost, lq = _np(gpu["cost"]), _np(gpu["length_q"])
     assert np.isfinite(cost).all()
     assert (cost >= 81 * lq - 1e-9).all()                 # penalties are non-negative

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cells", action="store_true")
+    ap.add_argument("--volume", action="store_true",
+                    help="cfg5: 1024^2 x 64 volume, packed copy, 100k pairs x 5 (K4h / K4)")
     a = ap.parse_args()
     import torch
     from uam_path_planning_amd.arcs import arc_table
@@ -38,10 +40,24 @@ def main():
     e = Engine(0)
     e.set_geometry(compile_map(build_region_map(spec)))
     e.set_params(canonical_params(spec, N=80, altitude=320.0))
-    raster = e.raster_build(raster_geo(a.R), synthetic_dem(a.R))
     D = 5
-    pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
     ut = e.tensor(arc_table(80, displacements(D)), torch.float64)
+    if a.volume:
+        from uam_path_planning_amd.scenario import layer_weights
+        from uam_path_planning_amd.synthetic import random_pairs3d
+        r2 = e.raster_build(raster_geo(1024), synthetic_dem(1024))
+        vol = e.volume_build(r2, 64, 0.0, 10.0, layer_weights(64))
+        e.volume_pack(vol)
+        pairs = e.tensor(random_pairs3d(a.pairs, seed=0), torch.float64)
+
+        def run():
+            e.eval_generated3d(pairs, ut, vol, outputs=outs)
+    else:
+        raster = e.raster_build(raster_geo(a.R), synthetic_dem(a.R))
+        pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
+
+        def run():
+            e.eval_generated(pairs, ut, raster=raster, outputs=outs)
     outs = e.outputs(a.pairs * D, 82, n_pairs=a.pairs, want_cells=a.cells)
     o = outs[0]
     settings = [s for s in a.settings.split(";") if s.strip()] or [""]
@@ -50,12 +66,12 @@ def main():
         for k, v in kv:
             e.set_option(k.strip(), int(v))
         for _ in range(3):
-            e.eval_generated(pairs, ut, raster=raster, outputs=outs)
+            run()
         torch.cuda.synchronize()
         e.kernel_timing(True)
         t0 = time.perf_counter()
         for _ in range(a.reps):
-            e.eval_generated(pairs, ut, raster=raster, outputs=outs)
+            run()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.reps * 1e3
         ms, n = e.kernel_time()

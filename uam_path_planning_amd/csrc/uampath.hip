@@ -4843,8 +4843,6 @@ struct KGrp {
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
     UGeo* __restrict__ ugeo;       // K2h: [D] unit sums, formed by k_g_hist's extra block
-    int32_t* __restrict__ gcnt;    // [bins] items per bin, zero on entry (k_g_hist adds its
-                                   // partitions' counts, the output launch re-zeroes it)
 };
 
 // K2h / K4h: the D rows' unit sums by one block: the table staged in LDS by every thread with
@@ -4955,41 +4953,20 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
     // the partition's place in each bin: its count added to the bin's total (the order of
     // the partitions inside a bin follows the atomics -- it only decides which lane evaluates
     // an item, never what the item computes); k_g_scatter scans the totals itself
-    for (int k = t; k < kg.bins; k += 1024)
-        if (h[k]) kg.cnt[(int64_t)k * G_NBK + b] = atomicAdd(&kg.gcnt[k], h[k]);
+    for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
-// launch 2: every block scans the bin totals in LDS (exclusive; bins <= G_BINS_MAX), its
-// cursors = bin start + the partition's place in the bin (k_g_hist), items scattered; U keys
-// per thread loaded before the first cursor update
+// launch 4 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered; U keys
+// per thread loaded before the first cursor update.  (A two-launch form -- device-scope
+// atomics on the bin totals in the histogram launch, their scan in this one -- ran the
+// histogram 11 -> 34 us at cfg3: 256 partitions' atomics on each bin address serialise
+// across the XCDs; profiles/r04/prof1.)
 __global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
     __shared__ int32_t cur[G_BINS_MAX];
-    __shared__ int32_t wsum[16];
     const int t = threadIdx.x, b = blockIdx.x;
-    const int per = (kg.bins + 1023) / 1024;  // bins per thread, consecutive
-    int run = 0;
-    for (int k = 0; k < per; ++k) {
-        const int i = t * per + k;
-        const int v = i < kg.bins ? kg.gcnt[i] : 0;
-        if (i < kg.bins) cur[i] = run;  // exclusive within the thread's run
-        run += v;
-    }
-    // exclusive scan of the 1024 thread totals: within the wave, then over the 16 waves
-    const int lane = t & 63, wv = t >> 6;
-    int inc = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int woff = 0;
-    for (int w = 0; w < wv; ++w) woff += wsum[w];
-    const int excl = woff + inc - run;
-    for (int k = 0; k < per; ++k) {
-        const int i = t * per + k;
-        if (i < kg.bins) cur[i] += excl + kg.cnt[(int64_t)i * G_NBK + b];
+    for (int k = t; k < kg.bins; k += 1024) {
+        const int64_t c = (int64_t)k * G_NBK + b;
+        cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
     }
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
@@ -5331,8 +5308,6 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     double* s_len = smem + 64 * D;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
-    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
-        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         double L = 0.0, len = 0.0, ksum = 0.0, nsum = 0.0, hmax = -INFINITY;
@@ -5420,12 +5395,15 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the arc
 // formula), CH unconditional 16-B loads (a slot past the group's end reads the plane's first
 // pair and is masked off in the consume step), then the branch-free consume.
+#ifndef UAM_K2H_MINW  // workgroups of 256 per CU the register budget allows (measurement builds)
+#define UAM_K2H_MINW 4
+#endif
 // BS, WIN (UAM_OPT_K2G_LDS_WINDOW; measured, not the default -- DESIGN.md §4 K2h): workgroups
 // of BS items, and a WIN x WIN-cell window of the packed plane staged in LDS around the
 // workgroup's middle item (its middle waypoint's cell): a code-1 waypoint inside it reads LDS,
 // its global load is the dummy line.  The window's staging reads each of its lines once.
 template <int CH, bool CELLS, int BS = 256, int WIN = 0>
-__global__ __launch_bounds__(BS, BS == 256 ? 4 : 1) void k_h_eval(KParams p, KRaster rs,
+__global__ __launch_bounds__(BS, BS == 256 ? UAM_K2H_MINW : 1) void k_h_eval(KParams p, KRaster rs,
                                                                   KGrp kg,
                                                                   const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -5637,8 +5615,6 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
     const HSlot* slot = reinterpret_cast<const HSlot*>(kg.slot);
-    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
-        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         HSlot g[NR > 0 ? NR : 1];
@@ -5756,9 +5732,70 @@ struct alignas(16) VSlot {  // 32 B per (path, group)
 struct KVol4 {  // the packed volume as K4h reads it
     int32_t nx, ny, nz, nbx4, nby2;
     double x0, y_top, z0, dz, inv_dx, inv_dy, inv_dz;
-    const uint4* __restrict__ vp;
+    const uint4* __restrict__ vp;   // 16-B voxels, 4 x 2-cell blocks
     int32_t zshift, nbands;
+    // the 8-B table {risk, terrain} in 4 x 4-cell blocks and the 2-bit code per 8 x 8-column
+    // block (3: a column of the block has psi != +-0 or the no-fly flag -> read vp; 1: vp8)
+    const uint2* __restrict__ vp8;
+    const uint32_t* __restrict__ cmap;
+    int32_t nby4, cnbx, cwords;
 };
+
+constexpr int VPK_CSHIFT = 3;          // code blocks of 8 x 8 columns
+constexpr int VPK_CMAP_LDS = 16 * 1024; // the code map in LDS up to this (2048^2 columns)
+
+__device__ __forceinline__ int64_t vpk8_index(int32_t nbx4, int32_t nby4, int32_t ix, int32_t iy,
+                                              int32_t iz) {
+    return ((((int64_t)iz * nby4 + (iy >> 2)) * nbx4 + (ix >> 2)) << 4) | ((iy & 3) << 2) |
+           (ix & 3);
+}
+
+// the 8-B table: one thread per entry (padding: zero)
+__global__ __launch_bounds__(256) void k_volume_pack8(const uint2* __restrict__ vox,
+                                                      const uint2* __restrict__ col, int nx,
+                                                      int ny, int nz, int nbx4, int nby4,
+                                                      uint2* __restrict__ out) {
+    const int64_t total = (int64_t)nbx4 * nby4 * 16 * nz;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t w = (int32_t)(i & 15);
+        const int64_t blk = i >> 4;
+        const int32_t bx = (int32_t)(blk % nbx4);
+        const int64_t r = blk / nbx4;
+        const int32_t by = (int32_t)(r % nby4), iz = (int32_t)(r / nby4);
+        const int32_t ix = bx * 4 + (w & 3), iy = by * 4 + (w >> 2);
+        uint2 o = make_uint2(0u, 0u);
+        if (ix < nx && iy < ny) {
+            const int64_t c = (int64_t)iy * nx + ix;
+            o = make_uint2(vox[c * nz + iz].x, col[c].x);
+        }
+        out[i] = o;
+    }
+}
+
+// the code map: one thread per 32-bit word (16 blocks of 8 x 8 columns)
+__global__ __launch_bounds__(256) void k_volume_codes(const uint2* __restrict__ vox,
+                                                      const uint2* __restrict__ col, int nx,
+                                                      int ny, int nz, int cnbx, int nblocks,
+                                                      int cwords, uint32_t* __restrict__ cmap) {
+    const int wd = blockIdx.x * blockDim.x + threadIdx.x;
+    if (wd >= cwords) return;
+    uint32_t word = 0;
+    for (int k = 0; k < 16; ++k) {
+        const int b = wd * 16 + k;
+        if (b >= nblocks) break;
+        const int by = b / cnbx, bx = b - by * cnbx;
+        uint32_t code = 1u;
+        for (int y = by << VPK_CSHIFT; y < min(ny, (by + 1) << VPK_CSHIFT); ++y)
+            for (int x = bx << VPK_CSHIFT; x < min(nx, (bx + 1) << VPK_CSHIFT); ++x) {
+                const int64_t c = (int64_t)y * nx + x;
+                const uint32_t psi = vox[c * nz].y;  // the column's psi (every layer's)
+                if ((psi & 0x7fffffffu) || (col[c].y & UAM_FLAG_NFZ)) code = 3u;
+            }
+        word |= code << (2 * k);
+    }
+    cmap[wd] = word;
+}
 
 // the altitude of waypoint j (uam_eval_generated3d: z0 + (zf - z0) (j / (N+1)))
 __device__ __forceinline__ double vz_at(double za, double zb, double jw) {
@@ -5814,8 +5851,7 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
         atomicAdd(&h[key], 1);
     }
     __syncthreads();
-    for (int k = t; k < kg.bins; k += 1024)
-        if (h[k]) kg.cnt[(int64_t)k * G_NBK + b] = atomicAdd(&kg.gcnt[k], h[k]);
+    for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
 // every (path, group) item in sorted order: points (x, y by the arc formula, z on the linear
@@ -5823,12 +5859,15 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 // the group's end reads the first voxel line and is masked off), the branch-free consume
 template <int CH>
 __global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg) {
-    extern __shared__ __attribute__((aligned(16))) double2 s_u[];  // unit-arc rows, then j / (W-1)
+    // unit-arc rows, then j / (W-1), then the code map
+    extern __shared__ __attribute__((aligned(16))) double2 s_u[];
     const int N = p.N, W = kg.W;
     const int nu = kg.D * N;
     double* s_jw = reinterpret_cast<double*>(s_u + nu);
+    uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_jw + W);
     for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
     for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
+    for (int i = threadIdx.x; i < vs.cwords; i += 256) s_cm[i] = vs.cmap[i];
     __syncthreads();
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     if (pos >= kg.n_items) return;
@@ -5859,7 +5898,7 @@ __global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg)
         uint4 r[CH];
         double zt[CH];
         int32_t izt[CH];
-        uint32_t inb = 0;
+        uint32_t inb = 0, full = 0, odd = 0;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int j = jc + t;
@@ -5879,19 +5918,30 @@ __global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg)
                 inb |= 1u << t;
                 const int32_t ix = (int32_t)tx, iy = (int32_t)ty, iz = (int32_t)tz;
                 izt[t] = iz;
-                ptr = vs.vp + vpk_index(vs.nbx4, vs.nby2, ix, iy, iz);
+                const int32_t b = (iy >> VPK_CSHIFT) * vs.cnbx + (ix >> VPK_CSHIFT);
+                if ((s_cm[b >> 4] >> ((b & 15) * 2)) & 2u) {  // no-fly support: 16-B voxel
+                    full |= 1u << t;
+                    ptr = vs.vp + vpk_index(vs.nbx4, vs.nby2, ix, iy, iz);
+                } else {  // the aligned pair of 8-B entries holding the voxel
+                    const int64_t a = vpk8_index(vs.nbx4, vs.nby4, ix, iy, iz);
+                    odd |= (uint32_t)(a & 1) << t;
+                    ptr = reinterpret_cast<const uint4*>(vs.vp8 + (a & ~(int64_t)1));
+                }
             }
             r[t] = *ptr;
         }
         const int nv = min(CH, j1 - jc);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const bool vl = t < nv, in = (inb >> t) & 1u;
+            const bool vl = t < nv, in = (inb >> t) & 1u, fl = (full >> t) & 1u,
+                       od = (odd >> t) & 1u;
             const uint4 rt = r[t];
-            const float ter = __uint_as_float(rt.z);
-            gc = gc + over_n(in ? (double)__uint_as_float(rt.x) : 0.0);
-            gn = gn + (in ? (double)__uint_as_float(rt.y) : 0.0);
-            nh += (in && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            // 8-B entries: psi is +-0 and no no-fly flag in the block (exact no-ops)
+            const uint32_t risk = fl ? rt.x : od ? rt.z : rt.x;
+            const float ter = __uint_as_float(fl ? rt.z : od ? rt.w : rt.y);
+            gc = gc + over_n(in ? (double)__uint_as_float(risk) : 0.0);
+            gn = gn + ((in && fl) ? (double)__uint_as_float(rt.y) : 0.0);
+            nh += (in && fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
             off += (vl && !in) ? 1u : 0u;
             bel += (in && (vs.z0 + ((double)izt[t] + 0.5) * vs.dz < (double)ter)) ? 1u : 0u;
             cm = in ? fmin(cm, zt[t] - (double)ter) : cm;
@@ -5919,8 +5969,6 @@ __global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
     const VSlot* slot = reinterpret_cast<const VSlot*>(kg.slot);
-    if (blockIdx.x == 0)  // the sort's bin totals back to zero for the next call
-        for (int k = t; k < kg.bins; k += blockDim.x) kg.gcnt[k] = 0;
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         const double* pr = kg.pairs + (q0 + qi) * 6;
@@ -6024,8 +6072,6 @@ struct uam_ctx {
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     bool k2g_attrs_cells = false;  // the same for the cell-writing K2g forms
-    int32_t* d_gcnt = nullptr;  // K2g / K2h sort: bin totals (zero between calls)
-    bool gcnt_dirty = false;    // re-zero them before the next sort
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     uint16_t* d_tkey = nullptr; // K2g: sort key of each tile (curve order), for tkey_bits/curve
@@ -6050,6 +6096,8 @@ struct uam_ctx {
                                 // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
                                 // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
+    int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
+                                // 0 = the fewest giving <= 16 bands)
     int k2g_lwin = 0;           // K2h LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW: 0, 96, 128)
     int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
@@ -6194,7 +6242,6 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventSynchronize(ctx->ev_ord);
     if (ctx->d_ord) (void)hipFree(ctx->d_ord);
     if (ctx->d_tkey) (void)hipFree(ctx->d_tkey);
-    if (ctx->d_gcnt) (void)hipFree(ctx->d_gcnt);
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -6757,6 +6804,12 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             (long long)value);
             ctx->k2g_chunk = (int)value;
             return UAM_OK;
+        case UAM_OPT_K4H_BAND:
+            if (value < 0 || value > 64 || (value & (value - 1)))
+                return fail(UAM_E_INVALID, "UAM_OPT_K4H_BAND %lld not 0 or a power of two <= 64",
+                            (long long)value);
+            ctx->k4h_band = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2G_LDS_WINDOW:
             if (value != 0 && value != 96 && value != 128)
                 return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_WINDOW %lld not 0, 96 or 128",
@@ -6797,6 +6850,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
         case UAM_OPT_K2G_LDS_WINDOW: *value = ctx->k2g_lwin; return UAM_OK;
+        case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
         default: return fail(UAM_E_INVALID, "unknown option %d", option);
@@ -7114,6 +7168,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int bins = tiles + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)bins * G_NBK;
+    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    if (nsb > 4096) return 0;
     // K2h (the similarity form) unless disabled or maxratio_smooth (its turn rows are not
     // scale-free): 24-B slots, the geometry in the output launch
     const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth;
@@ -7142,16 +7198,6 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
     if (st) return st;
     kg.tkey = ctx->d_tkey;
-    if (!ctx->d_gcnt) {  // the bin totals: zeroed here, left zero by every output launch
-        if (hipMalloc(&ctx->d_gcnt, sizeof(int32_t) * G_BINS_MAX) != hipSuccess)
-            return fail(UAM_E_NOMEM, "K2g bin totals");
-        ctx->gcnt_dirty = true;
-    }
-    if (ctx->gcnt_dirty) {  // first use, or a sequence that did not reach its output launch
-        HIP_TRY(hipMemsetAsync(ctx->d_gcnt, 0, sizeof(int32_t) * G_BINS_MAX, s));
-        ctx->gcnt_dirty = false;
-    }
-    kg.gcnt = ctx->d_gcnt;
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
@@ -7192,11 +7238,16 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = ktime_begin(ctx, s);
     if (st) return st;
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK + (sim ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
+                       kg.tot);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351)
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 8;
+    // K2h: 7 by default (groups of 21 = three full chunks; cfg3 0.316 vs 0.321 ms at 8, same
+    // box, profiles/r04/sweep3), K2g: 8
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : sim ? 7 : 8;
     const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : 4;
     const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                    (ctx->kp.length_smooth ? 2 : 0) +
@@ -7219,7 +7270,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         lds_run = lds_need + (size_t)ctx->k2g_lwin * ctx->k2g_lwin * 8;
         if (lds_run > 160 * 1024) return fail(UAM_E_INVALID, "LDS window too large");
         HIP_TRY(hipFuncSetAttribute((const void*)ev, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
+                                    (int)lds_run));
     }
     if (lds > 64 * 1024 && !ctx->k2g_attrs_cells && ko.cells) {
         for (EvalFn f : evals_cells)
@@ -7235,10 +7286,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                             : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
     hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
-    if (hipGetLastError() != hipSuccess) {
-        ctx->gcnt_dirty = true;
-        return fail(UAM_E_HIP, "grouped evaluation launch");
-    }
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
@@ -7259,22 +7307,29 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
     if ((size_t)D * ctx->kp.N * 16 > (size_t)G_UTAB_LDS) return 0;
-    const size_t lds = (size_t)D * ctx->kp.N * 16 + (size_t)W * 8;
+    if ((size_t)kv.cwords * 4 > (size_t)VPK_CMAP_LDS) return 0;
+    const size_t lds = (size_t)D * ctx->kp.N * 16 + (size_t)W * 8 + (size_t)kv.cwords * 4;
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
-    const int tbits = ctx->k2g_tbits ? std::min(ctx->k2g_tbits, 4) : 4;
+    // tiles: 8 x 8 by default (128^2 columns at 1024^2: cfg5 0.461 vs 0.491 ms at 16 x 16,
+    // profiles/r04/vol2), UAM_OPT_K2G_TILE_BITS otherwise
+    const int tbits = ctx->k2g_tbits ? ctx->k2g_tbits : 3;
     const int tiles = 1 << (2 * tbits);
-    if (tiles * kv.nbands * 2 + 1 > G_BINS_MAX) return 0;
+    if (tiles * kv.nbands * 2 + 1 > G_BINS_MAX)
+        return fail(UAM_E_INVALID, "K4h: %d tiles x %d altitude bands exceed the sort's bins",
+                    tiles, kv.nbands);
     const int last_bin = (W % G) ? tiles * kv.nbands : 0;
     const int bins = tiles * kv.nbands + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const int64_t ncnt = (int64_t)bins * G_NBK;
+    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    if (nsb > 4096) return 0;
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_ord = al((size_t)n_items * 4), b_slot = al((size_t)n_items * sizeof(VSlot)),
-                 b_ug = al((size_t)D * sizeof(UGeo));
+                 b_ug = al((size_t)D * sizeof(UGeo)), b_tot = al(4096 * 4);
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug + b_tot, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs6;
@@ -7294,16 +7349,6 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
     if (st) return st;
     kg.tkey = ctx->d_tkey;
-    if (!ctx->d_gcnt) {
-        if (hipMalloc(&ctx->d_gcnt, sizeof(int32_t) * G_BINS_MAX) != hipSuccess)
-            return fail(UAM_E_NOMEM, "K2g bin totals");
-        ctx->gcnt_dirty = true;
-    }
-    if (ctx->gcnt_dirty) {
-        HIP_TRY(hipMemsetAsync(ctx->d_gcnt, 0, sizeof(int32_t) * G_BINS_MAX, s));
-        ctx->gcnt_dirty = false;
-    }
-    kg.gcnt = ctx->d_gcnt;
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
@@ -7313,10 +7358,14 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.ugeo = (UGeo*)(w + o), o += b_ug;
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
+    kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.key = (uint16_t*)(w + o);
     st = ktime_begin(ctx, s);
     if (st) return st;
     hipLaunchKernelGGL(k_v_hist, dim3(G_NBK + 1), dim3(1024), 0, s, ctx->kp, kv, kg);
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
+                       kg.tot);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     using VEvalFn = void (*)(KParams, KVol4, KGrp);
@@ -7327,10 +7376,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kv, kg);
     hipLaunchKernelGGL(k_v_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
-    if (hipGetLastError() != hipSuccess) {
-        ctx->gcnt_dirty = true;
-        return fail(UAM_E_HIP, "grouped volume evaluation launch");
-    }
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped volume evaluation launch");
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
@@ -7725,10 +7771,21 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
 
 namespace {
 // the packed volume's dimensions (uam_volume_pack): 4 x 2-cell blocks, nz layer planes
-void vpk_dims(const uam_volume_desc* d, int32_t* nbx4, int32_t* nby2, int64_t* bytes) {
-    *nbx4 = (d->nx + 3) >> 2;
-    *nby2 = (d->ny + 1) >> 1;
-    *bytes = (int64_t)*nbx4 * *nby2 * 8 * d->nz * 16;
+// [16-B table | 8-B table | code map], 256-B aligned sections
+struct VpkDims {
+    int32_t nbx4, nby2, nby4, cnbx, cnby, cwords;
+    int64_t off8, offc, bytes;
+};
+void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
+    v->nbx4 = (d->nx + 3) >> 2;
+    v->nby2 = (d->ny + 1) >> 1;
+    v->nby4 = (d->ny + 3) >> 2;
+    v->cnbx = (d->nx + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
+    v->cnby = (d->ny + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
+    v->cwords = (v->cnbx * v->cnby + 15) / 16;
+    v->off8 = al256((int64_t)v->nbx4 * v->nby2 * 8 * d->nz * 16);
+    v->offc = v->off8 + al256((int64_t)v->nbx4 * v->nby4 * 16 * d->nz * 8);
+    v->bytes = v->offc + al256((int64_t)v->cwords * 4);
 }
 }  // namespace
 
@@ -7737,8 +7794,9 @@ int uam_volume_packed_bytes(const uam_volume_desc* vd, int64_t* bytes) {
     int st = make_kvolume(vd, &kv);
     if (st) return st;
     if (!bytes) return fail(UAM_E_INVALID, "bytes is NULL");
-    int32_t a, b;
-    vpk_dims(vd, &a, &b, bytes);
+    VpkDims v;
+    vpk_dims(vd, &v);
+    *bytes = v.bytes;
     return UAM_OK;
 }
 
@@ -7752,13 +7810,19 @@ int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, vo
     if (((uintptr_t)vol & 255) || ((uintptr_t)packed & 255))
         return fail(UAM_E_INVALID, "volume buffers not 256-B aligned");
     DeviceGuard dg(ctx->device);
-    int32_t nbx4, nby2;
-    int64_t bytes;
-    vpk_dims(vd, &nbx4, &nby2, &bytes);
-    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for(bytes / 16, 256)), dim3(256), 0,
-                       (hipStream_t)stream, (const uint2*)vol,
-                       (const uint2*)((const char*)vol + vol_col_offset(vd)), vd->nx, vd->ny,
-                       vd->nz, nbx4, nby2, (uint4*)packed);
+    VpkDims v;
+    vpk_dims(vd, &v);
+    const uint2* vx = (const uint2*)vol;
+    const uint2* cl = (const uint2*)((const char*)vol + vol_col_offset(vd));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for(v.off8 / 16, 256)), dim3(256), 0, s, vx, cl,
+                       vd->nx, vd->ny, vd->nz, v.nbx4, v.nby2, (uint4*)packed);
+    hipLaunchKernelGGL(k_volume_pack8, dim3(grid_for((v.offc - v.off8) / 8, 256)), dim3(256), 0,
+                       s, vx, cl, vd->nx, vd->ny, vd->nz, v.nbx4, v.nby4,
+                       (uint2*)((char*)packed + v.off8));
+    hipLaunchKernelGGL(k_volume_codes, dim3(grid_for(v.cwords, 256)), dim3(256), 0, s, vx, cl,
+                       vd->nx, vd->ny, vd->nz, v.cnbx, v.cnbx * v.cnby, v.cwords,
+                       (uint32_t*)((char*)packed + v.offc));
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
@@ -7780,12 +7844,19 @@ int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* vd, const void* 
         if ((uintptr_t)packed & 255) return fail(UAM_E_INVALID, "packed volume not 256-B aligned");
         KVol4 kv{};
         kv.nx = vd->nx, kv.ny = vd->ny, kv.nz = vd->nz;
-        int64_t bytes;
-        vpk_dims(vd, &kv.nbx4, &kv.nby2, &bytes);
+        VpkDims v;
+        vpk_dims(vd, &v);
+        kv.nbx4 = v.nbx4, kv.nby2 = v.nby2, kv.nby4 = v.nby4, kv.cnbx = v.cnbx;
+        kv.cwords = v.cwords;
+        kv.vp8 = (const uint2*)((const char*)packed + v.off8);
+        kv.cmap = (const uint32_t*)((const char*)packed + v.offc);
         kv.x0 = vd->x0, kv.y_top = vd->y_top, kv.z0 = vd->z0, kv.dz = vd->dz;
         kv.inv_dx = 1.0 / vd->dx, kv.inv_dy = 1.0 / vd->dy, kv.inv_dz = 1.0 / vd->dz;
         kv.vp = (const uint4*)packed;
-        int zs = 0;  // altitude bands: at most 16
+        int zs = 0;  // altitude bands: at most 16, or UAM_OPT_K4H_BAND layers each
+        if (ctx->k4h_band > 0) {
+            while ((1 << zs) < ctx->k4h_band) ++zs;
+        }
         while ((vd->nz - 1) >> zs >= 16) ++zs;
         kv.zshift = zs;
         kv.nbands = ((vd->nz - 1) >> zs) + 1;
