@@ -4761,7 +4761,7 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
 // off-raster counts are order-free.  Every (path, group) item is then independent, so ONE
 // counting sort on the Morton key of the raster tile under the item's middle waypoint and ONE
 // launch evaluate all of them in the XCD-placed sorted order: the items an XCD runs together
-// cover a few tiles, whose lines stay in its L2.  The partials go to a 16-B slot per item;
+// cover a few tiles, whose lines stay in its L2.  The partials go to a 48-B slot per item;
 // k_g_final combines them in group order with pass 1 and runs the main.py:175-180 selection.
 // Every per-path sum is grouped the same way -- each term attached to a waypoint (Phi/N, psi
 // of waypoint j; the length terms of segment p_{j-1} -> p_j; kinematic row k to k + 1) -- so
@@ -5416,6 +5416,15 @@ __global__ __launch_bounds__(BS, BS == 256 ? UAM_K2H_MINW : 1) void k_h_eval(KPa
     // WIN: the window (plane-A layout: 4 x 4-cell blocks of 8-B entries) after the cells slice
     uint2* s_win = reinterpret_cast<uint2*>(s_cells + (CELLS ? (BS / 64) * CH * 64 : 0));
     __shared__ int32_t s_org[2];
+    // the item's order entry and pair first: their two dependent round trips overlap the
+    // staging below instead of following it
+    const int64_t pos0 = xcd_chunk(blockIdx.x, gridDim.x) * BS;
+    const int64_t pos = pos0 + threadIdx.x;
+    const bool live = pos < kg.n_items;
+    const int32_t item = live ? kg.order[pos] : 0;
+    const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
     {  // staging as k_g_eval: every load of a thread issued before its first LDS store
         constexpr int U = 4;
         const int nv = rs.pwords >> 2, nu = kg.D * p.N;
@@ -5438,7 +5447,6 @@ __global__ __launch_bounds__(BS, BS == 256 ? UAM_K2H_MINW : 1) void k_h_eval(KPa
         }
         for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += BS) s_map[i] = rs.pmap[i];
     }
-    const int64_t pos0 = xcd_chunk(blockIdx.x, gridDim.x) * BS;
     if (WIN > 0) {
         if (threadIdx.x == 0) {  // the window around the middle item's middle waypoint
             const int64_t pm = min(pos0 + BS / 2, kg.n_items - 1);
@@ -5476,13 +5484,8 @@ __global__ __launch_bounds__(BS, BS == 256 ? UAM_K2H_MINW : 1) void k_h_eval(KPa
     __syncthreads();
     // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
     // last item evaluates nothing and writes nothing
-    const int64_t pos = pos0 + threadIdx.x;
-    const bool live = pos < kg.n_items;
-    const int32_t item = live ? kg.order[pos] : 0;
-    const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int s = item - path * kg.nseg;
-    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
-    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const int32_t d = path - q * kg.D;
     const int N = p.N, W = kg.W;
     const double2* urow = s_u + d * N;
     const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
@@ -5820,35 +5823,52 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
     const int N = p.N, W = kg.W;
     const int tiles = 1 << (2 * kg.tbits);
-    for (int64_t i = lo + t; i < hi; i += 1024) {
-        const int32_t path = (int32_t)div_magic((uint32_t)i, kg.m_nseg, kg.sh_nseg);
-        const int sg = (int)(i - (int64_t)path * kg.nseg);
-        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-        const int32_t d = path - q * kg.D;
-        const int j0 = sg * kg.G, j1 = min(j0 + kg.G, W);
-        const int jm = (j0 + j1 - 1) >> 1;
-        const double* pr = kg.pairs + (int64_t)q * 6;
-        double x0, x1;
-        if (jm == 0) {
-            x0 = pr[0], x1 = pr[1];
-        } else if (jm == W - 1) {
-            x0 = pr[3], x1 = pr[4];
-        } else {
-            const double2 u = reinterpret_cast<const double2*>(kg.utab)[d * N + jm - 1];
-            arc_point(pr[0], pr[1], pr[3], pr[4], u.x, u.y, x0, x1);
+    // U items per thread with all their loads issued first (k_g_hist's batching)
+    constexpr int U = 4;
+    for (int64_t i0 = lo + t; i0 < hi; i0 += 1024 * U) {
+        double pr[U][6];
+        double2 u[U];
+        int jm[U], sg[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = (int32_t)min(i0 + k * 1024, hi - 1);
+            const int32_t path = (int32_t)div_magic((uint32_t)i, kg.m_nseg, kg.sh_nseg);
+            sg[k] = (int)(i - (int64_t)path * kg.nseg);
+            const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+            const int32_t d = path - q * kg.D;
+            const int j0 = sg[k] * kg.G, j1 = min(j0 + kg.G, W);
+            jm[k] = (j0 + j1 - 1) >> 1;
+            const double2* pp = reinterpret_cast<const double2*>(kg.pairs + (int64_t)q * 6);
+            const double2 a = pp[0], b2 = pp[1], c = pp[2];
+            pr[k][0] = a.x, pr[k][1] = a.y, pr[k][2] = b2.x, pr[k][3] = b2.y, pr[k][4] = c.x,
+            pr[k][5] = c.y;
+            u[k] = reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(jm[k] - 1, 0), N - 1)];
         }
-        const double z = vz_at(pr[2], pr[5], (double)jm / (double)(W - 1));
-        const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
-        const double tz = (z - vs.z0) * vs.inv_dz;
-        uint32_t key = kg.bins - 1;
-        if ((tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) && (ty < (double)vs.ny) &&
-            (tz >= 0.0) && (tz < (double)vs.nz)) {
-            const uint32_t cx = (uint32_t)tx >> kg.tshift, cy = (uint32_t)ty >> kg.tshift;
-            key = ((uint32_t)tz >> vs.zshift) * tiles + tk[(cy << kg.tbits) | cx];
-            if (sg == kg.nseg - 1) key += kg.last_bin;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t i = i0 + k * 1024;
+            if (i >= hi) break;
+            double x0, x1;
+            if (jm[k] == 0) {
+                x0 = pr[k][0], x1 = pr[k][1];
+            } else if (jm[k] == W - 1) {
+                x0 = pr[k][3], x1 = pr[k][4];
+            } else {
+                arc_point(pr[k][0], pr[k][1], pr[k][3], pr[k][4], u[k].x, u[k].y, x0, x1);
+            }
+            const double z = vz_at(pr[k][2], pr[k][5], (double)jm[k] / (double)(W - 1));
+            const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
+            const double tz = (z - vs.z0) * vs.inv_dz;
+            uint32_t key = kg.bins - 1;
+            if ((tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) && (ty < (double)vs.ny) &&
+                (tz >= 0.0) && (tz < (double)vs.nz)) {
+                const uint32_t cx = (uint32_t)tx >> kg.tshift, cy = (uint32_t)ty >> kg.tshift;
+                key = ((uint32_t)tz >> vs.zshift) * tiles + tk[(cy << kg.tbits) | cx];
+                if (sg[k] == kg.nseg - 1) key += kg.last_bin;
+            }
+            kg.key[i] = (uint16_t)key;
+            atomicAdd(&h[key], 1);
         }
-        kg.key[i] = (uint16_t)key;
-        atomicAdd(&h[key], 1);
     }
     __syncthreads();
     for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
@@ -5865,13 +5885,10 @@ __global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg)
     const int nu = kg.D * N;
     double* s_jw = reinterpret_cast<double*>(s_u + nu);
     uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_jw + W);
-    for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
-    for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
-    for (int i = threadIdx.x; i < vs.cwords; i += 256) s_cm[i] = vs.cmap[i];
-    __syncthreads();
+    // the item's order entry and pair before the staging (their round trips overlap it)
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-    if (pos >= kg.n_items) return;
-    const int32_t item = kg.order[pos];
+    const bool live = pos < kg.n_items;
+    const int32_t item = live ? kg.order[pos] : 0;
     const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int s = item - path * kg.nseg;
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
@@ -5879,6 +5896,11 @@ __global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg)
     const double2 pa = *reinterpret_cast<const double2*>(prp);
     const double2 pb = *reinterpret_cast<const double2*>(prp + 2);
     const double2 pc = *reinterpret_cast<const double2*>(prp + 4);
+    for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
+    for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
+    for (int i = threadIdx.x; i < vs.cwords; i += 256) s_cm[i] = vs.cmap[i];
+    __syncthreads();
+    if (!live) return;
     const double ax = pa.x, ay = pa.y, za = pb.x, bx = pb.y, by = pc.x, zb = pc.y;
     const double2* urow = s_u + d * N;
     const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
