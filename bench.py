@@ -301,13 +301,13 @@ def main():
     skip = raster_mode and not args.no_skip and raster.summary is not None
     if last.startswith("K4h"):
         ktag = last.lower()
-        kernel_name = ("K4h sequence (k_v_hist (+ the unit-arc sums) / k_g_scatter, k_v_eval "
+        kernel_name = ("K4h sequence (k_v_hist / k_scan / k_g_scatter (+ the unit-arc sums), k_v_eval "
                        "over every (path, group) item: points, one 16-B packed voxel per "
                        "waypoint; k_v_final: the similarity-form geometry, grouped sums, "
                        "selection)")
     elif last.startswith("K2h"):
         ktag = last.lower()
-        kernel_name = ("K2h sequence (k_g_hist (+ the unit-arc sums) / k_scan / k_g_scatter, "
+        kernel_name = ("K2h sequence (k_g_hist / k_scan / k_g_scatter (+ the unit-arc sums), "
                        "k_h_eval over every (path, group) item: points, cells, records; "
                        "k_h_final: the similarity-form geometry, grouped sums, selection)")
     elif last.startswith("K2g"):

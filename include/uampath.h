@@ -453,10 +453,14 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4)
  *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6; 0
  *                                (default) = tiles of ~256 x 256 cells
- *   UAM_OPT_K2G_LDS_FLOOR        K2g evaluation: dynamic-LDS floor per workgroup in bytes, which
- *                                caps the workgroups resident per CU (default 0)
- *   UAM_OPT_K2G_CHUNK            K2g / K2h evaluation: gathers in flight per lane, 6/7/8/11/16
- *                                (K2g: 7 runs as 6, 16 at two waves per SIMD); 0 (default) = 8
+ *   UAM_OPT_K2G_LDS_FLOOR        K2g / K2h / K4h evaluation: dynamic-LDS floor per workgroup in
+ *                                bytes, which caps the workgroups resident per CU; 0 (default):
+ *                                none for K2g and K2h, 54 000 (3 per CU) for K2h over rasters of
+ *                                more than 2^25 cells, 60 000 (2 per CU) for K4h
+ *   UAM_OPT_K2G_CHUNK            K2g / K2h / K4h evaluation: gathers in flight per lane,
+ *                                6/7/8/11/16 (K2g: 7 runs as 6, 16 at two waves per SIMD; K4h:
+ *                                6/7/8/11); 0 (default) = 8 for K2g, 7 for K2h, 11 for K2h over
+ *                                rasters of more than 2^25 cells and for K4h
  *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order
  *   UAM_OPT_K2G_SIM              1 (default): generated raster batches take K2h, K2g's sort and
  *                                grouped raster sums with the geometry terms (L, length,
@@ -470,7 +474,7 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                code-1 waypoints inside it from there.  Same outputs.
  *   UAM_OPT_K4H_BAND             K4h sort key: altitude layers per band, a power of two
  *                                (default 0: the fewest giving at most 16 bands); tiles from
- *                                UAM_OPT_K2G_TILE_BITS (default 4: 16 x 16 tiles), at most
+ *                                UAM_OPT_K2G_TILE_BITS (default 3: 8 x 8 tiles), at most
  *                                4096 (tile, band) bins */
 enum {
     UAM_OPT_GROUP = 1,

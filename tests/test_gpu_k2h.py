@@ -155,6 +155,25 @@ def test_k2h_chunks_and_turn_rows(oracle_mod, chunk, group, maxalpha):
     _check(gpu, ref, oracle_mod, D)
 
 
+@pytest.mark.parametrize("chunk,floor", [(11, 54000), (7, 90000)])
+def test_k2h_lds_floor(oracle_mod, chunk, floor):
+    """Fewer workgroups per CU (the setting K2h takes by default on rasters over 2^25 cells:
+    54 000 B, 11 in flight) changes no bit."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 80, maxalpha=0.015)
+    e.set_option("k2g_chunk", chunk)
+    e.set_option("k2g_lds_floor", floor)
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs(2000, 13)
+    ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=21)
+    gpu = e.eval_generated(pairs, ut, raster=raster)
+    assert e.last_kernel() == "K2h+pack"
+    _check(gpu, ref, oracle_mod, D)
+
+
 def test_k2h_partial_raster(oracle_mod):
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.engine import RasterGeo

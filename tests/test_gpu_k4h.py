@@ -99,13 +99,17 @@ def test_k4h_vs_oracle(oracle_mod, R, nz, group):
     np.testing.assert_allclose(ref["cost"][ok], seq["cost"][ok], rtol=1e-12)
 
 
-@pytest.mark.parametrize("chunk", [6, 7, 11])
-def test_k4h_chunks(oracle_mod, chunk):
+@pytest.mark.parametrize("chunk,floor", [(6, 0), (7, 0), (8, 0), (11, 0), (0, 0), (6, 28000),
+                                         (11, 41000), (8, 90000)])
+def test_k4h_chunks(oracle_mod, chunk, floor):
+    """Gathers in flight (chunk; 0 = the default 11) and workgroups per CU (the LDS floor; 0 =
+    the default 60 000 B, 90 000 needs the raised dynamic-LDS attribute) only move work."""
     from uam_path_planning_amd.arcs import arc_table
     from uam_path_planning_amd.scenario import displacements
 
     e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21, maxalpha=0.015)
     e.set_option("k2g_chunk", chunk)
+    e.set_option("k2g_lds_floor", floor)
     D = 5
     ut = arc_table(80, displacements(D))
     pairs = _pairs3d(2000, 23)

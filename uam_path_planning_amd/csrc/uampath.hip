@@ -4845,32 +4845,100 @@ struct KGrp {
     UGeo* __restrict__ ugeo;       // K2h: [D] unit sums, formed by k_g_hist's extra block
 };
 
-// K2h / K4h: the D rows' unit sums by one block: the table staged in LDS by every thread with
-// one round trip of loads (the sums then read LDS: a row's 81 steps would otherwise each wait
-// for a global load), then one thread per row
-// (su: the calling kernel's histogram LDS, cap entries; a larger table is read from global)
+// K2h / K4h: the D rows' unit sums by one block (the extra block of the scatter launch).
+// The terms are independent, the sums are not: every (row, chord) term first, one thread each
+// (unit_geo_row's operations), into LDS; then one thread per (row, sum) adds its terms in
+// unit_geo_row's order, so the bits are unit_geo_row's.  (One thread per row walking its 81
+// chords took ~30 us, the term-parallel form ~5 us: hidden beside the scatter's 10.)
+// su: the calling kernel's histogram LDS, cap bytes; a table or term set that does not fit is
+// done by unit_geo_row per row.
 __device__ __forceinline__ void unit_geo_block(const KParams& p, const KGrp& kg, double2* su,
                                                int cap) {
-    const int n = kg.D * p.N;
+    const int N = p.N, D = kg.D, nk = N + 1;  // chords k = 1..N+1 (index k - 1)
+    const int nu = D * N;
+    const size_t need = (size_t)nu * 16 + (size_t)D * nk * 5 * 8;
     const double2* u = reinterpret_cast<const double2*>(kg.utab);
-    if (n <= cap) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) su[i] = u[i];
-        __syncthreads();
-        u = su;
+    if (need > (size_t)cap) {
+        if ((int)threadIdx.x < D) unit_geo_row(p, u + threadIdx.x * N, kg.ugeo + threadIdx.x);
+        return;
     }
-    if ((int)threadIdx.x < kg.D) unit_geo_row(p, u + threadIdx.x * p.N, kg.ugeo + threadIdx.x);
-}
-
-__device__ __forceinline__ PathSrc<true> grp_src(const KGrp& kg, int N, int32_t path) {
-    const int32_t q = path / kg.D, d = path - q * kg.D;
-    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-    PathSrc<true> src;
-    src.W = N + 2;
-    src.wp = nullptr;
-    src.x0 = pr.x, src.y0 = pr.y, src.xf = pr.z, src.yf = pr.w;
-    src.za = src.zb = 0.0;
-    src.u = kg.utab + (int64_t)d * N * 2;
-    return src;
+    for (int i = threadIdx.x; i < nu; i += blockDim.x) su[i] = u[i];
+    __syncthreads();
+    double* tb = reinterpret_cast<double*>(su + nu);  // [D][nk] b_k
+    double* tb2 = tb + D * nk;                        // b_k^2
+    double* tc1 = tb2 + D * nk;                       // row terms at their later chord
+    double* tc2 = tc1 + D * nk;
+    double* tc3 = tc2 + D * nk;
+    const double mincos = p.mincos, r = p.r_eff;
+    for (int i = threadIdx.x; i < D * nk; i += blockDim.x) {
+        const int d = i / nk, k = i - d * nk + 1;
+        const double2* ur = su + d * N;
+        auto pt = [&](int m, double& x, double& y) {  // u_0 = (1, 0), u_{N+1} = (-1, 0)
+            if (m == 0) {
+                x = 1.0, y = 0.0;
+            } else if (m == N + 1) {
+                x = -1.0, y = 0.0;
+            } else {
+                x = ur[m - 1].x, y = ur[m - 1].y;
+            }
+        };
+        double qx, qy, cx, cy;
+        pt(k - 1, qx, qy);
+        pt(k, cx, cy);
+        const double dx = cx - qx, dy = cy - qy;
+        const double b = sqrt(dx * dx + dy * dy);
+        tb[i] = b;
+        tb2[i] = b * b;
+        double c1 = 0.0, c2 = 0.0, c3 = 0.0;
+        if (k >= 2) {
+            double px, py;
+            pt(k - 2, px, py);
+            const double pdx = qx - px, pdy = qy - py;
+            const double pb = sqrt(pdx * pdx + pdy * pdy);
+            c1 = fmax(0.0, b - r * pb);
+            c2 = fmax(0.0, pb / r - b);
+            const double dt = pdx * dx + pdy * dy;
+            c3 = fmax(0.0, mincos - dt / (pb * b));
+        }
+        tc1[i] = c1, tc2[i] = c2, tc3[i] = c3;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < D * 5) {
+        const int d = threadIdx.x / 5, w = threadIdx.x - d * 5;
+        const double* b = tb + d * nk;
+        const double* b2 = tb2 + d * nk;
+        UGeo* g = kg.ugeo + d;
+        double acc = 0.0, acc2 = 0.0;
+        if (w == 0) {  // s1n, then s1a continues the same chain over k = N+1
+#pragma unroll 8
+            for (int k = 0; k < N; ++k) acc = acc + b[k];
+            g->s1n = acc;
+        } else if (w == 1) {
+#pragma unroll 8
+            for (int k = 0; k < N; ++k) acc = acc + b2[k];
+            g->s2n = acc;
+        } else if (w == 2) {
+#pragma unroll 8
+            for (int k = 0; k < nk; ++k) acc = acc + b[k];
+            g->s1a = acc;
+        } else if (w == 3) {
+#pragma unroll 8
+            for (int k = 0; k < nk; ++k) acc = acc + b2[k];
+            g->s2a = acc;
+        } else {  // the ratio rows, then the turn rows
+            const double* c1 = tc1 + d * nk;
+            const double* c2 = tc2 + d * nk;
+            const double* c3 = tc3 + d * nk;
+#pragma unroll 8
+            for (int k = 1; k < nk; ++k) {
+                acc = acc + c1[k];
+                acc = acc + c2[k];
+                acc2 = acc2 + c3[k];
+            }
+            g->e12 = acc;
+            g->e3 = acc2;
+        }
+    }
 }
 
 // a / D for a < 2^31 by one 64-bit multiply (Granlund-Montgomery): sh = 32 + ceil(log2 D),
@@ -4889,11 +4957,6 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
     const int t = threadIdx.x, b = blockIdx.x;
-    if (b == G_NBK) {  // the unit rows through LDS (the histogram's; one round trip)
-        if (kg.ugeo)
-            unit_geo_block(p, kg, reinterpret_cast<double2*>(h), (int)(sizeof(h) / 16));
-        return;
-    }
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
@@ -4961,9 +5024,13 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
 // atomics on the bin totals in the histogram launch, their scan in this one -- ran the
 // histogram 11 -> 34 us at cfg3: 256 partitions' atomics on each bin address serialise
 // across the XCDs; profiles/r04/prof1.)
-__global__ __launch_bounds__(1024) void k_g_scatter(KGrp kg) {
-    __shared__ int32_t cur[G_BINS_MAX];
+__global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
+    __shared__ __attribute__((aligned(16))) int32_t cur[G_BINS_MAX];
     const int t = threadIdx.x, b = blockIdx.x;
+    if (b == G_NBK) {  // K2h / K4h: the unit rows, through this block's LDS (hidden under the
+        unit_geo_block(p, kg, reinterpret_cast<double2*>(cur), (int)sizeof(cur));  // scatter)
+        return;
+    }
     for (int k = t; k < kg.bins; k += 1024) {
         const int64_t c = (int64_t)k * G_NBK + b;
         cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
@@ -5811,11 +5878,6 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];
     const int t = threadIdx.x, b = blockIdx.x;
-    if (b == G_NBK) {  // the unit rows through LDS (the histogram's; one round trip)
-        if (kg.ugeo)
-            unit_geo_block(p, kg, reinterpret_cast<double2*>(h), (int)(sizeof(h) / 16));
-        return;
-    }
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
@@ -5878,7 +5940,7 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 // climb), ONE 16-B load per waypoint from the packed volume (a slot outside the volume or past
 // the group's end reads the first voxel line and is masked off), the branch-free consume
 template <int CH>
-__global__ __launch_bounds__(256, 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg) {
+__global__ __launch_bounds__(256, CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg) {
     // unit-arc rows, then j / (W-1), then the code map
     extern __shared__ __attribute__((aligned(16))) double2 s_u[];
     const int N = p.N, W = kg.W;
@@ -6095,6 +6157,7 @@ struct uam_ctx {
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     bool k2g_attrs_cells = false;  // the same for the cell-writing K2g forms
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
+    bool k4h_attrs = false;     // the same for K4h
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
     uint16_t* d_tkey = nullptr; // K2g: sort key of each tile (curve order), for tkey_bits/curve
     int tkey_bits = -1, tkey_curve = -1;
@@ -6114,9 +6177,10 @@ struct uam_ctx {
                                 // 0 = tiles of ~256^2 cells: cfg3 (4096^2) Hilbert 4 0.329,
                                 // 5 0.343, 6 0.381 ms (k2g13); cfg4 (8192^2) 4 1.062, 5 0.996,
                                 // 6 1.043 ms (cfg4_tbits))
-    int k2g_lds = 0;            // K2g evaluation: dynamic-LDS floor per workgroup, which caps
-                                // the workgroups resident per CU (UAM_OPT_K2G_LDS_FLOOR; cfg3:
-                                // 45 / 54 / 80 KiB 0.43 / 0.54 / 0.52 ms against 0.39, k2g7)
+    int k2g_lds = 0;            // K2g / K2h / K4h evaluation: dynamic-LDS floor per workgroup,
+                                // which caps the workgroups resident per CU
+                                // (UAM_OPT_K2G_LDS_FLOOR; K2g cfg3: 45 / 54 / 80 KiB 0.43 / 0.54
+                                // / 0.52 ms against 0.39, k2g7; 0 = the launchers' defaults)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
     int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
                                 // 0 = the fewest giving <= 16 bands)
@@ -7233,7 +7297,12 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.key = (uint16_t*)(w + o);
     const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +  // + junk slot
                             (sim && ko.cells ? (size_t)4 * 8 * 64 * 4 : 0);    // K2h cells
-    const size_t lds = std::max(lds_need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+    // a raster far beyond the L2s (over 2^25 cells: cfg4's 8192^2, 1 GiB packed) misses more:
+    // K2h runs 3 workgroups per CU with 11 gathers in flight per lane there (cfg4 0.886 vs
+    // 0.936 ms at 5 workgroups and 7; cfg3 the same either way; profiles/r04/sweep7)
+    const bool big = sim && !ko.cells && (int64_t)kr.nx * kr.ny > ((int64_t)1 << 25);
+    const int floor_lds = ctx->k2g_lds ? ctx->k2g_lds : big ? 54000 : 0;
+    const size_t lds = std::max(lds_need, (size_t)std::min(floor_lds, 160 * 1024));
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
                         k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
@@ -7259,17 +7328,17 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     }
     st = ktime_begin(ctx, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK + (sim ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
-    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351)
     // K2h: 7 by default (groups of 21 = three full chunks; cfg3 0.316 vs 0.321 ms at 8, same
     // box, profiles/r04/sweep3), K2g: 8
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : sim ? 7 : 8;
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : big ? 11 : sim ? 7 : 8;
     const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : 4;
     const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                    (ctx->kp.length_smooth ? 2 : 0) +
@@ -7330,7 +7399,12 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
     if ((size_t)D * ctx->kp.N * 16 > (size_t)G_UTAB_LDS) return 0;
     if ((size_t)kv.cwords * 4 > (size_t)VPK_CMAP_LDS) return 0;
-    const size_t lds = (size_t)D * ctx->kp.N * 16 + (size_t)W * 8 + (size_t)kv.cwords * 4;
+    // workgroups per CU: 2 by default through an LDS floor of 60 000 B (UAM_OPT_K2G_LDS_FLOOR
+    // sets another): fewer items resident per XCD, so fewer of their lines miss L2 -- cfg5
+    // 0.415 ms at 2 with 11 gathers in flight, 0.418 at 3, 0.453 at the 6 the LDS allows with 6
+    // (profiles/r04/sweep7)
+    const size_t lds = std::max((size_t)D * ctx->kp.N * 16 + (size_t)W * 8 + (size_t)kv.cwords * 4,
+                                (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 60000, 160 * 1024));
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
@@ -7384,17 +7458,24 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.key = (uint16_t*)(w + o);
     st = ktime_begin(ctx, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_v_hist, dim3(G_NBK + 1), dim3(1024), 0, s, ctx->kp, kv, kg);
+    hipLaunchKernelGGL(k_v_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kv, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
-    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK), dim3(1024), 0, s, kg);
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     using VEvalFn = void (*)(KParams, KVol4, KGrp);
-    // gathers in flight per lane: 6 by default (k_v_eval<8> spills at 4 waves per SIMD)
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 6;
-    const VEvalFn ev = chl <= 6 ? k_v_eval<6> : chl == 7 ? k_v_eval<7> : chl <= 8 ? k_v_eval<8>
-                                                                        : k_v_eval<11>;
+    // gathers in flight per lane: 11 by default (k_v_eval<8> spills at 4 waves per SIMD, so 8 and
+    // 11 are built for 3)
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 11;
+    static const VEvalFn vevals[4] = {k_v_eval<6>, k_v_eval<7>, k_v_eval<8>, k_v_eval<11>};
+    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : 3];
+    if (lds > 64 * 1024 && !ctx->k4h_attrs) {
+        for (VEvalFn f : vevals)
+            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+        ctx->k4h_attrs = true;
+    }
     hipLaunchKernelGGL(ev, ge, dim3(256), lds, s, ctx->kp, kv, kg);
     hipLaunchKernelGGL(k_v_final, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
