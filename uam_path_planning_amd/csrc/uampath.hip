@@ -4838,11 +4838,14 @@ struct KGrp {
     uint16_t* __restrict__ key;    // [n_items]
     int32_t* __restrict__ cnt;     // [bins][G_NBK] counts -> offsets
     int32_t* __restrict__ tot;     // scan block totals
+    int32_t nsb_raw;               // > 0: tot holds nsb_raw (<= 1024) unscanned block totals,
+                                   // which k_g_scatter scans itself (no k_scan_totals launch)
     int32_t* __restrict__ order;   // [n_items] item of each sorted position
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
-    UGeo* __restrict__ ugeo;       // K2h: [D] unit sums, formed by k_g_hist's extra block
+    UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's extra
+                                   // block
 };
 
 // K2h / K4h: the D rows' unit sums by one block (the extra block of the scatter launch).
@@ -5026,14 +5029,37 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
 // across the XCDs; profiles/r04/prof1.)
 __global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t cur[G_BINS_MAX];
-    const int t = threadIdx.x, b = blockIdx.x;
-    if (b == G_NBK) {  // K2h / K4h: the unit rows, through this block's LDS (hidden under the
-        unit_geo_block(p, kg, reinterpret_cast<double2*>(cur), (int)sizeof(cur));  // scatter)
+    __shared__ int32_t stot[1024];
+    __shared__ int32_t wsum[16];
+    const int t = threadIdx.x;
+    // K2h / K4h: block 0 forms the unit rows through its LDS (dispatched first, so hidden under
+    // the scatter); the partitions are the other blocks
+    if (kg.ugeo && blockIdx.x == 0) {
+        unit_geo_block(p, kg, reinterpret_cast<double2*>(cur), (int)sizeof(cur));
         return;
+    }
+    const int b = blockIdx.x - (kg.ugeo ? 1 : 0);
+    const int nsb = kg.nsb_raw;
+    if (nsb > 0) {  // the scan's block totals, scanned here (replaces k_scan_totals' launch)
+        const int32_t v = t < nsb ? kg.tot[t] : 0;
+        const int lane = t & 63, wv = t >> 6;
+        int32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        int32_t woff = 0;
+        for (int k = 0; k < wv; ++k) woff += wsum[k];
+        stot[t] = woff + x - v;
+        __syncthreads();
     }
     for (int k = t; k < kg.bins; k += 1024) {
         const int64_t c = (int64_t)k * G_NBK + b;
-        cur[k] = kg.cnt[c] + kg.tot[c / (256 * SCAN_ITEMS)];
+        const int sb = (int)(c / (256 * SCAN_ITEMS));
+        cur[k] = kg.cnt[c] + (nsb > 0 ? stot[sb] : kg.tot[sb]);
     }
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
@@ -7331,7 +7357,9 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
+    kg.nsb_raw = nsb <= 1024 ? (int32_t)nsb : 0;  // up to 1024 totals: scanned by the scatter
+    if (!kg.nsb_raw)
+        hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
@@ -7461,7 +7489,9 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     hipLaunchKernelGGL(k_v_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kv, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
+    kg.nsb_raw = nsb <= 1024 ? (int32_t)nsb : 0;  // up to 1024 totals: scanned by the scatter
+    if (!kg.nsb_raw)
+        hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     using VEvalFn = void (*)(KParams, KVol4, KGrp);
