@@ -322,7 +322,7 @@ def main():
         ktag = "wave" if wave else ("raster+skip" if skip else mode)
         kernel_name = (f"k_eval_wave<{mode}> (one wave per path)" if wave else
                        f"k_eval_pairs<{ktag}>")
-    pkey = f"{args.workload}:{mode}:R{R}:Q{Q}:{ktag}"
+    pkey = f"{args.workload}:{mode}:R{R}:Q{Q}:{ktag}" + (":cells" if args.cells else "")
     prof = {}
     if os.path.exists(args.traffic_json):
         try:
