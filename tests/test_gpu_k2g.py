@@ -205,7 +205,7 @@ def test_k2g_options(oracle_mod):
     e.set_option("group", 12)
     assert e.get_option("group") == 12
     assert e.get_option("k2g_chunk") == 0
-    for bad in (-1, 5, 9, 10, 12, 17):
+    for bad in (-1, 5, 9, 10, 12, 17, 20, 22):
         with pytest.raises(ValueError):
             e.set_option("k2g_chunk", bad)
     e.set_option("k2g_chunk", 7)

@@ -134,7 +134,8 @@ def test_k2h_displacements_and_short_paths(oracle_mod, D, N):
 
 @pytest.mark.parametrize("maxalpha", [0.015, 0.3])
 @pytest.mark.parametrize("chunk,group", [(6, 24), (7, 21), (8, 21), (8, 26), (11, 21), (11, 5),
-                                         (16, 21), (16, 40), (0, 64)])
+                                         (16, 21), (16, 40), (21, 21), (21, 30), (21, 9),
+                                         (0, 64)])
 def test_k2h_chunks_and_turn_rows(oracle_mod, chunk, group, maxalpha):
     """The chunk length (gathers in flight) only changes how a group's waypoints are cut into
     load batches.  maxalpha 0.015 rad lies between the arcs' per-step turns (some turn rows
@@ -155,7 +156,7 @@ def test_k2h_chunks_and_turn_rows(oracle_mod, chunk, group, maxalpha):
     _check(gpu, ref, oracle_mod, D)
 
 
-@pytest.mark.parametrize("chunk,floor", [(11, 54000), (7, 90000)])
+@pytest.mark.parametrize("chunk,floor", [(11, 54000), (7, 90000), (21, 90000), (16, 60000)])
 def test_k2h_lds_floor(oracle_mod, chunk, floor):
     """Fewer workgroups per CU (the setting K2h takes by default on rasters over 2^25 cells:
     54 000 B, 11 in flight) changes no bit."""

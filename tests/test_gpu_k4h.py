@@ -100,7 +100,7 @@ def test_k4h_vs_oracle(oracle_mod, R, nz, group):
 
 
 @pytest.mark.parametrize("chunk,floor", [(6, 0), (7, 0), (8, 0), (11, 0), (0, 0), (6, 28000),
-                                         (11, 41000), (8, 90000)])
+                                         (11, 41000), (8, 90000), (16, 0), (21, 90000)])
 def test_k4h_chunks(oracle_mod, chunk, floor):
     """Gathers in flight (chunk; 0 = the default 11) and workgroups per CU (the LDS floor; 0 =
     the default 60 000 B, 90 000 needs the raised dynamic-LDS attribute) only move work."""

@@ -5496,7 +5496,8 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // workgroup's middle item (its middle waypoint's cell): a code-1 waypoint inside it reads LDS,
 // its global load is the dummy line.  The window's staging reads each of its lines once.
 template <int CH, bool CELLS, int BS = 256, int WIN = 0>
-__global__ __launch_bounds__(BS, BS == 256 ? UAM_K2H_MINW : 1) void k_h_eval(KParams p, KRaster rs,
+__global__ __launch_bounds__(BS, BS == 256 ? (CH >= 16 ? 2 : UAM_K2H_MINW) : 1) void k_h_eval(
+                                                                  KParams p, KRaster rs,
                                                                   KGrp kg,
                                                                   const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -5966,7 +5967,8 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 // climb), ONE 16-B load per waypoint from the packed volume (a slot outside the volume or past
 // the group's end reads the first voxel line and is masked off), the branch-free consume
 template <int CH>
-__global__ __launch_bounds__(256, CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs, KGrp kg) {
+__global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
+                                                                              KGrp kg) {
     // unit-arc rows, then j / (W-1), then the code map
     extern __shared__ __attribute__((aligned(16))) double2 s_u[];
     const int N = p.N, W = kg.W;
@@ -6213,8 +6215,8 @@ struct uam_ctx {
     int k2g_lwin = 0;           // K2h LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW: 0, 96, 128)
     int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
-    int k2g_chunk = 0;          // K2g gathers in flight per lane (UAM_OPT_K2G_CHUNK: 6, 8, 11;
-                                // 0 = 8)
+    int k2g_chunk = 0;          // K2g / K2h / K4h gathers in flight per lane (UAM_OPT_K2G_CHUNK:
+                                // 6, 7, 8, 11, 16, 21; 0 = the launchers' defaults)
 
 };
 
@@ -6911,8 +6913,9 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
             ctx->k2g_curve = (int)value;
             return UAM_OK;
         case UAM_OPT_K2G_CHUNK:
-            if (value != 0 && value != 6 && value != 7 && value != 8 && value != 11 && value != 16)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 7, 8, 11 or 16",
+            if (value != 0 && value != 6 && value != 7 && value != 8 && value != 11 &&
+                value != 16 && value != 21)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_CHUNK %lld not 0, 6, 7, 8, 11, 16 or 21",
                             (long long)value);
             ctx->k2g_chunk = (int)value;
             return UAM_OK;
@@ -7338,8 +7341,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8), UAM_G_EVALS(11),
                                      UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
-    static const EvalFn hevals[5] = {k_h_eval<6, false>, k_h_eval<7, false>, k_h_eval<8, false>,
-                                     k_h_eval<11, false>, k_h_eval<16, false>};
+    // (16 and 21: built for 2 waves per SIMD, so a whole group's gathers can be in flight)
+    static const EvalFn hevals[6] = {k_h_eval<6, false>,  k_h_eval<7, false>,
+                                     k_h_eval<8, false>,  k_h_eval<11, false>,
+                                     k_h_eval<16, false>, k_h_eval<21, false>};
     static const EvalFn hevals_cells[1] = {k_h_eval<8, true>};
     if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
         for (EvalFn f : evals)
@@ -7367,7 +7372,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     // K2h: 7 by default (groups of 21 = three full chunks; cfg3 0.316 vs 0.321 ms at 8, same
     // box, profiles/r04/sweep3), K2g: 8
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : big ? 11 : sim ? 7 : 8;
-    const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : 4;
+    const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : chl == 16 ? 4 : 5;
     const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                    (ctx->kp.length_smooth ? 2 : 0) +
                    (ctx->kp.maxratio_smooth ? 1 : 0);
@@ -7496,10 +7501,12 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     const dim3 ge((unsigned)((n_items + 255) / 256));
     using VEvalFn = void (*)(KParams, KVol4, KGrp);
     // gathers in flight per lane: 11 by default (k_v_eval<8> spills at 4 waves per SIMD, so 8 and
-    // 11 are built for 3)
+    // 11 are built for 3, 16 and 21 for 2)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 11;
-    static const VEvalFn vevals[4] = {k_v_eval<6>, k_v_eval<7>, k_v_eval<8>, k_v_eval<11>};
-    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : 3];
+    static const VEvalFn vevals[6] = {k_v_eval<6>,  k_v_eval<7>,  k_v_eval<8>,
+                                      k_v_eval<11>, k_v_eval<16>, k_v_eval<21>};
+    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3
+                                                                    : chl == 16 ? 4 : 5];
     if (lds > 64 * 1024 && !ctx->k4h_attrs) {
         for (VEvalFn f : vevals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
