@@ -334,7 +334,8 @@ def main():
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
-                                   packed=last in ("K2s+pack", "K2g+pack", "K2h+pack"),
+                                   packed=last in ("K2s+pack", "K2g+pack", "K2h+pack",
+                                                   "K2h-tile+pack"),
                                    volume=volume_mode,
                                    cells=args.cells and not volume_mode)
     roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "

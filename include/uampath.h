@@ -475,7 +475,12 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K4H_BAND             K4h sort key: altitude layers per band, a power of two
  *                                (default 0: the fewest giving at most 16 bands); tiles from
  *                                UAM_OPT_K2G_TILE_BITS (default 3: 8 x 8 tiles), at most
- *                                4096 (tile, band) bins */
+ *                                4096 (tile, band) bins
+ *   UAM_OPT_K2G_TILE_OWNER       K2h tile form (measured): 0 (default), or
+ *                                T = 64 / 128: sort tiles of T x T cells, one workgroup per tile
+ *                                that stages the tile's packed plane in LDS once and evaluates
+ *                                all of the tile's items, reading their code-1 waypoints inside
+ *                                the tile from LDS ("K2h-tile+pack").  Same outputs. */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -493,7 +498,8 @@ enum {
     UAM_OPT_K2G_CURVE = 14,
     UAM_OPT_K2G_SIM = 15,
     UAM_OPT_K2G_LDS_WINDOW = 16,
-    UAM_OPT_K4H_BAND = 17
+    UAM_OPT_K4H_BAND = 17,
+    UAM_OPT_K2G_TILE_OWNER = 18
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

@@ -193,6 +193,45 @@ def test_k2h_partial_raster(oracle_mod):
     _check(gpu, ref, oracle_mod, D)
 
 
+@pytest.mark.parametrize("tile,group,R,geo_kind", [(128, 21, 1024, "square"),
+                                                  (64, 21, 1024, "square"),
+                                                  (128, 7, 4096, "square"),
+                                                  (64, 30, 1024, "partial"),
+                                                  (128, 1, 1024, "partial")])
+def test_k2h_tile_form(oracle_mod, tile, group, R, geo_kind):
+    """The tile form (UAM_OPT_K2G_TILE_OWNER: one workgroup per T x T tile, its packed plane in
+    LDS) changes where code-1 waypoints inside the tile are read, nothing else: every output
+    equals orc_eval_generated_h bit for bit, with pairs off the raster (the off-raster bin's
+    workgroup), NaN pairs, start == goal, a raster that is not a multiple of the tile (edge
+    tiles zero-filled past the raster) and tiles without items."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.engine import RasterGeo
+    from uam_path_planning_amd.scenario import displacements
+
+    geo = None
+    if geo_kind == "partial":
+        geo = RasterGeo(nx=1000, ny=700, x0=8.0, y_top=5.0, dx=40.0 / 1000, dy=40.0 / 1000,
+                        nodata=-9999.0, dem_threshold=0.0)
+    e, orc, raster, rd, rec = _case(oracle_mod, group, 80, R=R, nfz=64, geo=geo,
+                                    maxalpha=0.015)
+    e.set_option("k2g_tile_owner", tile)
+    assert e.get_option("k2g_tile_owner") == tile
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs(3000, 41)
+    ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=group)
+    gpu = e.eval_generated(pairs, ut, raster=raster)
+    assert e.last_kernel() == "K2h-tile+pack" and e.last_group() == group
+    _check(gpu, ref, oracle_mod, D)
+    # with cells requested the launch is the cell-writing K2h, the same bits
+    cells = e.eval_generated(pairs, ut, raster=raster, want_cells=True)
+    assert e.last_kernel() == "K2h+pack"
+    _check(cells, ref, oracle_mod, D)
+    for bad in (1, 32, 256):
+        with pytest.raises(ValueError):
+            e.set_option("k2g_tile_owner", bad)
+
+
 @pytest.mark.parametrize("group", [21, 5, 64])
 def test_k2h_waypoint_cells(oracle_mod, group):
     """Waypoint cells from K2h at cfg3's geometry (4096^2, 70 no-fly shapes, N = 80) on a

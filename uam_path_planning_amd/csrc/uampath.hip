@@ -4846,6 +4846,9 @@ struct KGrp {
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
     UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's extra
                                    // block
+    int32_t* __restrict__ bstart;  // K2h tile form: [bins + 1] first sorted position of each
+                                   // bin (written by the scatter's partition 0), or null
+    const uint16_t* __restrict__ tinv;  // [2^tbits * 2^tbits] curve position -> tile (y n + x)
 };
 
 // K2h / K4h: the D rows' unit sums by one block (the extra block of the scatter launch).
@@ -5060,7 +5063,9 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
         const int64_t c = (int64_t)k * G_NBK + b;
         const int sb = (int)(c / (256 * SCAN_ITEMS));
         cur[k] = kg.cnt[c] + (nsb > 0 ? stot[sb] : kg.tot[sb]);
+        if (kg.bstart && b == 0) kg.bstart[k] = cur[k];  // partition 0's place = the bin's start
     }
+    if (kg.bstart && b == 0 && t == 0) kg.bstart[kg.bins] = (int32_t)kg.n_items;
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
@@ -5495,6 +5500,140 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // of BS items, and a WIN x WIN-cell window of the packed plane staged in LDS around the
 // workgroup's middle item (its middle waypoint's cell): a code-1 waypoint inside it reads LDS,
 // its global load is the dummy line.  The window's staging reads each of its lines once.
+// one (path, group) item of K2h: the group's points, cells and records -- the body of k_h_eval
+// and of the tile form k_h_tile.  s_map / s_u / s_cells: the workgroup's code map, unit-arc rows
+// and cell staging; WIN > 0: a WIN x WIN window of the packed plane (plane-A layout) at cell
+// (ox, oy) in s_win, whose code-1 waypoints read LDS instead of global memory.
+template <int CH, bool CELLS, int WIN>
+__device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, const KGrp& kg,
+                                       const uint4* __restrict__ rec,
+                                       const uint32_t* __restrict__ s_map,
+                                       const double2* __restrict__ s_u, int32_t* s_cells,
+                                       const uint2* __restrict__ s_win, int ox, int oy,
+                                       bool live, int32_t item, int32_t path, int32_t q,
+                                       const double4& pr) {
+    // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
+    // last item evaluates nothing and writes nothing
+    const int s = item - path * kg.nseg;
+    const int32_t d = path - q * kg.D;
+    const int N = p.N, W = kg.W;
+    const double2* urow = s_u + d * N;
+    const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
+    // chunks: the wave's most, so the loop is wave-uniform
+    int nch = (j1 - j0 + CH - 1) / CH;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nch = max(nch, __shfl_xor(nch, o));
+    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
+    const double dN = (double)N, yN = kg.inv_n;
+    auto over_n = [&](double a) {  // Phi / N exactly as k_g_eval forms it
+        if (yN == 0.0) return a / dN;
+        const double q0 = a * yN;
+        const double q1 = fma(fma(-q0, dN, a), yN, q0);
+        return __builtin_isinf(a) ? q0 : q1;
+    };
+    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
+    double gc = 0.0, gn = 0.0;
+    float hmax = -INFINITY;
+    uint32_t nh = 0, off = 0;
+    for (int c = 0; c < nch; ++c) {
+        const int jc = j0 + c * CH;
+        uint4 r[CH];
+        uint2 lv[WIN > 0 ? CH : 1];
+        int32_t cl[CH];
+        uint32_t inb = 0, need = 0, full = 0, odd = 0, inw = 0;
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int j = jc + t;
+            const double2 u = urow[min(max(j - 1, 0), N - 1)];
+            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
+            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+            x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
+            x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
+            const double tx = (x0 - rs.x0) * rs.inv_dx;
+            const double ty = (rs.y_top - x1) * rs.inv_dy;
+            const uint4* ptr = dummy;
+            cl[t] = -1;
+            if ((j < j1) && (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) &&
+                (ty < (double)rs.ny)) {
+                inb |= 1u << t;
+                const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
+                if (CELLS) cl[t] = iy * rs.nx + ix;
+                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
+                if (code & 2u) {
+                    need |= 1u << t;
+                    full |= 1u << t;
+                    ptr = rec + (iy * rs.nx + ix);
+                } else if (code) {
+                    need |= 1u << t;
+                    const int32_t a = pk_addr(rs, ix, iy);
+                    odd |= (uint32_t)(a & 1) << t;
+                    ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
+                    if (WIN > 0) {
+                        const int wx = ix - ox, wy = iy - oy;
+                        if ((uint32_t)wx < (uint32_t)WIN && (uint32_t)wy < (uint32_t)WIN) {
+                            inw |= 1u << t;
+                            ptr = dummy;
+                        }
+                    }
+                }
+            }
+            r[t] = *ptr;
+            if (WIN > 0) {  // the window's entry (index 0 when unused)
+                const int wx = ((inw >> t) & 1u) ? ((int32_t)((x0 - rs.x0) * rs.inv_dx) - ox) : 0;
+                const int wy = ((inw >> t) & 1u) ? ((int32_t)((rs.y_top - x1) * rs.inv_dy) - oy) : 0;
+                lv[t] = s_win[(((wy >> 2) * (WIN / 4) + (wx >> 2)) << 4) | ((wy & 3) << 2) | (wx & 3)];
+            }
+        }
+        const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const bool vl = t < nv;
+            const bool in = (inb >> t) & 1u, nd = (need >> t) & 1u, fl = (full >> t) & 1u,
+                       od = (odd >> t) & 1u;
+            const uint4 rt = r[t];
+            uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
+            uint32_t ter = nd ? (fl ? rt.z : od ? rt.w : rt.y) : 0u;
+            if (WIN > 0 && ((inw >> t) & 1u)) phi = lv[t].x, ter = lv[t].y;
+            const uint32_t psi = fl ? rt.y : 0u;
+            if (fl && (rt.w & UAM_FLAG_NODATA)) ter = 0u;
+            nh += (fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            off += (vl && !in) ? 1u : 0u;
+            gc = gc + over_n((double)__uint_as_float(phi));
+            gn = gn + (double)__uint_as_float(psi);
+            hmax = fmaxf(hmax, vl ? __uint_as_float(ter) : -INFINITY);
+        }
+        if (CELLS) {
+            // through the wave's LDS slice: lane l stages its CH cells, then each store
+            // instruction writes 64 / CH items' runs of CH consecutive cells (runs of
+            // cells[path][jc..jc+nv)), instead of 64 scattered 4-B stores per waypoint
+            int32_t* sw = s_cells + (threadIdx.x >> 6) * (CH * 64);
+            const int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int t = 0; t < CH; ++t) sw[t * 64 + lane] = cl[t];
+            __builtin_amdgcn_wave_barrier();
+            const int64_t base = (int64_t)path * W + jc;  // this lane's run
+            constexpr int IPS = 64 / CH;                 // items per store instruction
+#pragma unroll
+            for (int k = 0; k < (64 + IPS - 1) / IPS; ++k) {
+                const int it = k * IPS + lane / CH, t = lane % CH;
+                const int src = it < 64 ? it : 63;
+                const int64_t b_it = __shfl(base, src);
+                const int nv_it = __shfl(nv, src);
+                if (lane < IPS * CH && it < 64 && t < nv_it) kg.cells[b_it + t] = sw[t * 64 + it];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    HSlot o;
+    o.cost = gc;
+    o.psi = gn;
+    o.hmax = hmax;
+    o.cnt = nh | (off << 8);
+    if (live) reinterpret_cast<HSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
+}
+
 template <int CH, bool CELLS, int BS = 256, int WIN = 0>
 __global__ __launch_bounds__(BS, BS == 256 ? (CH >= 16 ? 2 : UAM_K2H_MINW) : 1) void k_h_eval(
                                                                   KParams p, KRaster rs,
@@ -5576,126 +5715,98 @@ __global__ __launch_bounds__(BS, BS == 256 ? (CH >= 16 ? 2 : UAM_K2H_MINW) : 1) 
         }
     }
     __syncthreads();
-    // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
-    // last item evaluates nothing and writes nothing
-    const int s = item - path * kg.nseg;
-    const int32_t d = path - q * kg.D;
-    const int N = p.N, W = kg.W;
-    const double2* urow = s_u + d * N;
-    const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
-    // chunks: the wave's most, so the loop is wave-uniform
-    int nch = (j1 - j0 + CH - 1) / CH;
+    h_item<CH, CELLS, WIN>(p, rs, kg, rec, s_map, s_u, s_cells, s_win, WIN > 0 ? s_org[0] : 0,
+                           WIN > 0 ? s_org[1] : 0, live, item, path, q, pr);
+}
+
+// K2h tile form (UAM_OPT_K2G_TILE_OWNER = T; the round-3 verdict's LDS prototype): the sort's
+// tiles are T x T cells, and workgroup w (XCD-placed, xcd_chunk) owns curve position w: it stages
+// that tile's packed plane (T^2 8-B entries, 128 KiB at T = 128) in LDS once and evaluates every
+// item of the tile's two bins (full groups, then the ragged last groups) in rounds of BS, each
+// item exactly as k_h_eval's (h_item: the same arithmetic and order, only the code-1 waypoints
+// inside the tile read LDS).  Workgroup `tiles` takes the off-raster bin without a window.
+template <int CH, int T, int BS>
+__global__ __launch_bounds__(BS, 1) void k_h_tile(KParams p, KRaster rs, KGrp kg,
+                                                  const uint4* __restrict__ rec) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint32_t* s_map = s_dyn;
+    const int mapw = (rs.pwords + 3) & ~3;
+    double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
+    uint2* s_win = reinterpret_cast<uint2*>(s_u + kg.D * p.N + 1);
+    const int tiles = 1 << (2 * kg.tbits);
+    const int w = (int)xcd_chunk(blockIdx.x, gridDim.x);
+    int a0, a1, b0 = 0, b1 = 0;
+    if (w < tiles) {
+        a0 = kg.bstart[w], a1 = kg.bstart[w + 1];
+        if (kg.last_bin) b0 = kg.bstart[w + kg.last_bin], b1 = kg.bstart[w + kg.last_bin + 1];
+    } else {
+        a0 = kg.bstart[kg.bins - 1], a1 = kg.bstart[kg.bins];
+    }
+    const int n0 = a1 - a0, n = n0 + (b1 - b0);
+    if (n <= 0) return;  // (the whole workgroup)
+    int ox = -(1 << 30), oy = -(1 << 30);  // no window: nothing falls inside it
+    if (w < tiles) {
+        const int tl = kg.tinv[w];
+        ox = (tl & ((1 << kg.tbits) - 1)) * T;
+        oy = (tl >> kg.tbits) * T;
+    }
+    {  // the code map and the unit-arc rows, as k_h_eval
+        constexpr int U = 4;
+        const int nv = rs.pwords >> 2, nu = kg.D * p.N;
+        const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
+        uint4* dst = reinterpret_cast<uint4*>(s_map);
+        const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
+        uint4* du = reinterpret_cast<uint4*>(s_u);
+        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += BS * U) {
+            uint4 v[U];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) nch = max(nch, __shfl_xor(nch, o));
-    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
-    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
-    const double dN = (double)N, yN = kg.inv_n;
-    auto over_n = [&](double a) {  // Phi / N exactly as k_g_eval forms it
-        if (yN == 0.0) return a / dN;
-        const double q0 = a * yN;
-        const double q1 = fma(fma(-q0, dN, a), yN, q0);
-        return __builtin_isinf(a) ? q0 : q1;
-    };
-    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
-    double gc = 0.0, gn = 0.0;
-    float hmax = -INFINITY;
-    uint32_t nh = 0, off = 0;
-    for (int c = 0; c < nch; ++c) {
-        const int jc = j0 + c * CH;
-        uint4 r[CH];
-        uint2 lv[WIN > 0 ? CH : 1];
-        int32_t cl[CH];
-        uint32_t inb = 0, need = 0, full = 0, odd = 0, inw = 0;
-#pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int j = jc + t;
-            const double2 u = urow[min(max(j - 1, 0), N - 1)];
-            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
-            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-            x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
-            x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
-            const double tx = (x0 - rs.x0) * rs.inv_dx;
-            const double ty = (rs.y_top - x1) * rs.inv_dy;
-            const uint4* ptr = dummy;
-            cl[t] = -1;
-            if ((j < j1) && (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) &&
-                (ty < (double)rs.ny)) {
-                inb |= 1u << t;
-                const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
-                if (CELLS) cl[t] = iy * rs.nx + ix;
-                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
-                if (code & 2u) {
-                    need |= 1u << t;
-                    full |= 1u << t;
-                    ptr = rec + (iy * rs.nx + ix);
-                } else if (code) {
-                    need |= 1u << t;
-                    const int32_t a = pk_addr(rs, ix, iy);
-                    odd |= (uint32_t)(a & 1) << t;
-                    ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
-                    if (WIN > 0) {
-                        const int wx = ix - s_org[0], wy = iy - s_org[1];
-                        if ((uint32_t)wx < (uint32_t)WIN && (uint32_t)wy < (uint32_t)WIN) {
-                            inw |= 1u << t;
-                            ptr = dummy;
-                        }
-                    }
-                }
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * BS;
+                v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
             }
-            r[t] = *ptr;
-            if (WIN > 0) {  // the window's entry (index 0 when unused)
-                const int wx = ((inw >> t) & 1u) ? ((int32_t)((x0 - rs.x0) * rs.inv_dx) - s_org[0]) : 0;
-                const int wy = ((inw >> t) & 1u) ? ((int32_t)((rs.y_top - x1) * rs.inv_dy) - s_org[1]) : 0;
-                lv[t] = s_win[(((wy >> 2) * (WIN / 4) + (wx >> 2)) << 4) | ((wy & 3) << 2) | (wx & 3)];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * BS;
+                *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
             }
         }
-        const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
+        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += BS) s_map[i] = rs.pmap[i];
+    }
+    if (w < tiles) {  // the tile: (T/4)^2 blocks of 16 entries, 8 x uint4 each, U in flight
+        constexpr int WB = T / 4, U = 4;
+        uint4* dw = reinterpret_cast<uint4*>(s_win);
+        for (int i0 = threadIdx.x; i0 < WB * WB * 8; i0 += BS * U) {
+            uint4 v[U];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const bool vl = t < nv;
-            const bool in = (inb >> t) & 1u, nd = (need >> t) & 1u, fl = (full >> t) & 1u,
-                       od = (odd >> t) & 1u;
-            const uint4 rt = r[t];
-            uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
-            uint32_t ter = nd ? (fl ? rt.z : od ? rt.w : rt.y) : 0u;
-            if (WIN > 0 && ((inw >> t) & 1u)) phi = lv[t].x, ter = lv[t].y;
-            const uint32_t psi = fl ? rt.y : 0u;
-            if (fl && (rt.w & UAM_FLAG_NODATA)) ter = 0u;
-            nh += (fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
-            off += (vl && !in) ? 1u : 0u;
-            gc = gc + over_n((double)__uint_as_float(phi));
-            gn = gn + (double)__uint_as_float(psi);
-            hmax = fmaxf(hmax, vl ? __uint_as_float(ter) : -INFINITY);
-        }
-        if (CELLS) {
-            // through the wave's LDS slice: lane l stages its CH cells, then each store
-            // instruction writes 64 / CH items' runs of CH consecutive cells (runs of
-            // cells[path][jc..jc+nv)), instead of 64 scattered 4-B stores per waypoint
-            int32_t* sw = s_cells + (threadIdx.x >> 6) * (CH * 64);
-            const int lane = threadIdx.x & 63;
-#pragma unroll
-            for (int t = 0; t < CH; ++t) sw[t * 64 + lane] = cl[t];
-            __builtin_amdgcn_wave_barrier();
-            const int64_t base = (int64_t)path * W + jc;  // this lane's run
-            constexpr int IPS = 64 / CH;                 // items per store instruction
-#pragma unroll
-            for (int k = 0; k < (64 + IPS - 1) / IPS; ++k) {
-                const int it = k * IPS + lane / CH, t = lane % CH;
-                const int src = it < 64 ? it : 63;
-                const int64_t b_it = __shfl(base, src);
-                const int nv_it = __shfl(nv, src);
-                if (lane < IPS * CH && it < 64 && t < nv_it) kg.cells[b_it + t] = sw[t * 64 + it];
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * BS;
+                const int blk = i >> 3, part = i & 7;
+                const int by = blk / WB, bx = blk - by * WB;
+                const int gy = (oy >> 2) + by, gx = (ox >> 2) + bx;
+                v[k] = make_uint4(0u, 0u, 0u, 0u);
+                if (i < WB * WB * 8 && gx * 4 < rs.nx && gy * 4 < rs.ny)
+                    v[k] = reinterpret_cast<const uint4*>(
+                        rs.pa + (((int64_t)gy * rs.pnbx + gx) << 4))[part];
             }
-            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * BS;
+                if (i < WB * WB * 8) dw[i] = v[k];
+            }
         }
     }
-    HSlot o;
-    o.cost = gc;
-    o.psi = gn;
-    o.hmax = hmax;
-    o.cnt = nh | (off << 8);
-    if (live) reinterpret_cast<HSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
+    __syncthreads();
+    for (int base = 0; base < n; base += BS) {  // rounds: the count is the workgroup's
+        const int i = base + (int)threadIdx.x;
+        const bool live = i < n;
+        const int pos = !live ? a0 : i < n0 ? a0 + i : b0 + (i - n0);
+        const int32_t item = live ? kg.order[pos] : 0;
+        const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
+        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+        h_item<CH, false, T>(p, rs, kg, rec, s_map, s_u, nullptr, s_win, ox, oy, live, item,
+                             path, q, pr);
+    }
 }
 
 // outputs of every path (block = 64 pairs x D, k_g_final's layout): the geometry terms from
@@ -6210,6 +6321,8 @@ struct uam_ctx {
                                 // (UAM_OPT_K2G_LDS_FLOOR; K2g cfg3: 45 / 54 / 80 KiB 0.43 / 0.54
                                 // / 0.52 ms against 0.39, k2g7; 0 = the launchers' defaults)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
+    int k2g_towner = 0;         // K2h tile form: tile side T (UAM_OPT_K2G_TILE_OWNER: 0, 64, 128)
+    bool k2h_tile_attrs = false;  // its dynamic-LDS attributes raised on this context's device
     int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
                                 // 0 = the fewest giving <= 16 bands)
     int k2g_lwin = 0;           // K2h LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW: 0, 96, 128)
@@ -6931,6 +7044,12 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             (long long)value);
             ctx->k2g_lwin = (int)value;
             return UAM_OK;
+        case UAM_OPT_K2G_TILE_OWNER:
+            if (value != 0 && value != 64 && value != 128)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2G_TILE_OWNER %lld not 0, 64 or 128",
+                            (long long)value);
+            ctx->k2g_towner = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2G_SIM:
             if (value != 0 && value != 1)
                 return fail(UAM_E_INVALID, "UAM_OPT_K2G_SIM %lld not 0 or 1", (long long)value);
@@ -6964,6 +7083,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
+        case UAM_OPT_K2G_TILE_OWNER: *value = ctx->k2g_towner; return UAM_OK;
         case UAM_OPT_K2G_LDS_WINDOW: *value = ctx->k2g_lwin; return UAM_OK;
         case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
@@ -7232,8 +7352,10 @@ static int tile_keys(uam_ctx* ctx, int bits, int curve, hipStream_t s) {
             }
             h[(size_t)y * n + x] = (uint16_t)k;
         }
+    h.resize((size_t)2 * n * n);  // then the inverse: curve position -> tile y n + x
+    for (uint32_t i = 0; i < n * n; ++i) h[(size_t)n * n + h[i]] = (uint16_t)i;
     if (!ctx->d_tkey) {
-        const size_t cap = sizeof(uint16_t) << (2 * G_TBITS_MAX);
+        const size_t cap = (2 * sizeof(uint16_t)) << (2 * G_TBITS_MAX);
         if (hipMalloc(&ctx->d_tkey, cap) != hipSuccess) return fail(UAM_E_NOMEM, "tile keys");
     }
     // stream-ordered: the launches that read the table follow on s
@@ -7269,8 +7391,18 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
+    // the tile form (K2h without cells): tiles of exactly towner x towner cells
+    const int towner = (ctx->k2g_sim && !ctx->kp.maxratio_smooth && !ko.cells) ? ctx->k2g_towner
+                                                                              : 0;
     int tbits = ctx->k2g_tbits;
-    if (tbits == 0) {  // tiles of ~256 x 256 cells
+    if (towner) {
+        const int tsh = towner == 64 ? 6 : 7;
+        tbits = 1;
+        while (((std::max(kr.nx, kr.ny) - 1) >> tsh) >= (1 << tbits)) ++tbits;
+        if (tbits > G_TBITS_MAX)
+            return fail(UAM_E_INVALID, "K2h tile form: %d x %d raster needs more than %d tile bits",
+                        kr.nx, kr.ny, G_TBITS_MAX);
+    } else if (tbits == 0) {  // tiles of ~256 x 256 cells
         tbits = 3;
         while (tbits < G_TBITS_MAX && (std::max(kr.nx, kr.ny) >> tbits) > 256) ++tbits;
     }
@@ -7291,9 +7423,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
                  b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot))),
-                 b_ug = al((size_t)D * sizeof(UGeo));
+                 b_ug = al((size_t)D * sizeof(UGeo)),
+                 b_bs = towner ? al((size_t)(bins + 1) * 4) : 0;
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_bs, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs;
@@ -7306,6 +7439,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.nseg = nseg;
     int tshift = 0;
     while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << tbits)) ++tshift;
+    if (towner) tshift = towner == 64 ? 6 : 7;
     kg.tshift = tshift;
     kg.tbits = tbits;
     kg.bins = bins;
@@ -7313,6 +7447,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
     if (st) return st;
     kg.tkey = ctx->d_tkey;
+    kg.tinv = ctx->d_tkey + ((size_t)1 << (2 * tbits));
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
@@ -7323,6 +7458,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
+    kg.bstart = towner ? (int32_t*)(w + o) : nullptr, o += b_bs;
     kg.key = (uint16_t*)(w + o);
     const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +  // + junk slot
                             (sim && ko.cells ? (size_t)4 * 8 * 64 * 4 : 0);    // K2h cells
@@ -7402,8 +7538,25 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                                         160 * 1024));
         ctx->k2g_attrs_cells = true;
     }
-    hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds_run, s,
-                       ctx->kp, kr, kg, (const uint4*)rec);
+    if (towner) {  // the tile form: one workgroup per tile (+ one for the off-raster bin)
+        const EvalFn tf = towner == 128 ? k_h_tile<8, 128, 1024> : k_h_tile<8, 64, 512>;
+        const int tbs = towner == 128 ? 1024 : 512;
+        const size_t lds_t = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +
+                             (size_t)towner * towner * 8;
+        if (lds_t > 160 * 1024) return fail(UAM_E_INVALID, "K2h tile form: LDS %zu B", lds_t);
+        if (!ctx->k2h_tile_attrs) {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_h_tile<8, 128, 1024>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            HIP_TRY(hipFuncSetAttribute((const void*)k_h_tile<8, 64, 512>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            ctx->k2h_tile_attrs = true;
+        }
+        hipLaunchKernelGGL(tf, dim3((unsigned)(tiles + 1)), dim3(tbs), lds_t, s, ctx->kp, kr, kg,
+                           (const uint4*)rec);
+    } else {
+        hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds_run, s,
+                           ctx->kp, kr, kg, (const uint4*)rec);
+    }
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
@@ -7414,7 +7567,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
-    ctx->last_kernel = sim ? "K2h+pack" : "K2g+pack";
+    ctx->last_kernel = towner ? "K2h-tile+pack" : sim ? "K2h+pack" : "K2g+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
