@@ -5356,7 +5356,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 int32_t cl = -1;
                 const uint4 r = *locate(x0, x1, 0, inb, need, full, odd, cl);
                 consume1(r, inb & 1u, need & 1u, full & 1u, odd & 1u);
-                if (CELLS) kg.cells[(int64_t)path * W + j] = cl;
+                if (CELLS) __builtin_nontemporal_store(cl, kg.cells + (int64_t)path * W + j);
             }
         }
     }
@@ -5621,7 +5621,10 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
                 const int src = it < 64 ? it : 63;
                 const int64_t b_it = __shfl(base, src);
                 const int nv_it = __shfl(nv, src);
-                if (lane < IPS * CH && it < 64 && t < nv_it) kg.cells[b_it + t] = sw[t * 64 + it];
+                // streaming stores: the cells are never re-read, and through L2 they evicted
+                // the gathers' lines (cfg3 --cells 0.471 -> 0.416 ms, profiles/r04/cellsnt)
+                if (lane < IPS * CH && it < 64 && t < nv_it)
+                    __builtin_nontemporal_store(sw[t * 64 + it], kg.cells + b_it + t);
             }
             __builtin_amdgcn_wave_barrier();
         }
