@@ -18,13 +18,14 @@ $LLVM/clang -O1 -g -std=c99 -fPIC -shared -ffp-contract=off $SAN -o "$OUT/libora
     -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
     -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer \
     -o "$OUT/libuampath.so" "$ROOT/uam_path_planning_amd/csrc/uampath.hip" \
-    "$ROOT/uam_path_planning_amd/csrc/polyproc.cpp"
+    "$ROOT/uam_path_planning_amd/csrc/polyproc.cpp" "$ROOT/uam_path_planning_amd/csrc/tiles.cpp" \
+    -lz
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 cd "$ROOT"
-LD_PRELOAD=$RT \
+LD_PRELOAD=$RT${LD_PRELOAD:+:$LD_PRELOAD} \
 ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:verify_asan_link_order=0 \
 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
 UAM_LIB_PATH=$OUT/libuampath.so UAM_ORACLE_LIB=$OUT/liboracle.so \
 python -m pytest -x -q -p no:cacheprovider -m "not gpu" \
     tests/test_polygons_cpu.py tests/test_oracle_golden.py tests/test_refine_cpu.py \
-    tests/test_crs_cpu.py tests/test_host_cpu.py "$@"
+    tests/test_crs_cpu.py tests/test_host_cpu.py tests/test_map_generation_cpu.py "$@"
