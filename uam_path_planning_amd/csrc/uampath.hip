@@ -4844,14 +4844,14 @@ struct KGrp {
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
-    UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's extra
-                                   // block
+    UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's block 0
     int32_t* __restrict__ bstart;  // K2h tile form: [bins + 1] first sorted position of each
                                    // bin (written by the scatter's partition 0), or null
     const uint16_t* __restrict__ tinv;  // [2^tbits * 2^tbits] curve position -> tile (y n + x)
 };
 
-// K2h / K4h: the D rows' unit sums by one block (the extra block of the scatter launch).
+// K2h / K4h: the D rows' unit sums by one block (block 0 of the scatter launch, one more than
+// its partitions, so the step has no launch for them).
 // The terms are independent, the sums are not: every (row, chord) term first, one thread each
 // (unit_geo_row's operations), into LDS; then one thread per (row, sum) adds its terms in
 // unit_geo_row's order, so the bits are unit_geo_row's.  (One thread per row walking its 81
@@ -4957,8 +4957,6 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
 // groups (the tile under the group's middle waypoint) and the partition's histogram, stored
 // bin-major so the scan yields each (bin, partition)'s offset
-// K2h launches one block more: it forms the D rows' unit sums (unit_geo_row) beside the
-// histogram blocks, so the step has no launch for them
 __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
@@ -5019,14 +5017,16 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
         }
     }
     __syncthreads();
-    // the partition's place in each bin: its count added to the bin's total (the order of
-    // the partitions inside a bin follows the atomics -- it only decides which lane evaluates
-    // an item, never what the item computes); k_g_scatter scans the totals itself
+    // the partition's count per bin, bin-major ([bin][partition]): k_scan_local's exclusive
+    // scan of it is each (bin, partition)'s place, up to its scan block's total
     for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
-// launch 4 (after k_scan_local / k_scan_totals over cnt): LDS cursors, items scattered; U keys
-// per thread loaded before the first cursor update.  (A two-launch form -- device-scope
+// launch 3 (after k_scan_local over cnt; the scan blocks' totals are scanned here, or by
+// k_scan_totals beyond 1024 of them): LDS cursors, items scattered; U keys per thread loaded
+// before the first cursor update.  The order of the items inside a (bin, partition) run follows
+// the LDS atomics: it only decides which lane evaluates an item, never what the item computes.
+// (A two-launch form -- device-scope
 // atomics on the bin totals in the histogram launch, their scan in this one -- ran the
 // histogram 11 -> 34 us at cfg3: 256 partitions' atomics on each bin address serialise
 // across the XCDs; profiles/r04/prof1.)
@@ -6013,8 +6013,7 @@ __device__ __forceinline__ double vz_at(double za, double zb, double jw) {
     return za + (zb - za) * jw;
 }
 
-// sort, launch 1 (K4h): keys on (altitude band, tile) of each item's middle waypoint; block
-// G_NBK forms the unit sums (k_g_hist's K2h block)
+// sort, launch 1 (K4h): keys on (altitude band, tile) of each item's middle waypoint
 __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];
