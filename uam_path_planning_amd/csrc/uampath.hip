@@ -6025,6 +6025,7 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
     const int N = p.N, W = kg.W;
     const int tiles = 1 << (2 * kg.tbits);
+    const double inv_w1 = 1.0 / (double)(W - 1);
     // U items per thread with all their loads issued first (k_g_hist's batching)
     constexpr int U = 4;
     for (int64_t i0 = lo + t; i0 < hi; i0 += 1024 * U) {
@@ -6058,7 +6059,8 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
             } else {
                 arc_point(pr[k][0], pr[k][1], pr[k][3], pr[k][4], u[k].x, u[k].y, x0, x1);
             }
-            const double z = vz_at(pr[k][2], pr[k][5], (double)jm[k] / (double)(W - 1));
+            // (the key only orders the items: j / (W-1) by a reciprocal is exact enough)
+            const double z = vz_at(pr[k][2], pr[k][5], (double)jm[k] * inv_w1);
             const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
             const double tz = (z - vs.z0) * vs.inv_dz;
             uint32_t key = kg.bins - 1;
