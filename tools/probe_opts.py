@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--cells", action="store_true")
     ap.add_argument("--volume", action="store_true",
                     help="cfg5: 1024^2 x 64 volume, packed copy, 100k pairs x 5 (K4h / K4)")
+    ap.add_argument("--analytic", action="store_true",
+                    help="cfg3 in analytic mode (K3b): the reference formulas, no raster")
     a = ap.parse_args()
     import torch
     from uam_path_planning_amd.arcs import arc_table
@@ -52,6 +54,11 @@ def main():
 
         def run():
             e.eval_generated3d(pairs, ut, vol, outputs=outs)
+    elif a.analytic:
+        pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
+
+        def run():
+            e.eval_generated(pairs, ut, raster=None, outputs=outs)
     else:
         raster = e.raster_build(raster_geo(a.R), synthetic_dem(a.R))
         pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
