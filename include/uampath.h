@@ -294,11 +294,16 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* desc, const void* rec2
 int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                          const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
                          int32_t D, const uam_path_outputs* out, uam_stream stream);
-/* The packed volume (K4h): one 16-B voxel {float risk, float psi_nfz, float terrain, uint32
- * flags} per (ix, iy, iz) -- the column's terrain and flags beside the layer's pair, so a
- * waypoint is one request -- in blocks of 4 x 2 cells of one layer (one 128-B line),
- * layer-major planes, padded to whole blocks.  uam_volume_pack derives it from a built volume
- * (vol_dev); packed_dev holds uam_volume_packed_bytes bytes, 256-B aligned. */
+/* The packed volume (K4h), three 256-B aligned sections, so a waypoint is one request:
+ *   1. 16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} per (ix, iy, iz) --
+ *      the column's terrain and flags beside the layer's pair -- in blocks of 4 x 2 cells of
+ *      one layer (one 128-B line), layer-major planes, padded to whole blocks;
+ *   2. 8-B voxels {float risk, float terrain} in blocks of 4 x 4 cells of one layer;
+ *   3. a 2-bit code per 8 x 8 columns: 3 where a column of the block has psi_nfz != +-0 or the
+ *      no-fly flag (its waypoints read section 1), else 1 (section 2: psi is +-0 and no flag
+ *      is set there, so the 8-B voxel's consume adds exact no-ops).
+ * uam_volume_pack derives it from a built volume (vol_dev); packed_dev holds
+ * uam_volume_packed_bytes bytes (1.5 GiB at 1024^2 x 64), 256-B aligned. */
 int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);
 int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                     void* packed_dev, uam_stream stream);

@@ -36,6 +36,30 @@ def test_header_symbols_exported(lib):
     assert lib.uam_abi_version() == 1
 
 
+def test_volume_packed_bytes(lib):
+    """uam_volume_packed_bytes (host only): the 16-B table (4 x 2 blocks per layer), the 8-B
+    table (4 x 4 blocks per layer) and the 2-bit code per 8 x 8 columns, each section 256-B
+    aligned; an invalid description fails loudly."""
+    from uam_path_planning_amd import _lib
+
+    al = lambda v: (v + 255) // 256 * 256
+    for nx, ny, nz in ((1024, 1024, 64), (300, 300, 7), (1, 1, 1), (1001, 77, 3)):
+        vd = _lib.VolumeDesc(nx, ny, nz, 0.0, 20.0, 60.0 / nx, 60.0 / nx, 0.0, 10.0)
+        n = ctypes.c_int64()
+        assert lib.uam_volume_packed_bytes(ctypes.byref(vd), ctypes.byref(n)) == _lib.UAM_OK
+        nbx4, nby2, nby4 = (nx + 3) // 4, (ny + 1) // 2, (ny + 3) // 4
+        cw = (((nx + 7) // 8) * ((ny + 7) // 8) + 15) // 16
+        want = al(nbx4 * nby2 * 8 * nz * 16) + al(nbx4 * nby4 * 16 * nz * 8) + al(cw * 4)
+        assert n.value == want, (nx, ny, nz)
+    assert n.value >= 0
+    vd = _lib.VolumeDesc(1024, 1024, 64, 0.0, 20.0, 60.0 / 1024, 60.0 / 1024, 0.0, 10.0)
+    assert lib.uam_volume_packed_bytes(ctypes.byref(vd), ctypes.byref(n)) == _lib.UAM_OK
+    assert n.value == 1536 * 2**20 + 256 * ((((128 * 128 + 15) // 16) * 4 + 255) // 256)
+    assert lib.uam_volume_packed_bytes(ctypes.byref(vd), None) == _lib.UAM_E_INVALID
+    bad = _lib.VolumeDesc(0, 1024, 64, 0.0, 20.0, 1.0, 1.0, 0.0, 10.0)
+    assert lib.uam_volume_packed_bytes(ctypes.byref(bad), ctypes.byref(n)) == _lib.UAM_E_INVALID
+
+
 def test_invalid_calls_fail_loudly(lib):
     from uam_path_planning_amd import _lib
 
