@@ -299,9 +299,10 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
  *      the column's terrain and flags beside the layer's pair -- in blocks of 4 x 2 cells of
  *      one layer (one 128-B line), layer-major planes, padded to whole blocks;
  *   2. 8-B voxels {float risk, float terrain} in blocks of 4 x 4 cells of one layer;
- *   3. a 2-bit code per 8 x 8 columns: 3 where a column of the block has psi_nfz != +-0 or the
- *      no-fly flag (its waypoints read section 1), else 1 (section 2: psi is +-0 and no flag
- *      is set there, so the 8-B voxel's consume adds exact no-ops).
+ *   3. a 2-bit code per 8 x 8 columns: 3 where a column of the block has psi_nfz != +-0 in
+ *      any layer or the no-fly flag (its waypoints read section 1), else 1 (section 2: psi is
+ *      +-0 in every layer and no flag is set there, so the 8-B voxel's consume adds exact
+ *      no-ops).
  * uam_volume_pack derives it from a built volume (vol_dev); packed_dev holds
  * uam_volume_packed_bytes bytes (1.5 GiB at 1024^2 x 64), 256-B aligned. */
 int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);

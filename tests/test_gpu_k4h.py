@@ -120,13 +120,24 @@ def test_k4h_chunks(oracle_mod, chunk, floor):
     _check(gpu, ref, oracle_mod, D)
 
 
+def _vary_psi(e, vol):
+    """Layer-varying psi in some columns (a psi of 0.25 at layer 3 only, every 13th row and
+    37th column from 5, inside and outside the no-fly support): their 8 x 8-column blocks
+    must take the 16-B table (code 3) although layer 0's psi is +0 in many of them; the packed
+    copy is rebuilt."""
+    vol.vox[::13, 5::37, 3, 1] = int(np.float32(0.25).view(np.int32))  # (int32 view)
+    torch.cuda.synchronize()
+    e.volume_pack(vol)
+
+
 def test_k4h_pack_layout(oracle_mod):
     """uam_volume_pack against its definition: the 16-B table (voxel (ix, iy, iz) at
     ((iz nby2 + iy/2) nbx4 + ix/4) 8 + (iy%2) 4 + ix%4: {risk, psi} of the voxel, {terrain,
     flags} of the column), the 8-B table ({risk, terrain} at ((iz nby4 + iy/4) nbx4 + ix/4) 16
     + (iy%4) 4 + ix%4), zero padding, and the 2-bit code per 8 x 8 columns (3 where a column
-    has psi != +-0 or the no-fly flag, else 1), 256-B aligned sections."""
+    has psi != +-0 in any layer or the no-fly flag, else 1), 256-B aligned sections."""
     e, orc, vol, vd, host = _case(oracle_mod, 300, 7, 10, 21)
+    _vary_psi(e, vol)
     raw = vol.packed.cpu().numpy()
     ny, nx, nz = 300, 300, 7
     al = lambda v: (v + 255) // 256 * 256
@@ -155,11 +166,36 @@ def test_k4h_pack_layout(oracle_mod):
         mask = np.ones(len(t), bool)
         mask[idx] = False
         assert (t[mask] == 0).all()
-    psi = vox[:, :, 0, 1].view(np.uint32) & 0x7fffffff
+    pb = vox[:, :, :, 1].view(np.uint32)
     nfz = cols[:, :, 1].view(np.uint32) & 1
-    hot = np.zeros((cnby * 8, cnbx * 8), bool)
-    hot[:ny, :nx] = (psi != 0) | (nfz != 0)
-    want = np.where(hot.reshape(cnby, 8, cnbx, 8).any(axis=(1, 3)), 3, 1).reshape(-1)
+    need = np.zeros((cnby * 8, cnbx * 8), bool)
+    need[:ny, :nx] = ((pb & 0x7fffffff) != 0).any(axis=2) | (nfz != 0)
+    layer0 = np.zeros_like(need)
+    layer0[:ny, :nx] = ((pb[:, :, 0] & 0x7fffffff) != 0) | (nfz != 0)
+    blk = lambda a: a.reshape(cnby, 8, cnbx, 8).any(axis=(1, 3)).reshape(-1)
+    want = np.where(blk(need), 3, 1)
     got = ((cm[:, None] >> (2 * np.arange(16))) & 3).reshape(-1)[:cnbx * cnby]
     np.testing.assert_array_equal(got, want)
     assert (want == 3).any() and (want == 1).any()
+    assert (blk(need) & ~blk(layer0)).any()  # blocks that only a later layer's psi marks
+
+
+@pytest.mark.parametrize("group", [21, 7])
+def test_k4h_layer_varying_psi(oracle_mod, group):
+    """A volume whose psi varies by layer in some columns, nonzero at layer 3 only in columns
+    outside the no-fly support: their blocks must read the 16-B table, or the 8-B voxel's
+    implied psi of +0 would drop the layer-3 terms; every output equals orc_eval_generated_h on
+    the same voxels bit for bit."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, group, maxalpha=0.015)
+    _vary_psi(e, vol)
+    host = (vol.vox.cpu().numpy().view(np.float32), vol.cols.cpu().numpy().view(np.float32))
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs3d(2000, 29)
+    ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=group)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack"
+    _check(gpu, ref, oracle_mod, D)

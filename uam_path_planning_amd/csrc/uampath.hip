@@ -6000,8 +6000,9 @@ __global__ __launch_bounds__(256) void k_volume_codes(const uint2* __restrict__ 
         for (int y = by << VPK_CSHIFT; y < min(ny, (by + 1) << VPK_CSHIFT); ++y)
             for (int x = bx << VPK_CSHIFT; x < min(nx, (bx + 1) << VPK_CSHIFT); ++x) {
                 const int64_t c = (int64_t)y * nx + x;
-                const uint32_t psi = vox[c * nz].y;  // the column's psi (every layer's)
-                if ((psi & 0x7fffffffu) || (col[c].y & UAM_FLAG_NFZ)) code = 3u;
+                if (col[c].y & UAM_FLAG_NFZ) code = 3u;
+                for (int iz = 0; iz < nz; ++iz)  // psi of every layer (a voxel's own)
+                    if (vox[c * nz + iz].y & 0x7fffffffu) code = 3u;
             }
         word |= code << (2 * k);
     }
