@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU box, round 4 (final tree): full GPU suite + smoke, bench lines (cfg3, cfg3 --cells, cfg4,
+# GPU box, round 4 (final tree; final2 = after the K4h code-map fix): full GPU suite + smoke, bench lines (cfg3, cfg3 --cells, cfg4,
 # cfg5), cfg3 and cfg3 --cells traces + PMC passes.
 cd "$GRAFT_REPO_ROOT"
-o=r04/final
+o=r04/final2
 mkdir -p gpurun_out/$o
 export TMPDIR=/tmp
 tools/gpu_session.sh \
