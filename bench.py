@@ -308,7 +308,8 @@ def main():
     elif last.startswith("K2h"):
         ktag = last.lower()
         kernel_name = ("K2h sequence (k_g_hist / k_scan / k_g_scatter (+ the unit-arc sums), "
-                       "k_h_eval over every (path, group) item: points, cells, records; "
+                       "k_h_eval over every (path, group) item: points, cells, packed entries "
+                       "and the terrain where its bound could be the path maximum; "
                        "k_h_final: the similarity-form geometry, grouped sums, selection)")
     elif last.startswith("K2g"):
         ktag = last.lower()
@@ -334,8 +335,8 @@ def main():
         roofline = analytic_roofline(prof, P, kern_ms, kernel_name)
     else:
         roofline = gather_roofline(prof, P, W, kern_ms, kernel_name,
-                                   packed=last in ("K2s+pack", "K2g+pack", "K2h+pack",
-                                                   "K2h-tile+pack"),
+                                   packed=last in ("K2s+pack", "K2g+pack", "K2h+pack"),
+                                   kernel_tag=last,
                                    volume=volume_mode,
                                    cells=args.cells and not volume_mode)
     roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "
@@ -440,7 +441,7 @@ def main():
                 wall += time.perf_counter() - ts
                 passes += 1
             seq = None
-            if group and mode == "raster":
+            if group and mode in ("raster", "volume"):
                 # every pair of the batch through the reference's sequential order (threads
                 # over pair shards): how far the grouped sums move the costs and whether they
                 # move either selection
@@ -493,7 +494,8 @@ def main():
         dist.destroy_process_group()
 
 
-def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False, cells=False):
+def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False, cells=False,
+                    kernel_tag=""):
     """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
     definition used in SURVEY, DESIGN §4 and here): raster, one 16-B record gather per waypoint
     + 16 B of outputs per path = 16 W + 16 B/path; volume, one 8-B voxel {risk, psi_nfz} + a
@@ -524,21 +526,39 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
          "l2_hit_rate": prof.get("l2_hit_rate"),
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
-         "record_source": ("8-B voxels {risk, psi_nfz} + the 8-B column plane {terrain, "
-                           "flags} (uam_volume_shape): 16 B requested per waypoint, 12 B of "
-                           "them information (the flags word carries the no-fly bit)" if volume
-                           else "packed (uam_raster_pack): 8-B {phi, terrain} entries outside "
-                           "the no-fly blocks, 16-B records inside them; the algorithmic bytes "
+         "record_source": ("packed volume (uam_volume_pack): 8-B {risk, terrain} voxels "
+                           "outside the no-fly columns, 16-B voxels inside them" if volume
+                           else "packed (uam_raster_pack): 4-B phi entries (32 cells per line) "
+                           "and 8-B {phi, psi|nfz} entries (16 per line) by block code, 16-B "
+                           "records where a psi is negative, the 4-B terrain plane where a "
+                           "waypoint's bound could be the path maximum; the algorithmic bytes "
                            "keep SURVEY's 16 B per waypoint, the information each waypoint "
                            "consumes" if packed else "16-B records"),
-         "note": "each gathered entry costs one 128-B line request: an L2 hit or a line "
-                 "from the Infinity Cache / HBM (PMC); the measured random-gather ceiling "
-                 "(tools/gather_ceiling.hip) bounds a kernel gathering in random order (K2); "
-                 "the tile-sorted forms (K2g, K2s) pass it through L2 reuse (l2_hit_rate). "
-                 "K2g at cfg3: 13.5M of its ~49M L2 requests per step miss and come from the "
-                 "Infinity Cache / HBM at <= 55-59 G lines/s; its evaluation launch is ~283 us "
-                 "of the ~0.34 ms step (profiles/r03/k2g_v9), DESIGN.md §4-5"}
+         "note": roofline_note(kernel_tag, prof, P, W)}
     return r
+
+
+def roofline_note(kernel, prof, P, W):
+    """What bounds the kernel that ran, from this build's own PMC key when there is one."""
+    miss = prof.get("tcc_miss")
+    hits = prof.get("tcc_hit")
+    tail = ""
+    if miss and hits:
+        tail = (f" This build's PMC (profiles/traffic.json, {prof.get('source')}): "
+                f"{(miss + hits) / 1e6:.1f}M L2 requests per step for {P * W / 1e6:.1f}M "
+                f"waypoints, {miss / 1e6:.2f}M of them misses.")
+    if kernel.startswith("K2h"):
+        return ("K2h: one 128-B line request per waypoint's packed entry (none in code-0 "
+                "blocks) plus one per terrain fetch (only where the waypoint's bound could "
+                "still be the path maximum); hits come from L2, misses from the Infinity "
+                "Cache / HBM at <= 55-59 G lines/s (tools/gather_ceiling.hip); DESIGN.md §4-5."
+                + tail)
+    if kernel.startswith("K4h"):
+        return ("K4h: one 128-B line request per waypoint's packed voxel; misses from the "
+                "Infinity Cache / HBM at <= 55-59 G lines/s; DESIGN.md §4-5." + tail)
+    return ("each gathered entry costs one 128-B line request: an L2 hit or a line from the "
+            "Infinity Cache / HBM; the measured random-gather ceiling (tools/gather_ceiling.hip) "
+            "bounds a kernel gathering in random order (K2); DESIGN.md §4-5." + tail)
 
 
 def analytic_roofline(prof, P, kern_ms, kernel_name):
@@ -585,7 +605,7 @@ def oracle_eval(O, orc, pairs, ut_host, mode, rd, rec, vd, vox, group=0, want_ce
             return orc.eval_generated_h(pairs, ut_host, mode="volume", vdesc=vd, vol=vox,
                                         group=group)
         return orc.eval_paths3d(O.gen_paths3d(pairs, ut_host), vd, vox)
-    if kernel == "K2h+pack":
+    if kernel and kernel.startswith("K2h"):
         return orc.eval_generated_h(pairs, ut_host, rdesc=rd, rec=rec, group=group,
                                     want_cells=want_cells)
     return orc.eval_paths(O.gen_paths(pairs, ut_host), mode=mode, rdesc=rd, rec=rec,
@@ -597,7 +617,7 @@ def order_name(group, kernel=None):
         return (f"volume sums as per-path partial sums over groups of {group} waypoints, added "
                 f"in group order; the geometry terms in the similarity form (oracle "
                 f"orc_eval_generated_h, volume mode)")
-    if kernel == "K2h+pack":
+    if kernel and kernel.startswith("K2h"):
         return (f"raster sums as per-path partial sums over groups of {group} waypoints, added "
                 f"in group order; the geometry terms in the similarity form (oracle "
                 f"orc_eval_generated_h)")

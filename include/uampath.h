@@ -222,9 +222,15 @@ int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* rec_dev, const double* wp_dev, int64_t n_paths,
                        const uam_path_outputs* out, uam_stream stream);
 
-/* K2/K3 with the candidate generator fused: path p = q*D + d. */
+/* K2/K3 with the candidate generator fused: path p = q*D + d.  Raster mode takes two optional
+ * derived copies of rec, both built with the same block (uam_raster_summary /
+ * uam_raster_pack, below; NULL = none; ignored in analytic mode): summary_dev, the gather-skip
+ * bitmap the lane- and wave-per-path forms read, and packed_dev, the packed raster the sorted
+ * forms read (K2h by default; without it the sorted batches run K2s on rec).  Every choice
+ * gives the same outputs (uam_last_group names the sum order). */
 int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
-                       const void* rec_dev, const double* pairs_dev, int64_t n_pairs,
+                       const void* rec_dev, const uint32_t* summary_dev, int32_t block,
+                       const void* packed_dev, const double* pairs_dev, int64_t n_pairs,
                        const double* utab_dev, int32_t D, const uam_path_outputs* out,
                        uam_stream stream);
 
@@ -241,32 +247,30 @@ int uam_raster_summary_shape(const uam_raster_desc* desc, int32_t block, int32_t
                              int32_t* nbx, int32_t* nby);
 int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
                        int32_t block, uint32_t* summary_dev, uam_stream stream);
-/* uam_eval_generated in raster mode with the gather skip (summary_dev NULL = no skip). */
-int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
-                         const uint32_t* summary_dev, int32_t block, const double* pairs_dev,
-                         int64_t n_pairs, const double* utab_dev, int32_t D,
-                         const uam_path_outputs* out, uam_stream stream);
-
-/* K2s packed raster (build-defined; no reference counterpart; results unchanged).  A derived
- * copy of rec for the segment-sorted evaluation: a 2-bit code per summary block (0 = nothing
- * to gather, the gather-skip rule above; 1 = phi/terrain only, every cell has psi_nfz == +-0
- * and no no-fly flag; 3 = the full 16-B record, read from rec) followed by one 8-B plane
- * {phi, terrain read as the evaluation reads it} in blocks of 4 x 4 cells (one 128-B line).
- * uam_raster_pack_shape gives the bytes of the caller's buffer (256-B aligned; 8 B per cell
- * plus the codes, padded to whole blocks); block as uam_raster_summary (0 = automatic), and the
- * same block must be passed to uam_eval_generated_p.  Rebuild the copy whenever rec changes.
- * uam_eval_generated_p = uam_eval_generated_s whose K2s launches gather from packed_dev
- * (NULL = from rec); the other kernels still read rec and summary_dev.  Replaces the same
- * reference call as uam_eval_generated (problem.py:38-44 per candidate, main.py:158-196). */
+/* Packed raster (build-defined; no reference counterpart; results unchanged).  A derived copy
+ * of rec for the sorted evaluations (K2h / K2g / K2s), 256-B aligned sections:
+ *   header  the 2-bit code per summary block (16 per 32-bit word): 0 = every cell has
+ *           phi == +-0, psi_nfz == +-0 and no no-fly flag (nothing to read but the terrain);
+ *           1 = psi_nfz == +-0 and no flag (phi from the 4-B plane); 2 = no psi_nfz below
+ *           zero (phi, |psi_nfz| and the flag from the 8-B plane); 3 = the 16-B record from rec;
+ *           then the terrain bounds: one u16 {ub code, lb code << 8} per bound block (the
+ *           smallest power-of-two square of >= 8 cells giving <= 16384 blocks), and one float2
+ *           {base, step} per superblock of 4 x 4 bound blocks; a bound decodes as
+ *           base + (float)code * step (f32, step a power of two) and holds every cell's terrain
+ *           as read (+0 on nodata); {NaN, NaN} where the superblock holds a non-finite terrain;
+ *   scratch the bound blocks' {min, max} (float2 each) while packing;
+ *   planes  phi (4 B) and the terrain as read (4 B) in 4 x 8-cell blocks (one 128-B line),
+ *           {phi, |psi_nfz| | nfz << 31} (8 B) in 4 x 4-cell blocks.
+ * K2h reads a waypoint's terrain only where its bound could still be the path's maximum (the
+ * maximum is order-free, so min_clearance is unchanged bit for bit); K2g and K2s read it for
+ * every waypoint.  uam_raster_pack_shape gives the bytes of the caller's buffer (4096^2:
+ * 56 KiB of header + 128 KiB of scratch + 256 MiB of planes); block as uam_raster_summary
+ * (0 = automatic), and the same block must be passed to uam_eval_generated.  Rebuild the copy
+ * whenever rec changes. */
 int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
                           int64_t* bytes);
 int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
                     int32_t block, void* packed_dev, uam_stream stream);
-int uam_eval_generated_p(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
-                         const uint32_t* summary_dev, int32_t block, const void* packed_dev,
-                         const double* pairs_dev, int64_t n_pairs, const double* utab_dev,
-                         int32_t D, const uam_path_outputs* out, uam_stream stream);
-
 /* K5: per group of G consecutive values, the reference's selection rule (main.py:175-180):
  * compare sqrt(v) when take_sqrt (fval = sqrt(cost), solver.py:48), else v. */
 int uam_argmin(uam_ctx* ctx, const double* values_dev, int64_t groups, int32_t G,
@@ -290,10 +294,16 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* desc, const void* rec2
 /* Config 5 path evaluation: pairs6_dev [Q][6] = (x0, y0, z0, xf, yf, zf) (km, km, m); x/y
  * candidates as uam_eval_generated, altitude z_j = z0 + (zf - z0) * (j / (N+1)); cost =
  * (N+1) L + sum_j risk(voxel_j) / N; min_clearance = min_j (z_j - terrain of the column);
- * below_terrain counts waypoints whose layer centre z0 + (iz + 0.5) dz lies below it.  D <= 16. */
+ * below_terrain counts waypoints whose layer centre z0 + (iz + 0.5) dz lies below it.  D <= 16.
+ * packed_dev (uam_volume_pack, below; NULL = none): batches of >= UAM_OPT_SORTED_MIN_PATHS
+ * paths (maxratio_smooth off, no cells) run K4h on it -- the (path, group) items sorted on the
+ * altitude band and x/y tile of their middle waypoint, grouped partial sums (UAM_OPT_GROUP),
+ * the geometry terms in the similarity form (oracle orc_eval_generated_h mode 2;
+ * uam_last_kernel "K4h+pack"); every other batch runs on vol_dev. */
 int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
-                         const double* pairs6_dev, int64_t n_pairs, const double* utab_dev,
-                         int32_t D, const uam_path_outputs* out, uam_stream stream);
+                         const void* packed_dev, const double* pairs6_dev, int64_t n_pairs,
+                         const double* utab_dev, int32_t D, const uam_path_outputs* out,
+                         uam_stream stream);
 /* The packed volume (K4h), three 256-B aligned sections, so a waypoint is one request:
  *   1. 16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} per (ix, iy, iz) --
  *      the column's terrain and flags beside the layer's pair -- in blocks of 4 x 2 cells of
@@ -308,16 +318,6 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
 int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);
 int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                     void* packed_dev, uam_stream stream);
-/* uam_eval_generated3d with the packed copy: batches of >= UAM_OPT_SORTED_MIN_PATHS paths
- * (maxratio_smooth off, no cells) run K4h -- the (path, group) items sorted on the altitude
- * band and x/y tile of their middle waypoint, grouped partial sums (UAM_OPT_GROUP), the
- * geometry terms in the similarity form (oracle orc_eval_generated_h mode 2; uam_last_kernel
- * "K4h+pack"); every other batch runs uam_eval_generated3d on vol_dev.  packed_dev NULL: the
- * same as uam_eval_generated3d. */
-int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
-                           const void* packed_dev, const double* pairs6_dev, int64_t n_pairs,
-                           const double* utab_dev, int32_t D, const uam_path_outputs* out,
-                           uam_stream stream);
 
 /* ---- Raster broadcast over RCCL / xGMI (the reference has no
  * collective at all -- its only IPC is the solver's TCP socket, path_generation/solver.py:26-38).
@@ -461,12 +461,12 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                (default) = tiles of ~256 x 256 cells
  *   UAM_OPT_K2G_LDS_FLOOR        K2g / K2h / K4h evaluation: dynamic-LDS floor per workgroup in
  *                                bytes, which caps the workgroups resident per CU; 0 (default):
- *                                none for K2g and K2h, 54 000 (3 per CU) for K2h over rasters of
- *                                more than 2^25 cells, 60 000 (2 per CU) for K4h
+ *                                none for K2g and K2h (512-item workgroups, 2 per CU by their
+ *                                ~62 KiB of tables), 60 000 (2 per CU) for K4h
  *   UAM_OPT_K2G_CHUNK            K2g / K2h / K4h evaluation: gathers in flight per lane,
- *                                6/7/8/11/16 (K2g: 7 runs as 6, 16 at two waves per SIMD; K4h:
- *                                6/7/8/11); 0 (default) = 8 for K2g, 7 for K2h, 11 for K2h over
- *                                rasters of more than 2^25 cells and for K4h
+ *                                6/7/8/11/16/21 (K2g: 7 runs as 6, 16 at two waves per SIMD, 21
+ *                                as 16; K2h: 6/7/8/11, 16 and 21 as 11; K4h: 6/7/8/11/16/21);
+ *                                0 (default) = 8 for K2g, 7 for K2h, 11 for K4h
  *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order
  *   UAM_OPT_K2G_SIM              1 (default): generated raster batches take K2h, K2g's sort and
  *                                grouped raster sums with the geometry terms (L, length,
@@ -474,19 +474,14 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                scaled by |x0 - xf| / 2 (oracle orc_eval_generated_h; needs
  *                                maxratio_smooth = 0); 0: K2g, the geometry per waypoint
  *                                segment in the grouped order (orc_eval_paths_g)
- *   UAM_OPT_K2G_LDS_WINDOW       K2h experiment (not faster): 0 (default), or
- *                                96 / 128: 1024-item workgroups that stage a window of that
- *                                many cells square of the packed plane in LDS and serve the
- *                                code-1 waypoints inside it from there.  Same outputs.
  *   UAM_OPT_K4H_BAND             K4h sort key: altitude layers per band, a power of two
  *                                (default 0: the fewest giving at most 16 bands); tiles from
  *                                UAM_OPT_K2G_TILE_BITS (default 3: 8 x 8 tiles), at most
  *                                4096 (tile, band) bins
- *   UAM_OPT_K2G_TILE_OWNER       K2h tile form (measured): 0 (default), or
- *                                T = 64 / 128: sort tiles of T x T cells, one workgroup per tile
- *                                that stages the tile's packed plane in LDS once and evaluates
- *                                all of the tile's items, reading their code-1 waypoints inside
- *                                the tile from LDS ("K2h-tile+pack").  Same outputs. */
+ *   UAM_OPT_K2H_LB_STRIDE        K2h terrain bounds: every item takes the maximum lower bound
+ *                                over every n-th waypoint of its path as the path's lower bound
+ *                                (1..1024; default 8); fewer terrain fetches at smaller n, more
+ *                                arithmetic per item.  Same outputs. */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -503,9 +498,8 @@ enum {
     UAM_OPT_K2G_CHUNK = 13,
     UAM_OPT_K2G_CURVE = 14,
     UAM_OPT_K2G_SIM = 15,
-    UAM_OPT_K2G_LDS_WINDOW = 16,
     UAM_OPT_K4H_BAND = 17,
-    UAM_OPT_K2G_TILE_OWNER = 18
+    UAM_OPT_K2H_LB_STRIDE = 19
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

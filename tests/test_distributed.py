@@ -72,6 +72,27 @@ def _worker(rank, world, port, q):
         rb = _Rebuild()
         D.broadcast_raster(cr, src=0, rebuild=rb)
         res["rebuilt"] = (rb.calls, cr.summary, cr.packed)
+
+        # a RiskVolume's packed copy (K4h) is likewise stale after its buffer's broadcast
+        from uam_path_planning_amd.engine import RiskVolume
+
+        def stale_volume(seed):
+            g = torch.Generator().manual_seed(seed)
+            b = torch.randint(-2**31, 2**31 - 1, (4096,), dtype=torch.int32, generator=g)
+            return RiskVolume(geo=None, buf=b, vox=None, cols=None,
+                              packed=torch.full((16,), 5 + rank))
+
+        vol = stale_volume(7 if rank == 0 else 8)
+        D.broadcast_raster(vol, src=0)
+        res["vol_dropped"] = (vol.packed is None, int(vol.buf.to(torch.int64).sum()))
+
+        class _Repack:
+            def volume_pack(self, v):
+                v.packed = int(v.buf.to(torch.int64).sum())
+
+        vol = stale_volume(7 if rank == 0 else 8)
+        D.broadcast_raster(vol, src=0, rebuild=_Repack())
+        res["vol_rebuilt"] = (vol.packed, int(vol.buf.to(torch.int64).sum()))
         res["max"] = D.max_over_ranks([float(rank), 10.0 - rank])
 
         # the RCCL communicator setup of uam_comm_init: rank 0 draws the id, every rank joins
@@ -122,6 +143,9 @@ def test_gloo_world2():
     ck = out[0]["dropped"][2]
     assert out[0]["dropped"] == out[1]["dropped"] == (True, True, ck)
     assert out[0]["rebuilt"] == out[1]["rebuilt"] == ([(8, True)], ck, ck)
+    vk = out[0]["vol_dropped"][1]
+    assert out[0]["vol_dropped"] == out[1]["vol_dropped"] == (True, vk)
+    assert out[0]["vol_rebuilt"] == out[1]["vol_rebuilt"] == (vk, vk)
     assert out[0]["max"] == out[1]["max"] == [1.0, 10.0]
     assert out[0]["comm"] == (True, 2, 0) and out[1]["comm"] == (True, 2, 1)
     assert out[0]["best"] == out[1]["best"] == (0.5, 57)

@@ -9,8 +9,9 @@ within rounding (north_star: 1e-5; here 1e-12).
 Exercised: groups 1-64 (ragged last groups), D = 1-16, N = 1 and 80, canonical and all-zero
 weights over a below-sea-level DEM with NaN cells, NaN pairs and a pair with start == goal
 (h = 0), paths that leave the raster, a raster over part of the map, waypoint cells, chunk
-lengths 6/7/8/11/16, two streams sharing one context, the fallback to K2g under
-maxratio_smooth.  Reference rules: problem.py:38-44 (cost), 84-114 (rows), 130-146 (length_of),
+lengths 6/7/8/11, two streams sharing one context, the fallback to K2g under
+maxratio_smooth; the packed copy against its definition and the terrain-bound rule's sample
+strides over DEMs with non-finite, flat and -0.0 terrain.  Reference rules: problem.py:38-44 (cost), 84-114 (rows), 130-146 (length_of),
 solver.py:103-136 (the arcs), main.py:175-180 (selection)."""
 import numpy as np
 import pytest
@@ -26,7 +27,7 @@ ORDER_FREE = ("nfz_hits", "offmap", "min_clearance")
 
 
 def _case(oracle_mod, group, N, weights="canonical", R=1024, nfz=16, geo=None, maxalpha=None,
-          maxratio_smooth=False):
+          maxratio_smooth=False, obstacle_smooth=None, dem_edit=None):
     from uam_path_planning_amd import build
     from uam_path_planning_amd.engine import Engine, PathParams
     from uam_path_planning_amd.geometry import compile_map
@@ -44,6 +45,8 @@ def _case(oracle_mod, group, N, weights="canonical", R=1024, nfz=16, geo=None, m
     w = spec["weights"] if weights == "canonical" else [0.0] * len(spec["weights"])
     opts = dict(spec["options"])
     opts["maxratio_smooth"] = maxratio_smooth
+    if obstacle_smooth is not None:
+        opts["obstacle_smooth"] = obstacle_smooth
     ma = spec["maxalpha"] if maxalpha is None else maxalpha
     e.set_geometry(compile_map(build_region_map(spec)))
     e.set_params(PathParams(N=N, **opts, maxratio=spec["maxratio"], maxalpha=ma,
@@ -55,6 +58,13 @@ def _case(oracle_mod, group, N, weights="canonical", R=1024, nfz=16, geo=None, m
     if weights == "zero":
         dem = np.where(dem == -9999.0, dem, -np.abs(dem) - 1.0).astype(np.float32)
         dem[::97, ::89] = np.float32(np.nan)
+    if dem_edit == "nonfinite":   # unbounded superblocks
+        dem[100:104, 300:302] = np.float32(np.inf)
+        dem[::211, ::157] = np.float32(np.nan)
+    elif dem_edit == "flat":      # a few values: many blocks of one value
+        dem = np.where(dem == -9999.0, dem, np.round(dem / 200.0) * 200.0).astype(np.float32)
+    elif dem_edit == "negzero":
+        dem = np.where(np.abs(dem) < 40.0, np.float32(-0.0), dem).astype(np.float32)
     raster = e.raster_build(geo, dem, summary=False)
     e.raster_summary(raster, 0, packed=True)
     rd = oracle_mod.Oracle.raster_desc(geo.nx, geo.ny, geo.x0, geo.y_top, geo.dx, geo.dy,
@@ -193,43 +203,132 @@ def test_k2h_partial_raster(oracle_mod):
     _check(gpu, ref, oracle_mod, D)
 
 
-@pytest.mark.parametrize("tile,group,R,geo_kind", [(128, 21, 1024, "square"),
-                                                  (64, 21, 1024, "square"),
-                                                  (128, 7, 4096, "square"),
-                                                  (64, 30, 1024, "partial"),
-                                                  (128, 1, 1024, "partial")])
-def test_k2h_tile_form(oracle_mod, tile, group, R, geo_kind):
-    """The tile form (UAM_OPT_K2G_TILE_OWNER: one workgroup per T x T tile, its packed plane in
-    LDS) changes where code-1 waypoints inside the tile are read, nothing else: every output
-    equals orc_eval_generated_h bit for bit, with pairs off the raster (the off-raster bin's
-    workgroup), NaN pairs, start == goal, a raster that is not a multiple of the tile (edge
-    tiles zero-filled past the raster) and tiles without items."""
-    from uam_path_planning_amd.arcs import arc_table
+def _pack_dims(nx, ny, block):
+    """The packed raster's sections (uampath.hip PackDims / uam_raster_pack_shape)."""
+    nbx, nby = -(-nx // block), -(-ny // block)
+    words = (nbx * nby * 2 + 31) // 32
+    bsh = 3
+    while (-(-nx // (1 << bsh))) * (-(-ny // (1 << bsh))) > 16384:
+        bsh += 1
+    bnbx, bnby = -(-nx // (1 << bsh)), -(-ny // (1 << bsh))
+    w16 = lambda v: -(-v // 16) * 4
+    bnd_off = w16(words * 4)
+    sbt_off = bnd_off + w16(bnbx * bnby * 2)
+    sbnbx, sbnby = -(-bnbx // 4), -(-bnby // 4)
+    hwords = sbt_off + w16(sbnbx * sbnby * 8)
+    a256 = lambda v: -(-v // 256) * 256
+    nb8, nb4, lnby = -(-nx // 8), -(-nx // 4), -(-ny // 4)
+    off_p4 = a256(hwords * 4) + a256(bnbx * bnby * 8)
+    off_t4 = off_p4 + a256(lnby * nb8 * 32 * 4)
+    off_e8 = off_t4 + a256(lnby * nb8 * 32 * 4)
+    return dict(words=words, bsh=bsh, bnbx=bnbx, bnby=bnby, bnd_off=bnd_off, sbt_off=sbt_off,
+                sbnbx=sbnbx, sbnby=sbnby, hwords=hwords, nb8=nb8, nb4=nb4, off_p4=off_p4,
+                off_t4=off_t4, off_e8=off_e8)
+
+
+def _check_pack(raster, rec):
+    """uam_raster_pack against its definition (uampath.hip, packed raster): the block codes,
+    the three planes bit for bit, and bounds that hold every cell's terrain."""
+    ny, nx = rec.shape[:2]
+    B = raster.block
+    d = _pack_dims(nx, ny, B)
+    raw = raster.packed.cpu().numpy().view(np.uint8)
+    bits = rec.view(np.uint32)
+    phi, psi, fl = bits[..., 0], bits[..., 1], bits[..., 3]
+    ter = np.where(fl & 4, np.float32(0.0), rec[..., 2]).astype(np.float32)
+    # codes
+    nbx, nby = -(-nx // B), -(-ny // B)
+    cw = raw[:d["words"] * 4].view(np.uint32)
+    for by in range(nby):
+        for bx in range(nbx):
+            sl = (slice(by * B, (by + 1) * B), slice(bx * B, (bx + 1) * B))
+            need = ((psi[sl] & 0x7fffffff) != 0).any() or ((fl[sl] & 1) != 0).any()
+            neg = (((psi[sl] >> 31) != 0) & (psi[sl] != 0x80000000)).any()
+            nz = ((phi[sl] & 0x7fffffff) != 0).any()
+            want = (3 if neg else 2) if need else (1 if nz else 0)
+            b = by * nbx + bx
+            assert (cw[b >> 4] >> ((b & 15) * 2)) & 3 == want, (bx, by)
+    # planes
+    iy, ix = np.mgrid[0:ny, 0:nx]
+    a4 = (((iy >> 2) * d["nb8"] + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7)
+    a8 = (((iy >> 2) * d["nb4"] + (ix >> 2)) << 4) | ((iy & 3) << 2) | (ix & 3)
+    p4 = raw[d["off_p4"]:d["off_t4"]].view(np.uint32)
+    t4 = raw[d["off_t4"]:d["off_e8"]].view(np.float32)
+    e8 = raw[d["off_e8"]:].view(np.uint32).reshape(-1, 2)
+    np.testing.assert_array_equal(p4[a4], phi)
+    np.testing.assert_array_equal(t4[a4].view(np.uint32), ter.view(np.uint32))
+    np.testing.assert_array_equal(e8[a8, 0], phi)
+    np.testing.assert_array_equal(e8[a8, 1], (psi & 0x7fffffff) | ((fl & 1) << 31).astype(np.uint32))
+    # bounds: decoded as the kernels decode them (f32: base + q * step)
+    bnd = raw[d["bnd_off"] * 4:].view(np.uint16)[:d["bnbx"] * d["bnby"]]
+    sbt = raw[d["sbt_off"] * 4:].view(np.float32)[:2 * d["sbnbx"] * d["sbnby"]].reshape(-1, 2)
+    bx, by = ix >> d["bsh"], iy >> d["bsh"]
+    e = bnd[by * d["bnbx"] + bx].astype(np.uint32)
+    sb = sbt[(by >> 2) * d["sbnbx"] + (bx >> 2)]
+    with np.errstate(invalid="ignore"):
+        ub = sb[..., 0] + (e & 255).astype(np.float32) * sb[..., 1]
+        lb = sb[..., 0] + (e >> 8).astype(np.float32) * sb[..., 1]
+    assert ub.dtype == np.float32
+    # a superblock is unbounded (NaN) exactly where it holds a non-finite terrain value
+    bad = ~np.isfinite(ter)
+    sbi = (by >> 2) * d["sbnbx"] + (bx >> 2)
+    bad_sb = np.zeros(d["sbnbx"] * d["sbnby"], bool)
+    np.logical_or.at(bad_sb, sbi.ravel(), bad.ravel())
+    np.testing.assert_array_equal(np.isnan(sb[..., 0]), bad_sb[sbi])
+    ok = ~bad_sb[sbi]
+    assert (lb[ok] <= ter[ok]).all() and (ter[ok] <= ub[ok]).all()
+    return ok.mean(), np.mean((ub - lb)[ok])
+
+
+@pytest.mark.parametrize("R,block", [(1024, 0), (1024, 4), (1000, 8)])
+def test_raster_pack_layout(oracle_mod, R, block):
+    """The packed copy (uam_raster_pack) equals its definition; with a DEM holding NaN and
+    +inf cells and obstacle_smooth off (negative psi: code-3 blocks) as well."""
     from uam_path_planning_amd.engine import RasterGeo
-    from uam_path_planning_amd.scenario import displacements
 
     geo = None
-    if geo_kind == "partial":
+    if R == 1000:
         geo = RasterGeo(nx=1000, ny=700, x0=8.0, y_top=5.0, dx=40.0 / 1000, dy=40.0 / 1000,
                         nodata=-9999.0, dem_threshold=0.0)
-    e, orc, raster, rd, rec = _case(oracle_mod, group, 80, R=R, nfz=64, geo=geo,
-                                    maxalpha=0.015)
-    e.set_option("k2g_tile_owner", tile)
-    assert e.get_option("k2g_tile_owner") == tile
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 40, R=R, geo=geo)
+    if block:
+        e.raster_summary(raster, block, packed=True)
+    frac, width = _check_pack(raster, rec)
+    assert frac == 1.0 and width < 60.0
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 40, weights="zero", R=R, geo=geo,
+                                    obstacle_smooth=False, dem_edit="nonfinite")
+    if block:
+        e.raster_summary(raster, block, packed=True)
+    codes = _check_pack(raster, rec)
+    assert 0.0 < codes[0] < 1.0
+
+
+@pytest.mark.parametrize("dem_edit", [None, "nonfinite", "flat", "negzero"])
+@pytest.mark.parametrize("stride", [1, 5, 8, 1024])
+def test_k2h_terrain_bounds(oracle_mod, stride, dem_edit):
+    """The terrain maximum through the bounds (h_item): only where a waypoint's bound could
+    still be the path's maximum is its terrain fetched; min_clearance (and every other output)
+    equals orc_eval_generated_h bit for bit for every sample stride of the path lower bound
+    (1: every waypoint; 1024: p_0 only), with unbounded superblocks (NaN / +inf cells), a
+    terrain of a few values (blocks whose bounds coincide), -0.0 terrain cells, and no-fly
+    psi below zero (obstacle_smooth off: code-3 records carry the terrain)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 80, R=1024, nfz=64, maxalpha=0.015,
+                                    dem_edit=dem_edit, obstacle_smooth=dem_edit != "flat")
+    e.set_option("k2h_lb_stride", stride)
+    assert e.get_option("k2h_lb_stride") == stride
     D = 5
     ut = arc_table(80, displacements(D))
-    pairs = _pairs(3000, 41)
-    ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=group)
+    pairs = _pairs(3000, 43)
+    ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=21)
     gpu = e.eval_generated(pairs, ut, raster=raster)
-    assert e.last_kernel() == "K2h-tile+pack" and e.last_group() == group
-    _check(gpu, ref, oracle_mod, D)
-    # with cells requested the launch is the cell-writing K2h, the same bits
-    cells = e.eval_generated(pairs, ut, raster=raster, want_cells=True)
     assert e.last_kernel() == "K2h+pack"
-    _check(cells, ref, oracle_mod, D)
-    for bad in (1, 32, 256):
+    _check(gpu, ref, oracle_mod, D)
+    for bad in (0, -3, 1025):
         with pytest.raises(ValueError):
-            e.set_option("k2g_tile_owner", bad)
+            e.set_option("k2h_lb_stride", bad)
 
 
 @pytest.mark.parametrize("group", [21, 5, 64])

@@ -120,6 +120,27 @@ def test_k4h_chunks(oracle_mod, chunk, floor):
     _check(gpu, ref, oracle_mod, D)
 
 
+@pytest.mark.parametrize("tile_bits,band", [(5, 0), (6, 0), (4, 2), (3, 16), (3, 1)])
+def test_k4h_tile_bits_and_bands(oracle_mod, tile_bits, band):
+    """The sort key's tiles (UAM_OPT_K2G_TILE_BITS, a raster setting: 5 and 6 give more
+    (tile, band) bins than the sort holds at 64 layers, so the key takes the finest tiles that
+    fit) and altitude bands (UAM_OPT_K4H_BAND: 1, 2, 16 layers) only move work."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, 256, 64, 80, 21, maxalpha=0.015)
+    e.set_option("k2g_tile_bits", tile_bits)
+    e.set_option("k4h_band", band)
+    assert e.get_option("k4h_band") == band
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs3d(2000, 29)
+    ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=21)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack"
+    _check(gpu, ref, oracle_mod, D)
+
+
 def _vary_psi(e, vol):
     """Layer-varying psi in some columns (a psi of 0.25 at layer 3 only, every 13th row and
     37th column from 5, inside and outside the no-fly support): their 8 x 8-column blocks

@@ -80,10 +80,25 @@ def test_invalid_calls_fail_loudly(lib):
     nbytes = ctypes.c_int64()
     assert lib.uam_raster_pack_shape(ctypes.byref(rd), 0, ctypes.byref(b),
                                      ctypes.byref(nbytes)) == _lib.UAM_OK
-    # 2-bit codes of 65536 blocks (16 KiB), then one 8-B plane of 4096^2 cells
-    assert (b.value, nbytes.value) == (16, 16384 + 8 * 4096 * 4096)
+    # header: 2-bit codes of 65536 blocks (16 KiB), 128^2 bound blocks of 32^2 cells (u16,
+    # 32 KiB), 32^2 superblocks (float2, 8 KiB); the bound scratch (float2 per bound block);
+    # the 4-B phi and terrain planes and the 8-B {phi, psi | nfz} plane of 4096^2 cells
+    assert (b.value, nbytes.value) == (16, 16384 + 32768 + 8192 + 8 * 16384 +
+                                       (4 + 4 + 8) * 4096 * 4096)
+    # a raster that is no multiple of the blocks: every section padded to whole blocks
+    rd2 = _lib.RasterDesc(1000, 700, 0.0, 20.0, 0.05, 0.05, -9999.0, 0.0)
+    assert lib.uam_raster_pack_shape(ctypes.byref(rd2), 4, ctypes.byref(b),
+                                     ctypes.byref(nbytes)) == _lib.UAM_OK
+    words = (250 * 175 * 2 + 31) // 32                 # 4-cell code blocks
+    nbb = 125 * 88                                     # 8-cell bound blocks (11000 <= 16384)
+    hdr = -(-words * 4 // 16) * 16 + -(-nbb * 2 // 16) * 16 + 32 * 22 * 8
+    a256 = lambda v: -(-v // 256) * 256
+    planes = 2 * a256(175 * 125 * 32 * 4) + a256(175 * 250 * 16 * 8)
+    assert (b.value, nbytes.value) == (4, a256(hdr) + a256(nbb * 8) + planes)
     assert lib.uam_raster_pack(None, None, None, 0, None, None) == _lib.UAM_E_INVALID
-    assert lib.uam_eval_generated_p(None, None, None, None, 0, None, None, 0, None, 5, None,
+    assert lib.uam_eval_generated(None, 1, None, None, None, 0, None, None, 0, None, 5, None,
+                                  None) == _lib.UAM_E_INVALID
+    assert lib.uam_eval_generated3d(None, None, None, None, None, 0, None, 5, None,
                                     None) == _lib.UAM_E_INVALID
 
 

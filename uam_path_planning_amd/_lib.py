@@ -22,8 +22,8 @@ UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -
 OPTIONS = {"group": 1, "sorted_min_paths": 2, "k2s_segments": 3, "wave_max_paths": 4,
            "pair_order": 5, "k1_rows": 6, "k3b_segment": 7, "k3b_points_per_lane": 8,
            "k8_tiled": 9, "k8_streams": 10, "k2g_tile_bits": 11, "k2g_lds_floor": 12,
-           "k2g_chunk": 13, "k2g_curve": 14, "k2g_sim": 15, "k2g_lds_window": 16, "k4h_band": 17,
-           "k2g_tile_owner": 18}
+           "k2g_chunk": 13, "k2g_curve": 14, "k2g_sim": 15, "k4h_band": 17,
+           "k2h_lb_stride": 19}
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
 MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
 FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4
@@ -115,22 +115,16 @@ SIGNATURES = {
     "uam_eval_waypoints": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(RasterDesc), _vp,
                                           _vp, ctypes.c_int64, ctypes.POINTER(PathOutputs), _vp]),
     "uam_eval_generated": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(RasterDesc), _vp,
-                                          _vp, ctypes.c_int64, _vp, ctypes.c_int32,
-                                          ctypes.POINTER(PathOutputs), _vp]),
+                                          _vp, ctypes.c_int32, _vp, _vp, ctypes.c_int64, _vp,
+                                          ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
     "uam_raster_summary_shape": (ctypes.c_int, [ctypes.POINTER(RasterDesc), ctypes.c_int32,
                                                 _i32p, _i32p, _i32p]),
     "uam_raster_summary": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, ctypes.c_int32,
                                           _vp, _vp]),
-    "uam_eval_generated_s": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp,
-                                            ctypes.c_int32, _vp, ctypes.c_int64, _vp,
-                                            ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
     "uam_raster_pack_shape": (ctypes.c_int, [ctypes.POINTER(RasterDesc), ctypes.c_int32,
                                              _i32p, ctypes.POINTER(ctypes.c_int64)]),
     "uam_raster_pack": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, ctypes.c_int32,
                                        _vp, _vp]),
-    "uam_eval_generated_p": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp,
-                                            ctypes.c_int32, _vp, _vp, ctypes.c_int64, _vp,
-                                            ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
     "uam_argmin": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp,
                                   _vp]),
     "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
@@ -150,15 +144,12 @@ SIGNATURES = {
     "uam_volume_shape": (ctypes.c_int, [ctypes.POINTER(VolumeDesc), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_build": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp, _vp]),
-    "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp,
+    "uam_eval_generated3d": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp,
                                             ctypes.c_int64, _vp, ctypes.c_int32,
                                             ctypes.POINTER(PathOutputs), _vp]),
     "uam_volume_packed_bytes": (ctypes.c_int, [ctypes.POINTER(VolumeDesc),
                                                ctypes.POINTER(ctypes.c_int64)]),
     "uam_volume_pack": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp]),
-    "uam_eval_generated3d_p": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeDesc), _vp, _vp, _vp,
-                                              ctypes.c_int64, _vp, ctypes.c_int32,
-                                              ctypes.POINTER(PathOutputs), _vp]),
     "uam_comm_unique_id": (ctypes.c_int, [_vp]),
     "uam_comm_init": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32]),
     "uam_comm_destroy": (ctypes.c_int, [_vp]),

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <type_traits>
 #include <string>
 #include <thread>
 #include <vector>
@@ -131,12 +132,19 @@ struct KRaster {
     // blocks per row, swords 32-bit words; null = gather every waypoint
     const uint32_t* __restrict__ sum;
     int32_t sshift, snbx, swords;
-    // K2s packed raster (uam_raster_pack; null = K2s gathers rec): a 2-bit code per summary
-    // block (pmap, pwords words) and plane A {phi, terrain} of 8 B per cell in a blocked layout
-    // of 2^phb x 2^pwb cells per block, pnbx blocks per row
+    // packed raster (uam_raster_pack; null = the sorted forms gather rec; layout: PackDims).
+    // Header (hwords words, staged in LDS by K2h): the 2-bit code per summary block (pwords
+    // words), the terrain bound table (one u16 per 2^bshift-square bound block, bnbx per row,
+    // at word bnd_off) and the superblock table (float2 {base, step} per 4 x 4 bound blocks,
+    // sbnbx per row, at word sbt_off).  Planes: p4 {phi} and t4 {terrain as read} in 4 x 8-cell
+    // blocks (one 128-B line, nb8 per row), e8 {phi, psi | nfz << 31} in 4 x 4-cell blocks (nb4
+    // per row).
     const uint32_t* __restrict__ pmap;
-    const uint2* __restrict__ pa;
-    int32_t pwords, phb, pwb, pnbx;
+    int32_t pwords, hwords, bnd_off, sbt_off;
+    int32_t bshift, bnbx, sbnbx, nb8, nb4;
+    const uint32_t* __restrict__ p4;
+    const float* __restrict__ t4;
+    const uint2* __restrict__ e8;
 };
 
 // volume (config 5): 8-B voxels {risk, psi_nfz} [ny][nx][nz], the 8-B column plane
@@ -664,20 +672,54 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
         out[w] = (uint32_t)(lane ? (m >> 32) : m);
 }
 
-// ---- K2s packed raster (uam_raster_pack; build-defined, no reference counterpart) --------
-// K2s's gathers are bound by 128-B lines, of which a 16-B record uses one eighth.  Outside the
-// no-fly zones a waypoint needs only phi and the terrain, so the packed copy keeps them as an
-// 8-B plane A = {phi, terrain as consume_chunk reads it (+0.0 on a nodata cell)}, stored in
-// blocks of 2^phb x 2^pwb cells: half the table, twice the cells per line.  A 2-bit code per
-// summary block says what a waypoint there needs: 0 = nothing (the gather-skip rule), 1 = plane
-// A only (every cell of the block has psi == +-0 and no no-fly flag: the psi term is an exact
-// no-op and the hit count adds 0), 3 = the full 16-B record from rec.  Every path sees exactly
-// the values and the operations of raster_pass2_skip, so the outputs are bit-identical.
-__device__ __forceinline__ int32_t pk_addr(const KRaster& rs, int32_t ix, int32_t iy) {
-    const int32_t blk = (iy >> rs.phb) * rs.pnbx + (ix >> rs.pwb);
-    return (blk << (rs.phb + rs.pwb)) | ((iy & ((1 << rs.phb) - 1)) << rs.pwb) |
-           (ix & ((1 << rs.pwb) - 1));
+// ---- Packed raster (uam_raster_pack; build-defined, no reference counterpart) --------------
+// The sorted forms are bound by 128-B lines; a 16-B record uses one eighth of its line, and most
+// waypoints need less of it.  The packed copy (layout: PackDims) keeps what each block needs in
+// the narrowest entry, with a 2-bit code per summary block saying which one a waypoint reads:
+//   0  nothing: every cell has phi == +-0, psi == +-0 and no no-fly flag (the phi and psi terms
+//      are exact no-ops on accumulators that are never -0, the hit count adds 0);
+//   1  the 4-B phi plane p4 (psi == +-0 and no flag over the block), 32 cells per line;
+//   2  the 8-B plane e8 {phi, |psi| with the no-fly flag in the sign bit}, 16 cells per line:
+//      every psi of the block is >= +0 or -0 (its decoded +0 adds exactly what -0 adds);
+//   3  the whole 16-B record from rec (a psi of the block is negative or a sign-bit NaN).
+// The terrain (as the evaluation reads it: +0.0 on a nodata cell) is out of codes 0-2: it feeds
+// only the order-free path maximum, so K2h fetches it from the 4-B plane t4 only for waypoints
+// whose block's upper bound could still be that maximum (h_item), and the forms without the
+// bound rule read t4 for every in-raster waypoint outside code 3.  Bounds: per bound block
+// (2^bshift cells square) a u16 {ub code, lb code << 8}, decoded ub = base + q * step in f32
+// (the superblock's {base, step}, step a power of two, so q * step is exact and the sum rounds
+// once, the same operations here and in the kernels); every cell's terrain lies in [lb, ub].  A
+// superblock holding a non-finite terrain value stores {NaN, NaN}: its bounds decode to NaN,
+// which the evaluation reads as "no bound" (always fetched, no lower bound).
+constexpr int PK_BOUND_MAX = 16384;  // bound blocks at most (32 KiB of u16 in LDS)
+
+__device__ __forceinline__ int32_t p4_addr(const KRaster& rs, int32_t ix, int32_t iy) {
+    return ((((iy >> 2) * rs.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7));
 }
+__device__ __forceinline__ int32_t e8_addr(const KRaster& rs, int32_t ix, int32_t iy) {
+    return ((((iy >> 2) * rs.nb4 + (ix >> 2)) << 4) | ((iy & 3) << 2) | (ix & 3));
+}
+
+// the decoded bounds of cell (ix, iy) from a header copy (LDS or global)
+__device__ __forceinline__ void pk_bounds(const KRaster& rs, const uint32_t* __restrict__ hdr,
+                                          int32_t ix, int32_t iy, float& ub, float& lb) {
+    const int32_t bx = ix >> rs.bshift, by = iy >> rs.bshift;
+    const uint32_t e =
+        reinterpret_cast<const uint16_t*>(hdr + rs.bnd_off)[by * rs.bnbx + bx];
+    const float2 sb =
+        reinterpret_cast<const float2*>(hdr + rs.sbt_off)[(by >> 2) * rs.sbnbx + (bx >> 2)];
+    ub = sb.x + (float)(e & 255u) * sb.y;
+    lb = sb.x + (float)(e >> 8) * sb.y;
+}
+
+// component k of a 16-B entry
+__device__ __forceinline__ uint32_t u4_comp(const uint4& r, uint32_t k) {
+    return (k & 2u) ? ((k & 1u) ? r.w : r.z) : ((k & 1u) ? r.y : r.x);
+}
+
+// a chunk's per-slot codes, 4 bits per slot
+template <int CH>
+using PkCodes = typename std::conditional<(CH > 8), uint64_t, uint32_t>::type;
 
 // spread the 16 low bits of v to the even bits of the result
 __device__ __forceinline__ uint32_t spread16(uint32_t v) {
@@ -689,15 +731,61 @@ __device__ __forceinline__ uint32_t spread16(uint32_t v) {
     return v;
 }
 
-// one thread per cell, rows coalesced: plane A at its blocked address
+// the generic reads of an in-raster waypoint (the forms without the bound rule: K2s+pack, K2g):
+// its value entry vp (rec in code 3, the aligned 16 B of e8 / p4 holding its cell in codes 2 / 1,
+// left at the caller's dummy line in code 0) and its terrain tp (t4 outside code 3, left at the
+// caller's dummy otherwise); returns cs = code | sub << 2 for pk_terms (sub: the cell's first
+// component in the 16 B)
+__device__ __forceinline__ uint32_t pk_locate(const KRaster& rs, const uint4* __restrict__ rec,
+                                              const uint32_t* __restrict__ map, int32_t ix,
+                                              int32_t iy, const uint4*& vp, const float*& tp) {
+    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+    const uint32_t code = (map[b >> 4] >> ((b & 15) * 2)) & 3u;
+    if (code == 3u) {
+        vp = rec + (iy * rs.nx + ix);
+        return 3u;
+    }
+    const int32_t a4 = p4_addr(rs, ix, iy);
+    tp = rs.t4 + a4;
+    uint32_t sub = 0;
+    if (code == 2u) {
+        const int32_t a8 = e8_addr(rs, ix, iy);
+        vp = reinterpret_cast<const uint4*>(rs.e8 + (a8 & ~1));
+        sub = (uint32_t)(a8 & 1) * 2u;
+    } else if (code == 1u) {
+        vp = reinterpret_cast<const uint4*>(rs.p4 + (a4 & ~3));
+        sub = (uint32_t)(a4 & 3);
+    }
+    return code | (sub << 2);
+}
+
+// the terms of a located waypoint from its 16 B r: phi and psi bits (+0 where the code holds
+// none), the no-fly hit, and the record's terrain as read (meaningful in code 3 only)
+__device__ __forceinline__ void pk_terms(const uint4& r, uint32_t cs, uint32_t& phi,
+                                         uint32_t& psi, uint32_t& hit, float& rter) {
+    const uint32_t code = cs & 3u, sub = cs >> 2;
+    phi = code ? u4_comp(r, sub) : 0u;
+    const uint32_t praw = (code & 2u) ? u4_comp(r, sub + 1u) : 0u;
+    psi = code == 2u ? (praw & 0x7fffffffu) : praw;
+    hit = code == 2u ? (praw >> 31) : (code == 3u && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+    rter = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+}
+
+// one thread per cell, rows coalesced: the three planes at their blocked addresses (e8 is
+// written everywhere, read only in code-2 blocks)
 __global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ rec, KRaster rs,
-                                                     uint2* __restrict__ pa) {
+                                                     uint32_t* __restrict__ p4,
+                                                     float* __restrict__ t4,
+                                                     uint2* __restrict__ e8) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= (int64_t)rs.nx * rs.ny) return;
     const int32_t iy = (int32_t)(c / rs.nx), ix = (int32_t)(c - (int64_t)iy * rs.nx);
     const uint4 r = rec[c];
-    const int32_t a = pk_addr(rs, ix, iy);
-    pa[a] = make_uint2(r.x, (r.w & UAM_FLAG_NODATA) ? 0u : r.z);
+    const int32_t a4 = p4_addr(rs, ix, iy);
+    p4[a4] = r.x;
+    t4[a4] = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+    e8[e8_addr(rs, ix, iy)] =
+        make_uint2(r.x, (r.y & 0x7fffffffu) | ((r.w & UAM_FLAG_NFZ) ? 0x80000000u : 0u));
 }
 
 // one thread per summary block: its 2-bit code; lanes 0/16/32/48 write the wave's 4 words
@@ -712,15 +800,15 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
         const int bx = blk % nbx, by = blk / nbx;
         const int x0 = bx << shift, y0 = by << shift;
         const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
-        bool skip = true, needb = false;
+        bool need = false, neg = false, nz = false;
         for (int iy = y0; iy < y1; ++iy)
             for (int ix = x0; ix < x1; ++ix) {
                 const uint4 r = rec[(int64_t)iy * nx + ix];
-                const uint32_t t = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
-                if ((r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ)) needb = true;
-                if ((r.x & 0x7fffffffu) || t) skip = false;
+                if ((r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ)) need = true;
+                if ((r.y >> 31) && r.y != 0x80000000u) neg = true;  // negative, or a -NaN
+                if (r.x & 0x7fffffffu) nz = true;
             }
-        code = needb ? 3u : skip ? 0u : 1u;
+        code = need ? (neg ? 3u : 2u) : nz ? 1u : 0u;
     }
     const uint64_t lo = __ballot(code & 1u), hi = __ballot(code >> 1);
     const int lane = threadIdx.x & 63;
@@ -728,6 +816,83 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
         const int sh = lane;  // this lane's 16 blocks are bits [lane, lane + 16) of the ballots
         out[blk >> 4] = spread16((uint32_t)(lo >> sh)) | (spread16((uint32_t)(hi >> sh)) << 1);
     }
+}
+
+// one wave per bound block: {min, max} of its terrain as read (+0.0 on nodata); min = NaN when
+// the block holds a non-finite value
+__global__ __launch_bounds__(256) void k_raster_bminmax(const uint4* __restrict__ rec,
+                                                        int32_t nx, int32_t ny, int32_t bshift,
+                                                        int32_t bnbx, int32_t nbb,
+                                                        float2* __restrict__ scr) {
+    const int32_t blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (blk >= nbb) return;  // (whole waves)
+    const int B = 1 << bshift;
+    const int bx = blk % bnbx, by = blk / bnbx;
+    const int x0 = bx << bshift, y0 = by << bshift;
+    const int w = min(B, nx - x0), h = min(B, ny - y0);
+    float mn = INFINITY, mx = -INFINITY;
+    bool bad = false;
+    for (int k = lane; k < w * h; k += 64) {
+        const int iy = y0 + k / w, ix = x0 + k % w;
+        const uint4 r = rec[(int64_t)iy * nx + ix];
+        const float t = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+        if (!__builtin_isfinite(t)) bad = true;
+        mn = fminf(mn, t);
+        mx = fmaxf(mx, t);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, o));
+        mx = fmaxf(mx, __shfl_xor(mx, o));
+    }
+    bad = __any(bad);
+    if (lane == 0) scr[blk] = make_float2(bad ? __builtin_nanf("") : mn, mx);
+}
+
+// one thread per bound block: its superblock's {base, step} from the members' {min, max} (every
+// member forms the same ones; the member at (0, 0) stores them) and its own u16 codes
+__global__ __launch_bounds__(256) void k_raster_bounds(const float2* __restrict__ scr,
+                                                       int32_t bnbx, int32_t bnby,
+                                                       int32_t sbnbx,
+                                                       uint16_t* __restrict__ bnd,
+                                                       float2* __restrict__ sbt) {
+    const int32_t blk = blockIdx.x * 256 + threadIdx.x;
+    if (blk >= bnbx * bnby) return;
+    const int bx = blk % bnbx, by = blk / bnbx;
+    const int sx = bx >> 2, sy = by >> 2;
+    float base = INFINITY, top = -INFINITY;
+    bool bad = false;
+    for (int yy = sy * 4; yy < min(sy * 4 + 4, bnby); ++yy)
+        for (int xx = sx * 4; xx < min(sx * 4 + 4, bnbx); ++xx) {
+            const float2 m = scr[yy * bnbx + xx];
+            if (!(m.x == m.x)) bad = true;
+            base = fminf(base, m.x);
+            top = fmaxf(top, m.y);
+        }
+    float step = 1.0f;
+    if (!bad) {  // the smallest power of two with (top - base) / step <= 253 (2 codes of margin)
+        const double range = (double)top - (double)base;
+        int e = -126;
+        while (e < 127 && ldexp(253.0, e) < range) ++e;
+        step = ldexpf(1.0f, e);
+    }
+    const bool lead = ((bx & 3) == 0) && ((by & 3) == 0);
+    if (bad) {
+        if (lead) sbt[sy * sbnbx + sx] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+        bnd[blk] = 0;
+        return;
+    }
+    if (lead) sbt[sy * sbnbx + sx] = make_float2(base, step);
+    const float2 m = scr[blk];
+    // the kernels' decode: base + (float)q * step (q * step exact, one rounding)
+    int qu = (int)ceil(((double)m.y - (double)base) / (double)step);
+    qu = min(max(qu, 0), 255);
+    while (qu < 255 && base + (float)qu * step < m.y) ++qu;
+    int ql = (int)floor(((double)m.x - (double)base) / (double)step);
+    ql = min(max(ql, 0), 255);
+    while (ql > 0 && base + (float)ql * step > m.x) --ql;
+    bnd[blk] = (uint16_t)(qu | (ql << 8));
 }
 
 // Raster mode with the gather skip (internal; KRaster::sum set, raster_pass2_skip): its own
@@ -4585,25 +4750,25 @@ __device__ __forceinline__ void seg_pass2(const KRaster& rs, const uint4* __rest
     }
 }
 
-// waypoints [j0, j1) of one path from the packed raster (KRaster::pmap/pa, the 2-bit block
-// codes in LDS): raster_pass2_skip's cell arithmetic, values and sums.  A code-1 waypoint
-// gathers its 8-B plane-A entry (its psi term is +-0 and its hit 0 there: exact no-ops, not
-// added); a code-3 waypoint gathers its whole 16-B record from rec, so no waypoint costs more
-// than one request.
+// waypoints [j0, j1) of one path from the packed raster (KRaster::pmap and planes, the 2-bit
+// block codes in LDS): raster_pass2_skip's cell arithmetic, values and sums.  Per waypoint one
+// value load (pk_locate: the record, the e8 or p4 entry, or the dummy line) and one terrain load
+// (t4 outside code 3), both outside every branch; a code-0 waypoint adds no phi / psi term (exact
+// no-ops), a code-1 waypoint no psi term and no hit.
 template <int CH>
 __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* __restrict__ rec,
                                                const uint32_t* map, const PathSrc<true>& src,
                                                int j0, int j1, double dN, PathAcc& a) {
-    // one 16-B load per waypoint outside every branch (as k_g_eval: the branchy form made the
-    // compiler wait for each gather): the record in a code-3 block, the aligned pair of
-    // plane-A entries in a code-1 block, the plane's first pair otherwise (value unused)
-    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
+    const uint4* const vdummy = reinterpret_cast<const uint4*>(rs.p4);
     for (int jc = j0; jc < j1; jc += CH) {
         uint4 r[CH];
-        uint32_t inb = 0, need = 0, full = 0, odd = 0;
+        float tv[CH];
+        uint32_t inb = 0;
+        PkCodes<CH> cs = 0;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const uint4* ptr = dummy;
+            const uint4* vp = vdummy;
+            const float* tp = rs.t4;
             if (jc + t < j1) {
                 double x0, x1;
                 src.at(jc + t, x0, x1);
@@ -4611,22 +4776,12 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
                 const double fy = floor((rs.y_top - x1) * rs.inv_dy);
                 if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
                     inb |= 1u << t;
-                    const int32_t ix = (int32_t)fx, iy = (int32_t)fy;
-                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                    const uint32_t code = (map[b >> 4] >> ((b & 15) * 2)) & 3u;
-                    if (code & 2u) {
-                        need |= 1u << t;
-                        full |= 1u << t;
-                        ptr = rec + (iy * rs.nx + ix);
-                    } else if (code) {
-                        need |= 1u << t;
-                        const int32_t pa = pk_addr(rs, ix, iy);
-                        odd |= (uint32_t)(pa & 1) << t;
-                        ptr = reinterpret_cast<const uint4*>(rs.pa + (pa & ~1));
-                    }
+                    cs |= (PkCodes<CH>)pk_locate(rs, rec, map, (int32_t)fx, (int32_t)fy, vp, tp)
+                          << (4 * t);
                 }
             }
-            r[t] = *ptr;
+            r[t] = *vp;
+            tv[t] = *tp;
         }
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
@@ -4636,24 +4791,16 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
                 a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
                 continue;
             }
-            if (!((need >> t) & 1u)) {  // phi, psi +-0 (exact no-ops), terrain +0.0
-                a.hmax = fmax(a.hmax, 0.0);
-                continue;
+            const uint32_t c = (uint32_t)(cs >> (4 * t)) & 15u, code = c & 3u;
+            uint32_t phi, psi, hit;
+            float rter;
+            pk_terms(r[t], c, phi, psi, hit, rter);
+            if (code) a.cost = a.cost + (double)__uint_as_float(phi) / dN;
+            if (code & 2u) {
+                a.nsum = a.nsum + (double)__uint_as_float(psi);
+                a.nh += (int)hit;
             }
-            if (!((full >> t) & 1u) && ((odd >> t) & 1u)) {  // the pair's second cell
-                r[t].x = r[t].z;
-                r[t].z = r[t].w;
-            } else if (!((full >> t) & 1u)) {
-                r[t].z = r[t].y;
-            }
-            a.cost = a.cost + (double)__uint_as_float(r[t].x) / dN;
-            double terrain = (double)__uint_as_float(r[t].z);
-            if ((full >> t) & 1u) {
-                a.nsum = a.nsum + (double)__uint_as_float(r[t].y);
-                a.nh += (r[t].w & UAM_FLAG_NFZ) ? 1 : 0;
-                if (r[t].w & UAM_FLAG_NODATA) terrain = 0.0;
-            }
-            a.hmax = fmax(a.hmax, terrain);
+            a.hmax = fmax(a.hmax, (double)(code == 3u ? rter : tv[t]));
         }
     }
 }
@@ -4845,9 +4992,11 @@ struct KGrp {
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
     UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's block 0
-    int32_t* __restrict__ bstart;  // K2h tile form: [bins + 1] first sorted position of each
-                                   // bin (written by the scatter's partition 0), or null
-    const uint16_t* __restrict__ tinv;  // [2^tbits * 2^tbits] curve position -> tile (y n + x)
+    int32_t lb_stride;             // K2h: the path lower bound's sample stride (>= 1)
+    int32_t* __restrict__ err;     // the sort's check word: zeroed by the histogram launch, set
+                                   // by the scatter on a position outside the order (keys of the
+                                   // two launches disagreeing); the output launch then writes
+                                   // NaN costs and -1 selections for the whole batch
 };
 
 // K2h / K4h: the D rows' unit sums by one block (block 0 of the scatter launch, one more than
@@ -4961,6 +5110,7 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
     const int t = threadIdx.x, b = blockIdx.x;
+    if (b == 0 && t == 0) *kg.err = 0;
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
@@ -5063,9 +5213,7 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
         const int64_t c = (int64_t)k * G_NBK + b;
         const int sb = (int)(c / (256 * SCAN_ITEMS));
         cur[k] = kg.cnt[c] + (nsb > 0 ? stot[sb] : kg.tot[sb]);
-        if (kg.bstart && b == 0) kg.bstart[k] = cur[k];  // partition 0's place = the bin's start
     }
-    if (kg.bstart && b == 0 && t == 0) kg.bstart[kg.bins] = (int32_t)kg.n_items;
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
@@ -5079,7 +5227,10 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
             const int64_t i = i0 + k * 1024;
             if (i < hi) {
                 const int32_t at = atomicAdd(&cur[kk[k]], 1);
-                if ((uint32_t)at < (uint32_t)kg.n_items) kg.order[at] = (int32_t)i;  // (bound)
+                if ((uint32_t)at < (uint32_t)kg.n_items)
+                    kg.order[at] = (int32_t)i;
+                else
+                    atomicOr(kg.err, 1);  // never in a consistent sort: poisons the outputs
             }
         }
     }
@@ -5248,66 +5399,57 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;  // -0 / N comes out +0: both add to gc alike
     };
-    // the gather of point (x0, x1): one 16-B load per waypoint, issued outside every branch so
-    // the compiler's wait counts stay exact and CH gathers are really in flight.  A code-3
-    // waypoint reads its record from rec; a code-1 waypoint the aligned pair of 8-B plane-A
-    // entries holding its cell (both cells of a pair share a 128-B line, so the request is the
-    // same); a waypoint with nothing to gather (code 0, off the raster, past the group's end)
-    // reads the plane's first pair, one line per wave, and its value is not used.
-    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
-    auto locate = [&](double x0, double x1, int t, uint32_t& inb, uint32_t& need,
-                      uint32_t& full, uint32_t& odd, int32_t& cell) -> const uint4* {
+    // the gathers of point (x0, x1): one value load and one terrain load per waypoint
+    // (pk_locate), issued outside every branch so the compiler's wait counts stay exact and CH
+    // gathers are really in flight; a waypoint with nothing to read (code 0's value, code 3's
+    // terrain, off the raster) reads the planes' first line, one line per wave, unused.
+    const uint4* const vdummy = reinterpret_cast<const uint4*>(rs.p4);
+    auto locate = [&](double x0, double x1, int t, uint32_t& inb, auto& cs, int32_t& cell,
+                      const float*& tp) -> const uint4* {
         // the cell: floor(t) in [0, n) <=> t in [0, n) for integer n, and the truncating
         // conversion equals floor for t >= 0 (NaN fails both tests)
         const double tx = (x0 - rs.x0) * rs.inv_dx;
         const double ty = (rs.y_top - x1) * rs.inv_dy;
-        const uint4* ptr = dummy;
+        const uint4* vp = vdummy;
+        tp = rs.t4;
         if ((tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny)) {
             inb |= 1u << t;
             const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
             if (CELLS) cell = iy * rs.nx + ix;
-            const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-            const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
-            if (code & 2u) {
-                need |= 1u << t;
-                full |= 1u << t;
-                ptr = rec + (iy * rs.nx + ix);
-            } else if (code) {
-                need |= 1u << t;
-                const int32_t a = pk_addr(rs, ix, iy);
-                odd |= (uint32_t)(a & 1) << t;
-                ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
-            }
+            cs |= (std::remove_reference_t<decltype(cs)>)pk_locate(rs, rec, s_map, ix, iy, vp,
+                                                                   tp) << (4 * t);
         }
-#ifdef UAM_K2G_DIAG_NOGATHER  // measurement build: every load reads the plane's first pair
-        ptr = dummy;
+#ifdef UAM_K2G_DIAG_NOGATHER  // measurement build: every load reads the planes' first line
+        vp = vdummy;
+        tp = rs.t4;
 #endif
-        return ptr;
+        return vp;
     };
     // the consume step, branch-free: a lane with nothing gathered adds +0.0 (an exact no-op on
-    // accumulators that are never -0) and takes fmax(hmax, +0.0), exactly what the branches of
-    // raster_pass2_skip do
+    // accumulators that are never -0) and takes fmax(hmax, +0.0) off the raster, exactly what
+    // the branches of raster_pass2_skip do
     double gc = 0.0, gn = 0.0;
     float hmax = -INFINITY;
     uint32_t nh = 0, off = 0;
-    auto consume1 = [&](const uint4& r, bool in, bool nd, bool fl, bool od) {
-        const uint32_t phi = nd ? (od ? r.z : r.x) : 0u;
-        uint32_t ter = nd ? (fl ? r.z : od ? r.w : r.y) : 0u;
-        const uint32_t psi = fl ? r.y : 0u;
-        if (fl && (r.w & UAM_FLAG_NODATA)) ter = 0u;
-        nh += (fl && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+    auto consume1 = [&](const uint4& r, float tv, bool in, uint32_t c) {
+        uint32_t phi, psi, hit;
+        float rter;
+        pk_terms(r, c, phi, psi, hit, rter);
+        nh += hit;
         off += in ? 0u : 1u;
         gc = gc + over_n((double)__uint_as_float(phi));
         gn = gn + (double)__uint_as_float(psi);
-        hmax = fmaxf(hmax, __uint_as_float(ter));
+        hmax = fmaxf(hmax, !in ? 0.0f : (c & 3u) == 3u ? rter : tv);
     };
     for (int jc = j0, it = 0; jc < j1; jc += CH, ++it) {
         const int je = min(jc + CH, j1);
         if (__all(je - jc == CH && je < W)) {  // wave-uniform: the straight-line form
             const bool first = it == 0;
             uint4 r[CH];
+            float tv[CH];
             int32_t cl[CH];
-            uint32_t inb = 0, need = 0, full = 0, odd = 0;
+            uint32_t inb = 0;
+            PkCodes<CH> cs = 0;
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int j = jc + t;
@@ -5331,12 +5473,13 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 }
 #endif
                 cl[t] = -1;
-                r[t] = *locate(x0, x1, t, inb, need, full, odd, cl[t]);
+                const float* tp;
+                r[t] = *locate(x0, x1, t, inb, cs, cl[t], tp);
+                tv[t] = *tp;
             }
 #pragma unroll
             for (int t = 0; t < CH; ++t)
-                consume1(r[t], (inb >> t) & 1u, (need >> t) & 1u, (full >> t) & 1u,
-                         (odd >> t) & 1u);
+                consume1(r[t], tv[t], (inb >> t) & 1u, (uint32_t)(cs >> (4 * t)) & 15u);
             if (CELLS) {
                 int32_t* dst = kg.cells + (int64_t)path * W + jc;
 #pragma unroll
@@ -5352,10 +5495,11 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                     segment(j, x0, x1);
 #endif
                 }
-                uint32_t inb = 0, need = 0, full = 0, odd = 0;
+                uint32_t inb = 0, cs = 0;
                 int32_t cl = -1;
-                const uint4 r = *locate(x0, x1, 0, inb, need, full, odd, cl);
-                consume1(r, inb & 1u, need & 1u, full & 1u, odd & 1u);
+                const float* tp;
+                const uint4 r = *locate(x0, x1, 0, inb, cs, cl, tp);
+                consume1(r, *tp, inb & 1u, cs & 15u);
                 if (CELLS) __builtin_nontemporal_store(cl, kg.cells + (int64_t)path * W + j);
             }
         }
@@ -5449,6 +5593,7 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
             cost = (double)(p.N + 1) * L;
             for (int s = 0; s < kg.nseg; ++s) cost = cost + kg.slot[(int64_t)s * kg.P + gp].cost;
         }
+        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
         if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = L;
         if (out.length) out.length[gp] = len;
@@ -5463,8 +5608,8 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     }
     __syncthreads();
     if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
     }
 }
 
@@ -5489,27 +5634,37 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
     uint32_t cnt;  // nfz hits | off-raster << 8
 };
 
-// every (path, group) item in K2g's sorted order: the group's points, cells and records only.
-// Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the arc
-// formula), CH unconditional 16-B loads (a slot past the group's end reads the plane's first
-// pair and is masked off in the consume step), then the branch-free consume.
-#ifndef UAM_K2H_MINW  // workgroups of 256 per CU the register budget allows (measurement builds)
+// every (path, group) item in K2g's sorted order: the group's points, cells and packed entries
+// only.  Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the
+// arc formula), CH unconditional 16-B value loads and CH unconditional 4-B terrain loads (a slot
+// with nothing to read takes the planes' first line, one per wave), then the branch-free consume.
+//
+// The terrain maximum by bounds (build-defined; the outputs are exactly the per-waypoint
+// maximum's): min_clearance needs only the path's maximum terrain M, an order-free maximum, so
+// a waypoint's exact terrain is fetched (t4) only when it could still be M.  Every in-raster
+// waypoint w has decoded bounds lb_w <= terrain_w <= ub_w (pk_bounds, from LDS).  The item keeps
+//   Lb: the maximum lb over a sample of the path's waypoints (every kg.lb_stride-th, positions
+//       by the same operations as the waypoints' own: lb of a real waypoint, so Lb <= M) and
+//       over its own waypoints so far; off-raster waypoints count +0.0, their exact value;
+//   E:  the maximum of the exact terrain values it has taken (fetched, code-3 records,
+//       off-raster +0.0, blocks whose bounds coincide).
+// It fetches w iff !(ub_w <= E) && !(ub_w < Lb) (NaN bounds: "no bound", always fetched).
+// Exactness: let w* hold M, in this item's group.  If w* was not taken exactly, then either
+// ub_w* <= E, so M <= E and E -- an exact terrain value of the path -- is M; or ub_w* < Lb <= M,
+// impossible since M <= ub_w*.  So the group holding M reports M, every group reports at most
+// its own maximum (E holds exact values), and the output launch's maximum over the groups is M.
+// (A group without M may report less than its own maximum: only the path's is an output.)
+// The slot's hmax is that E.  tools/sim_terrain_bound.py models the fetches (0.17 per waypoint
+// at cfg3, sample stride 8).
+#ifndef UAM_K2H_MINW  // waves per SIMD the register budget allows (measurement builds)
 #define UAM_K2H_MINW 4
 #endif
-// BS, WIN (UAM_OPT_K2G_LDS_WINDOW; measured, not the default -- DESIGN.md §4 K2h): workgroups
-// of BS items, and a WIN x WIN-cell window of the packed plane staged in LDS around the
-// workgroup's middle item (its middle waypoint's cell): a code-1 waypoint inside it reads LDS,
-// its global load is the dummy line.  The window's staging reads each of its lines once.
-// one (path, group) item of K2h: the group's points, cells and records -- the body of k_h_eval
-// and of the tile form k_h_tile.  s_map / s_u / s_cells: the workgroup's code map, unit-arc rows
-// and cell staging; WIN > 0: a WIN x WIN window of the packed plane (plane-A layout) at cell
-// (ox, oy) in s_win, whose code-1 waypoints read LDS instead of global memory.
-template <int CH, bool CELLS, int WIN>
+constexpr int H_BS = 512;  // K2h workgroup (2 per CU at 4 waves per SIMD; LDS <= 80 KiB each)
+template <int CH, bool CELLS>
 __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, const KGrp& kg,
                                        const uint4* __restrict__ rec,
-                                       const uint32_t* __restrict__ s_map,
+                                       const uint32_t* __restrict__ s_hdr,
                                        const double2* __restrict__ s_u, int32_t* s_cells,
-                                       const uint2* __restrict__ s_win, int ox, int oy,
                                        bool live, int32_t item, int32_t path, int32_t q,
                                        const double4& pr) {
     // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
@@ -5532,77 +5687,100 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;
     };
-    const uint4* const dummy = reinterpret_cast<const uint4*>(rs.pa);
+    // waypoint j's raster cell (arc_point's operations; false off the raster or NaN)
+    auto cell_of = [&](int j, int32_t& ix, int32_t& iy) -> bool {
+        const double2 u = urow[min(max(j - 1, 0), N - 1)];
+        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
+        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+        x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
+        x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
+        const double tx = (x0 - rs.x0) * rs.inv_dx;
+        const double ty = (rs.y_top - x1) * rs.inv_dy;
+        const bool in = (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny);
+        ix = in ? (int32_t)tx : 0;
+        iy = in ? (int32_t)ty : 0;
+        return in;
+    };
+    // the path's sampled lower bound (the same for all its items)
+    float Lb = -INFINITY;
+    for (int j = 0; j < W; j += kg.lb_stride) {  // (lb_stride >= 1; uniform trip count)
+        int32_t ix, iy;
+        const bool in = cell_of(j, ix, iy);
+        float ub, lb;
+        pk_bounds(rs, s_hdr, ix, iy, ub, lb);
+        Lb = fmaxf(Lb, in ? lb : 0.0f);
+    }
+    const uint4* const vdummy = reinterpret_cast<const uint4*>(rs.p4);
     double gc = 0.0, gn = 0.0;
-    float hmax = -INFINITY;
+    float E = -INFINITY;
     uint32_t nh = 0, off = 0;
     for (int c = 0; c < nch; ++c) {
         const int jc = j0 + c * CH;
         uint4 r[CH];
-        uint2 lv[WIN > 0 ? CH : 1];
+        float tv[CH];
         int32_t cl[CH];
-        uint32_t inb = 0, need = 0, full = 0, odd = 0, inw = 0;
+        uint32_t inb = 0, tk = 0;
+        PkCodes<CH> cs = 0;  // per slot: code | sub << 2, 4 bits each
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int j = jc + t;
-            const double2 u = urow[min(max(j - 1, 0), N - 1)];
-            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
-            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-            x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
-            x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
-            const double tx = (x0 - rs.x0) * rs.inv_dx;
-            const double ty = (rs.y_top - x1) * rs.inv_dy;
-            const uint4* ptr = dummy;
+            int32_t ix, iy;
+            const bool in = cell_of(j, ix, iy);
+            const uint4* vp = vdummy;
+            const float* tp = rs.t4;
             cl[t] = -1;
-            if ((j < j1) && (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) &&
-                (ty < (double)rs.ny)) {
-                inb |= 1u << t;
-                const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
-                if (CELLS) cl[t] = iy * rs.nx + ix;
-                const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                const uint32_t code = (s_map[b >> 4] >> ((b & 15) * 2)) & 3u;
-                if (code & 2u) {
-                    need |= 1u << t;
-                    full |= 1u << t;
-                    ptr = rec + (iy * rs.nx + ix);
-                } else if (code) {
-                    need |= 1u << t;
-                    const int32_t a = pk_addr(rs, ix, iy);
-                    odd |= (uint32_t)(a & 1) << t;
-                    ptr = reinterpret_cast<const uint4*>(rs.pa + (a & ~1));
-                    if (WIN > 0) {
-                        const int wx = ix - ox, wy = iy - oy;
-                        if ((uint32_t)wx < (uint32_t)WIN && (uint32_t)wy < (uint32_t)WIN) {
-                            inw |= 1u << t;
-                            ptr = dummy;
+            if (j < j1) {
+                if (in) {
+                    inb |= 1u << t;
+                    if (CELLS) cl[t] = iy * rs.nx + ix;
+                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+                    const uint32_t code = (s_hdr[b >> 4] >> ((b & 15) * 2)) & 3u;
+                    float ub, lb;
+                    pk_bounds(rs, s_hdr, ix, iy, ub, lb);
+                    Lb = fmaxf(Lb, lb);
+                    if (lb == ub) E = fmaxf(E, ub);  // a block of one value: that value
+                    uint32_t sub = 0;
+                    if (code == 3u) {
+                        vp = rec + (iy * rs.nx + ix);
+                    } else {
+                        const int32_t a4 = p4_addr(rs, ix, iy);
+                        if (code == 2u) {
+                            const int32_t a8 = e8_addr(rs, ix, iy);
+                            vp = reinterpret_cast<const uint4*>(rs.e8 + (a8 & ~1));
+                            sub = (uint32_t)(a8 & 1) * 2u;
+                        } else if (code == 1u) {
+                            vp = reinterpret_cast<const uint4*>(rs.p4 + (a4 & ~3));
+                            sub = (uint32_t)(a4 & 3);
+                        }
+                        if (!(ub <= E) && !(ub < Lb)) {
+                            tk |= 1u << t;
+                            tp = rs.t4 + a4;
                         }
                     }
+                    cs |= (PkCodes<CH>)(code | (sub << 2)) << (4 * t);
+                } else {  // off the raster: sea level, exactly
+                    E = fmaxf(E, 0.0f);
+                    Lb = fmaxf(Lb, 0.0f);
                 }
             }
-            r[t] = *ptr;
-            if (WIN > 0) {  // the window's entry (index 0 when unused)
-                const int wx = ((inw >> t) & 1u) ? ((int32_t)((x0 - rs.x0) * rs.inv_dx) - ox) : 0;
-                const int wy = ((inw >> t) & 1u) ? ((int32_t)((rs.y_top - x1) * rs.inv_dy) - oy) : 0;
-                lv[t] = s_win[(((wy >> 2) * (WIN / 4) + (wx >> 2)) << 4) | ((wy & 3) << 2) | (wx & 3)];
-            }
+            r[t] = *vp;
+            tv[t] = *tp;
         }
         const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const bool vl = t < nv;
-            const bool in = (inb >> t) & 1u, nd = (need >> t) & 1u, fl = (full >> t) & 1u,
-                       od = (odd >> t) & 1u;
-            const uint4 rt = r[t];
-            uint32_t phi = nd ? (od ? rt.z : rt.x) : 0u;
-            uint32_t ter = nd ? (fl ? rt.z : od ? rt.w : rt.y) : 0u;
-            if (WIN > 0 && ((inw >> t) & 1u)) phi = lv[t].x, ter = lv[t].y;
-            const uint32_t psi = fl ? rt.y : 0u;
-            if (fl && (rt.w & UAM_FLAG_NODATA)) ter = 0u;
-            nh += (fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            const bool in = (inb >> t) & 1u;
+            const uint32_t cst = (uint32_t)(cs >> (4 * t)) & 15u;
+            uint32_t phi, psi, hit;
+            float rter;
+            pk_terms(r[t], cst, phi, psi, hit, rter);
+            nh += hit;
             off += (vl && !in) ? 1u : 0u;
             gc = gc + over_n((double)__uint_as_float(phi));
             gn = gn + (double)__uint_as_float(psi);
-            hmax = fmaxf(hmax, vl ? __uint_as_float(ter) : -INFINITY);
+            const float ter = (cst & 3u) == 3u ? rter : ((tk >> t) & 1u) ? tv[t] : -INFINITY;
+            E = fmaxf(E, ter);
         }
         if (CELLS) {
             // through the wave's LDS slice: lane l stages its CH cells, then each store
@@ -5632,184 +5810,53 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
     HSlot o;
     o.cost = gc;
     o.psi = gn;
-    o.hmax = hmax;
+    o.hmax = E;
     o.cnt = nh | (off << 8);
     if (live) reinterpret_cast<HSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
 }
 
-template <int CH, bool CELLS, int BS = 256, int WIN = 0>
-__global__ __launch_bounds__(BS, BS == 256 ? (CH >= 16 ? 2 : UAM_K2H_MINW) : 1) void k_h_eval(
-                                                                  KParams p, KRaster rs,
-                                                                  KGrp kg,
-                                                                  const uint4* __restrict__ rec) {
+// K2h evaluation: workgroups of H_BS items (xcd_chunk), the packed raster's header (codes,
+// bounds, superblocks) and the unit-arc rows staged in LDS, then one item per lane (h_item)
+template <int CH, bool CELLS>
+__global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaster rs, KGrp kg,
+                                                               const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    uint32_t* s_map = s_dyn;
-    const int mapw = (rs.pwords + 3) & ~3;
-    double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
+    uint32_t* s_hdr = s_dyn;
+    double2* s_u = reinterpret_cast<double2*>(s_dyn + rs.hwords);
     // CELLS: each wave's [CH][64] staging slice of waypoint cells, after the unit-arc rows and
     // their junk slot
     int32_t* s_cells = reinterpret_cast<int32_t*>(s_u + kg.D * p.N + 1);
-    // WIN: the window (plane-A layout: 4 x 4-cell blocks of 8-B entries) after the cells slice
-    uint2* s_win = reinterpret_cast<uint2*>(s_cells + (CELLS ? (BS / 64) * CH * 64 : 0));
-    __shared__ int32_t s_org[2];
     // the item's order entry and pair first: their two dependent round trips overlap the
     // staging below instead of following it
-    const int64_t pos0 = xcd_chunk(blockIdx.x, gridDim.x) * BS;
-    const int64_t pos = pos0 + threadIdx.x;
+    const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * H_BS + threadIdx.x;
     const bool live = pos < kg.n_items;
     const int32_t item = live ? kg.order[pos] : 0;
     const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-    {  // staging as k_g_eval: every load of a thread issued before its first LDS store
+    {  // staging: every load of a thread issued before its first LDS store (hwords % 4 == 0)
         constexpr int U = 4;
-        const int nv = rs.pwords >> 2, nu = kg.D * p.N;
+        const int nv = rs.hwords >> 2, nu = kg.D * p.N;
         const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
-        uint4* dst = reinterpret_cast<uint4*>(s_map);
+        uint4* dst = reinterpret_cast<uint4*>(s_hdr);
         const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
         uint4* du = reinterpret_cast<uint4*>(s_u);
-        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += BS * U) {
+        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += H_BS * U) {
             uint4 v[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
+            for (int k = 0; k < U; ++k) {  // unconditional loads (past the end: the first word)
+                const int i = i0 + k * H_BS;
                 v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
             }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
+            for (int k = 0; k < U; ++k) {  // unconditional stores (past the end: a junk slot)
+                const int i = i0 + k * H_BS;
                 *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
-            }
-        }
-        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += BS) s_map[i] = rs.pmap[i];
-    }
-    if (WIN > 0) {
-        if (threadIdx.x == 0) {  // the window around the middle item's middle waypoint
-            const int64_t pm = min(pos0 + BS / 2, kg.n_items - 1);
-            const int32_t it = kg.order[pm];
-            const int32_t pth = (int32_t)div_magic((uint32_t)it, kg.m_nseg, kg.sh_nseg);
-            const int sg = it - pth * kg.nseg;
-            const int32_t qq = (int32_t)div_magic((uint32_t)pth, kg.m_d, kg.sh_d);
-            const int32_t dd = pth - qq * kg.D;
-            const double4 pm4 = reinterpret_cast<const double4*>(kg.pairs)[qq];
-            const int jj0 = sg * kg.G, jj1 = min(jj0 + kg.G, kg.W);
-            const int jm = min(max((jj0 + jj1 - 1) >> 1, 1), p.N);
-            const double2 um = reinterpret_cast<const double2*>(kg.utab)[dd * p.N + jm - 1];
-            double mx, my;
-            arc_point(pm4.x, pm4.y, pm4.z, pm4.w, um.x, um.y, mx, my);
-            const double tx = (mx - rs.x0) * rs.inv_dx, ty = (rs.y_top - my) * rs.inv_dy;
-            const int32_t cx0 = (tx >= 0.0 && tx < (double)rs.nx) ? (int32_t)tx : 0;
-            const int32_t cy0 = (ty >= 0.0 && ty < (double)rs.ny) ? (int32_t)ty : 0;
-            s_org[0] = max(0, min(cx0 - WIN / 2, rs.nx - WIN)) & ~3;
-            s_org[1] = max(0, min(cy0 - WIN / 2, rs.ny - WIN)) & ~3;
-        }
-        __syncthreads();
-        const int ox = s_org[0], oy = s_org[1];
-        constexpr int WB = WIN / 4;  // window blocks per side; a block = 16 entries = 8 x uint4
-        uint4* dw = reinterpret_cast<uint4*>(s_win);
-        for (int i = threadIdx.x; i < WB * WB * 8; i += BS) {
-            const int blk = i >> 3, part = i & 7;
-            const int by = blk / WB, bx = blk - by * WB;
-            const int gy = (oy >> 2) + by, gx = (ox >> 2) + bx;
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (gx * 4 < rs.nx && gy * 4 < rs.ny)
-                v = reinterpret_cast<const uint4*>(rs.pa + (((int64_t)gy * rs.pnbx + gx) << 4))[part];
-            dw[i] = v;
-        }
-    }
-    __syncthreads();
-    h_item<CH, CELLS, WIN>(p, rs, kg, rec, s_map, s_u, s_cells, s_win, WIN > 0 ? s_org[0] : 0,
-                           WIN > 0 ? s_org[1] : 0, live, item, path, q, pr);
-}
-
-// K2h tile form (UAM_OPT_K2G_TILE_OWNER = T; the round-3 verdict's LDS prototype): the sort's
-// tiles are T x T cells, and workgroup w (XCD-placed, xcd_chunk) owns curve position w: it stages
-// that tile's packed plane (T^2 8-B entries, 128 KiB at T = 128) in LDS once and evaluates every
-// item of the tile's two bins (full groups, then the ragged last groups) in rounds of BS, each
-// item exactly as k_h_eval's (h_item: the same arithmetic and order, only the code-1 waypoints
-// inside the tile read LDS).  Workgroup `tiles` takes the off-raster bin without a window.
-template <int CH, int T, int BS>
-__global__ __launch_bounds__(BS, 1) void k_h_tile(KParams p, KRaster rs, KGrp kg,
-                                                  const uint4* __restrict__ rec) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    uint32_t* s_map = s_dyn;
-    const int mapw = (rs.pwords + 3) & ~3;
-    double2* s_u = reinterpret_cast<double2*>(s_dyn + mapw);
-    uint2* s_win = reinterpret_cast<uint2*>(s_u + kg.D * p.N + 1);
-    const int tiles = 1 << (2 * kg.tbits);
-    const int w = (int)xcd_chunk(blockIdx.x, gridDim.x);
-    int a0, a1, b0 = 0, b1 = 0;
-    if (w < tiles) {
-        a0 = kg.bstart[w], a1 = kg.bstart[w + 1];
-        if (kg.last_bin) b0 = kg.bstart[w + kg.last_bin], b1 = kg.bstart[w + kg.last_bin + 1];
-    } else {
-        a0 = kg.bstart[kg.bins - 1], a1 = kg.bstart[kg.bins];
-    }
-    const int n0 = a1 - a0, n = n0 + (b1 - b0);
-    if (n <= 0) return;  // (the whole workgroup)
-    int ox = -(1 << 30), oy = -(1 << 30);  // no window: nothing falls inside it
-    if (w < tiles) {
-        const int tl = kg.tinv[w];
-        ox = (tl & ((1 << kg.tbits) - 1)) * T;
-        oy = (tl >> kg.tbits) * T;
-    }
-    {  // the code map and the unit-arc rows, as k_h_eval
-        constexpr int U = 4;
-        const int nv = rs.pwords >> 2, nu = kg.D * p.N;
-        const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
-        uint4* dst = reinterpret_cast<uint4*>(s_map);
-        const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
-        uint4* du = reinterpret_cast<uint4*>(s_u);
-        for (int i0 = threadIdx.x; i0 < nv + nu; i0 += BS * U) {
-            uint4 v[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
-                v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
-                *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
-            }
-        }
-        for (int i = (nv << 2) + threadIdx.x; i < rs.pwords; i += BS) s_map[i] = rs.pmap[i];
-    }
-    if (w < tiles) {  // the tile: (T/4)^2 blocks of 16 entries, 8 x uint4 each, U in flight
-        constexpr int WB = T / 4, U = 4;
-        uint4* dw = reinterpret_cast<uint4*>(s_win);
-        for (int i0 = threadIdx.x; i0 < WB * WB * 8; i0 += BS * U) {
-            uint4 v[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
-                const int blk = i >> 3, part = i & 7;
-                const int by = blk / WB, bx = blk - by * WB;
-                const int gy = (oy >> 2) + by, gx = (ox >> 2) + bx;
-                v[k] = make_uint4(0u, 0u, 0u, 0u);
-                if (i < WB * WB * 8 && gx * 4 < rs.nx && gy * 4 < rs.ny)
-                    v[k] = reinterpret_cast<const uint4*>(
-                        rs.pa + (((int64_t)gy * rs.pnbx + gx) << 4))[part];
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * BS;
-                if (i < WB * WB * 8) dw[i] = v[k];
             }
         }
     }
     __syncthreads();
-    for (int base = 0; base < n; base += BS) {  // rounds: the count is the workgroup's
-        const int i = base + (int)threadIdx.x;
-        const bool live = i < n;
-        const int pos = !live ? a0 : i < n0 ? a0 + i : b0 + (i - n0);
-        const int32_t item = live ? kg.order[pos] : 0;
-        const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
-        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-        h_item<CH, false, T>(p, rs, kg, rec, s_map, s_u, nullptr, s_win, ox, oy, live, item,
-                             path, q, pr);
-    }
+    h_item<CH, CELLS>(p, rs, kg, rec, s_hdr, s_u, s_cells, live, item, path, q, pr);
 }
 
 // outputs of every path (block = 64 pairs x D, k_g_final's layout): the geometry terms from
@@ -5875,6 +5922,7 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
                 off += (int32_t)((gs.cnt >> 8) & 255u);
             }
         }
+        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
         if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = L;
         if (out.length) out.length[gp] = len;
@@ -5889,8 +5937,8 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
     }
     __syncthreads();
     if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
     }
 }
 
@@ -6019,6 +6067,7 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];
     const int t = threadIdx.x, b = blockIdx.x;
+    if (b == 0 && t == 0) *kg.err = 0;
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
     __syncthreads();
@@ -6229,6 +6278,7 @@ __global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
             off += (int32_t)((g.cnt >> 8) & 255u);
             bel += (int32_t)((g.cnt >> 16) & 255u);
         }
+        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
         if (out.cost) out.cost[gp] = cost;
         if (out.length_q) out.length_q[gp] = L;
         if (out.length) out.length[gp] = len;
@@ -6243,8 +6293,8 @@ __global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
     }
     __syncthreads();
     if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = select_best(s_len + t, 64, D, false);
+        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
+        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
     }
 }
 
@@ -6299,7 +6349,7 @@ struct uam_ctx {
     int k2s_segs = 2;           // K2s segments per path (UAM_OPT_K2S_SEGMENTS: 2..8)
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
-    bool k2g_attrs_cells = false;  // the same for the cell-writing K2g forms
+    bool k2h_attrs = false;     // K2h's dynamic-LDS attributes raised on this context's device
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     bool k4h_attrs = false;     // the same for K4h
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
@@ -6326,11 +6376,11 @@ struct uam_ctx {
                                 // (UAM_OPT_K2G_LDS_FLOOR; K2g cfg3: 45 / 54 / 80 KiB 0.43 / 0.54
                                 // / 0.52 ms against 0.39, k2g7; 0 = the launchers' defaults)
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
-    int k2g_towner = 0;         // K2h tile form: tile side T (UAM_OPT_K2G_TILE_OWNER: 0, 64, 128)
-    bool k2h_tile_attrs = false;  // its dynamic-LDS attributes raised on this context's device
     int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
                                 // 0 = the fewest giving <= 16 bands)
-    int k2g_lwin = 0;           // K2h LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW: 0, 96, 128)
+    int k2h_lbs = 8;            // K2h: the path lower bound's sample stride (UAM_OPT_K2H_LB_STRIDE;
+                                // tools/sim_terrain_bound.py at cfg3: fetches per waypoint 0.17
+                                // at 8, 0.15 at 4, 0.37 without the path bound)
     int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
     int k2g_chunk = 0;          // K2g / K2h / K4h gathers in flight per lane (UAM_OPT_K2G_CHUNK:
@@ -7043,17 +7093,11 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             (long long)value);
             ctx->k4h_band = (int)value;
             return UAM_OK;
-        case UAM_OPT_K2G_LDS_WINDOW:
-            if (value != 0 && value != 96 && value != 128)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_LDS_WINDOW %lld not 0, 96 or 128",
+        case UAM_OPT_K2H_LB_STRIDE:
+            if (value < 1 || value > 1024)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2H_LB_STRIDE %lld outside [1, 1024]",
                             (long long)value);
-            ctx->k2g_lwin = (int)value;
-            return UAM_OK;
-        case UAM_OPT_K2G_TILE_OWNER:
-            if (value != 0 && value != 64 && value != 128)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2G_TILE_OWNER %lld not 0, 64 or 128",
-                            (long long)value);
-            ctx->k2g_towner = (int)value;
+            ctx->k2h_lbs = (int)value;
             return UAM_OK;
         case UAM_OPT_K2G_SIM:
             if (value != 0 && value != 1)
@@ -7088,8 +7132,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_LDS_FLOOR: *value = ctx->k2g_lds; return UAM_OK;
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
-        case UAM_OPT_K2G_TILE_OWNER: *value = ctx->k2g_towner; return UAM_OK;
-        case UAM_OPT_K2G_LDS_WINDOW: *value = ctx->k2g_lwin; return UAM_OK;
+        case UAM_OPT_K2H_LB_STRIDE: *value = ctx->k2h_lbs; return UAM_OK;
         case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
@@ -7396,18 +7439,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
-    // the tile form (K2h without cells): tiles of exactly towner x towner cells
-    const int towner = (ctx->k2g_sim && !ctx->kp.maxratio_smooth && !ko.cells) ? ctx->k2g_towner
-                                                                              : 0;
     int tbits = ctx->k2g_tbits;
-    if (towner) {
-        const int tsh = towner == 64 ? 6 : 7;
-        tbits = 1;
-        while (((std::max(kr.nx, kr.ny) - 1) >> tsh) >= (1 << tbits)) ++tbits;
-        if (tbits > G_TBITS_MAX)
-            return fail(UAM_E_INVALID, "K2h tile form: %d x %d raster needs more than %d tile bits",
-                        kr.nx, kr.ny, G_TBITS_MAX);
-    } else if (tbits == 0) {  // tiles of ~256 x 256 cells
+    if (tbits == 0) {  // tiles of ~256 x 256 cells
         tbits = 3;
         while (tbits < G_TBITS_MAX && (std::max(kr.nx, kr.ny) >> tbits) > 256) ++tbits;
     }
@@ -7428,10 +7461,9 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
                  b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot))),
-                 b_ug = al((size_t)D * sizeof(UGeo)),
-                 b_bs = towner ? al((size_t)(bins + 1) * 4) : 0;
+                 b_ug = al((size_t)D * sizeof(UGeo)), b_err = 256;
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_bs, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_err, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs;
@@ -7444,7 +7476,6 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.nseg = nseg;
     int tshift = 0;
     while (((std::max(kr.nx, kr.ny) - 1) >> tshift) >= (1 << tbits)) ++tshift;
-    if (towner) tshift = towner == 64 ? 6 : 7;
     kg.tshift = tshift;
     kg.tbits = tbits;
     kg.bins = bins;
@@ -7452,52 +7483,77 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
     if (st) return st;
     kg.tkey = ctx->d_tkey;
-    kg.tinv = ctx->d_tkey + ((size_t)1 << (2 * tbits));
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
     kg.n_items = n_items;
+    kg.lb_stride = ctx->k2h_lbs;
     size_t o = 0;
     kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first (HSlot for K2h)
     kg.ugeo = sim ? (UGeo*)(w + o) : nullptr, o += b_ug;
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
-    kg.bstart = towner ? (int32_t*)(w + o) : nullptr, o += b_bs;
+    kg.err = (int32_t*)(w + o), o += b_err;
     kg.key = (uint16_t*)(w + o);
-    const size_t lds_need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +  // + junk slot
-                            (sim && ko.cells ? (size_t)4 * 8 * 64 * 4 : 0);    // K2h cells
-    // a raster far beyond the L2s (over 2^25 cells: cfg4's 8192^2, 1 GiB packed) misses more:
-    // K2h runs 3 workgroups per CU with 11 gathers in flight per lane there (cfg4 0.886 vs
-    // 0.936 ms at 5 workgroups and 7; cfg3 the same either way; profiles/r04/sweep7)
-    const bool big = sim && !ko.cells && (int64_t)kr.nx * kr.ny > ((int64_t)1 << 25);
-    const int floor_lds = ctx->k2g_lds ? ctx->k2g_lds : big ? 54000 : 0;
-    const size_t lds = std::max(lds_need, (size_t)std::min(floor_lds, 160 * 1024));
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
+    // gathers in flight per lane (K2g, profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
+    // 10 0.369, 6 0.351; K2h: 7, groups of 21 = three full chunks)
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : sim ? 7 : 8;
+    size_t lds;
+    int bs;
+    EvalFn ev;
+    if (sim) {  // K2h: H_BS-item workgroups, the packed header in LDS
+        static const EvalFn hevals[4] = {k_h_eval<6, false>, k_h_eval<7, false>,
+                                         k_h_eval<8, false>, k_h_eval<11, false>};
+        static const EvalFn hevals_cells[1] = {k_h_eval<7, true>};
+        constexpr int CH_CELLS = 7;
+        ev = ko.cells ? hevals_cells[0]
+                      : hevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3];
+        bs = H_BS;
+        const size_t need = (size_t)kr.hwords * 4 + ubytes + 16 +  // + the junk slot
+                            (ko.cells ? (size_t)(H_BS / 64) * CH_CELLS * 64 * 4 : 0);
+        lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+        if (lds > 160 * 1024) return 0;
+        if (!ctx->k2h_attrs) {  // per context = per device (DeviceGuard active)
+            for (EvalFn f : hevals)
+                HIP_TRY(hipFuncSetAttribute((const void*)f,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            HIP_TRY(hipFuncSetAttribute((const void*)hevals_cells[0],
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            ctx->k2h_attrs = true;
+        }
+    } else {  // K2g: 256-item workgroups, the code map in LDS
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
                         k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
-    #ifndef UAM_K2G_CH6
+#ifndef UAM_K2G_CH6
 #define UAM_K2G_CH6 6
 #endif
-    static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8), UAM_G_EVALS(11),
-                                     UAM_G_EVALS(16)};
+        static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8),
+                                         UAM_G_EVALS(11), UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
-    // (16 and 21: built for 2 waves per SIMD, so a whole group's gathers can be in flight)
-    static const EvalFn hevals[6] = {k_h_eval<6, false>,  k_h_eval<7, false>,
-                                     k_h_eval<8, false>,  k_h_eval<11, false>,
-                                     k_h_eval<16, false>, k_h_eval<21, false>};
-    static const EvalFn hevals_cells[1] = {k_h_eval<8, true>};
-    if (lds > 64 * 1024 && !ctx->k2g_attrs) {  // per context = per device (DeviceGuard active)
-        for (EvalFn f : evals)
-            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024));
-        for (EvalFn f : hevals)
-            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024));
-        HIP_TRY(hipFuncSetAttribute((const void*)hevals_cells[0],
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        ctx->k2g_attrs = true;
+        // with waypoint cells requested: the CH = 8 form that also writes them
+        static const EvalFn evals_cells[4] = {k_g_eval<8, false, false, true>,
+                                              k_g_eval<8, false, true, true>,
+                                              k_g_eval<8, true, false, true>,
+                                              k_g_eval<8, true, true, true>};
+        const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
+                       (ctx->kp.length_smooth ? 2 : 0) + (ctx->kp.maxratio_smooth ? 1 : 0);
+        ev = ko.cells ? evals_cells[ch & 3] : evals[ch];
+        bs = 256;
+        const size_t need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16;
+        lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+        if (lds > 64 * 1024 && !ctx->k2g_attrs) {
+            for (EvalFn f : evals)
+                HIP_TRY(hipFuncSetAttribute((const void*)f,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            for (EvalFn f : evals_cells)
+                HIP_TRY(hipFuncSetAttribute((const void*)f,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            ctx->k2g_attrs = true;
+        }
     }
+    kg.cells = ko.cells;
     st = ktime_begin(ctx, s);
     if (st) return st;
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
@@ -7507,61 +7563,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (!kg.nsb_raw)
         hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
-    const dim3 ge((unsigned)((n_items + 255) / 256));
-    // gathers in flight per lane (profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
-    // 10 0.369, 6 0.351)
-    // K2h: 7 by default (groups of 21 = three full chunks; cfg3 0.316 vs 0.321 ms at 8, same
-    // box, profiles/r04/sweep3), K2g: 8
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : big ? 11 : sim ? 7 : 8;
-    const int hch = chl == 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : chl == 11 ? 3 : chl == 16 ? 4 : 5;
-    const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
-                   (ctx->kp.length_smooth ? 2 : 0) +
-                   (ctx->kp.maxratio_smooth ? 1 : 0);
-    // with waypoint cells requested: the CH = 8 form that also writes them
-    static const EvalFn evals_cells[4] = {k_g_eval<8, false, false, true>,
-                                          k_g_eval<8, false, true, true>,
-                                          k_g_eval<8, true, false, true>,
-                                          k_g_eval<8, true, true, true>};
-    kg.cells = ko.cells;
-    EvalFn ev = sim ? (ko.cells ? hevals_cells[0] : hevals[hch])
-                    : ko.cells ? evals_cells[ch & 3] : evals[ch];
-    // the LDS-window experiment (UAM_OPT_K2G_LDS_WINDOW, K2h without cells): 1024-item
-    // workgroups, one per CU, a WIN x WIN window (WIN = 96: 72 KiB; 128: 128 KiB)
-    int bs = 256;
-    size_t lds_run = lds;
-    if (sim && !ko.cells && ctx->k2g_lwin) {
-        ev = ctx->k2g_lwin == 96 ? k_h_eval<8, false, 1024, 96> : k_h_eval<8, false, 1024, 128>;
-        bs = 1024;
-        lds_run = lds_need + (size_t)ctx->k2g_lwin * ctx->k2g_lwin * 8;
-        if (lds_run > 160 * 1024) return fail(UAM_E_INVALID, "LDS window too large");
-        HIP_TRY(hipFuncSetAttribute((const void*)ev, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_run));
-    }
-    if (lds > 64 * 1024 && !ctx->k2g_attrs_cells && ko.cells) {
-        for (EvalFn f : evals_cells)
-            HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024));
-        ctx->k2g_attrs_cells = true;
-    }
-    if (towner) {  // the tile form: one workgroup per tile (+ one for the off-raster bin)
-        const EvalFn tf = towner == 128 ? k_h_tile<8, 128, 1024> : k_h_tile<8, 64, 512>;
-        const int tbs = towner == 128 ? 1024 : 512;
-        const size_t lds_t = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16 +
-                             (size_t)towner * towner * 8;
-        if (lds_t > 160 * 1024) return fail(UAM_E_INVALID, "K2h tile form: LDS %zu B", lds_t);
-        if (!ctx->k2h_tile_attrs) {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_h_tile<8, 128, 1024>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            HIP_TRY(hipFuncSetAttribute((const void*)k_h_tile<8, 64, 512>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            ctx->k2h_tile_attrs = true;
-        }
-        hipLaunchKernelGGL(tf, dim3((unsigned)(tiles + 1)), dim3(tbs), lds_t, s, ctx->kp, kr, kg,
-                           (const uint4*)rec);
-    } else {
-        hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds_run, s,
-                           ctx->kp, kr, kg, (const uint4*)rec);
-    }
+    hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s, ctx->kp,
+                       kr, kg, (const uint4*)rec);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
@@ -7572,7 +7575,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
-    ctx->last_kernel = towner ? "K2h-tile+pack" : sim ? "K2h+pack" : "K2g+pack";
+    ctx->last_kernel = sim ? "K2h+pack" : "K2g+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -7601,11 +7604,12 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     if (n_items >= INT32_MAX) return 0;
     // tiles: 8 x 8 by default (128^2 columns at 1024^2: cfg5 0.461 vs 0.491 ms at 16 x 16,
     // profiles/r04/vol2), UAM_OPT_K2G_TILE_BITS otherwise
-    const int tbits = ctx->k2g_tbits ? ctx->k2g_tbits : 3;
+    // (a tile-bits setting made for 2-D rasters may give more (tile, band) bins than the sort
+    // holds: the key then takes the finest tiles that fit, which moves no bit of the outputs)
+    int tbits = ctx->k2g_tbits ? ctx->k2g_tbits : 3;
+    while (tbits > 1 && (2 << (2 * tbits)) * kv.nbands + 1 > G_BINS_MAX) --tbits;
     const int tiles = 1 << (2 * tbits);
-    if (tiles * kv.nbands * 2 + 1 > G_BINS_MAX)
-        return fail(UAM_E_INVALID, "K4h: %d tiles x %d altitude bands exceed the sort's bins",
-                    tiles, kv.nbands);
+    if (tiles * kv.nbands * 2 + 1 > G_BINS_MAX) return 0;  // (more bands than bins: K4)
     const int last_bin = (W % G) ? tiles * kv.nbands : 0;
     const int bins = tiles * kv.nbands + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
@@ -7614,9 +7618,9 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     if (nsb > 4096) return 0;
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_ord = al((size_t)n_items * 4), b_slot = al((size_t)n_items * sizeof(VSlot)),
-                 b_ug = al((size_t)D * sizeof(UGeo)), b_tot = al(4096 * 4);
+                 b_ug = al((size_t)D * sizeof(UGeo)), b_tot = al(4096 * 4), b_err = 256;
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug + b_tot, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug + b_tot + b_err, s, &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs6;
@@ -7646,6 +7650,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.order = (int32_t*)(w + o), o += b_ord;
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
+    kg.err = (int32_t*)(w + o), o += b_err;
     kg.key = (uint16_t*)(w + o);
     st = ktime_begin(ctx, s);
     if (st) return st;
@@ -7706,39 +7711,71 @@ static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shi
     return UAM_OK;
 }
 
-// packed-raster layout (uam_raster_pack): 2^hb x 2^wb cells per block, 2 x 2 = 4 x 4 cells of
-// 8 B = one 128-B line (row-major measured the same on cfg3: 0.554 vs 0.555 ms, r02)
-static void pack_layout(int32_t* hb, int32_t* wb) {
-    *hb = 2;
-    *wb = 2;
-}
-
+// packed-raster layout (uam_raster_pack), 256-B aligned sections:
+//   header (hwords words, the part K2h stages in LDS): the code map (words, 2 bits per summary
+//   block, padded to 16 B), the bound table (nbb u16, padded to 16 B; bound blocks of 2^bsh
+//   cells square, the smallest with at most PK_BOUND_MAX of them and at least 8 cells wide), the
+//   superblock table (nsb float2, 4 x 4 bound blocks each);
+//   scratch (nbb float2: the bound blocks' {min, max} while packing);
+//   p4 (4-B phi) and t4 (4-B terrain) in 4 x 8-cell blocks, e8 (8 B) in 4 x 4-cell blocks.
 struct PackDims {
-    int32_t sh, nbx, nby, words, hb, wb, lnbx;
-    int64_t off_a, bytes;
+    int32_t sh, nbx, nby, words;           // summary blocks, code-map words
+    int32_t bsh, bnbx, bnby, nbb;          // bound blocks
+    int32_t sbnbx, sbnby, nsb;             // superblocks
+    int32_t hwords, bnd_off, sbt_off;      // header words, word offsets
+    int32_t nb8, nb4, lnby;                // blocks per row (4 x 8, 4 x 4), block rows
+    int64_t off_scr, off_p4, off_t4, off_e8, bytes;
 };
 
 static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
     int st = summary_dims(desc, block, &d->sh, &d->nbx, &d->nby);
     if (st) return st;
     d->words = (int32_t)(((int64_t)d->nbx * d->nby * 2 + 31) / 32);
-    pack_layout(&d->hb, &d->wb);
-    d->lnbx = (desc->nx + (1 << d->wb) - 1) >> d->wb;
-    const int64_t lnby = (desc->ny + (1 << d->hb) - 1) >> d->hb;
-    const int64_t cells = ((int64_t)d->lnbx * lnby) << (d->hb + d->wb);
-    if (cells >= ((int64_t)1 << 31)) return fail(UAM_E_INVALID, "packed raster too large");
-    d->off_a = ((int64_t)d->words * 4 + 255) & ~(int64_t)255;
-    d->bytes = d->off_a + cells * 8;
+    d->bsh = 3;
+    auto nblk = [&](int s) {
+        return (int64_t)((desc->nx + (1 << s) - 1) >> s) * ((desc->ny + (1 << s) - 1) >> s);
+    };
+    while (nblk(d->bsh) > PK_BOUND_MAX) ++d->bsh;
+    d->bnbx = (desc->nx + (1 << d->bsh) - 1) >> d->bsh;
+    d->bnby = (desc->ny + (1 << d->bsh) - 1) >> d->bsh;
+    d->nbb = d->bnbx * d->bnby;
+    d->sbnbx = (d->bnbx + 3) >> 2;
+    d->sbnby = (d->bnby + 3) >> 2;
+    d->nsb = d->sbnbx * d->sbnby;
+    auto w16 = [](int64_t bytes) { return (int32_t)(((bytes + 15) & ~(int64_t)15) / 4); };
+    d->bnd_off = w16((int64_t)d->words * 4);
+    d->sbt_off = d->bnd_off + w16((int64_t)d->nbb * 2);
+    d->hwords = d->sbt_off + w16((int64_t)d->nsb * 8);
+    d->nb8 = (desc->nx + 7) >> 3;
+    d->nb4 = (desc->nx + 3) >> 2;
+    d->lnby = (desc->ny + 3) >> 2;
+    const int64_t c4 = (int64_t)d->lnby * d->nb8 * 32, c8 = (int64_t)d->lnby * d->nb4 * 16;
+    if (c4 >= ((int64_t)1 << 31) || c8 >= ((int64_t)1 << 31))
+        return fail(UAM_E_INVALID, "packed raster too large");
+    auto a256 = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+    d->off_scr = a256((int64_t)d->hwords * 4);
+    d->off_p4 = d->off_scr + a256((int64_t)d->nbb * 8);
+    d->off_t4 = d->off_p4 + a256(c4 * 4);
+    d->off_e8 = d->off_t4 + a256(c4 * 4);
+    d->bytes = d->off_e8 + a256(c8 * 8);
     return UAM_OK;
 }
 
 static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
-    kr->pmap = (const uint32_t*)packed;
-    kr->pa = (const uint2*)((const char*)packed + d.off_a);
+    const char* b = (const char*)packed;
+    kr->pmap = (const uint32_t*)b;
     kr->pwords = d.words;
-    kr->phb = d.hb;
-    kr->pwb = d.wb;
-    kr->pnbx = d.lnbx;
+    kr->hwords = d.hwords;
+    kr->bnd_off = d.bnd_off;
+    kr->sbt_off = d.sbt_off;
+    kr->bshift = d.bsh;
+    kr->bnbx = d.bnbx;
+    kr->sbnbx = d.sbnbx;
+    kr->nb8 = d.nb8;
+    kr->nb4 = d.nb4;
+    kr->p4 = (const uint32_t*)(b + d.off_p4);
+    kr->t4 = (const float*)(b + d.off_t4);
+    kr->e8 = (const uint2*)(b + d.off_e8);
 }
 
 static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
@@ -7908,26 +7945,12 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
 extern "C" {
 
 int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
-                       const void* rec, const double* pairs, int64_t n_pairs,
+                       const void* rec, const uint32_t* summary, int32_t block,
+                       const void* packed, const double* pairs, int64_t n_pairs,
                        const double* utab, int32_t D, const uam_path_outputs* out,
                        uam_stream stream) {
-    return eval_generated(ctx, mode, desc, rec, nullptr, 0, pairs, n_pairs, utab, D, out, stream);
-}
-
-int uam_eval_generated_s(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
-                         const uint32_t* summary, int32_t block, const double* pairs,
-                         int64_t n_pairs, const double* utab, int32_t D,
-                         const uam_path_outputs* out, uam_stream stream) {
-    return eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs, n_pairs, utab,
-                          D, out, stream);
-}
-
-int uam_eval_generated_p(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
-                         const uint32_t* summary, int32_t block, const void* packed,
-                         const double* pairs, int64_t n_pairs, const double* utab, int32_t D,
-                         const uam_path_outputs* out, uam_stream stream) {
-    return eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs, n_pairs, utab,
-                          D, out, stream, packed);
+    return eval_generated(ctx, mode, desc, rec, summary, block, pairs, n_pairs, utab, D, out,
+                          stream, packed);
 }
 
 int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
@@ -7954,13 +7977,23 @@ int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, 
     set_kpack(&kr, d, packed);
     DeviceGuard dg(ctx->device);
     hipStream_t s = (hipStream_t)stream;
+    char* b = (char*)packed;
+    const uint4* r4 = (const uint4*)rec;
+    // header padding and the planes' padding cells: zero (never addressed, but defined bytes)
+    HIP_TRY(hipMemsetAsync(b, 0, (size_t)d.off_scr, s));
+    HIP_TRY(hipMemsetAsync(b + d.off_p4, 0, (size_t)(d.bytes - d.off_p4), s));
     const int32_t nb = d.nbx * d.nby;
-    hipLaunchKernelGGL(k_raster_pack_map, dim3(grid_for(nb, 256)), dim3(256), 0, s,
-                       (const uint4*)rec, kr.nx, kr.ny, d.sh, d.nbx, nb, (uint32_t*)packed);
-    // padding cells of the blocked layout are never addressed; the plane holds every cell
+    hipLaunchKernelGGL(k_raster_pack_map, dim3(grid_for(nb, 256)), dim3(256), 0, s, r4, kr.nx,
+                       kr.ny, d.sh, d.nbx, nb, (uint32_t*)b);
     const int64_t cells = (int64_t)kr.nx * kr.ny;
-    hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s,
-                       (const uint4*)rec, kr, (uint2*)((char*)packed + d.off_a));
+    hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, r4,
+                       kr, (uint32_t*)(b + d.off_p4), (float*)(b + d.off_t4),
+                       (uint2*)(b + d.off_e8));
+    hipLaunchKernelGGL(k_raster_bminmax, dim3((unsigned)((d.nbb + 3) / 4)), dim3(256), 0, s, r4,
+                       kr.nx, kr.ny, d.bsh, d.bnbx, d.nbb, (float2*)(b + d.off_scr));
+    hipLaunchKernelGGL(k_raster_bounds, dim3((unsigned)((d.nbb + 255) / 256)), dim3(256), 0, s,
+                       (const float2*)(b + d.off_scr), d.bnbx, d.bnby, d.sbnbx,
+                       (uint16_t*)(b + (size_t)d.bnd_off * 4), (float2*)(b + (size_t)d.sbt_off * 4));
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
@@ -8125,10 +8158,14 @@ int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, vo
     return UAM_OK;
 }
 
-int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
-                           const void* packed, const double* pairs6, int64_t n_pairs,
-                           const double* utab, int32_t D, const uam_path_outputs* out,
-                           uam_stream stream) {
+static int eval_generated3d_vol(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
+                                const double* pairs6, int64_t n_pairs, const double* utab,
+                                int32_t D, const uam_path_outputs* out, uam_stream stream);
+
+int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
+                         const void* packed, const double* pairs6, int64_t n_pairs,
+                         const double* utab, int32_t D, const uam_path_outputs* out,
+                         uam_stream stream) {
     if (packed) {
         int st = check_ctx(ctx, true);
         if (st) return st;
@@ -8168,12 +8205,12 @@ int uam_eval_generated3d_p(uam_ctx* ctx, const uam_volume_desc* vd, const void* 
             if (st == 1) return UAM_OK;
         }
     }
-    return uam_eval_generated3d(ctx, vd, vol, pairs6, n_pairs, utab, D, out, stream);
+    return eval_generated3d_vol(ctx, vd, vol, pairs6, n_pairs, utab, D, out, stream);
 }
 
-int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
-                         const double* pairs6, int64_t n_pairs, const double* utab, int32_t D,
-                         const uam_path_outputs* out, uam_stream stream) {
+static int eval_generated3d_vol(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol,
+                                const double* pairs6, int64_t n_pairs, const double* utab,
+                                int32_t D, const uam_path_outputs* out, uam_stream stream) {
     int st = check_ctx(ctx, true);
     if (st) return st;
     if (n_pairs < 0 || D < 1 || D > 16)

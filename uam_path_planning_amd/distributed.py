@@ -52,18 +52,20 @@ def broadcast_raster(raster, src=0, group=None, engine=None, rebuild=None):
     (synchronised on the tensor's device before and after).
 
     raster: a CostRaster, whose rec is broadcast and whose derived copies -- the gather-skip
-    bitmap (summary) and the packed copy K2g / K2s read (packed) -- were built from the
+    bitmap (summary) and the packed copy K2h / K2g / K2s read (packed) -- were built from the
     receiver's OLD records, so they are rebuilt from the broadcast records with `rebuild`
     (default: `engine`) or, with no engine at hand, dropped (the evaluation then gathers rec);
-    or a bare tensor (rec of a CostRaster, a volume's voxels), broadcast as is -- its caller
-    owns any derived copy.  With an engine whose communicator init_raster_comm set up, the
+    a RiskVolume, whose buffer is broadcast and whose packed copy (K4h) is rebuilt
+    (`volume_pack`) or dropped the same way; or a bare tensor (rec of a CostRaster, a volume's
+    buffer), broadcast as is -- its caller owns any derived copy.  With an engine whose communicator init_raster_comm set up, the
     bytes move by libuampath's RCCL broadcast (uam_bcast_raster, xGMI on the GPU node), whose
     ranks are the process group's ranks (src is converted); without one (CPU tensors: the gloo
     tests, or several ranks sharing one GPU in a rehearsal) by torch.distributed.broadcast."""
     import torch
 
     dist = _dist()
-    rec = getattr(raster, "rec", raster)
+    volume = hasattr(raster, "buf") and hasattr(raster, "packed")
+    rec = raster.buf if volume else getattr(raster, "rec", raster)
     dev = rec.device
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -76,8 +78,14 @@ def broadcast_raster(raster, src=0, group=None, engine=None, rebuild=None):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     secs = time.perf_counter() - t0
-    if rec is not raster and (raster.summary is not None or raster.packed is not None):
-        eng = rebuild if rebuild is not None else engine
+    eng = rebuild if rebuild is not None else engine
+    if volume:
+        if raster.packed is not None:
+            if eng is not None:
+                eng.volume_pack(raster)
+            else:
+                raster.packed = None
+    elif rec is not raster and (raster.summary is not None or raster.packed is not None):
         if eng is not None:
             eng.raster_summary(raster, raster.block, packed=raster.packed is not None)
         else:

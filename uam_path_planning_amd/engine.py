@@ -400,20 +400,14 @@ class Engine:
             o, s = outputs
             _check_outputs(o, Q * D, Q, self.params.N + 2)
         geo = None if raster is None else ctypes.byref(raster.geo.as_struct())
-        if raster is not None and raster.packed is not None:
-            _lib.check(self.lib.uam_eval_generated_p(
-                self._ctx, geo, _ptr(raster.rec), _ptr(raster.summary), int(raster.block),
-                _ptr(raster.packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
-                "uam_eval_generated_p")
-            return o
-        if raster is not None and raster.summary is not None:
-            _lib.check(self.lib.uam_eval_generated_s(
-                self._ctx, geo, _ptr(raster.rec), _ptr(raster.summary), int(raster.block),
-                _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated_s")
-            return o
+        rec = summary = packed = None
+        block = 0
+        if raster is not None:
+            rec, summary, packed, block = raster.rec, raster.summary, raster.packed, raster.block
         _lib.check(self.lib.uam_eval_generated(
-            self._ctx, self._mode(raster), geo, _ptr(None if raster is None else raster.rec),
-            _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream), "uam_eval_generated")
+            self._ctx, self._mode(raster), geo, _ptr(rec), _ptr(summary), int(block or 0),
+            _ptr(packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
+            "uam_eval_generated")
         return o
 
     # -- volume (config 5) -------------------------------------------------------------
@@ -473,10 +467,10 @@ class Engine:
         else:
             o, s = self._outputs(Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False,
                                  n_pairs=Q)
-        _lib.check(self.lib.uam_eval_generated3d_p(
+        _lib.check(self.lib.uam_eval_generated3d(
             self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.buf),
             _ptr(volume.packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
-            "uam_eval_generated3d_p")
+            "uam_eval_generated3d")
         return o
 
     def gen_paths(self, pairs, utab):
