@@ -82,6 +82,9 @@ def parse():
                     help="also return every waypoint's raster cell index (outputs cells "
                          "[P, W] int32, the reference's returned waypoints); priced at "
                          "16 W + 16 + 4 W B/path (SURVEY §8(d))")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="libuampath context option (uam_set_option; names in _lib.OPTIONS), "
+                         "repeatable: measurement sweeps of forms that give the same outputs")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -256,6 +259,9 @@ def main():
     o = outs[0]
     if args.group is not None:
         eng.set_option("group", args.group)
+    for kv in args.opt:
+        name, val = kv.split("=", 1)
+        eng.set_option(name.strip(), int(val))
 
     def step():
         # one call: sort + arc generation + gather + cost reduction + selection
@@ -348,6 +354,8 @@ def main():
     group = eng.last_group()   # the sum order the library used (0 = sequential)
     roofline["sum_group"] = group
     roofline["profile_key"] = pkey
+    if args.opt:
+        roofline["options"] = list(args.opt)
     result = {
         "metric": METRIC,
         "value": round(value, 1),

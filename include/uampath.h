@@ -304,17 +304,21 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
                          const void* packed_dev, const double* pairs6_dev, int64_t n_pairs,
                          const double* utab_dev, int32_t D, const uam_path_outputs* out,
                          uam_stream stream);
-/* The packed volume (K4h), three 256-B aligned sections, so a waypoint is one request:
- *   1. 16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} per (ix, iy, iz) --
- *      the column's terrain and flags beside the layer's pair -- in blocks of 4 x 2 cells of
- *      one layer (one 128-B line), layer-major planes, padded to whole blocks;
- *   2. 8-B voxels {float risk, float terrain} in blocks of 4 x 4 cells of one layer;
- *   3. a 2-bit code per 8 x 8 columns: 3 where a column of the block has psi_nfz != +-0 in
- *      any layer or the no-fly flag (its waypoints read section 1), else 1 (section 2: psi is
- *      +-0 in every layer and no flag is set there, so the 8-B voxel's consume adds exact
- *      no-ops).
- * uam_volume_pack derives it from a built volume (vol_dev); packed_dev holds
- * uam_volume_packed_bytes bytes (1.5 GiB at 1024^2 x 64), 256-B aligned. */
+/* The packed volume (K4h), 256-B aligned sections:
+ *   header  a 2-bit code per 8 x 8 columns (0: risk, psi_nfz +-0 in every layer and no no-fly
+ *           flag; 1: psi_nfz +-0 and no flag; 2: no psi_nfz below zero; 3: otherwise), then the
+ *           column terrain's bounds in the packed raster's scheme (u16 per bound block of
+ *           columns, float2 {base, step} per 4 x 4 bound blocks);
+ *   scratch the bound blocks' {min, max} while packing;
+ *   16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} per (ix, iy, iz) in
+ *           4 x 2-column blocks of one layer (code 3);
+ *   4-B risk per voxel in 4 x 8-column blocks of one layer (code 1);
+ *   8-B {risk, |psi_nfz| | nfz << 31} per voxel in 4 x 4-column blocks of one layer (code 2);
+ *   the 4-B column terrain (+0 on nodata) in 4 x 8-column blocks.
+ * K4h reads a waypoint's terrain only where it could still decide min_clearance or
+ * below_terrain (the outputs are unchanged bit for bit).  uam_volume_pack derives it from a
+ * built volume (vol_dev); packed_dev holds uam_volume_packed_bytes bytes (1.75 GiB at
+ * 1024^2 x 64), 256-B aligned. */
 int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);
 int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                     void* packed_dev, uam_stream stream);
@@ -465,7 +469,8 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                ~62 KiB of tables), 60 000 (2 per CU) for K4h
  *   UAM_OPT_K2G_CHUNK            K2g / K2h / K4h evaluation: gathers in flight per lane,
  *                                6/7/8/11/16/21 (K2g: 7 runs as 6, 16 at two waves per SIMD, 21
- *                                as 16; K2h: 6/7/8/11, 16 and 21 as 11; K4h: 6/7/8/11/16/21);
+ *                                as 16; K2h: 6/7/8/11, 16 and 21 as 11; K4h: 6/7/8/11/16, 21
+ *                                as 16);
  *                                0 (default) = 8 for K2g, 7 for K2h, 11 for K4h
  *   UAM_OPT_K2G_CURVE            K2g sort key: tiles in Hilbert (1, default) or Morton (0) order
  *   UAM_OPT_K2G_SIM              1 (default): generated raster batches take K2h, K2g's sort and

@@ -152,28 +152,28 @@ def _vary_psi(e, vol):
 
 
 def test_k4h_pack_layout(oracle_mod):
-    """uam_volume_pack against its definition: the 16-B table (voxel (ix, iy, iz) at
-    ((iz nby2 + iy/2) nbx4 + ix/4) 8 + (iy%2) 4 + ix%4: {risk, psi} of the voxel, {terrain,
-    flags} of the column), the 8-B table ({risk, terrain} at ((iz nby4 + iy/4) nbx4 + ix/4) 16
-    + (iy%4) 4 + ix%4), zero padding, and the 2-bit code per 8 x 8 columns (3 where a column
-    has psi != +-0 in any layer or the no-fly flag, else 1), 256-B aligned sections."""
+    """uam_volume_pack against its definition (uampath.hip VpkDims / KVol4): the 16-B voxels
+    ({risk, psi} of the voxel, {terrain, flags} of the column, 4 x 2-column blocks per layer),
+    the 4-B risk (4 x 8) and 8-B {risk, |psi| | nfz << 31} (4 x 4) planes per layer, the column
+    terrain (4 x 8), zero padding, the 2-bit code per 8 x 8 columns (3: a psi below zero in any
+    layer; 2: another nonzero psi or the no-fly flag; 1: a nonzero risk; 0: none), and terrain
+    bounds that hold every column."""
+    from test_host_cpu import _vpk_sections
+
     e, orc, vol, vd, host = _case(oracle_mod, 300, 7, 10, 21)
     _vary_psi(e, vol)
     raw = vol.packed.cpu().numpy()
     ny, nx, nz = 300, 300, 7
-    al = lambda v: (v + 255) // 256 * 256
-    nbx4, nby2, nby4 = (nx + 3) // 4, (ny + 1) // 2, (ny + 3) // 4
-    n16 = nbx4 * nby2 * 8 * nz
-    off8 = al(n16 * 16)
-    n8 = nbx4 * nby4 * 16 * nz
-    offc = off8 + al(n8 * 8)
-    cnbx = cnby = (nx + 7) // 8
-    cw = (cnbx * cnby + 15) // 16
-    assert raw.nbytes == offc + al(cw * 4)
+    sec = _vpk_sections(nx, ny, nz)
+    off = np.cumsum([0] + sec)
+    assert raw.nbytes == off[-1]
     b = raw.view(np.uint8)
-    t16 = b[:n16 * 16].view(np.int32).reshape(-1, 4)
-    t8 = b[off8:off8 + n8 * 8].view(np.int32).reshape(-1, 2)
-    cm = b[offc:offc + cw * 4].view(np.uint32)
+    nbx4, nby2, nb8, nb4, lnby4 = (nx + 3) // 4, (ny + 1) // 2, (nx + 7) // 8, (nx + 3) // 4, \
+        (ny + 3) // 4
+    t16 = b[off[2]:off[2] + nbx4 * nby2 * 8 * nz * 16].view(np.int32).reshape(-1, 4)
+    r4 = b[off[3]:off[3] + lnby4 * nb8 * 32 * nz * 4].view(np.uint32)
+    e8 = b[off[4]:off[4] + lnby4 * nb4 * 16 * nz * 8].view(np.uint32).reshape(-1, 2)
+    t4 = b[off[5]:off[5] + lnby4 * nb8 * 32 * 4].view(np.float32)
     iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     vox = vol.vox.cpu().numpy()            # [ny, nx, nz, 2]
     cols = vol.cols.cpu().numpy()          # [ny, nx, 2]
@@ -181,24 +181,52 @@ def test_k4h_pack_layout(oracle_mod):
     cz = np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)
     i16 = (((iz * nby2 + iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
     np.testing.assert_array_equal(t16[i16], np.concatenate([vz, cz], axis=1))
-    i8 = (((iz * nby4 + iy // 4) * nbx4 + ix // 4) * 16 + (iy % 4) * 4 + ix % 4).reshape(-1)
-    np.testing.assert_array_equal(t8[i8], np.stack([vz[:, 0], cz[:, 0]], axis=1))
-    for t, idx in ((t16, i16), (t8, i8)):
+    i4 = (((iz * lnby4 + iy // 4) * nb8 + ix // 8) * 32 + (iy % 4) * 8 + ix % 8).reshape(-1)
+    np.testing.assert_array_equal(r4[i4], vz[:, 0].view(np.uint32))
+    i8 = (((iz * lnby4 + iy // 4) * nb4 + ix // 4) * 16 + (iy % 4) * 4 + ix % 4).reshape(-1)
+    pz = (vz[:, 1].view(np.uint32) & 0x7fffffff) | ((cz[:, 1].view(np.uint32) & 1) << 31)
+    np.testing.assert_array_equal(e8[i8], np.stack([vz[:, 0].view(np.uint32), pz], axis=1))
+    it = (((iy[0] // 4) * nb8 + ix[0] // 8) * 32 + (iy[0] % 4) * 8 + ix[0] % 8)
+    np.testing.assert_array_equal(t4[it].view(np.uint32), cols[:, :, 0].view(np.uint32))
+    for t, idx in ((t16, i16), (r4, i4), (e8, i8), (t4.view(np.uint32), it.reshape(-1))):
         mask = np.ones(len(t), bool)
         mask[idx] = False
         assert (t[mask] == 0).all()
+    # codes
+    cnbx = cnby = (nx + 7) // 8
+    cw = (cnbx * cnby + 15) // 16
+    cm = b[:cw * 4].view(np.uint32)
     pb = vox[:, :, :, 1].view(np.uint32)
+    rb = vox[:, :, :, 0].view(np.uint32)
     nfz = cols[:, :, 1].view(np.uint32) & 1
-    need = np.zeros((cnby * 8, cnbx * 8), bool)
-    need[:ny, :nx] = ((pb & 0x7fffffff) != 0).any(axis=2) | (nfz != 0)
-    layer0 = np.zeros_like(need)
-    layer0[:ny, :nx] = ((pb[:, :, 0] & 0x7fffffff) != 0) | (nfz != 0)
-    blk = lambda a: a.reshape(cnby, 8, cnbx, 8).any(axis=(1, 3)).reshape(-1)
-    want = np.where(blk(need), 3, 1)
+
+    def blk(a):
+        full = np.zeros((cnby * 8, cnbx * 8), bool)
+        full[:ny, :nx] = a
+        return full.reshape(cnby, 8, cnbx, 8).any(axis=(1, 3)).reshape(-1)
+
+    need = blk(((pb & 0x7fffffff) != 0).any(axis=2) | (nfz != 0))
+    neg = blk((((pb >> 31) != 0) & (pb != 0x80000000)).any(axis=2))
+    nzr = blk(((rb & 0x7fffffff) != 0).any(axis=2))
+    want = np.where(need, np.where(neg, 3, 2), np.where(nzr, 1, 0))
     got = ((cm[:, None] >> (2 * np.arange(16))) & 3).reshape(-1)[:cnbx * cnby]
     np.testing.assert_array_equal(got, want)
-    assert (want == 3).any() and (want == 1).any()
-    assert (blk(need) & ~blk(layer0)).any()  # blocks that only a later layer's psi marks
+    assert (want == 2).any() and (want == 1).any()
+    # bounds hold every column's terrain
+    bsh = 3
+    bnbx = -(-nx // 8)
+    w16 = lambda v: -(-v // 16) * 16
+    bnd = b[w16(cw * 4):].view(np.uint16)[:bnbx * bnbx]
+    sbo = w16(cw * 4) + w16(bnbx * bnbx * 2)
+    sbnbx = -(-bnbx // 4)
+    sbt = b[sbo:sbo + sbnbx * sbnbx * 8].view(np.float32).reshape(-1, 2)
+    yy, xx = np.mgrid[0:ny, 0:nx]
+    e = bnd[(yy >> bsh) * bnbx + (xx >> bsh)].astype(np.uint32)
+    sb = sbt[((yy >> bsh) >> 2) * sbnbx + ((xx >> bsh) >> 2)]
+    ub = sb[..., 0] + (e & 255).astype(np.float32) * sb[..., 1]
+    lb = sb[..., 0] + (e >> 8).astype(np.float32) * sb[..., 1]
+    ter = cols[:, :, 0].view(np.float32)
+    assert (lb <= ter).all() and (ter <= ub).all()
 
 
 @pytest.mark.parametrize("group", [21, 7])

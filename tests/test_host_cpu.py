@@ -36,25 +36,39 @@ def test_header_symbols_exported(lib):
     assert lib.uam_abi_version() == 1
 
 
+def _vpk_sections(nx, ny, nz):
+    """The packed volume's sections (uampath.hip VpkDims): header (codes, bounds, superblocks),
+    bound scratch, 16-B voxels (4 x 2 columns), 4-B risk (4 x 8), 8-B risk/psi (4 x 4), the 4-B
+    column terrain (4 x 8), each 256-B aligned."""
+    al = lambda v: (v + 255) // 256 * 256
+    w16 = lambda v: -(-v // 16) * 16
+    cw = (((nx + 7) // 8) * ((ny + 7) // 8) + 15) // 16
+    bsh = 3
+    while (-(-nx // (1 << bsh))) * (-(-ny // (1 << bsh))) > 16384:
+        bsh += 1
+    bnbx, bnby = -(-nx // (1 << bsh)), -(-ny // (1 << bsh))
+    hdr = w16(cw * 4) + w16(bnbx * bnby * 2) + w16(-(-bnbx // 4) * -(-bnby // 4) * 8)
+    nbx4, nby2, nb8, nb4, lnby4 = (nx + 3) // 4, (ny + 1) // 2, (nx + 7) // 8, (nx + 3) // 4, \
+        (ny + 3) // 4
+    return [al(hdr), al(bnbx * bnby * 8), al(nbx4 * nby2 * 8 * nz * 16),
+            al(lnby4 * nb8 * 32 * nz * 4), al(lnby4 * nb4 * 16 * nz * 8), al(lnby4 * nb8 * 32 * 4)]
+
+
 def test_volume_packed_bytes(lib):
-    """uam_volume_packed_bytes (host only): the 16-B table (4 x 2 blocks per layer), the 8-B
-    table (4 x 4 blocks per layer) and the 2-bit code per 8 x 8 columns, each section 256-B
-    aligned; an invalid description fails loudly."""
+    """uam_volume_packed_bytes (host only) against the packed volume's sections; an invalid
+    description fails loudly."""
     from uam_path_planning_amd import _lib
 
-    al = lambda v: (v + 255) // 256 * 256
     for nx, ny, nz in ((1024, 1024, 64), (300, 300, 7), (1, 1, 1), (1001, 77, 3)):
         vd = _lib.VolumeDesc(nx, ny, nz, 0.0, 20.0, 60.0 / nx, 60.0 / nx, 0.0, 10.0)
         n = ctypes.c_int64()
         assert lib.uam_volume_packed_bytes(ctypes.byref(vd), ctypes.byref(n)) == _lib.UAM_OK
-        nbx4, nby2, nby4 = (nx + 3) // 4, (ny + 1) // 2, (ny + 3) // 4
-        cw = (((nx + 7) // 8) * ((ny + 7) // 8) + 15) // 16
-        want = al(nbx4 * nby2 * 8 * nz * 16) + al(nbx4 * nby4 * 16 * nz * 8) + al(cw * 4)
-        assert n.value == want, (nx, ny, nz)
-    assert n.value >= 0
+        assert n.value == sum(_vpk_sections(nx, ny, nz)), (nx, ny, nz)
     vd = _lib.VolumeDesc(1024, 1024, 64, 0.0, 20.0, 60.0 / 1024, 60.0 / 1024, 0.0, 10.0)
     assert lib.uam_volume_packed_bytes(ctypes.byref(vd), ctypes.byref(n)) == _lib.UAM_OK
-    assert n.value == 1536 * 2**20 + 256 * ((((128 * 128 + 15) // 16) * 4 + 255) // 256)
+    # 1024^2 x 64: 1 GiB of 16-B voxels, 256 MiB of risk, 512 MiB of risk/psi, 4 MiB of terrain,
+    # a 44 KiB header (4 KiB of codes, 32 KiB of 8-column bound blocks, 8 KiB of superblocks)
+    assert n.value == (1024 + 256 + 512 + 4) * 2**20 + 45056 + 131072
     assert lib.uam_volume_packed_bytes(ctypes.byref(vd), None) == _lib.UAM_E_INVALID
     bad = _lib.VolumeDesc(0, 1024, 64, 0.0, 20.0, 1.0, 1.0, 0.0, 10.0)
     assert lib.uam_volume_packed_bytes(ctypes.byref(bad), ctypes.byref(n)) == _lib.UAM_E_INVALID

@@ -720,6 +720,7 @@ __device__ __forceinline__ uint32_t u4_comp(const uint4& r, uint32_t k) {
 // a chunk's per-slot codes, 4 bits per slot
 template <int CH>
 using PkCodes = typename std::conditional<(CH > 8), uint64_t, uint32_t>::type;
+#define PK_CODES_CHECK(CH) static_assert((CH) <= 16, "4 code bits per slot in 64 bits")
 
 // spread the 16 low bits of v to the even bits of the result
 __device__ __forceinline__ uint32_t spread16(uint32_t v) {
@@ -818,12 +819,13 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
     }
 }
 
-// one wave per bound block: {min, max} of its terrain as read (+0.0 on nodata); min = NaN when
-// the block holds a non-finite value
-__global__ __launch_bounds__(256) void k_raster_bminmax(const uint4* __restrict__ rec,
-                                                        int32_t nx, int32_t ny, int32_t bshift,
-                                                        int32_t bnbx, int32_t nbb,
-                                                        float2* __restrict__ scr) {
+// one wave per bound block: {min, max} of its terrain as read, from the 4-B terrain plane (4 x 8-
+// cell blocks, nb8 per row: the raster's t4, the volume's column terrain); min = NaN when the
+// block holds a non-finite value
+__global__ __launch_bounds__(256) void k_t4_bminmax(const float* __restrict__ t4, int32_t nx,
+                                                    int32_t ny, int32_t nb8, int32_t bshift,
+                                                    int32_t bnbx, int32_t nbb,
+                                                    float2* __restrict__ scr) {
     const int32_t blk = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (blk >= nbb) return;  // (whole waves)
@@ -835,8 +837,7 @@ __global__ __launch_bounds__(256) void k_raster_bminmax(const uint4* __restrict_
     bool bad = false;
     for (int k = lane; k < w * h; k += 64) {
         const int iy = y0 + k / w, ix = x0 + k % w;
-        const uint4 r = rec[(int64_t)iy * nx + ix];
-        const float t = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
+        const float t = t4[((((iy >> 2) * nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7))];
         if (!__builtin_isfinite(t)) bad = true;
         mn = fminf(mn, t);
         mx = fmaxf(mx, t);
@@ -5988,48 +5989,80 @@ struct alignas(16) VSlot {  // 32 B per (path, group)
     uint32_t pad;
 };
 
-struct KVol4 {  // the packed volume as K4h reads it
+// The packed volume as K4h reads it (uam_volume_pack; layout: VpkDims).  Header (staged in
+// LDS): a 2-bit code per 8 x 8-column block -- 0: every voxel of its columns has risk == +-0,
+// psi == +-0 and no no-fly flag (nothing to read but the terrain); 1: psi == +-0 and no flag (the
+// 4-B risk plane r4); 2: no psi below zero (the 8-B plane e8 {risk, |psi| | nfz << 31}); 3: the
+// 16-B voxels vp -- then the column terrain's bounds (the raster's scheme: u16 codes per bound
+// block of columns, float2 {base, step} per 4 x 4 bound blocks).  Planes: r4 and the column
+// terrain t4 in 4 x 8-column blocks, e8 in 4 x 4-column blocks (one layer per plane, layer-
+// major), vp in 4 x 2-column blocks.
+struct KVol4 {
     int32_t nx, ny, nz, nbx4, nby2;
     double x0, y_top, z0, dz, inv_dx, inv_dy, inv_dz;
-    const uint4* __restrict__ vp;   // 16-B voxels, 4 x 2-cell blocks
+    const uint4* __restrict__ vp;
     int32_t zshift, nbands;
-    // the 8-B table {risk, terrain} in 4 x 4-cell blocks and the 2-bit code per 8 x 8-column
-    // block (3: a column of the block has psi != +-0 or the no-fly flag -> read vp; 1: vp8)
-    const uint2* __restrict__ vp8;
-    const uint32_t* __restrict__ cmap;
-    int32_t nby4, cnbx, cwords;
+    const uint32_t* __restrict__ hdr;   // codes | bounds | superblocks
+    int32_t hwords, cnbx, bnd_off, sbt_off, bshift, bnbx, sbnbx;
+    int32_t nb8, nb4, lnby4;
+    const uint32_t* __restrict__ r4;
+    const uint2* __restrict__ e8;
+    const float* __restrict__ t4;
 };
 
-constexpr int VPK_CSHIFT = 3;          // code blocks of 8 x 8 columns
-constexpr int VPK_CMAP_LDS = 16 * 1024; // the code map in LDS up to this (2048^2 columns)
+constexpr int VPK_CSHIFT = 3;           // code blocks of 8 x 8 columns
+constexpr int VPK_HDR_LDS = 64 * 1024;  // the header in LDS up to this
 
-__device__ __forceinline__ int64_t vpk8_index(int32_t nbx4, int32_t nby4, int32_t ix, int32_t iy,
-                                              int32_t iz) {
-    return ((((int64_t)iz * nby4 + (iy >> 2)) * nbx4 + (ix >> 2)) << 4) | ((iy & 3) << 2) |
+__device__ __forceinline__ int64_t vr4_index(const KVol4& v, int32_t ix, int32_t iy, int32_t iz) {
+    return ((((int64_t)iz * v.lnby4 + (iy >> 2)) * v.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) |
+           (ix & 7);
+}
+__device__ __forceinline__ int64_t ve8_index(const KVol4& v, int32_t ix, int32_t iy, int32_t iz) {
+    return ((((int64_t)iz * v.lnby4 + (iy >> 2)) * v.nb4 + (ix >> 2)) << 4) | ((iy & 3) << 2) |
            (ix & 3);
 }
+__device__ __forceinline__ int32_t vt4_index(const KVol4& v, int32_t ix, int32_t iy) {
+    return ((((iy >> 2) * v.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7));
+}
 
-// the 8-B table: one thread per entry (padding: zero)
-__global__ __launch_bounds__(256) void k_volume_pack8(const uint2* __restrict__ vox,
-                                                      const uint2* __restrict__ col, int nx,
-                                                      int ny, int nz, int nbx4, int nby4,
-                                                      uint2* __restrict__ out) {
-    const int64_t total = (int64_t)nbx4 * nby4 * 16 * nz;
+// the 4-B risk plane and the 8-B {risk, |psi| | nfz << 31} plane: one thread per r4 entry,
+// which also writes its cell's e8 entry (padding: zero)
+__global__ __launch_bounds__(256) void k_volume_pack_re(const uint2* __restrict__ vox,
+                                                        const uint2* __restrict__ col, KVol4 v,
+                                                        uint32_t* __restrict__ r4,
+                                                        uint2* __restrict__ e8) {
+    const int64_t total = (int64_t)v.nz * v.lnby4 * v.nb8 * 32;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t w = (int32_t)(i & 15);
-        const int64_t blk = i >> 4;
-        const int32_t bx = (int32_t)(blk % nbx4);
-        const int64_t r = blk / nbx4;
-        const int32_t by = (int32_t)(r % nby4), iz = (int32_t)(r / nby4);
-        const int32_t ix = bx * 4 + (w & 3), iy = by * 4 + (w >> 2);
-        uint2 o = make_uint2(0u, 0u);
-        if (ix < nx && iy < ny) {
-            const int64_t c = (int64_t)iy * nx + ix;
-            o = make_uint2(vox[c * nz + iz].x, col[c].x);
+        const int32_t w = (int32_t)(i & 31);
+        const int64_t blk = i >> 5;
+        const int32_t bx = (int32_t)(blk % v.nb8);
+        const int64_t r = blk / v.nb8;
+        const int32_t by = (int32_t)(r % v.lnby4), iz = (int32_t)(r / v.lnby4);
+        const int32_t ix = bx * 8 + (w & 7), iy = by * 4 + (w >> 3);
+        uint32_t risk = 0u, pz = 0u;
+        if (ix < v.nx && iy < v.ny) {
+            const int64_t c = (int64_t)iy * v.nx + ix;
+            const uint2 a = vox[c * v.nz + iz];
+            risk = a.x;
+            pz = (a.y & 0x7fffffffu) | ((col[c].y & UAM_FLAG_NFZ) ? 0x80000000u : 0u);
         }
-        out[i] = o;
+        r4[i] = risk;
+        if (ix < v.nb4 * 4) e8[ve8_index(v, ix, iy, iz)] = make_uint2(risk, pz);
     }
+}
+
+// the column terrain plane (one thread per entry; padding: zero)
+__global__ __launch_bounds__(256) void k_volume_pack_t4(const uint2* __restrict__ col, KVol4 v,
+                                                        float* __restrict__ t4) {
+    const int64_t total = (int64_t)v.lnby4 * v.nb8 * 32;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int32_t w = (int32_t)(i & 31);
+    const int64_t blk = i >> 5;
+    const int32_t bx = (int32_t)(blk % v.nb8), by = (int32_t)(blk / v.nb8);
+    const int32_t ix = bx * 8 + (w & 7), iy = by * 4 + (w >> 3);
+    t4[i] = (ix < v.nx && iy < v.ny) ? __uint_as_float(col[(int64_t)iy * v.nx + ix].x) : 0.0f;
 }
 
 // the code map: one thread per 32-bit word (16 blocks of 8 x 8 columns)
@@ -6044,14 +6077,19 @@ __global__ __launch_bounds__(256) void k_volume_codes(const uint2* __restrict__ 
         const int b = wd * 16 + k;
         if (b >= nblocks) break;
         const int by = b / cnbx, bx = b - by * cnbx;
-        uint32_t code = 1u;
+        bool need = false, neg = false, nz_r = false;
         for (int y = by << VPK_CSHIFT; y < min(ny, (by + 1) << VPK_CSHIFT); ++y)
             for (int x = bx << VPK_CSHIFT; x < min(nx, (bx + 1) << VPK_CSHIFT); ++x) {
                 const int64_t c = (int64_t)y * nx + x;
-                if (col[c].y & UAM_FLAG_NFZ) code = 3u;
-                for (int iz = 0; iz < nz; ++iz)  // psi of every layer (a voxel's own)
-                    if (vox[c * nz + iz].y & 0x7fffffffu) code = 3u;
+                if (col[c].y & UAM_FLAG_NFZ) need = true;
+                for (int iz = 0; iz < nz; ++iz) {  // every layer's own psi and risk
+                    const uint2 a = vox[c * nz + iz];
+                    if (a.y & 0x7fffffffu) need = true;
+                    if ((a.y >> 31) && a.y != 0x80000000u) neg = true;
+                    if (a.x & 0x7fffffffu) nz_r = true;
+                }
             }
+        const uint32_t code = need ? (neg ? 3u : 2u) : nz_r ? 1u : 0u;
         word |= code << (2 * k);
     }
     cmap[wd] = word;
@@ -6129,17 +6167,31 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 }
 
 // every (path, group) item in sorted order: points (x, y by the arc formula, z on the linear
-// climb), ONE 16-B load per waypoint from the packed volume (a slot outside the volume or past
-// the group's end reads the first voxel line and is masked off), the branch-free consume
+// climb), per waypoint one 16-B value load (by the column block's code: the r4 / e8 entries'
+// aligned 16 B, the 16-B voxel, or the dummy line) and a 4-B terrain load only where the
+// terrain could still decide an output (the dummy line otherwise), then the branch-free consume.
+//
+// The terrain by bounds (as K2h's; the outputs are exactly the per-waypoint ones).  Waypoint j
+// in the volume has lb_j <= T_j <= ub_j (pk_bounds over the column grid) and
+//   below_j = zc_j < T_j (zc_j its layer centre): decided when zc_j < lb_j (1) or zc_j >= ub_j
+//       (0), else its terrain is fetched;
+//   c_j = z_j - T_j, whose path minimum is min_clearance: z_j - ub_j <= c_j <= z_j - lb_j (the
+//       float64 subtraction is monotone).  The item keeps Ub, the minimum of z - lb over a sample
+//       of its path's in-volume waypoints (every kg.lb_stride-th, the waypoints' own
+//       operations) and over its own so far, an upper bound of the path minimum M, and E, the
+//       minimum of the c_j it has taken exactly; it fetches w iff !(z_w - ub_w >= E) &&
+//       !(z_w - ub_w > Ub).  If w* holds M and is not taken: z - ub >= E gives M >= E >= M,
+//       and z - ub > Ub >= M is impossible.  NaN bounds (no bound) always fetch.
 template <int CH>
 __global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
                                                                               KGrp kg) {
-    // unit-arc rows, then j / (W-1), then the code map
+    PK_CODES_CHECK(CH);
+    // unit-arc rows, then j / (W-1), then the header
     extern __shared__ __attribute__((aligned(16))) double2 s_u[];
     const int N = p.N, W = kg.W;
     const int nu = kg.D * N;
     double* s_jw = reinterpret_cast<double*>(s_u + nu);
-    uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_jw + W);
+    uint32_t* s_hdr = reinterpret_cast<uint32_t*>(s_jw + ((W + 1) & ~1));
     // the item's order entry and pair before the staging (their round trips overlap it)
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const bool live = pos < kg.n_items;
@@ -6153,7 +6205,11 @@ __global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     const double2 pc = *reinterpret_cast<const double2*>(prp + 4);
     for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
     for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
-    for (int i = threadIdx.x; i < vs.cwords; i += 256) s_cm[i] = vs.cmap[i];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(vs.hdr);
+        uint4* dst = reinterpret_cast<uint4*>(s_hdr);
+        for (int i = threadIdx.x; i < (vs.hwords >> 2); i += 256) dst[i] = src[i];
+    }
     __syncthreads();
     if (!live) return;
     const double ax = pa.x, ay = pa.y, za = pb.x, bx = pb.y, by = pc.x, zb = pc.y;
@@ -6168,66 +6224,129 @@ __global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;
     };
-    const uint4* const dummy = vs.vp;
-    double gc = 0.0, gn = 0.0, cm = INFINITY;
+    // waypoint j: its altitude, and its voxel (false outside the volume or NaN)
+    auto voxel_of = [&](int j, double& z, int32_t& ix, int32_t& iy, int32_t& iz) -> bool {
+        const double2 u = urow[min(max(j - 1, 0), N - 1)];
+        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
+        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+        x0 = j == 0 ? ax : j == W - 1 ? bx : x0;
+        x1 = j == 0 ? ay : j == W - 1 ? by : x1;
+        z = vz_at(za, zb, s_jw[min(j, W - 1)]);
+        const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
+        const double tz = (z - vs.z0) * vs.inv_dz;
+        const bool in = (tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) &&
+                        (ty < (double)vs.ny) && (tz >= 0.0) && (tz < (double)vs.nz);
+        ix = in ? (int32_t)tx : 0;
+        iy = in ? (int32_t)ty : 0;
+        iz = in ? (int32_t)tz : 0;
+        return in;
+    };
+    auto bounds = [&](int32_t ix, int32_t iy, float& ub, float& lb) {
+        const int32_t bx2 = ix >> vs.bshift, by2 = iy >> vs.bshift;
+        const uint32_t e = reinterpret_cast<const uint16_t*>(s_hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
+        const float2 sb = reinterpret_cast<const float2*>(s_hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx +
+                                                                              (bx2 >> 2)];
+        ub = sb.x + (float)(e & 255u) * sb.y;
+        lb = sb.x + (float)(e >> 8) * sb.y;
+    };
+    // the path's sampled upper bound of its minimum clearance
+    double Ub = INFINITY;
+    for (int j = 0; j < W; j += kg.lb_stride) {
+        double z;
+        int32_t ix, iy, iz;
+        const bool in = voxel_of(j, z, ix, iy, iz);
+        float ub, lb;
+        bounds(ix, iy, ub, lb);
+        if (in) Ub = fmin(Ub, z - (double)lb);
+    }
+    const uint4* const vdummy = reinterpret_cast<const uint4*>(vs.r4);
+    double gc = 0.0, gn = 0.0, E = INFINITY;
     uint32_t nh = 0, off = 0, bel = 0;
     for (int jc = j0; jc < j1; jc += CH) {
         uint4 r[CH];
+        float tv[CH];
         double zt[CH];
         int32_t izt[CH];
-        uint32_t inb = 0, full = 0, odd = 0;
+        uint32_t inb = 0, tk = 0, kb = 0, bv = 0;  // in; terrain taken; below known; its value
+        // the layer centre of layer iz (k_v_eval's below-terrain test)
+        auto zc_of = [&](int32_t iz) { return vs.z0 + ((double)iz + 0.5) * vs.dz; };
+        PkCodes<CH> cs = 0;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int j = jc + t;
-            const double2 u = urow[min(max(j - 1, 0), N - 1)];
-            double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
-            double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-            x0 = j == 0 ? ax : j == W - 1 ? bx : x0;
-            x1 = j == 0 ? ay : j == W - 1 ? by : x1;
-            const double z = vz_at(za, zb, s_jw[min(j, W - 1)]);
-            zt[t] = z;
-            const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
-            const double tz = (z - vs.z0) * vs.inv_dz;
-            const uint4* ptr = dummy;
-            izt[t] = 0;
-            if ((j < j1) && (tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) &&
-                (ty < (double)vs.ny) && (tz >= 0.0) && (tz < (double)vs.nz)) {
+            int32_t ix, iy, iz;
+            const bool in = voxel_of(j, zt[t], ix, iy, iz);
+            const uint4* ptr = vdummy;
+            const float* tp = vs.t4;
+            izt[t] = iz;
+            const double zc = zc_of(iz);
+            if ((j < j1) && in) {
                 inb |= 1u << t;
-                const int32_t ix = (int32_t)tx, iy = (int32_t)ty, iz = (int32_t)tz;
-                izt[t] = iz;
                 const int32_t b = (iy >> VPK_CSHIFT) * vs.cnbx + (ix >> VPK_CSHIFT);
-                if ((s_cm[b >> 4] >> ((b & 15) * 2)) & 2u) {  // no-fly support: 16-B voxel
-                    full |= 1u << t;
+                const uint32_t code = (s_hdr[b >> 4] >> ((b & 15) * 2)) & 3u;
+                uint32_t sub = 0;
+                if (code == 3u) {
                     ptr = vs.vp + vpk_index(vs.nbx4, vs.nby2, ix, iy, iz);
-                } else {  // the aligned pair of 8-B entries holding the voxel
-                    const int64_t a = vpk8_index(vs.nbx4, vs.nby4, ix, iy, iz);
-                    odd |= (uint32_t)(a & 1) << t;
-                    ptr = reinterpret_cast<const uint4*>(vs.vp8 + (a & ~(int64_t)1));
+                } else {
+                    if (code == 2u) {
+                        const int64_t a = ve8_index(vs, ix, iy, iz);
+                        ptr = reinterpret_cast<const uint4*>(vs.e8 + (a & ~(int64_t)1));
+                        sub = (uint32_t)(a & 1) * 2u;
+                    } else if (code == 1u) {
+                        const int64_t a = vr4_index(vs, ix, iy, iz);
+                        ptr = reinterpret_cast<const uint4*>(vs.r4 + (a & ~(int64_t)3));
+                        sub = (uint32_t)(a & 3);
+                    }
+                    float ub, lb;
+                    bounds(ix, iy, ub, lb);
+                    const double clo = zt[t] - (double)ub;
+                    Ub = fmin(Ub, zt[t] - (double)lb);
+                    if (lb == ub) {  // a block of one terrain value: every term exactly
+                        E = fmin(E, zt[t] - (double)ub);
+                        kb |= 1u << t;
+                        bv |= (zc < (double)ub ? 1u : 0u) << t;
+                    } else {
+                        if (zc < (double)lb) {
+                            kb |= 1u << t;
+                            bv |= 1u << t;
+                        } else if (zc >= (double)ub) {
+                            kb |= 1u << t;
+                        }
+                        if (!((kb >> t) & 1u) || (!(clo >= E) && !(clo > Ub))) {
+                            tk |= 1u << t;
+                            tp = vs.t4 + vt4_index(vs, ix, iy);
+                        }
+                    }
                 }
+                cs |= (PkCodes<CH>)(code | (sub << 2)) << (4 * t);
             }
             r[t] = *ptr;
+            tv[t] = *tp;
         }
         const int nv = min(CH, j1 - jc);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const bool vl = t < nv, in = (inb >> t) & 1u, fl = (full >> t) & 1u,
-                       od = (odd >> t) & 1u;
-            const uint4 rt = r[t];
-            // 8-B entries: psi is +-0 and no no-fly flag in the block (exact no-ops)
-            const uint32_t risk = fl ? rt.x : od ? rt.z : rt.x;
-            const float ter = __uint_as_float(fl ? rt.z : od ? rt.w : rt.y);
+            const bool vl = t < nv, in = (inb >> t) & 1u;
+            const uint32_t cst = (uint32_t)(cs >> (4 * t)) & 15u, code = cst & 3u;
+            uint32_t risk, psi, hit;
+            float rter;
+            pk_terms(r[t], cst, risk, psi, hit, rter);
             gc = gc + over_n(in ? (double)__uint_as_float(risk) : 0.0);
-            gn = gn + ((in && fl) ? (double)__uint_as_float(rt.y) : 0.0);
-            nh += (in && fl && (rt.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+            gn = gn + ((in && (code & 2u)) ? (double)__uint_as_float(psi) : 0.0);
+            nh += in ? hit : 0u;
             off += (vl && !in) ? 1u : 0u;
-            bel += (in && (vs.z0 + ((double)izt[t] + 0.5) * vs.dz < (double)ter)) ? 1u : 0u;
-            cm = in ? fmin(cm, zt[t] - (double)ter) : cm;
+            // the exact terrain, where taken: the 16-B voxel's (code 3) or the fetched one
+            const bool ex = in && (code == 3u || ((tk >> t) & 1u));
+            const float ter = code == 3u ? rter : tv[t];
+            const uint32_t below = ex ? (zc_of(izt[t]) < (double)ter ? 1u : 0u) : ((bv >> t) & 1u);
+            bel += in ? below : 0u;
+            E = ex ? fmin(E, zt[t] - (double)ter) : E;
         }
     }
     VSlot o;
     o.cost = gc;
     o.psi = gn;
-    o.cm = cm;
+    o.cm = E;
     o.cnt = nh | (off << 8) | (bel << 16);
     o.pad = 0;
     reinterpret_cast<VSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
@@ -7592,12 +7711,13 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
     if ((size_t)D * ctx->kp.N * 16 > (size_t)G_UTAB_LDS) return 0;
-    if ((size_t)kv.cwords * 4 > (size_t)VPK_CMAP_LDS) return 0;
+    if ((size_t)kv.hwords * 4 > (size_t)VPK_HDR_LDS) return 0;
     // workgroups per CU: 2 by default through an LDS floor of 60 000 B (UAM_OPT_K2G_LDS_FLOOR
     // sets another): fewer items resident per XCD, so fewer of their lines miss L2 -- cfg5
     // 0.415 ms at 2 with 11 gathers in flight, 0.418 at 3, 0.453 at the 6 the LDS allows with 6
     // (profiles/r04/sweep7)
-    const size_t lds = std::max((size_t)D * ctx->kp.N * 16 + (size_t)W * 8 + (size_t)kv.cwords * 4,
+    const size_t lds = std::max((size_t)D * ctx->kp.N * 16 + (size_t)((W + 1) & ~1) * 8 +
+                                    (size_t)kv.hwords * 4,
                                 (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 60000, 160 * 1024));
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
@@ -7643,6 +7763,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
+    kg.lb_stride = ctx->k2h_lbs;
     kg.n_items = n_items;
     size_t o = 0;
     kg.slot = (GSlot*)(w + o), o += b_slot;  // VSlot
@@ -7666,10 +7787,10 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     // gathers in flight per lane: 11 by default (k_v_eval<8> spills at 4 waves per SIMD, so 8 and
     // 11 are built for 3, 16 and 21 for 2)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 11;
-    static const VEvalFn vevals[6] = {k_v_eval<6>,  k_v_eval<7>,  k_v_eval<8>,
-                                      k_v_eval<11>, k_v_eval<16>, k_v_eval<21>};
-    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3
-                                                                    : chl == 16 ? 4 : 5];
+    // (21 runs as 16: a chunk's per-slot codes take 4 bits each of 64)
+    static const VEvalFn vevals[5] = {k_v_eval<6>, k_v_eval<7>, k_v_eval<8>, k_v_eval<11>,
+                                      k_v_eval<16>};
+    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3 : 4];
     if (lds > 64 * 1024 && !ctx->k4h_attrs) {
         for (VEvalFn f : vevals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -7989,8 +8110,9 @@ int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, 
     hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, r4,
                        kr, (uint32_t*)(b + d.off_p4), (float*)(b + d.off_t4),
                        (uint2*)(b + d.off_e8));
-    hipLaunchKernelGGL(k_raster_bminmax, dim3((unsigned)((d.nbb + 3) / 4)), dim3(256), 0, s, r4,
-                       kr.nx, kr.ny, d.bsh, d.bnbx, d.nbb, (float2*)(b + d.off_scr));
+    hipLaunchKernelGGL(k_t4_bminmax, dim3((unsigned)((d.nbb + 3) / 4)), dim3(256), 0, s,
+                       (const float*)(b + d.off_t4), kr.nx, kr.ny, d.nb8, d.bsh, d.bnbx, d.nbb,
+                       (float2*)(b + d.off_scr));
     hipLaunchKernelGGL(k_raster_bounds, dim3((unsigned)((d.nbb + 255) / 256)), dim3(256), 0, s,
                        (const float2*)(b + d.off_scr), d.bnbx, d.bnby, d.sbnbx,
                        (uint16_t*)(b + (size_t)d.bnd_off * 4), (float2*)(b + (size_t)d.sbt_off * 4));
@@ -8103,20 +8225,64 @@ int uam_volume_build(uam_ctx* ctx, const uam_volume_desc* vd, const void* rec2d,
 namespace {
 // the packed volume's dimensions (uam_volume_pack): 4 x 2-cell blocks, nz layer planes
 // [16-B table | 8-B table | code map], 256-B aligned sections
+// packed-volume layout (uam_volume_pack), 256-B aligned sections: header (the code map, cwords
+// words padded to 16 B; the column terrain's bound table, u16 per bound block of 2^bsh columns,
+// at most PK_BOUND_MAX, padded to 16 B; the superblock table, float2 per 4 x 4 bound blocks) |
+// scratch (float2 per bound block) | 16-B voxels in 4 x 2-column blocks | 4-B risk in 4 x 8-
+// column blocks | 8-B {risk, |psi| | nfz} in 4 x 4-column blocks | the 4-B column terrain in
+// 4 x 8-column blocks (one plane)
 struct VpkDims {
-    int32_t nbx4, nby2, nby4, cnbx, cnby, cwords;
-    int64_t off8, offc, bytes;
+    int32_t nbx4, nby2, cnbx, cnby, cwords;
+    int32_t bsh, bnbx, bnby, nbb, sbnbx, sbnby;
+    int32_t hwords, bnd_off, sbt_off;
+    int32_t nb8, nb4, lnby4;
+    int64_t off_scr, off_vp, off_r4, off_e8, off_t4, bytes;
 };
 void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
     v->nbx4 = (d->nx + 3) >> 2;
     v->nby2 = (d->ny + 1) >> 1;
-    v->nby4 = (d->ny + 3) >> 2;
     v->cnbx = (d->nx + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
     v->cnby = (d->ny + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
     v->cwords = (v->cnbx * v->cnby + 15) / 16;
-    v->off8 = al256((int64_t)v->nbx4 * v->nby2 * 8 * d->nz * 16);
-    v->offc = v->off8 + al256((int64_t)v->nbx4 * v->nby4 * 16 * d->nz * 8);
-    v->bytes = v->offc + al256((int64_t)v->cwords * 4);
+    v->bsh = 3;
+    auto nblk = [&](int s) {
+        return (int64_t)((d->nx + (1 << s) - 1) >> s) * ((d->ny + (1 << s) - 1) >> s);
+    };
+    while (nblk(v->bsh) > PK_BOUND_MAX) ++v->bsh;
+    v->bnbx = (d->nx + (1 << v->bsh) - 1) >> v->bsh;
+    v->bnby = (d->ny + (1 << v->bsh) - 1) >> v->bsh;
+    v->nbb = v->bnbx * v->bnby;
+    v->sbnbx = (v->bnbx + 3) >> 2;
+    v->sbnby = (v->bnby + 3) >> 2;
+    auto w16 = [](int64_t bytes) { return (int32_t)(((bytes + 15) & ~(int64_t)15) / 4); };
+    v->bnd_off = w16((int64_t)v->cwords * 4);
+    v->sbt_off = v->bnd_off + w16((int64_t)v->nbb * 2);
+    v->hwords = v->sbt_off + w16((int64_t)v->sbnbx * v->sbnby * 8);
+    v->nb8 = (d->nx + 7) >> 3;
+    v->nb4 = (d->nx + 3) >> 2;
+    v->lnby4 = (d->ny + 3) >> 2;
+    v->off_scr = al256((int64_t)v->hwords * 4);
+    v->off_vp = v->off_scr + al256((int64_t)v->nbb * 8);
+    v->off_r4 = v->off_vp + al256((int64_t)v->nbx4 * v->nby2 * 8 * d->nz * 16);
+    v->off_e8 = v->off_r4 + al256((int64_t)v->lnby4 * v->nb8 * 32 * d->nz * 4);
+    v->off_t4 = v->off_e8 + al256((int64_t)v->lnby4 * v->nb4 * 16 * d->nz * 8);
+    v->bytes = v->off_t4 + al256((int64_t)v->lnby4 * v->nb8 * 32 * 4);
+}
+// the packed volume's view for K4h
+void vpk_kvol(const uam_volume_desc* vd, const VpkDims& v, const void* packed, KVol4* kv) {
+    const char* b = (const char*)packed;
+    kv->nx = vd->nx, kv->ny = vd->ny, kv->nz = vd->nz;
+    kv->nbx4 = v.nbx4, kv->nby2 = v.nby2;
+    kv->x0 = vd->x0, kv->y_top = vd->y_top, kv->z0 = vd->z0, kv->dz = vd->dz;
+    kv->inv_dx = 1.0 / vd->dx, kv->inv_dy = 1.0 / vd->dy, kv->inv_dz = 1.0 / vd->dz;
+    kv->vp = (const uint4*)(b + v.off_vp);
+    kv->hdr = (const uint32_t*)b;
+    kv->hwords = v.hwords, kv->cnbx = v.cnbx, kv->bnd_off = v.bnd_off, kv->sbt_off = v.sbt_off;
+    kv->bshift = v.bsh, kv->bnbx = v.bnbx, kv->sbnbx = v.sbnbx;
+    kv->nb8 = v.nb8, kv->nb4 = v.nb4, kv->lnby4 = v.lnby4;
+    kv->r4 = (const uint32_t*)(b + v.off_r4);
+    kv->e8 = (const uint2*)(b + v.off_e8);
+    kv->t4 = (const float*)(b + v.off_t4);
 }
 }  // namespace
 
@@ -8134,8 +8300,8 @@ int uam_volume_packed_bytes(const uam_volume_desc* vd, int64_t* bytes) {
 int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, void* packed,
                     uam_stream stream) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
-    KVolume kv;
-    int st = make_kvolume(vd, &kv);
+    KVolume kv0;
+    int st = make_kvolume(vd, &kv0);
     if (st) return st;
     if (!vol || !packed) return fail(UAM_E_INVALID, "volume pack pointer is NULL");
     if (((uintptr_t)vol & 255) || ((uintptr_t)packed & 255))
@@ -8143,17 +8309,29 @@ int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, vo
     DeviceGuard dg(ctx->device);
     VpkDims v;
     vpk_dims(vd, &v);
+    KVol4 kv{};
+    vpk_kvol(vd, v, packed, &kv);
     const uint2* vx = (const uint2*)vol;
     const uint2* cl = (const uint2*)((const char*)vol + vol_col_offset(vd));
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for(v.off8 / 16, 256)), dim3(256), 0, s, vx, cl,
-                       vd->nx, vd->ny, vd->nz, v.nbx4, v.nby2, (uint4*)packed);
-    hipLaunchKernelGGL(k_volume_pack8, dim3(grid_for((v.offc - v.off8) / 8, 256)), dim3(256), 0,
-                       s, vx, cl, vd->nx, vd->ny, vd->nz, v.nbx4, v.nby4,
-                       (uint2*)((char*)packed + v.off8));
+    char* b = (char*)packed;
+    HIP_TRY(hipMemsetAsync(b, 0, (size_t)v.off_scr, s));  // header padding
+    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for((v.off_r4 - v.off_vp) / 16, 256)), dim3(256),
+                       0, s, vx, cl, vd->nx, vd->ny, vd->nz, v.nbx4, v.nby2,
+                       (uint4*)(b + v.off_vp));
+    hipLaunchKernelGGL(k_volume_pack_re, dim3(grid_for((v.off_e8 - v.off_r4) / 4, 256)), dim3(256),
+                       0, s, vx, cl, kv, (uint32_t*)(b + v.off_r4), (uint2*)(b + v.off_e8));
+    const int64_t nt4 = (int64_t)v.lnby4 * v.nb8 * 32;
+    hipLaunchKernelGGL(k_volume_pack_t4, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s, cl,
+                       kv, (float*)(b + v.off_t4));
     hipLaunchKernelGGL(k_volume_codes, dim3(grid_for(v.cwords, 256)), dim3(256), 0, s, vx, cl,
-                       vd->nx, vd->ny, vd->nz, v.cnbx, v.cnbx * v.cnby, v.cwords,
-                       (uint32_t*)((char*)packed + v.offc));
+                       vd->nx, vd->ny, vd->nz, v.cnbx, v.cnbx * v.cnby, v.cwords, (uint32_t*)b);
+    hipLaunchKernelGGL(k_t4_bminmax, dim3((unsigned)((v.nbb + 3) / 4)), dim3(256), 0, s,
+                       (const float*)(b + v.off_t4), vd->nx, vd->ny, v.nb8, v.bsh, v.bnbx, v.nbb,
+                       (float2*)(b + v.off_scr));
+    hipLaunchKernelGGL(k_raster_bounds, dim3((unsigned)((v.nbb + 255) / 256)), dim3(256), 0, s,
+                       (const float2*)(b + v.off_scr), v.bnbx, v.bnby, v.sbnbx,
+                       (uint16_t*)(b + (size_t)v.bnd_off * 4), (float2*)(b + (size_t)v.sbt_off * 4));
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
@@ -8178,16 +8356,9 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
         if (!pairs6 || !utab) return fail(UAM_E_INVALID, "pointer is NULL");
         if ((uintptr_t)packed & 255) return fail(UAM_E_INVALID, "packed volume not 256-B aligned");
         KVol4 kv{};
-        kv.nx = vd->nx, kv.ny = vd->ny, kv.nz = vd->nz;
         VpkDims v;
         vpk_dims(vd, &v);
-        kv.nbx4 = v.nbx4, kv.nby2 = v.nby2, kv.nby4 = v.nby4, kv.cnbx = v.cnbx;
-        kv.cwords = v.cwords;
-        kv.vp8 = (const uint2*)((const char*)packed + v.off8);
-        kv.cmap = (const uint32_t*)((const char*)packed + v.offc);
-        kv.x0 = vd->x0, kv.y_top = vd->y_top, kv.z0 = vd->z0, kv.dz = vd->dz;
-        kv.inv_dx = 1.0 / vd->dx, kv.inv_dy = 1.0 / vd->dy, kv.inv_dz = 1.0 / vd->dz;
-        kv.vp = (const uint4*)packed;
+        vpk_kvol(vd, v, packed, &kv);
         int zs = 0;  // altitude bands: at most 16, or UAM_OPT_K4H_BAND layers each
         if (ctx->k4h_band > 0) {
             while ((1 << zs) < ctx->k4h_band) ++zs;
