@@ -230,7 +230,7 @@ def main():
             setup["raster_bytes"] = table.numel() * 4
         if volume_mode and not args.no_pack:
             t1 = time.perf_counter()
-            # every rank derives K4h's packed copy (16-B voxels in 4 x 2-cell blocks) locally
+            # every rank derives K4h's packed copy (uam_volume_pack) locally
             eng.volume_pack(volume)
             torch.cuda.synchronize()
             setup["volume_pack_ms"] = round((time.perf_counter() - t1) * 1e3, 3)

@@ -260,11 +260,14 @@ int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* re
  *           as read (+0 on nodata); {NaN, NaN} where the superblock holds a non-finite terrain;
  *   scratch the bound blocks' {min, max} (float2 each) while packing;
  *   planes  phi (4 B) and the terrain as read (4 B) in 4 x 8-cell blocks (one 128-B line),
- *           {phi, |psi_nfz| | nfz << 31} (8 B) in 4 x 4-cell blocks.
+ *           {phi, |psi_nfz| | nfz << 31} (8 B) in the same blocks (two 128-B lines) and the
+ *           16-B records (four lines), at one index for all four.
  * K2h reads a waypoint's terrain only where its bound could still be the path's maximum (the
  * maximum is order-free, so min_clearance is unchanged bit for bit); K2g and K2s read it for
- * every waypoint.  uam_raster_pack_shape gives the bytes of the caller's buffer (4096^2:
- * 56 KiB of header + 128 KiB of scratch + 256 MiB of planes); block as uam_raster_summary
+ * every waypoint.  K2h addresses the copy by 32-bit offsets (it stands aside for a copy of
+ * 4 GiB or more); packing needs nx, ny < 2^24.  uam_raster_pack_shape gives the bytes of the
+ * caller's buffer (4096^2: 56 KiB of header + 128 KiB of scratch + 512 MiB of planes); block as
+ * uam_raster_summary
  * (0 = automatic), and the same block must be passed to uam_eval_generated.  Rebuild the copy
  * whenever rec changes. */
 int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
@@ -310,11 +313,12 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
  *           column terrain's bounds in the packed raster's scheme (u16 per bound block of
  *           columns, float2 {base, step} per 4 x 4 bound blocks);
  *   scratch the bound blocks' {min, max} while packing;
- *   16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} per (ix, iy, iz) in
- *           4 x 2-column blocks of one layer (code 3);
- *   4-B risk per voxel in 4 x 8-column blocks of one layer (code 1);
- *   8-B {risk, |psi_nfz| | nfz << 31} per voxel in 4 x 4-column blocks of one layer (code 2);
- *   the 4-B column terrain (+0 on nodata) in 4 x 8-column blocks.
+ *   4-B risk per voxel in 4 x 8-column blocks of one layer, layer-major (code 1; index i4);
+ *   the 4-B column terrain (+0 on nodata) in the same blocks (one layer);
+ *   8-B {risk, |psi_nfz| | nfz << 31} per voxel at i4 (code 2);
+ *   16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} at i4 (code 3).
+ * K4h addresses the copy by 32-bit offsets: it stands aside (the batch runs on vol_dev) for a
+ * copy of 4 GiB or more or a layer of 2^24 or more entries.
  * K4h reads a waypoint's terrain only where it could still decide min_clearance or
  * below_terrain (the outputs are unchanged bit for bit).  uam_volume_pack derives it from a
  * built volume (vol_dev); packed_dev holds uam_volume_packed_bytes bytes (1.75 GiB at

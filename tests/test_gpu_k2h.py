@@ -217,22 +217,24 @@ def _pack_dims(nx, ny, block):
     sbnbx, sbnby = -(-bnbx // 4), -(-bnby // 4)
     hwords = sbt_off + w16(sbnbx * sbnby * 8)
     a256 = lambda v: -(-v // 256) * 256
-    nb8, nb4, lnby = -(-nx // 8), -(-nx // 4), -(-ny // 4)
+    nb8, lnby = -(-nx // 8), -(-ny // 4)
     off_p4 = a256(hwords * 4) + a256(bnbx * bnby * 8)
     off_t4 = off_p4 + a256(lnby * nb8 * 32 * 4)
     off_e8 = off_t4 + a256(lnby * nb8 * 32 * 4)
+    off_r16 = off_e8 + a256(lnby * nb8 * 32 * 8)
     return dict(words=words, bsh=bsh, bnbx=bnbx, bnby=bnby, bnd_off=bnd_off, sbt_off=sbt_off,
-                sbnbx=sbnbx, sbnby=sbnby, hwords=hwords, nb8=nb8, nb4=nb4, off_p4=off_p4,
-                off_t4=off_t4, off_e8=off_e8)
+                sbnbx=sbnbx, sbnby=sbnby, hwords=hwords, nb8=nb8, off_p4=off_p4,
+                off_t4=off_t4, off_e8=off_e8, off_r16=off_r16,
+                bytes=off_r16 + a256(lnby * nb8 * 32 * 16))
 
 
 def _check_pack(raster, rec):
     """uam_raster_pack against its definition (uampath.hip, packed raster): the block codes,
-    the three planes bit for bit, and bounds that hold every cell's terrain."""
+    the four planes bit for bit, and bounds that hold every cell's terrain."""
     ny, nx = rec.shape[:2]
     B = raster.block
     d = _pack_dims(nx, ny, B)
-    raw = raster.packed.cpu().numpy().view(np.uint8)
+    raw = raster.packed.cpu().numpy().view(np.uint8).reshape(-1)
     bits = rec.view(np.uint32)
     phi, psi, fl = bits[..., 0], bits[..., 1], bits[..., 3]
     ter = np.where(fl & 4, np.float32(0.0), rec[..., 2]).astype(np.float32)
@@ -247,18 +249,20 @@ def _check_pack(raster, rec):
             nz = ((phi[sl] & 0x7fffffff) != 0).any()
             want = (3 if neg else 2) if need else (1 if nz else 0)
             b = by * nbx + bx
-            assert (cw[b >> 4] >> ((b & 15) * 2)) & 3 == want, (bx, by)
+            assert ((int(cw[b >> 4]) >> ((b & 15) * 2)) & 3) == want, (bx, by)
     # planes
     iy, ix = np.mgrid[0:ny, 0:nx]
     a4 = (((iy >> 2) * d["nb8"] + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7)
-    a8 = (((iy >> 2) * d["nb4"] + (ix >> 2)) << 4) | ((iy & 3) << 2) | (ix & 3)
     p4 = raw[d["off_p4"]:d["off_t4"]].view(np.uint32)
     t4 = raw[d["off_t4"]:d["off_e8"]].view(np.float32)
-    e8 = raw[d["off_e8"]:].view(np.uint32).reshape(-1, 2)
+    e8 = raw[d["off_e8"]:d["off_r16"]].view(np.uint32).reshape(-1, 2)
+    r16 = raw[d["off_r16"]:d["bytes"]].view(np.uint32).reshape(-1, 4)
+    assert raw.size >= d["bytes"]
+    np.testing.assert_array_equal(r16[a4], bits.reshape(ny, nx, 4))
     np.testing.assert_array_equal(p4[a4], phi)
     np.testing.assert_array_equal(t4[a4].view(np.uint32), ter.view(np.uint32))
-    np.testing.assert_array_equal(e8[a8, 0], phi)
-    np.testing.assert_array_equal(e8[a8, 1], (psi & 0x7fffffff) | ((fl & 1) << 31).astype(np.uint32))
+    np.testing.assert_array_equal(e8[a4, 0], phi)
+    np.testing.assert_array_equal(e8[a4, 1], (psi & 0x7fffffff) | ((fl & 1) << 31).astype(np.uint32))
     # bounds: decoded as the kernels decode them (f32: base + q * step)
     bnd = raw[d["bnd_off"] * 4:].view(np.uint16)[:d["bnbx"] * d["bnby"]]
     sbt = raw[d["sbt_off"] * 4:].view(np.float32)[:2 * d["sbnbx"] * d["sbnby"]].reshape(-1, 2)

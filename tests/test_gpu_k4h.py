@@ -1,5 +1,6 @@
 """K4h -- the volume (BASELINE config 5) in K2h's form: the packed copy (uam_volume_pack: one
-16-B voxel {risk, psi_nfz, terrain, flags} per cell and layer, 4 x 2-cell blocks per layer),
+4-B risk / 8-B risk+psi / 16-B voxel {risk, psi_nfz, terrain, flags} planes per layer in 4 x 8-
+column blocks at one index, chosen per 8 x 8 columns by a code; the column terrain by bounds),
 the (path, group) items sorted on the altitude band and x/y tile of their middle waypoint,
 grouped partial sums, the geometry terms in the similarity form.  Against the oracle's
 statement of it (orc_eval_generated_h, mode 2) bit for bit; against the sequential
@@ -152,10 +153,10 @@ def _vary_psi(e, vol):
 
 
 def test_k4h_pack_layout(oracle_mod):
-    """uam_volume_pack against its definition (uampath.hip VpkDims / KVol4): the 16-B voxels
-    ({risk, psi} of the voxel, {terrain, flags} of the column, 4 x 2-column blocks per layer),
-    the 4-B risk (4 x 8) and 8-B {risk, |psi| | nfz << 31} (4 x 4) planes per layer, the column
-    terrain (4 x 8), zero padding, the 2-bit code per 8 x 8 columns (3: a psi below zero in any
+    """uam_volume_pack against its definition (uampath.hip VpkDims / KVol4): the 4-B risk, 8-B
+    {risk, |psi| | nfz << 31} and 16-B voxel ({risk, psi} of the voxel, {terrain, flags} of the
+    column) planes per layer (4 x 8-column blocks, one index), the column terrain (4 x 8), zero
+    padding, the 2-bit code per 8 x 8 columns (3: a psi below zero in any
     layer; 2: another nonzero psi or the no-fly flag; 1: a nonzero risk; 0: none), and terrain
     bounds that hold every column."""
     from test_host_cpu import _vpk_sections
@@ -168,27 +169,25 @@ def test_k4h_pack_layout(oracle_mod):
     off = np.cumsum([0] + sec)
     assert raw.nbytes == off[-1]
     b = raw.view(np.uint8)
-    nbx4, nby2, nb8, nb4, lnby4 = (nx + 3) // 4, (ny + 1) // 2, (nx + 7) // 8, (nx + 3) // 4, \
-        (ny + 3) // 4
-    t16 = b[off[2]:off[2] + nbx4 * nby2 * 8 * nz * 16].view(np.int32).reshape(-1, 4)
-    r4 = b[off[3]:off[3] + lnby4 * nb8 * 32 * nz * 4].view(np.uint32)
-    e8 = b[off[4]:off[4] + lnby4 * nb4 * 16 * nz * 8].view(np.uint32).reshape(-1, 2)
-    t4 = b[off[5]:off[5] + lnby4 * nb8 * 32 * 4].view(np.float32)
+    nb8, lnby4 = (nx + 7) // 8, (ny + 3) // 4
+    layer = lnby4 * nb8 * 32
+    r4 = b[off[2]:off[2] + layer * nz * 4].view(np.uint32)
+    t4 = b[off[3]:off[3] + layer * 4].view(np.float32)
+    e8 = b[off[4]:off[4] + layer * nz * 8].view(np.uint32).reshape(-1, 2)
+    t16 = b[off[5]:off[5] + layer * nz * 16].view(np.int32).reshape(-1, 4)
     iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     vox = vol.vox.cpu().numpy()            # [ny, nx, nz, 2]
     cols = vol.cols.cpu().numpy()          # [ny, nx, 2]
     vz = vox.transpose(2, 0, 1, 3).reshape(-1, 2)
     cz = np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)
-    i16 = (((iz * nby2 + iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
-    np.testing.assert_array_equal(t16[i16], np.concatenate([vz, cz], axis=1))
     i4 = (((iz * lnby4 + iy // 4) * nb8 + ix // 8) * 32 + (iy % 4) * 8 + ix % 8).reshape(-1)
+    np.testing.assert_array_equal(t16[i4], np.concatenate([vz, cz], axis=1))
     np.testing.assert_array_equal(r4[i4], vz[:, 0].view(np.uint32))
-    i8 = (((iz * lnby4 + iy // 4) * nb4 + ix // 4) * 16 + (iy % 4) * 4 + ix % 4).reshape(-1)
     pz = (vz[:, 1].view(np.uint32) & 0x7fffffff) | ((cz[:, 1].view(np.uint32) & 1) << 31)
-    np.testing.assert_array_equal(e8[i8], np.stack([vz[:, 0].view(np.uint32), pz], axis=1))
+    np.testing.assert_array_equal(e8[i4], np.stack([vz[:, 0].view(np.uint32), pz], axis=1))
     it = (((iy[0] // 4) * nb8 + ix[0] // 8) * 32 + (iy[0] % 4) * 8 + ix[0] % 8)
     np.testing.assert_array_equal(t4[it].view(np.uint32), cols[:, :, 0].view(np.uint32))
-    for t, idx in ((t16, i16), (r4, i4), (e8, i8), (t4.view(np.uint32), it.reshape(-1))):
+    for t, idx in ((t16, i4), (r4, i4), (e8, i4), (t4.view(np.uint32), it.reshape(-1))):
         mask = np.ones(len(t), bool)
         mask[idx] = False
         assert (t[mask] == 0).all()

@@ -744,11 +744,12 @@ def test_raster_summary_table(eng, oracle_mod):
 
 
 def test_raster_pack_table(eng, oracle_mod):
-    """uam_raster_pack == its definition (numpy on the record raster, uampath.h): 2-bit code per
-    summary block (0 = the skip rule above, 3 = some cell has psi != +-0 or the NFZ flag,
-    1 = otherwise), then plane A {phi, terrain read as K2 reads it: +0.0 on nodata} at the
-    4 x 4-cell blocked address of every cell; ragged edges (300 x 262 is no multiple of 4 or of
-    the summary block)."""
+    """uam_raster_pack == its definition (uampath.hip, packed raster; test_gpu_k2h._check_pack:
+    the 2-bit codes, the four planes at the blocked index, bounds holding every cell's terrain)
+    on ragged edges (300 x 262 is no multiple of the 4 x 8-cell blocks or of the summary block),
+    a NaN terrain cell (its superblock unbounded) and a strip of +0.0 terrain, summary blocks
+    4 and 16."""
+    from test_gpu_k2h import _check_pack
     from uam_path_planning_amd.scenario import canonical_spec, raster_geo
     from uam_path_planning_amd.synthetic import synthetic_dem
 
@@ -761,37 +762,12 @@ def test_raster_pack_table(eng, oracle_mod):
     dem[5, 7] = np.float32(np.nan)
     dem[150:166, 0:64] = np.float32(0.0)
     raster = eng.raster_build(geo, dem, summary=False)
-    rec = _np(raster.rec)
-    ny, nx = rec.shape[:2]
-    phi, psi = rec[..., 0].view(np.float32), rec[..., 1].view(np.float32)
-    nfz = (rec[..., 3] & 1) != 0
-    terr_bits = np.where(rec[..., 3] & 4, 0, rec[..., 2])
-    ok = (phi == 0) & (psi == 0) & ~nfz & (terr_bits == 0)
-    needb = (psi != 0) | nfz
-    iy, ix = np.mgrid[0:ny, 0:nx]
-    lnbx = -(-nx // 4)
-    adr = (((iy >> 2) * lnbx + (ix >> 2)) << 4) | ((iy & 3) << 2) | (ix & 3)
+    rec = _np(raster.rec).view(np.float32).reshape(262, 300, 4)
     for block in (4, 16):
         eng.raster_summary(raster, block, packed=True)
-        pk = _np(raster.packed).reshape(-1)
-        nby, nbx = -(-ny // block), -(-nx // block)
-        codes = []
-        for by in range(nby):
-            for bx in range(nbx):
-                sl = (slice(by * block, (by + 1) * block), slice(bx * block, (bx + 1) * block))
-                codes.append(3 if needb[sl].any() else 0 if ok[sl].all() else 1)
-        words = -(-2 * len(codes) // 32)
-        got = np.unpackbits(pk[:4 * words], bitorder="little").reshape(-1, 2)
-        got = got[:, 0] + 2 * got[:, 1]
-        np.testing.assert_array_equal(got[:len(codes)], codes, err_msg=f"B{block}")
-        assert not got[len(codes):].any()
-        assert {0, 1, 3} <= set(codes)
-        off_a = (4 * words + 255) // 256 * 256
-        cells = lnbx * (-(-ny // 4)) * 16
-        assert pk.size >= off_a + 8 * cells
-        pa = pk[off_a:off_a + 8 * cells].view(np.uint32).reshape(-1, 2)
-        np.testing.assert_array_equal(pa[adr, 0], rec[..., 0].view(np.uint32))
-        np.testing.assert_array_equal(pa[adr, 1], terr_bits.view(np.uint32))
+        assert raster.block == block
+        frac_bounded, _ = _check_pack(raster, rec)
+        assert 0.0 < frac_bounded < 1.0  # the NaN cell's superblock is unbounded
 
 
 @pytest.mark.parametrize("mode", ["analytic", "raster"])

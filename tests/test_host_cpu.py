@@ -38,8 +38,8 @@ def test_header_symbols_exported(lib):
 
 def _vpk_sections(nx, ny, nz):
     """The packed volume's sections (uampath.hip VpkDims): header (codes, bounds, superblocks),
-    bound scratch, 16-B voxels (4 x 2 columns), 4-B risk (4 x 8), 8-B risk/psi (4 x 4), the 4-B
-    column terrain (4 x 8), each 256-B aligned."""
+    bound scratch, then in 4 x 8-column blocks the 4-B risk layers, the 4-B column terrain, the
+    8-B risk/psi layers and the 16-B voxel layers, each 256-B aligned."""
     al = lambda v: (v + 255) // 256 * 256
     w16 = lambda v: -(-v // 16) * 16
     cw = (((nx + 7) // 8) * ((ny + 7) // 8) + 15) // 16
@@ -48,10 +48,9 @@ def _vpk_sections(nx, ny, nz):
         bsh += 1
     bnbx, bnby = -(-nx // (1 << bsh)), -(-ny // (1 << bsh))
     hdr = w16(cw * 4) + w16(bnbx * bnby * 2) + w16(-(-bnbx // 4) * -(-bnby // 4) * 8)
-    nbx4, nby2, nb8, nb4, lnby4 = (nx + 3) // 4, (ny + 1) // 2, (nx + 7) // 8, (nx + 3) // 4, \
-        (ny + 3) // 4
-    return [al(hdr), al(bnbx * bnby * 8), al(nbx4 * nby2 * 8 * nz * 16),
-            al(lnby4 * nb8 * 32 * nz * 4), al(lnby4 * nb4 * 16 * nz * 8), al(lnby4 * nb8 * 32 * 4)]
+    layer = ((ny + 3) // 4) * ((nx + 7) // 8) * 32
+    return [al(hdr), al(bnbx * bnby * 8), al(layer * nz * 4), al(layer * 4), al(layer * nz * 8),
+            al(layer * nz * 16)]
 
 
 def test_volume_packed_bytes(lib):
@@ -96,9 +95,10 @@ def test_invalid_calls_fail_loudly(lib):
                                      ctypes.byref(nbytes)) == _lib.UAM_OK
     # header: 2-bit codes of 65536 blocks (16 KiB), 128^2 bound blocks of 32^2 cells (u16,
     # 32 KiB), 32^2 superblocks (float2, 8 KiB); the bound scratch (float2 per bound block);
-    # the 4-B phi and terrain planes and the 8-B {phi, psi | nfz} plane of 4096^2 cells
+    # the 4-B phi and terrain planes, the 8-B {phi, psi | nfz} plane and the 16-B record plane
+    # of 4096^2 cells
     assert (b.value, nbytes.value) == (16, 16384 + 32768 + 8192 + 8 * 16384 +
-                                       (4 + 4 + 8) * 4096 * 4096)
+                                       (4 + 4 + 8 + 16) * 4096 * 4096)
     # a raster that is no multiple of the blocks: every section padded to whole blocks
     rd2 = _lib.RasterDesc(1000, 700, 0.0, 20.0, 0.05, 0.05, -9999.0, 0.0)
     assert lib.uam_raster_pack_shape(ctypes.byref(rd2), 4, ctypes.byref(b),
@@ -107,7 +107,7 @@ def test_invalid_calls_fail_loudly(lib):
     nbb = 125 * 88                                     # 8-cell bound blocks (11000 <= 16384)
     hdr = -(-words * 4 // 16) * 16 + -(-nbb * 2 // 16) * 16 + 32 * 22 * 8
     a256 = lambda v: -(-v // 256) * 256
-    planes = 2 * a256(175 * 125 * 32 * 4) + a256(175 * 250 * 16 * 8)
+    planes = 2 * a256(175 * 125 * 32 * 4) + a256(175 * 250 * 16 * 8) + a256(175 * 500 * 8 * 16)
     assert (b.value, nbytes.value) == (4, a256(hdr) + a256(nbb * 8) + planes)
     assert lib.uam_raster_pack(None, None, None, 0, None, None) == _lib.UAM_E_INVALID
     assert lib.uam_eval_generated(None, 1, None, None, None, 0, None, None, 0, None, 5, None,

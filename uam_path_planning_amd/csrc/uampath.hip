@@ -137,14 +137,20 @@ struct KRaster {
     // words), the terrain bound table (one u16 per 2^bshift-square bound block, bnbx per row,
     // at word bnd_off) and the superblock table (float2 {base, step} per 4 x 4 bound blocks,
     // sbnbx per row, at word sbt_off).  Planes: p4 {phi} and t4 {terrain as read} in 4 x 8-cell
-    // blocks (one 128-B line, nb8 per row), e8 {phi, psi | nfz << 31} in 4 x 4-cell blocks (nb4
-    // per row).
+    // blocks (one 128-B line, nb8 per row), e8 {phi, psi | nfz << 31} in the same 4 x 8-cell
+    // blocks (256 B: two lines of 2 x 8 cells), r16 (the records) in the same blocks (512 B),
+    // all four at one index.
     const uint32_t* __restrict__ pmap;
     int32_t pwords, hwords, bnd_off, sbt_off;
-    int32_t bshift, bnbx, sbnbx, nb8, nb4;
+    int32_t bshift, bnbx, sbnbx, nb8;
     const uint32_t* __restrict__ p4;
     const float* __restrict__ t4;
     const uint2* __restrict__ e8;
+    // K2h's addressing: the whole packed copy from one base by 32-bit byte offsets (the planes
+    // p4 / e8 / r16 (the 16-B records, same blocks and index) and t4 at o4 / o8 / o16 / ot4);
+    // null when the copy is 4 GiB or larger (K2h then stands aside)
+    const char* __restrict__ pk;
+    uint32_t o4, o8, o16, ot4;
 };
 
 // volume (config 5): 8-B voxels {risk, psi_nfz} [ny][nx][nz], the 8-B column plane
@@ -693,34 +699,71 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
 // which the evaluation reads as "no bound" (always fetched, no lower bound).
 constexpr int PK_BOUND_MAX = 16384;  // bound blocks at most (32 KiB of u16 in LDS)
 
+// (index products by 24-bit multiplies, full rate: cells and block counts are < 2^24,
+// uam_raster_pack's limits)
 __device__ __forceinline__ int32_t p4_addr(const KRaster& rs, int32_t ix, int32_t iy) {
-    return ((((iy >> 2) * rs.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7));
+    return (int32_t)(((__umul24((uint32_t)(iy >> 2), (uint32_t)rs.nb8) + (uint32_t)(ix >> 3)) << 5) |
+                     (((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u));
 }
-__device__ __forceinline__ int32_t e8_addr(const KRaster& rs, int32_t ix, int32_t iy) {
-    return ((((iy >> 2) * rs.nb4 + (ix >> 2)) << 4) | ((iy & 3) << 2) | (ix & 3));
+
+// the summary-block index of cell (ix, iy) (its 2-bit code: word b >> 4, bits 2 (b & 15))
+__device__ __forceinline__ int32_t pk_block(const KRaster& rs, int32_t ix, int32_t iy) {
+    return (int32_t)(__umul24((uint32_t)(iy >> rs.sshift), (uint32_t)rs.snbx) +
+                     (uint32_t)(ix >> rs.sshift));
+}
+
+// the bound entry (u16) and superblock {base, step} of cell (ix, iy) from a header copy
+__device__ __forceinline__ void pk_bound_raw(const KRaster& rs, const uint32_t* __restrict__ hdr,
+                                             int32_t ix, int32_t iy, uint32_t& e, float2& sb) {
+    const uint32_t bx = (uint32_t)(ix >> rs.bshift), by = (uint32_t)(iy >> rs.bshift);
+    e = reinterpret_cast<const uint16_t*>(hdr + rs.bnd_off)[__umul24(by, (uint32_t)rs.bnbx) + bx];
+    sb = reinterpret_cast<const float2*>(hdr + rs.sbt_off)[__umul24(by >> 2, (uint32_t)rs.sbnbx) +
+                                                           (bx >> 2)];
+}
+
+// decode: base + q * step with q * step exact (step a power of two), so the fused form rounds
+// once exactly as the separate one (k_raster_bounds' check)
+__device__ __forceinline__ void pk_bound_decode(uint32_t e, float2 sb, float& ub, float& lb) {
+    ub = fmaf((float)(e & 255u), sb.y, sb.x);
+    lb = fmaf((float)(e >> 8), sb.y, sb.x);
 }
 
 // the decoded bounds of cell (ix, iy) from a header copy (LDS or global)
 __device__ __forceinline__ void pk_bounds(const KRaster& rs, const uint32_t* __restrict__ hdr,
                                           int32_t ix, int32_t iy, float& ub, float& lb) {
-    const int32_t bx = ix >> rs.bshift, by = iy >> rs.bshift;
-    const uint32_t e =
-        reinterpret_cast<const uint16_t*>(hdr + rs.bnd_off)[by * rs.bnbx + bx];
-    const float2 sb =
-        reinterpret_cast<const float2*>(hdr + rs.sbt_off)[(by >> 2) * rs.sbnbx + (bx >> 2)];
-    ub = sb.x + (float)(e & 255u) * sb.y;
-    lb = sb.x + (float)(e >> 8) * sb.y;
+    uint32_t e;
+    float2 sb;
+    pk_bound_raw(rs, hdr, ix, iy, e, sb);
+    pk_bound_decode(e, sb, ub, lb);
 }
 
-// component k of a 16-B entry
-__device__ __forceinline__ uint32_t u4_comp(const uint4& r, uint32_t k) {
-    return (k & 2u) ? ((k & 1u) ? r.w : r.z) : ((k & 1u) ? r.y : r.x);
+// the raster cell of a generated point (arc_point's or the pair's coordinates; uampath.h's float64
+// floor): false off the raster or NaN, with (ix, iy) = (0, 0) then (a valid header index)
+__device__ __forceinline__ bool gen_cell(const KRaster& rs, double x0, double x1, int32_t& ix,
+                                         int32_t& iy) {
+    const double tx = (x0 - rs.x0) * rs.inv_dx;
+    const double ty = (rs.y_top - x1) * rs.inv_dy;
+    // (bitwise: no short-circuit branches)
+    const bool in = (tx >= 0.0) & (tx < (double)rs.nx) & (ty >= 0.0) & (ty < (double)rs.ny);
+    ix = in ? (int32_t)tx : 0;
+    iy = in ? (int32_t)ty : 0;
+    return in;
 }
 
-// a chunk's per-slot codes, 4 bits per slot
-template <int CH>
-using PkCodes = typename std::conditional<(CH > 8), uint64_t, uint32_t>::type;
-#define PK_CODES_CHECK(CH) static_assert((CH) <= 16, "4 code bits per slot in 64 bits")
+// a chunk's per-slot entry kinds: the code (2 bits) and the cell's first component in the
+// aligned 16 B (sub, 2 bits), one bit mask per bit so the consume selects components with
+// independent conditions (a select on bits of one index folds into a dynamic vector index,
+// which put the chunk's loads in scratch memory)
+struct PkSlots {
+    uint32_t c0 = 0, c1 = 0, s0 = 0, s1 = 0;
+    __device__ __forceinline__ void set(int t, uint32_t v) {  // v = code | sub << 2
+        c0 |= (v & 1u) << t;
+        c1 |= ((v >> 1) & 1u) << t;
+        s0 |= ((v >> 2) & 1u) << t;
+        s1 |= ((v >> 3) & 1u) << t;
+    }
+};
+#define PK_CODES_CHECK(CH) static_assert((CH) <= 32, "one bit per slot in 32")
 
 // spread the 16 low bits of v to the even bits of the result
 __device__ __forceinline__ uint32_t spread16(uint32_t v) {
@@ -740,7 +783,7 @@ __device__ __forceinline__ uint32_t spread16(uint32_t v) {
 __device__ __forceinline__ uint32_t pk_locate(const KRaster& rs, const uint4* __restrict__ rec,
                                               const uint32_t* __restrict__ map, int32_t ix,
                                               int32_t iy, const uint4*& vp, const float*& tp) {
-    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
+    const int32_t b = pk_block(rs, ix, iy);
     const uint32_t code = (map[b >> 4] >> ((b & 15) * 2)) & 3u;
     if (code == 3u) {
         vp = rec + (iy * rs.nx + ix);
@@ -750,9 +793,8 @@ __device__ __forceinline__ uint32_t pk_locate(const KRaster& rs, const uint4* __
     tp = rs.t4 + a4;
     uint32_t sub = 0;
     if (code == 2u) {
-        const int32_t a8 = e8_addr(rs, ix, iy);
-        vp = reinterpret_cast<const uint4*>(rs.e8 + (a8 & ~1));
-        sub = (uint32_t)(a8 & 1) * 2u;
+        vp = reinterpret_cast<const uint4*>(rs.e8 + (a4 & ~1));
+        sub = (uint32_t)(a4 & 1) * 2u;
     } else if (code == 1u) {
         vp = reinterpret_cast<const uint4*>(rs.p4 + (a4 & ~3));
         sub = (uint32_t)(a4 & 3);
@@ -760,24 +802,36 @@ __device__ __forceinline__ uint32_t pk_locate(const KRaster& rs, const uint4* __
     return code | (sub << 2);
 }
 
-// the terms of a located waypoint from its 16 B r: phi and psi bits (+0 where the code holds
-// none), the no-fly hit, and the record's terrain as read (meaningful in code 3 only)
-__device__ __forceinline__ void pk_terms(const uint4& r, uint32_t cs, uint32_t& phi,
+// the terms of slot t's located waypoint from its 16 B r: phi and psi bits (+0 where the code
+// holds none), the no-fly hit, and the record's terrain as read (meaningful in code 3 only)
+__device__ __forceinline__ void pk_terms(const uint4& r, const PkSlots& k, int t, uint32_t& phi,
                                          uint32_t& psi, uint32_t& hit, float& rter) {
-    const uint32_t code = cs & 3u, sub = cs >> 2;
-    phi = code ? u4_comp(r, sub) : 0u;
-    const uint32_t praw = (code & 2u) ? u4_comp(r, sub + 1u) : 0u;
-    psi = code == 2u ? (praw & 0x7fffffffu) : praw;
-    hit = code == 2u ? (praw >> 31) : (code == 3u && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+    const bool c0 = (k.c0 >> t) & 1u, c1 = (k.c1 >> t) & 1u;
+    const bool s0 = (k.s0 >> t) & 1u, s1 = (k.s1 >> t) & 1u;
+    const uint32_t lo = s0 ? r.y : r.x, hi = s0 ? r.w : r.z;
+    phi = (c0 || c1) ? (s1 ? hi : lo) : 0u;
+    // psi and the flag: code 2 at its cell's second word (sub 0 or 2), code 3 the record's y
+    const uint32_t praw = c1 ? (s1 ? r.w : r.y) : 0u;
+    psi = (c1 && !c0) ? (praw & 0x7fffffffu) : praw;
+    hit = (c1 && !c0) ? (praw >> 31) : (c1 && c0 && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
     rter = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
 }
 
-// one thread per cell, rows coalesced: the three planes at their blocked addresses (e8 is
-// written everywhere, read only in code-2 blocks)
+// pk_terms of one slot's kind word k = code | word << 2 (K2h: one register per slot)
+__device__ __forceinline__ void pk_terms_k(const uint4& r, uint32_t k, uint32_t& phi,
+                                           uint32_t& psi, uint32_t& hit, float& rter) {
+    PkSlots s;
+    s.set(0, k);
+    pk_terms(r, s, 0, phi, psi, hit, rter);
+}
+
+// one thread per cell, rows coalesced: the four planes at their blocked addresses (e8 and r16
+// are written everywhere, read only in code-2 / code-3 blocks)
 __global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ rec, KRaster rs,
                                                      uint32_t* __restrict__ p4,
                                                      float* __restrict__ t4,
-                                                     uint2* __restrict__ e8) {
+                                                     uint2* __restrict__ e8,
+                                                     uint4* __restrict__ r16) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= (int64_t)rs.nx * rs.ny) return;
     const int32_t iy = (int32_t)(c / rs.nx), ix = (int32_t)(c - (int64_t)iy * rs.nx);
@@ -785,8 +839,9 @@ __global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ r
     const int32_t a4 = p4_addr(rs, ix, iy);
     p4[a4] = r.x;
     t4[a4] = (r.w & UAM_FLAG_NODATA) ? 0.0f : __uint_as_float(r.z);
-    e8[e8_addr(rs, ix, iy)] =
+    e8[a4] =
         make_uint2(r.x, (r.y & 0x7fffffffu) | ((r.w & UAM_FLAG_NFZ) ? 0x80000000u : 0u));
+    r16[a4] = r;
 }
 
 // one thread per summary block: its 2-bit code; lanes 0/16/32/48 write the wave's 4 words
@@ -4765,7 +4820,7 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
         uint4 r[CH];
         float tv[CH];
         uint32_t inb = 0;
-        PkCodes<CH> cs = 0;
+        PkSlots cs;
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const uint4* vp = vdummy;
@@ -4777,8 +4832,7 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
                 const double fy = floor((rs.y_top - x1) * rs.inv_dy);
                 if ((fx >= 0.0) && (fx < (double)rs.nx) && (fy >= 0.0) && (fy < (double)rs.ny)) {
                     inb |= 1u << t;
-                    cs |= (PkCodes<CH>)pk_locate(rs, rec, map, (int32_t)fx, (int32_t)fy, vp, tp)
-                          << (4 * t);
+                    cs.set(t, pk_locate(rs, rec, map, (int32_t)fx, (int32_t)fy, vp, tp));
                 }
             }
             r[t] = *vp;
@@ -4792,10 +4846,10 @@ __device__ __forceinline__ void seg_pass2_pack(const KRaster& rs, const uint4* _
                 a.hmax = fmax(a.hmax, 0.0);  // off-raster counts as sea level
                 continue;
             }
-            const uint32_t c = (uint32_t)(cs >> (4 * t)) & 15u, code = c & 3u;
+            const uint32_t code = ((cs.c0 >> t) & 1u) | (((cs.c1 >> t) & 1u) << 1);
             uint32_t phi, psi, hit;
             float rter;
-            pk_terms(r[t], c, phi, psi, hit, rter);
+            pk_terms(r[t], cs, t, phi, psi, hit, rter);
             if (code) a.cost = a.cost + (double)__uint_as_float(phi) / dN;
             if (code & 2u) {
                 a.nsum = a.nsum + (double)__uint_as_float(psi);
@@ -4991,9 +5045,12 @@ struct KGrp {
     int32_t* __restrict__ order;   // [n_items] item of each sorted position
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
-    int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_g_eval<..., CELLS>), or null
+    int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_cells), or null
     UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's block 0
     int32_t lb_stride;             // K2h: the path lower bound's sample stride (>= 1)
+    float* __restrict__ lbp;       // K2h: [P] each path's sampled terrain lower bound (formed by
+                                   // the histogram launch), or null
+    double* __restrict__ ubp;      // K4h: [P] each path's sampled clearance upper bound, likewise
     int32_t* __restrict__ err;     // the sort's check word: zeroed by the histogram launch, set
                                    // by the scatter on a position outside the order (keys of the
                                    // two launches disagreeing); the output launch then writes
@@ -5104,6 +5161,55 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
     return (uint32_t)(((uint64_t)a * m) >> sh);
 }
 
+// K2h: a path's sampled terrain lower bound Lb (h_item): the maximum decoded lb over its
+// waypoints j = 0, s, 2s, ... (s = kg.lb_stride) and j = W - 1, each at its own cell by the
+// evaluation's operations (the pair's points, arc_point's), +0.0 for one off the raster (its
+// exact terrain); -inf without the packed header.  Every sample is a real waypoint, so Lb is at
+// most the path's maximum terrain.
+__device__ __forceinline__ float h_path_lb(const KParams& p, const KRaster& rs, const KGrp& kg,
+                                           int32_t path) {
+    if (!rs.pmap) return -INFINITY;
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+    const int32_t d = path - q * kg.D;
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const double2* u = reinterpret_cast<const double2*>(kg.utab) + (int64_t)d * p.N - 1;
+    const int W = kg.W;
+    float Lb = -INFINITY;
+    auto take = [&](bool in, int32_t ix, int32_t iy) {
+        float ub, lb;
+        pk_bounds(rs, rs.pmap, ix, iy, ub, lb);
+        Lb = fmaxf(Lb, in ? lb : 0.0f);
+    };
+    int32_t ix, iy;
+    take(gen_cell(rs, pr.x, pr.y, ix, iy), ix, iy);
+    take(gen_cell(rs, pr.z, pr.w, ix, iy), ix, iy);
+    // four samples at a time, every load of the four issued together (a sample past the last
+    // interior waypoint repeats it)
+    constexpr int K = 4;
+    for (int j0 = kg.lb_stride; j0 < W - 1; j0 += K * kg.lb_stride) {
+        double2 uu[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) uu[k] = u[min(j0 + k * kg.lb_stride, W - 2)];
+        uint32_t e[K];
+        float2 sb[K];
+        bool in[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double x0, x1;
+            arc_point(pr.x, pr.y, pr.z, pr.w, uu[k].x, uu[k].y, x0, x1);
+            in[k] = gen_cell(rs, x0, x1, ix, iy);
+            pk_bound_raw(rs, rs.pmap, ix, iy, e[k], sb[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float ub, lb;
+            pk_bound_decode(e[k], sb[k], ub, lb);
+            Lb = fmaxf(Lb, in[k] ? lb : 0.0f);
+        }
+    }
+    return Lb;
+}
+
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
 // groups (the tile under the group's middle waypoint) and the partition's histogram, stored
 // bin-major so the scan yields each (bin, partition)'s offset
@@ -5166,6 +5272,11 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
             kg.key[i] = (uint16_t)key;
             atomicAdd(&h[key], 1);
         }
+    }
+    if (kg.lbp) {  // K2h: the partition's paths' sampled lower bounds, one thread per path
+        const int64_t plo = (int64_t)kg.P * b / G_NBK, phi = (int64_t)kg.P * (b + 1) / G_NBK;
+        for (int64_t pth = plo + t; pth < phi; pth += 1024)
+            kg.lbp[pth] = h_path_lb(p, rs, kg, (int32_t)pth);
     }
     __syncthreads();
     // the partition's count per bin, bin-major ([bin][partition]): k_scan_local's exclusive
@@ -5269,10 +5380,8 @@ __device__ __forceinline__ double sqrt_mid(double x) {
 // when the whole wave's squared norms are in its range.  Any other chunk runs the general form
 // with the endpoint, range and row tests per waypoint.  Both add exactly the same terms in the
 // same order.
-// CELLS: also write every waypoint's raster cell index (iy nx + ix, -1 off the raster) to
-// kg.cells[path][j], the reference's returned waypoints as raster cells (solver.py:49,
-// main.py:186-190); a compile-time flag, so the form without it is unchanged.
-template <int CH, bool LS, bool MS, bool CELLS = false>
+// (The waypoint cells, when requested, come from k_cells beside this launch.)
+template <int CH, bool LS, bool MS>
 __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRaster rs, KGrp kg,
                                                 const uint4* __restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -5405,7 +5514,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
     // gathers are really in flight; a waypoint with nothing to read (code 0's value, code 3's
     // terrain, off the raster) reads the planes' first line, one line per wave, unused.
     const uint4* const vdummy = reinterpret_cast<const uint4*>(rs.p4);
-    auto locate = [&](double x0, double x1, int t, uint32_t& inb, auto& cs, int32_t& cell,
+    auto locate = [&](double x0, double x1, int t, uint32_t& inb, auto& cs,
                       const float*& tp) -> const uint4* {
         // the cell: floor(t) in [0, n) <=> t in [0, n) for integer n, and the truncating
         // conversion equals floor for t >= 0 (NaN fails both tests)
@@ -5416,9 +5525,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
         if ((tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny)) {
             inb |= 1u << t;
             const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
-            if (CELLS) cell = iy * rs.nx + ix;
-            cs |= (std::remove_reference_t<decltype(cs)>)pk_locate(rs, rec, s_map, ix, iy, vp,
-                                                                   tp) << (4 * t);
+            cs.set(t, pk_locate(rs, rec, s_map, ix, iy, vp, tp));
         }
 #ifdef UAM_K2G_DIAG_NOGATHER  // measurement build: every load reads the planes' first line
         vp = vdummy;
@@ -5432,10 +5539,11 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
     double gc = 0.0, gn = 0.0;
     float hmax = -INFINITY;
     uint32_t nh = 0, off = 0;
-    auto consume1 = [&](const uint4& r, float tv, bool in, uint32_t c) {
+    auto consume1 = [&](const uint4& r, float tv, bool in, const PkSlots& cs, int t) {
+        const uint32_t c = ((cs.c0 >> t) & 1u) | (((cs.c1 >> t) & 1u) << 1);
         uint32_t phi, psi, hit;
         float rter;
-        pk_terms(r, c, phi, psi, hit, rter);
+        pk_terms(r, cs, t, phi, psi, hit, rter);
         nh += hit;
         off += in ? 0u : 1u;
         gc = gc + over_n((double)__uint_as_float(phi));
@@ -5448,9 +5556,8 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
             const bool first = it == 0;
             uint4 r[CH];
             float tv[CH];
-            int32_t cl[CH];
             uint32_t inb = 0;
-            PkCodes<CH> cs = 0;
+            PkSlots cs;
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int j = jc + t;
@@ -5473,19 +5580,13 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                     segment_fast(x0, x1, rv);
                 }
 #endif
-                cl[t] = -1;
                 const float* tp;
-                r[t] = *locate(x0, x1, t, inb, cs, cl[t], tp);
+                r[t] = *locate(x0, x1, t, inb, cs, tp);
                 tv[t] = *tp;
             }
 #pragma unroll
             for (int t = 0; t < CH; ++t)
-                consume1(r[t], tv[t], (inb >> t) & 1u, (uint32_t)(cs >> (4 * t)) & 15u);
-            if (CELLS) {
-                int32_t* dst = kg.cells + (int64_t)path * W + jc;
-#pragma unroll
-                for (int t = 0; t < CH; ++t) dst[t] = cl[t];
-            }
+                consume1(r[t], tv[t], (inb >> t) & 1u, cs, t);
         } else {  // the general form, one waypoint at a time (the ragged and last chunks)
 #pragma unroll 1
             for (int j = jc; j < je; ++j) {
@@ -5496,12 +5597,11 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                     segment(j, x0, x1);
 #endif
                 }
-                uint32_t inb = 0, cs = 0;
-                int32_t cl = -1;
+                uint32_t inb = 0;
+                PkSlots cs;
                 const float* tp;
-                const uint4 r = *locate(x0, x1, 0, inb, cs, cl, tp);
-                consume1(r, *tp, inb & 1u, cs & 15u);
-                if (CELLS) __builtin_nontemporal_store(cl, kg.cells + (int64_t)path * W + j);
+                const uint4 r = *locate(x0, x1, 0, inb, cs, tp);
+                consume1(r, *tp, inb & 1u, cs, 0);
             }
         }
     }
@@ -5636,17 +5736,20 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 };
 
 // every (path, group) item in K2g's sorted order: the group's points, cells and packed entries
-// only.  Every chunk is straight-line: CH points (p_0 / p_{W-1} from the pair, the rest by the
-// arc formula), CH unconditional 16-B value loads and CH unconditional 4-B terrain loads (a slot
-// with nothing to read takes the planes' first line, one per wave), then the branch-free consume.
+// only.  Every chunk is straight-line, in three phases so the LDS and memory round trips of its
+// CH slots overlap: the CH cells (the arc formula; p_0 / p_{W-1} from the pair's cells), the CH
+// header reads (code word, bound entry, superblock), then per slot the decisions and two
+// unconditional loads -- the code's entry (a slot with nothing to read takes the first p4 line)
+// and the terrain (the first t4 word unless fetched) -- by 32-bit offsets from the packed
+// copy's base; then the branch-free consume.
 //
 // The terrain maximum by bounds (build-defined; the outputs are exactly the per-waypoint
 // maximum's): min_clearance needs only the path's maximum terrain M, an order-free maximum, so
 // a waypoint's exact terrain is fetched (t4) only when it could still be M.  Every in-raster
 // waypoint w has decoded bounds lb_w <= terrain_w <= ub_w (pk_bounds, from LDS).  The item keeps
-//   Lb: the maximum lb over a sample of the path's waypoints (every kg.lb_stride-th, positions
-//       by the same operations as the waypoints' own: lb of a real waypoint, so Lb <= M) and
-//       over its own waypoints so far; off-raster waypoints count +0.0, their exact value;
+//   Lb: the path's sampled lower bound (h_path_lb, formed once per path by the histogram
+//       launch: lb of real waypoints, so Lb <= M) raised by its own waypoints' lb as it goes;
+//       off-raster waypoints count +0.0, their exact value;
 //   E:  the maximum of the exact terrain values it has taken (fetched, code-3 records,
 //       off-raster +0.0, blocks whose bounds coincide).
 // It fetches w iff !(ub_w <= E) && !(ub_w < Lb) (NaN bounds: "no bound", always fetched).
@@ -5661,19 +5764,18 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 #define UAM_K2H_MINW 4
 #endif
 constexpr int H_BS = 512;  // K2h workgroup (2 per CU at 4 waves per SIMD; LDS <= 80 KiB each)
-template <int CH, bool CELLS>
+template <int CH>
 __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, const KGrp& kg,
-                                       const uint4* __restrict__ rec,
                                        const uint32_t* __restrict__ s_hdr,
-                                       const double2* __restrict__ s_u, int32_t* s_cells,
-                                       bool live, int32_t item, int32_t path, int32_t q,
-                                       const double4& pr) {
-    // every lane stays to the end (the cell stores shuffle between lanes): a lane past the
-    // last item evaluates nothing and writes nothing
+                                       const double2* __restrict__ s_u, bool live, int32_t item,
+                                       int32_t path, int32_t q, const double4& pr, float Lb) {
+    // a lane past the last item evaluates nothing and writes nothing
     const int s = item - path * kg.nseg;
     const int32_t d = path - q * kg.D;
     const int N = p.N, W = kg.W;
-    const double2* urow = s_u + d * N;
+    // waypoint j's unit vector is urow[j] (j = 1..N); the slots past a row's ends read the
+    // neighbouring rows or the staged padding (LDS either way), and their cells are replaced
+    const double2* urow = s_u + d * N - 1;
     const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
     // chunks: the wave's most, so the loop is wave-uniform
     int nch = (j1 - j0 + CH - 1) / CH;
@@ -5682,131 +5784,122 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
     const double vx = pr.x - pr.z, vy = pr.y - pr.w;
     const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
     const double dN = (double)N, yN = kg.inv_n;
-    auto over_n = [&](double a) {  // Phi / N exactly as k_g_eval forms it
-        if (yN == 0.0) return a / dN;
+    auto over_n = [&](double a) {  // Phi / N exactly as k_g_eval forms it (K2h: N <= 4096)
         const double q0 = a * yN;
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;
     };
-    // waypoint j's raster cell (arc_point's operations; false off the raster or NaN)
-    auto cell_of = [&](int j, int32_t& ix, int32_t& iy) -> bool {
-        const double2 u = urow[min(max(j - 1, 0), N - 1)];
-        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
-        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-        x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
-        x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
-        const double tx = (x0 - rs.x0) * rs.inv_dx;
-        const double ty = (rs.y_top - x1) * rs.inv_dy;
-        const bool in = (tx >= 0.0) && (tx < (double)rs.nx) && (ty >= 0.0) && (ty < (double)rs.ny);
-        ix = in ? (int32_t)tx : 0;
-        iy = in ? (int32_t)ty : 0;
-        return in;
-    };
-    // the path's sampled lower bound (the same for all its items)
-    float Lb = -INFINITY;
-    for (int j = 0; j < W; j += kg.lb_stride) {  // (lb_stride >= 1; uniform trip count)
-        int32_t ix, iy;
-        const bool in = cell_of(j, ix, iy);
-        float ub, lb;
-        pk_bounds(rs, s_hdr, ix, iy, ub, lb);
-        Lb = fmaxf(Lb, in ? lb : 0.0f);
-    }
-    const uint4* const vdummy = reinterpret_cast<const uint4*>(rs.p4);
+    // the end points' cells, formed once
+    int32_t ixF, iyF, ixL, iyL;
+    const bool inF = gen_cell(rs, pr.x, pr.y, ixF, iyF);
+    const bool inL = gen_cell(rs, pr.z, pr.w, ixL, iyL);
+    const uint16_t* const bnd = reinterpret_cast<const uint16_t*>(s_hdr + rs.bnd_off);
+    const float2* const sbt = reinterpret_cast<const float2*>(s_hdr + rs.sbt_off);
+    const char* const pk = rs.pk;
+    // the plane offsets as values (a select between the struct's fields otherwise becomes a
+    // select of their addresses and a memory read per slot)
+    const uint32_t o4 = __builtin_amdgcn_readfirstlane(rs.o4);
+    const uint32_t o8 = __builtin_amdgcn_readfirstlane(rs.o8);
+    const uint32_t o16 = __builtin_amdgcn_readfirstlane(rs.o16);
+    const uint32_t ot4 = __builtin_amdgcn_readfirstlane(rs.ot4);
     double gc = 0.0, gn = 0.0;
     float E = -INFINITY;
     uint32_t nh = 0, off = 0;
-    for (int c = 0; c < nch; ++c) {
-        const int jc = j0 + c * CH;
-        uint4 r[CH];
-        float tv[CH];
-        int32_t cl[CH];
-        uint32_t inb = 0, tk = 0;
-        PkCodes<CH> cs = 0;  // per slot: code | sub << 2, 4 bits each
+    // one chunk ahead: chunk c + 1's loads are issued before chunk c is consumed (the fetch
+    // rule then sees E without chunk c's fetched values: valid, E only holds exact values).
+    // Iteration c issues chunk c + 1 into the B arrays and consumes chunk c from the A arrays.
+    uint4 rA[CH];
+    float tvA[CH];
+    uint32_t kcA[CH], vinA = 0, tkA = 0;
+    int nvA = 0;
+    for (int c = -1; c < nch; ++c) {  // (nch wave-uniform)
+        uint4 rB[CH];
+        float tvB[CH];
+        uint32_t kcB[CH], vinB = 0, tkB = 0;
+        int nvB = 0;
+        if (c + 1 < nch) {
+            const int jc = j0 + (c + 1) * CH;
+            const double2* uc = urow + jc;
+            // phase 1: the cells (in-raster and in-group bits per slot)
+            int32_t ix[CH], iy[CH];
+            uint32_t vjb = 0;
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int j = jc + t;
-            int32_t ix, iy;
-            const bool in = cell_of(j, ix, iy);
-            const uint4* vp = vdummy;
-            const float* tp = rs.t4;
-            cl[t] = -1;
-            if (j < j1) {
-                if (in) {
-                    inb |= 1u << t;
-                    if (CELLS) cl[t] = iy * rs.nx + ix;
-                    const int32_t b = (iy >> rs.sshift) * rs.snbx + (ix >> rs.sshift);
-                    const uint32_t code = (s_hdr[b >> 4] >> ((b & 15) * 2)) & 3u;
-                    float ub, lb;
-                    pk_bounds(rs, s_hdr, ix, iy, ub, lb);
-                    Lb = fmaxf(Lb, lb);
-                    if (lb == ub) E = fmaxf(E, ub);  // a block of one value: that value
-                    uint32_t sub = 0;
-                    if (code == 3u) {
-                        vp = rec + (iy * rs.nx + ix);
-                    } else {
-                        const int32_t a4 = p4_addr(rs, ix, iy);
-                        if (code == 2u) {
-                            const int32_t a8 = e8_addr(rs, ix, iy);
-                            vp = reinterpret_cast<const uint4*>(rs.e8 + (a8 & ~1));
-                            sub = (uint32_t)(a8 & 1) * 2u;
-                        } else if (code == 1u) {
-                            vp = reinterpret_cast<const uint4*>(rs.p4 + (a4 & ~3));
-                            sub = (uint32_t)(a4 & 3);
-                        }
-                        if (!(ub <= E) && !(ub < Lb)) {
-                            tk |= 1u << t;
-                            tp = rs.t4 + a4;
-                        }
-                    }
-                    cs |= (PkCodes<CH>)(code | (sub << 2)) << (4 * t);
-                } else {  // off the raster: sea level, exactly
-                    E = fmaxf(E, 0.0f);
-                    Lb = fmaxf(Lb, 0.0f);
+            for (int t = 0; t < CH; ++t) {
+                const int j = jc + t;
+                const double2 u = uc[t];
+                int32_t x, y;
+                bool in = gen_cell(rs, cx + 0.5 * (vx * u.x - vy * u.y),
+                                   cy + 0.5 * (vy * u.x + vx * u.y), x, y);
+                if (t == 0) {  // (j == 0 only in a chunk's first slot)
+                    const bool f = jc == 0;
+                    x = f ? ixF : x;
+                    y = f ? iyF : y;
+                    in = f ? inF : in;
                 }
+                const bool l = j == W - 1;
+                ix[t] = l ? ixL : x;
+                iy[t] = l ? iyL : y;
+                in = l ? inL : in;
+                const bool vj = j < j1;
+                vjb |= (uint32_t)vj << t;
+                vinB |= (uint32_t)(in & vj) << t;
             }
-            r[t] = *vp;
-            tv[t] = *tp;
-        }
-        const int nv = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
+            // phase 2: the header reads (cell (0, 0) for a slot off the raster: valid reads)
+            uint32_t cw[CH], be[CH];
+            float2 sb[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const bool vl = t < nv;
-            const bool in = (inb >> t) & 1u;
-            const uint32_t cst = (uint32_t)(cs >> (4 * t)) & 15u;
-            uint32_t phi, psi, hit;
-            float rter;
-            pk_terms(r[t], cst, phi, psi, hit, rter);
-            nh += hit;
-            off += (vl && !in) ? 1u : 0u;
-            gc = gc + over_n((double)__uint_as_float(phi));
-            gn = gn + (double)__uint_as_float(psi);
-            const float ter = (cst & 3u) == 3u ? rter : ((tk >> t) & 1u) ? tv[t] : -INFINITY;
-            E = fmaxf(E, ter);
-        }
-        if (CELLS) {
-            // through the wave's LDS slice: lane l stages its CH cells, then each store
-            // instruction writes 64 / CH items' runs of CH consecutive cells (runs of
-            // cells[path][jc..jc+nv)), instead of 64 scattered 4-B stores per waypoint
-            int32_t* sw = s_cells + (threadIdx.x >> 6) * (CH * 64);
-            const int lane = threadIdx.x & 63;
-#pragma unroll
-            for (int t = 0; t < CH; ++t) sw[t * 64 + lane] = cl[t];
-            __builtin_amdgcn_wave_barrier();
-            const int64_t base = (int64_t)path * W + jc;  // this lane's run
-            constexpr int IPS = 64 / CH;                 // items per store instruction
-#pragma unroll
-            for (int k = 0; k < (64 + IPS - 1) / IPS; ++k) {
-                const int it = k * IPS + lane / CH, t = lane % CH;
-                const int src = it < 64 ? it : 63;
-                const int64_t b_it = __shfl(base, src);
-                const int nv_it = __shfl(nv, src);
-                // streaming stores: the cells are never re-read, and through L2 they evicted
-                // the gathers' lines (cfg3 --cells 0.471 -> 0.416 ms, profiles/r04/cellsnt)
-                if (lane < IPS * CH && it < 64 && t < nv_it)
-                    __builtin_nontemporal_store(sw[t * 64 + it], kg.cells + b_it + t);
+            for (int t = 0; t < CH; ++t) {
+                const int32_t b = pk_block(rs, ix[t], iy[t]);
+                cw[t] = s_hdr[b >> 4] >> ((b & 15) * 2);
+                const uint32_t bx = (uint32_t)(ix[t] >> rs.bshift);
+                const uint32_t by = (uint32_t)(iy[t] >> rs.bshift);
+                be[t] = bnd[__umul24(by, (uint32_t)rs.bnbx) + bx];
+                sb[t] = sbt[__umul24(by >> 2, (uint32_t)rs.sbnbx) + (bx >> 2)];
             }
-            __builtin_amdgcn_wave_barrier();
+            // phase 3: the decisions and the loads
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool vin = (vinB >> t) & 1u, vj = (vjb >> t) & 1u;
+                const uint32_t code = cw[t] & (vin ? 3u : 0u);
+                float ub, lb;
+                pk_bound_decode(be[t], sb[t], ub, lb);
+                // off the raster: +0.0, an exact value and a lower bound; a block of one
+                // value: ub
+                Lb = fmaxf(Lb, vin ? lb : vj ? 0.0f : -INFINITY);
+                E = fmaxf(E, vin ? (lb == ub ? ub : -INFINITY) : vj ? 0.0f : -INFINITY);
+                const bool fetch = vin & (code != 3u) & !(ub <= E) & !(ub < Lb);
+                const uint32_t a4 = (uint32_t)p4_addr(rs, ix[t], iy[t]);
+                // the entry's byte offset in its plane: a4 * 4 / 8 / 16 for codes 1 / 2 / 3;
+                // its aligned 16 B and the cell's word in them
+                const uint32_t ab = a4 << (code + 1u);
+                const uint32_t base = (code & 2u) ? ((code & 1u) ? o16 : o8) : o4;
+                const uint32_t voff = base + (code ? (ab & ~15u) : 0u);
+                kcB[t] = code | (ab & 12u);
+                rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
+                tvB[t] = *reinterpret_cast<const float*>(pk + (ot4 + (fetch ? a4 * 4u : 0u)));
+                tkB |= (uint32_t)fetch << t;
+            }
+            nvB = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
         }
+        if (c >= 0) {
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool vl = t < nvA;
+                const bool in = (vinA >> t) & 1u;
+                uint32_t phi, psi, hit;
+                float rter;
+                pk_terms_k(rA[t], kcA[t], phi, psi, hit, rter);
+                nh += hit;
+                off += (vl && !in) ? 1u : 0u;
+                gc = gc + over_n((double)__uint_as_float(phi));
+                gn = gn + (double)__uint_as_float(psi);
+                const float ter = (kcA[t] & 3u) == 3u ? rter : ((tkA >> t) & 1u) ? tvA[t] : -INFINITY;
+                E = fmaxf(E, ter);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+        vinA = vinB, tkA = tkB, nvA = nvB;
     }
     HSlot o;
     o.cost = gc;
@@ -5817,27 +5910,27 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
 }
 
 // K2h evaluation: workgroups of H_BS items (xcd_chunk), the packed raster's header (codes,
-// bounds, superblocks) and the unit-arc rows staged in LDS, then one item per lane (h_item)
-template <int CH, bool CELLS>
-__global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaster rs, KGrp kg,
-                                                               const uint4* __restrict__ rec) {
+// bounds, superblocks) and the unit-arc rows (+ G + CH padding slots) staged in LDS, then one item
+// per lane (h_item)
+template <int CH>
+__global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaster rs, KGrp kg) {
+    PK_CODES_CHECK(CH);
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_hdr = s_dyn;
     double2* s_u = reinterpret_cast<double2*>(s_dyn + rs.hwords);
-    // CELLS: each wave's [CH][64] staging slice of waypoint cells, after the unit-arc rows and
-    // their junk slot
-    int32_t* s_cells = reinterpret_cast<int32_t*>(s_u + kg.D * p.N + 1);
-    // the item's order entry and pair first: their two dependent round trips overlap the
-    // staging below instead of following it
+    // the item's order entry, pair and path bound first: their dependent round trips overlap
+    // the staging below instead of following it
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * H_BS + threadIdx.x;
     const bool live = pos < kg.n_items;
     const int32_t item = live ? kg.order[pos] : 0;
     const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const float Lb = kg.lbp[path];
+    const int nu = kg.D * p.N;
     {  // staging: every load of a thread issued before its first LDS store (hwords % 4 == 0)
         constexpr int U = 4;
-        const int nv = rs.hwords >> 2, nu = kg.D * p.N;
+        const int nv = rs.hwords >> 2;
         const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
         uint4* dst = reinterpret_cast<uint4*>(s_hdr);
         const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
@@ -5850,14 +5943,49 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
                 v[k] = *(i < nv ? src + i : i < nv + nu ? gu + (i - nv) : src);
             }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {  // unconditional stores (past the end: a junk slot)
+            for (int k = 0; k < U; ++k) {  // unconditional stores (past the end: a pad slot)
                 const int i = i0 + k * H_BS;
                 *(i < nv ? dst + i : du + min(i - nv, nu)) = v[k];
             }
         }
     }
     __syncthreads();
-    h_item<CH, CELLS>(p, rs, kg, rec, s_hdr, s_u, s_cells, live, item, path, q, pr);
+    // the padding: a lane's slots reach index nu + G + CH - 2 at most (a last group of one
+    // waypoint in a wave of full ones)
+    if ((int)threadIdx.x < kg.G + CH) s_u[nu + threadIdx.x] = make_double2(0.0, 0.0);
+    __syncthreads();
+    h_item<CH>(p, rs, kg, s_hdr, s_u, live, item, path, q, pr, Lb);
+}
+
+// The waypoint cells (the reference's returned waypoints as raster cells, solver.py:49,
+// main.py:186-190) of the sorted forms: cells[path][j] = iy nx + ix (-1 off the raster) by the
+// evaluations' own point and cell arithmetic (gen_cell), one thread per (path, j), so
+// consecutive threads write consecutive cells -- whole lines, no gathers.  (Written by the
+// evaluation's lanes through LDS instead, the 21-cell runs of scattered items cost K2h ~120 us
+// of partial-line writes per cfg3 step: 402 MB of WRITE_SIZE for 164 MB of cells,
+// profiles/r04/final2/cells.)
+__global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
+                                               int32_t* __restrict__ cells) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int W = kg.W, N = p.N;
+    if (i >= (int64_t)kg.P * W) return;
+    const int32_t path = (int32_t)(i / W);
+    const int j = (int)(i - (int64_t)path * W);
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+    const int32_t d = path - q * kg.D;
+    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+    const double2 u = reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(j - 1, 0), N - 1)];
+    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
+    double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
+    double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+    x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
+    x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
+    int32_t ix, iy;
+    const bool in = gen_cell(rs, x0, x1, ix, iy);
+    // plain stores: a wave writes 256 contiguous bytes, whole lines the L2 writes back once
+    // (streaming stores of such runs measured ~3.7x slower, tools/write_runs.hip)
+    cells[i] = in ? iy * rs.nx + ix : -1;
 }
 
 // outputs of every path (block = 64 pairs x D, k_g_final's layout): the geometry terms from
@@ -5944,42 +6072,18 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
 }
 
 // ---- K4h: the volume (config 5) in K2h's form -------------------------------------------------
-// The packed volume (uam_volume_pack): one 16-B voxel {risk, psi_nfz, terrain, flags} per
-// (ix, iy, iz) -- the column's terrain / flags beside the layer's pair, so a waypoint is ONE
-// request -- in blocks of 4 x 2 cells of one layer (one 128-B line), layer-major planes.  The
-// (path, group) items are sorted on the altitude band and the Hilbert tile of the middle
-// waypoint (band-major, so the items an XCD runs together share a band's lines), evaluated
-// with K2h's grouped partial sums, and the output launch adds the similarity-form geometry.
-// Definition: oracle orc_eval_generated_h, mode 2.
-__device__ __forceinline__ int64_t vpk_index(int32_t nbx4, int32_t nby2, int32_t ix, int32_t iy,
-                                             int32_t iz) {
-    return ((((int64_t)iz * nby2 + (iy >> 1)) * nbx4 + (ix >> 2)) << 3) | ((iy & 1) << 2) |
-           (ix & 3);
-}
-
-// one thread per packed voxel (padding cells: zero)
-__global__ __launch_bounds__(256) void k_volume_pack(const uint2* __restrict__ vox,
-                                                     const uint2* __restrict__ col, int nx,
-                                                     int ny, int nz, int nbx4, int nby2,
-                                                     uint4* __restrict__ out) {
-    const int64_t total = (int64_t)nbx4 * nby2 * 8 * nz;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t w = (int32_t)(i & 7);
-        const int64_t blk = i >> 3;
-        const int32_t bx = (int32_t)(blk % nbx4);
-        const int64_t r = blk / nbx4;
-        const int32_t by = (int32_t)(r % nby2), iz = (int32_t)(r / nby2);
-        const int32_t ix = bx * 4 + (w & 3), iy = by * 2 + (w >> 2);
-        uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (ix < nx && iy < ny) {
-            const int64_t c = (int64_t)iy * nx + ix;
-            const uint2 a = vox[c * nz + iz], b = col[c];
-            o = make_uint4(a.x, a.y, b.x, b.y);
-        }
-        out[i] = o;
-    }
-}
+// The packed volume (uam_volume_pack; layout: VpkDims).  Planes in K2h's 4 x 8-column blocks,
+// one per layer (layer-major), all at one index i4: r4 {risk}, e8 {risk, |psi| | nfz << 31} and
+// v16, the whole voxel {risk, psi_nfz, terrain, flags} (the column's terrain and flags beside
+// the layer's pair); t4 the column terrain (one layer, the same column index).  A header
+// (staged in LDS) holds a 2-bit code per 8 x 8-column block -- 0: every voxel of its columns has
+// risk == +-0, psi == +-0 and no no-fly flag (nothing to read but the terrain); 1: psi == +-0 and
+// no flag (r4); 2: no psi below zero (e8); 3: v16 -- then the column terrain's bounds (the
+// raster's scheme: u16 codes per bound block of columns, float2 {base, step} per 4 x 4 bound
+// blocks).  The (path, group) items are sorted on the altitude band and the Hilbert tile of the
+// middle waypoint (band-major, so the items an XCD runs together share a band's lines),
+// evaluated with K2h's grouped partial sums, and the output launch adds the similarity-form
+// geometry.  Definition: oracle orc_eval_generated_h, mode 2.
 
 struct alignas(16) VSlot {  // 32 B per (path, group)
     double cost;   // risk / N of the group's waypoints, from +0.0 in waypoint order
@@ -5989,49 +6093,37 @@ struct alignas(16) VSlot {  // 32 B per (path, group)
     uint32_t pad;
 };
 
-// The packed volume as K4h reads it (uam_volume_pack; layout: VpkDims).  Header (staged in
-// LDS): a 2-bit code per 8 x 8-column block -- 0: every voxel of its columns has risk == +-0,
-// psi == +-0 and no no-fly flag (nothing to read but the terrain); 1: psi == +-0 and no flag (the
-// 4-B risk plane r4); 2: no psi below zero (the 8-B plane e8 {risk, |psi| | nfz << 31}); 3: the
-// 16-B voxels vp -- then the column terrain's bounds (the raster's scheme: u16 codes per bound
-// block of columns, float2 {base, step} per 4 x 4 bound blocks).  Planes: r4 and the column
-// terrain t4 in 4 x 8-column blocks, e8 in 4 x 4-column blocks (one layer per plane, layer-
-// major), vp in 4 x 2-column blocks.
 struct KVol4 {
-    int32_t nx, ny, nz, nbx4, nby2;
+    int32_t nx, ny, nz;
     double x0, y_top, z0, dz, inv_dx, inv_dy, inv_dz;
-    const uint4* __restrict__ vp;
     int32_t zshift, nbands;
     const uint32_t* __restrict__ hdr;   // codes | bounds | superblocks
     int32_t hwords, cnbx, bnd_off, sbt_off, bshift, bnbx, sbnbx;
-    int32_t nb8, nb4, lnby4;
-    const uint32_t* __restrict__ r4;
-    const uint2* __restrict__ e8;
-    const float* __restrict__ t4;
+    int32_t nb8, lnby4;
+    uint32_t layer;                     // i4 entries per layer (lnby4 nb8 32)
+    // the planes from the packed base by 32-bit byte offsets (o4: r4, o8: e8, o16: v16, ot4:
+    // t4); null when the copy is 4 GiB or larger or a layer holds 2^24 entries (K4h stands aside)
+    const char* __restrict__ pk;
+    uint32_t o4, o8, o16, ot4;
 };
 
 constexpr int VPK_CSHIFT = 3;           // code blocks of 8 x 8 columns
 constexpr int VPK_HDR_LDS = 64 * 1024;  // the header in LDS up to this
 
-__device__ __forceinline__ int64_t vr4_index(const KVol4& v, int32_t ix, int32_t iy, int32_t iz) {
-    return ((((int64_t)iz * v.lnby4 + (iy >> 2)) * v.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) |
-           (ix & 7);
-}
-__device__ __forceinline__ int64_t ve8_index(const KVol4& v, int32_t ix, int32_t iy, int32_t iz) {
-    return ((((int64_t)iz * v.lnby4 + (iy >> 2)) * v.nb4 + (ix >> 2)) << 4) | ((iy & 3) << 2) |
-           (ix & 3);
-}
-__device__ __forceinline__ int32_t vt4_index(const KVol4& v, int32_t ix, int32_t iy) {
-    return ((((iy >> 2) * v.nb8 + (ix >> 3)) << 5) | ((iy & 3) << 3) | (ix & 7));
+// the column (ix, iy)'s index in the 4 x 8-column blocks (t4; i4 = it + iz layer)
+__device__ __forceinline__ uint32_t vt4_index(const KVol4& v, int32_t ix, int32_t iy) {
+    return ((__umul24((uint32_t)(iy >> 2), (uint32_t)v.nb8) + (uint32_t)(ix >> 3)) << 5) |
+           (((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u);
 }
 
-// the 4-B risk plane and the 8-B {risk, |psi| | nfz << 31} plane: one thread per r4 entry,
-// which also writes its cell's e8 entry (padding: zero)
-__global__ __launch_bounds__(256) void k_volume_pack_re(const uint2* __restrict__ vox,
-                                                        const uint2* __restrict__ col, KVol4 v,
-                                                        uint32_t* __restrict__ r4,
-                                                        uint2* __restrict__ e8) {
-    const int64_t total = (int64_t)v.nz * v.lnby4 * v.nb8 * 32;
+// the layer planes r4, e8 and v16: one thread per i4 entry, which writes all three (padding:
+// zero)
+__global__ __launch_bounds__(256) void k_volume_pack_planes(const uint2* __restrict__ vox,
+                                                            const uint2* __restrict__ col,
+                                                            KVol4 v, uint32_t* __restrict__ r4,
+                                                            uint2* __restrict__ e8,
+                                                            uint4* __restrict__ v16) {
+    const int64_t total = (int64_t)v.nz * v.layer;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t w = (int32_t)(i & 31);
@@ -6040,15 +6132,15 @@ __global__ __launch_bounds__(256) void k_volume_pack_re(const uint2* __restrict_
         const int64_t r = blk / v.nb8;
         const int32_t by = (int32_t)(r % v.lnby4), iz = (int32_t)(r / v.lnby4);
         const int32_t ix = bx * 8 + (w & 7), iy = by * 4 + (w >> 3);
-        uint32_t risk = 0u, pz = 0u;
+        uint2 a = make_uint2(0u, 0u), cl = make_uint2(0u, 0u);
         if (ix < v.nx && iy < v.ny) {
             const int64_t c = (int64_t)iy * v.nx + ix;
-            const uint2 a = vox[c * v.nz + iz];
-            risk = a.x;
-            pz = (a.y & 0x7fffffffu) | ((col[c].y & UAM_FLAG_NFZ) ? 0x80000000u : 0u);
+            a = vox[c * v.nz + iz];
+            cl = col[c];
         }
-        r4[i] = risk;
-        if (ix < v.nb4 * 4) e8[ve8_index(v, ix, iy, iz)] = make_uint2(risk, pz);
+        r4[i] = a.x;
+        e8[i] = make_uint2(a.x, (a.y & 0x7fffffffu) | ((cl.y & UAM_FLAG_NFZ) ? 0x80000000u : 0u));
+        v16[i] = make_uint4(a.x, a.y, cl.x, cl.y);
     }
 }
 
@@ -6098,6 +6190,82 @@ __global__ __launch_bounds__(256) void k_volume_codes(const uint2* __restrict__ 
 // the altitude of waypoint j (uam_eval_generated3d: z0 + (zf - z0) (j / (N+1)))
 __device__ __forceinline__ double vz_at(double za, double zb, double jw) {
     return za + (zb - za) * jw;
+}
+
+// the voxel of a generated point (false outside the volume or NaN, with (0, 0, 0) then: valid
+// header and plane indices)
+__device__ __forceinline__ bool vol_voxel(const KVol4& vs, double x0, double x1, double z,
+                                          int32_t& ix, int32_t& iy, int32_t& iz) {
+    const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
+    const double tz = (z - vs.z0) * vs.inv_dz;
+    const bool in = (tx >= 0.0) & (tx < (double)vs.nx) & (ty >= 0.0) & (ty < (double)vs.ny) &
+                    (tz >= 0.0) & (tz < (double)vs.nz);
+    ix = in ? (int32_t)tx : 0;
+    iy = in ? (int32_t)ty : 0;
+    iz = in ? (int32_t)tz : 0;
+    return in;
+}
+
+// K4h: a path's sampled upper bound of its minimum clearance (k_v_eval's Ub): the minimum of
+// z - lb over its in-volume waypoints j = 0, s, 2s, ... (s = kg.lb_stride) and j = W - 1, at
+// their own voxels and altitudes by the evaluation's operations (+inf: none)
+__device__ __forceinline__ double v_path_ub(const KParams& p, const KVol4& vs, const KGrp& kg,
+                                            int32_t path) {
+    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
+    const double* pr = kg.pairs + (int64_t)q * 6;
+    const double ax = pr[0], ay = pr[1], za = pr[2], bx = pr[3], by = pr[4], zb = pr[5];
+    const double2* u = reinterpret_cast<const double2*>(kg.utab) + (int64_t)d * p.N - 1;
+    const int W = kg.W;
+    double Ub = INFINITY;
+    auto take = [&](double x0, double x1, int j) {
+        const double z = vz_at(za, zb, (double)j / (double)(W - 1));
+        int32_t ix, iy, iz;
+        const bool in = vol_voxel(vs, x0, x1, z, ix, iy, iz);
+        const uint32_t bx2 = (uint32_t)(ix >> vs.bshift), by2 = (uint32_t)(iy >> vs.bshift);
+        const uint32_t e = reinterpret_cast<const uint16_t*>(vs.hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
+        const float2 sb =
+            reinterpret_cast<const float2*>(vs.hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx + (bx2 >> 2)];
+        float ub, lb;
+        pk_bound_decode(e, sb, ub, lb);
+        if (in) Ub = fmin(Ub, z - (double)lb);
+    };
+    take(ax, ay, 0);
+    take(bx, by, W - 1);
+    // four samples at a time, every load of the four issued together (a sample past the last
+    // interior waypoint repeats it)
+    constexpr int K = 4;
+    for (int j0 = kg.lb_stride; j0 < W - 1; j0 += K * kg.lb_stride) {
+        double2 uu[K];
+        int jj[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            jj[k] = min(j0 + k * kg.lb_stride, W - 2);
+            uu[k] = u[jj[k]];
+        }
+        uint32_t e[K];
+        float2 sb[K];
+        double z[K];
+        bool in[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double x0, x1;
+            arc_point(ax, ay, bx, by, uu[k].x, uu[k].y, x0, x1);
+            z[k] = vz_at(za, zb, (double)jj[k] / (double)(W - 1));
+            int32_t ix, iy, iz;
+            in[k] = vol_voxel(vs, x0, x1, z[k], ix, iy, iz);
+            const uint32_t bx2 = (uint32_t)(ix >> vs.bshift), by2 = (uint32_t)(iy >> vs.bshift);
+            e[k] = reinterpret_cast<const uint16_t*>(vs.hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
+            sb[k] = reinterpret_cast<const float2*>(vs.hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx +
+                                                                         (bx2 >> 2)];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float ub, lb;
+            pk_bound_decode(e[k], sb[k], ub, lb);
+            if (in[k]) Ub = fmin(Ub, z[k] - (double)lb);
+        }
+    }
+    return Ub;
 }
 
 // sort, launch 1 (K4h): keys on (altitude band, tile) of each item's middle waypoint
@@ -6162,37 +6330,45 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
             atomicAdd(&h[key], 1);
         }
     }
+    if (kg.ubp) {  // the partition's paths' sampled clearance upper bounds, one thread per path
+        const int64_t plo = (int64_t)kg.P * b / G_NBK, phi = (int64_t)kg.P * (b + 1) / G_NBK;
+        for (int64_t pth = plo + t; pth < phi; pth += 1024)
+            kg.ubp[pth] = v_path_ub(p, vs, kg, (int32_t)pth);
+    }
     __syncthreads();
     for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
 }
 
-// every (path, group) item in sorted order: points (x, y by the arc formula, z on the linear
-// climb), per waypoint one 16-B value load (by the column block's code: the r4 / e8 entries'
-// aligned 16 B, the 16-B voxel, or the dummy line) and a 4-B terrain load only where the
-// terrain could still decide an output (the dummy line otherwise), then the branch-free consume.
+// every (path, group) item in sorted order (h_item's phases): the CH waypoints' voxels (x, y by
+// the arc formula or the pair's end points, z on the linear climb), the header reads, then per
+// slot the decisions and two unconditional loads -- the code's entry (r4 / e8 / v16, the dummy
+// line in code 0 or outside the volume) and the terrain (the first t4 word unless fetched) -- by
+// 32-bit offsets from the packed base; then the branch-free consume.
 //
 // The terrain by bounds (as K2h's; the outputs are exactly the per-waypoint ones).  Waypoint j
-// in the volume has lb_j <= T_j <= ub_j (pk_bounds over the column grid) and
+// in the volume has lb_j <= T_j <= ub_j (the column grid's bounds) and
 //   below_j = zc_j < T_j (zc_j its layer centre): decided when zc_j < lb_j (1) or zc_j >= ub_j
 //       (0), else its terrain is fetched;
 //   c_j = z_j - T_j, whose path minimum is min_clearance: z_j - ub_j <= c_j <= z_j - lb_j (the
-//       float64 subtraction is monotone).  The item keeps Ub, the minimum of z - lb over a sample
-//       of its path's in-volume waypoints (every kg.lb_stride-th, the waypoints' own
-//       operations) and over its own so far, an upper bound of the path minimum M, and E, the
-//       minimum of the c_j it has taken exactly; it fetches w iff !(z_w - ub_w >= E) &&
-//       !(z_w - ub_w > Ub).  If w* holds M and is not taken: z - ub >= E gives M >= E >= M,
-//       and z - ub > Ub >= M is impossible.  NaN bounds (no bound) always fetch.
+//       float64 subtraction is monotone).  The item keeps Ub, an upper bound of the path minimum
+//       M (v_path_ub's samples, then its own waypoints' z - lb), and E, the minimum of the c_j
+//       it has taken exactly (fetched, v16's, one-value blocks); it fetches w iff it is
+//       undecided or !(z_w - ub_w >= E) && !(z_w - ub_w > Ub).  If w* holds M and is not
+//       taken: z - ub >= E gives M >= E >= M, and z - ub > Ub >= M is impossible.  NaN bounds
+//       (no bound) always fetch.
 template <int CH>
-__global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
+__global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
                                                                               KGrp kg) {
     PK_CODES_CHECK(CH);
-    // unit-arc rows, then j / (W-1), then the header
+    // unit-arc rows + padding, then j / (W-1) (+ padding), then the header
     extern __shared__ __attribute__((aligned(16))) double2 s_u[];
     const int N = p.N, W = kg.W;
-    const int nu = kg.D * N;
-    double* s_jw = reinterpret_cast<double*>(s_u + nu);
-    uint32_t* s_hdr = reinterpret_cast<uint32_t*>(s_jw + ((W + 1) & ~1));
-    // the item's order entry and pair before the staging (their round trips overlap it)
+    const int nu = kg.D * N, npad = kg.G + 16;  // a lane's slots reach j <= W + G + CH - 3
+    double* s_jw = reinterpret_cast<double*>(s_u + nu + npad);
+    const int njw = W + npad;
+    uint32_t* s_hdr = reinterpret_cast<uint32_t*>(s_jw + ((njw + 1) & ~1));
+    // the item's order entry, pair and path bound before the staging (their round trips
+    // overlap it)
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const bool live = pos < kg.n_items;
     const int32_t item = live ? kg.order[pos] : 0;
@@ -6203,145 +6379,156 @@ __global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     const double2 pa = *reinterpret_cast<const double2*>(prp);
     const double2 pb = *reinterpret_cast<const double2*>(prp + 2);
     const double2 pc = *reinterpret_cast<const double2*>(prp + 4);
-    for (int i = threadIdx.x; i < nu; i += 256) s_u[i] = reinterpret_cast<const double2*>(kg.utab)[i];
-    for (int j = threadIdx.x; j < W; j += 256) s_jw[j] = (double)j / (double)(W - 1);
+    double Ub = kg.ubp[path];
+    for (int i = threadIdx.x; i < nu + npad; i += 256)
+        s_u[i] = i < nu ? reinterpret_cast<const double2*>(kg.utab)[i] : make_double2(0.0, 0.0);
+    for (int j = threadIdx.x; j < njw; j += 256)
+        s_jw[j] = j < W ? (double)j / (double)(W - 1) : 0.0;
     {
         const uint4* src = reinterpret_cast<const uint4*>(vs.hdr);
         uint4* dst = reinterpret_cast<uint4*>(s_hdr);
         for (int i = threadIdx.x; i < (vs.hwords >> 2); i += 256) dst[i] = src[i];
     }
     __syncthreads();
-    if (!live) return;
     const double ax = pa.x, ay = pa.y, za = pb.x, bx = pb.y, by = pc.x, zb = pc.y;
-    const double2* urow = s_u + d * N;
-    const int j0 = s * kg.G, j1 = min(j0 + kg.G, W);
+    const double2* urow = s_u + d * N - 1;  // waypoint j's unit vector: urow[j]
+    const int j0 = s * kg.G, j1 = live ? min(j0 + kg.G, W) : j0;
+    int nch = (j1 - j0 + CH - 1) / CH;  // the wave's most: a wave-uniform loop
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nch = max(nch, __shfl_xor(nch, o));
     const double vx = ax - bx, vy = ay - by;
     const double cx = (bx + ax) * 0.5, cy = (by + ay) * 0.5;
     const double dN = (double)N, yN = kg.inv_n;
-    auto over_n = [&](double a) {
-        if (yN == 0.0) return a / dN;
+    auto over_n = [&](double a) {  // (K4h: N <= 4096)
         const double q0 = a * yN;
         const double q1 = fma(fma(-q0, dN, a), yN, q0);
         return __builtin_isinf(a) ? q0 : q1;
     };
-    // waypoint j: its altitude, and its voxel (false outside the volume or NaN)
-    auto voxel_of = [&](int j, double& z, int32_t& ix, int32_t& iy, int32_t& iz) -> bool {
-        const double2 u = urow[min(max(j - 1, 0), N - 1)];
-        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);
-        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-        x0 = j == 0 ? ax : j == W - 1 ? bx : x0;
-        x1 = j == 0 ? ay : j == W - 1 ? by : x1;
-        z = vz_at(za, zb, s_jw[min(j, W - 1)]);
-        const double tx = (x0 - vs.x0) * vs.inv_dx, ty = (vs.y_top - x1) * vs.inv_dy;
-        const double tz = (z - vs.z0) * vs.inv_dz;
-        const bool in = (tx >= 0.0) && (tx < (double)vs.nx) && (ty >= 0.0) &&
-                        (ty < (double)vs.ny) && (tz >= 0.0) && (tz < (double)vs.nz);
-        ix = in ? (int32_t)tx : 0;
-        iy = in ? (int32_t)ty : 0;
-        iz = in ? (int32_t)tz : 0;
-        return in;
-    };
-    auto bounds = [&](int32_t ix, int32_t iy, float& ub, float& lb) {
-        const int32_t bx2 = ix >> vs.bshift, by2 = iy >> vs.bshift;
-        const uint32_t e = reinterpret_cast<const uint16_t*>(s_hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
-        const float2 sb = reinterpret_cast<const float2*>(s_hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx +
-                                                                              (bx2 >> 2)];
-        ub = sb.x + (float)(e & 255u) * sb.y;
-        lb = sb.x + (float)(e >> 8) * sb.y;
-    };
-    // the path's sampled upper bound of its minimum clearance
-    double Ub = INFINITY;
-    for (int j = 0; j < W; j += kg.lb_stride) {
-        double z;
-        int32_t ix, iy, iz;
-        const bool in = voxel_of(j, z, ix, iy, iz);
-        float ub, lb;
-        bounds(ix, iy, ub, lb);
-        if (in) Ub = fmin(Ub, z - (double)lb);
-    }
-    const uint4* const vdummy = reinterpret_cast<const uint4*>(vs.r4);
+    // the layer centre of layer iz (the below-terrain test)
+    auto zc_of = [&](int32_t iz) { return vs.z0 + ((double)iz + 0.5) * vs.dz; };
+    // the end points' voxels, formed once
+    int32_t ixF, iyF, izF, ixL, iyL, izL;
+    const double zF = vz_at(za, zb, s_jw[0]), zL = vz_at(za, zb, s_jw[W - 1]);
+    const bool inF = vol_voxel(vs, ax, ay, zF, ixF, iyF, izF);
+    const bool inL = vol_voxel(vs, bx, by, zL, ixL, iyL, izL);
+    const uint16_t* const bnd = reinterpret_cast<const uint16_t*>(s_hdr + vs.bnd_off);
+    const float2* const sbt = reinterpret_cast<const float2*>(s_hdr + vs.sbt_off);
+    const char* const pk = vs.pk;
+    const uint32_t o4 = __builtin_amdgcn_readfirstlane(vs.o4);
+    const uint32_t o8 = __builtin_amdgcn_readfirstlane(vs.o8);
+    const uint32_t o16 = __builtin_amdgcn_readfirstlane(vs.o16);
+    const uint32_t ot4 = __builtin_amdgcn_readfirstlane(vs.ot4);
+    const uint32_t layer = __builtin_amdgcn_readfirstlane(vs.layer);
     double gc = 0.0, gn = 0.0, E = INFINITY;
     uint32_t nh = 0, off = 0, bel = 0;
-    for (int jc = j0; jc < j1; jc += CH) {
-        uint4 r[CH];
-        float tv[CH];
-        double zt[CH];
-        int32_t izt[CH];
-        uint32_t inb = 0, tk = 0, kb = 0, bv = 0;  // in; terrain taken; below known; its value
-        // the layer centre of layer iz (k_v_eval's below-terrain test)
-        auto zc_of = [&](int32_t iz) { return vs.z0 + ((double)iz + 0.5) * vs.dz; };
-        PkCodes<CH> cs = 0;
+    // one chunk ahead, as h_item: iteration c issues chunk c + 1 (B arrays) and consumes chunk
+    // c (A arrays)
+    // (the slot's layer rides in its kind word's high bits; consume recomputes its altitude)
+    uint4 rA[CH];
+    float tvA[CH];
+    uint32_t kcA[CH], vinA = 0, tkA = 0, bvA = 0;
+    int nvA = 0, jcA = 0;
+    for (int c = -1; c < nch; ++c) {  // (nch wave-uniform)
+        uint4 rB[CH];
+        float tvB[CH];
+        uint32_t kcB[CH], vinB = 0, tkB = 0, bvB = 0;
+        int nvB = 0;
+        const int jc = j0 + (c + 1) * CH;
+        if (c + 1 < nch) {
+            double zB[CH];
+            int32_t izB[CH];
+            const double2* uc = urow + jc;
+            // phase 1: the voxels
+            int32_t ix[CH], iy[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int j = jc + t;
-            int32_t ix, iy, iz;
-            const bool in = voxel_of(j, zt[t], ix, iy, iz);
-            const uint4* ptr = vdummy;
-            const float* tp = vs.t4;
-            izt[t] = iz;
-            const double zc = zc_of(iz);
-            if ((j < j1) && in) {
-                inb |= 1u << t;
-                const int32_t b = (iy >> VPK_CSHIFT) * vs.cnbx + (ix >> VPK_CSHIFT);
-                const uint32_t code = (s_hdr[b >> 4] >> ((b & 15) * 2)) & 3u;
-                uint32_t sub = 0;
-                if (code == 3u) {
-                    ptr = vs.vp + vpk_index(vs.nbx4, vs.nby2, ix, iy, iz);
-                } else {
-                    if (code == 2u) {
-                        const int64_t a = ve8_index(vs, ix, iy, iz);
-                        ptr = reinterpret_cast<const uint4*>(vs.e8 + (a & ~(int64_t)1));
-                        sub = (uint32_t)(a & 1) * 2u;
-                    } else if (code == 1u) {
-                        const int64_t a = vr4_index(vs, ix, iy, iz);
-                        ptr = reinterpret_cast<const uint4*>(vs.r4 + (a & ~(int64_t)3));
-                        sub = (uint32_t)(a & 3);
-                    }
-                    float ub, lb;
-                    bounds(ix, iy, ub, lb);
-                    const double clo = zt[t] - (double)ub;
-                    Ub = fmin(Ub, zt[t] - (double)lb);
-                    if (lb == ub) {  // a block of one terrain value: every term exactly
-                        E = fmin(E, zt[t] - (double)ub);
-                        kb |= 1u << t;
-                        bv |= (zc < (double)ub ? 1u : 0u) << t;
-                    } else {
-                        if (zc < (double)lb) {
-                            kb |= 1u << t;
-                            bv |= 1u << t;
-                        } else if (zc >= (double)ub) {
-                            kb |= 1u << t;
-                        }
-                        if (!((kb >> t) & 1u) || (!(clo >= E) && !(clo > Ub))) {
-                            tk |= 1u << t;
-                            tp = vs.t4 + vt4_index(vs, ix, iy);
-                        }
-                    }
+            for (int t = 0; t < CH; ++t) {
+                const int j = jc + t;
+                const double2 u = uc[t];
+                const double z = vz_at(za, zb, s_jw[j]);
+                int32_t x, y, zz;
+                bool in = vol_voxel(vs, cx + 0.5 * (vx * u.x - vy * u.y),
+                                    cy + 0.5 * (vy * u.x + vx * u.y), z, x, y, zz);
+                if (t == 0) {  // (j == 0 only in a chunk's first slot)
+                    const bool f = jc == 0;
+                    x = f ? ixF : x;
+                    y = f ? iyF : y;
+                    zz = f ? izF : zz;
+                    in = f ? inF : in;
                 }
-                cs |= (PkCodes<CH>)(code | (sub << 2)) << (4 * t);
+                const bool l = j == W - 1;
+                ix[t] = l ? ixL : x;
+                iy[t] = l ? iyL : y;
+                izB[t] = l ? izL : zz;
+                in = l ? inL : in;
+                zB[t] = z;  // (the end points' z by the same formula)
+                vinB |= (uint32_t)(in & (j < j1)) << t;
             }
-            r[t] = *ptr;
-            tv[t] = *tp;
-        }
-        const int nv = min(CH, j1 - jc);
+            // phase 2: the header reads (column (0, 0) outside the volume: valid reads)
+            uint32_t cw[CH], be[CH];
+            float2 sb[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const bool vl = t < nv, in = (inb >> t) & 1u;
-            const uint32_t cst = (uint32_t)(cs >> (4 * t)) & 15u, code = cst & 3u;
-            uint32_t risk, psi, hit;
-            float rter;
-            pk_terms(r[t], cst, risk, psi, hit, rter);
-            gc = gc + over_n(in ? (double)__uint_as_float(risk) : 0.0);
-            gn = gn + ((in && (code & 2u)) ? (double)__uint_as_float(psi) : 0.0);
-            nh += in ? hit : 0u;
-            off += (vl && !in) ? 1u : 0u;
-            // the exact terrain, where taken: the 16-B voxel's (code 3) or the fetched one
-            const bool ex = in && (code == 3u || ((tk >> t) & 1u));
-            const float ter = code == 3u ? rter : tv[t];
-            const uint32_t below = ex ? (zc_of(izt[t]) < (double)ter ? 1u : 0u) : ((bv >> t) & 1u);
-            bel += in ? below : 0u;
-            E = ex ? fmin(E, zt[t] - (double)ter) : E;
+            for (int t = 0; t < CH; ++t) {
+                const uint32_t b = __umul24((uint32_t)(iy[t] >> VPK_CSHIFT), (uint32_t)vs.cnbx) +
+                                   (uint32_t)(ix[t] >> VPK_CSHIFT);
+                cw[t] = s_hdr[b >> 4] >> ((b & 15u) * 2u);
+                const uint32_t bx2 = (uint32_t)(ix[t] >> vs.bshift);
+                const uint32_t by2 = (uint32_t)(iy[t] >> vs.bshift);
+                be[t] = bnd[__umul24(by2, (uint32_t)vs.bnbx) + bx2];
+                sb[t] = sbt[__umul24(by2 >> 2, (uint32_t)vs.sbnbx) + (bx2 >> 2)];
+            }
+            // phase 3: the decisions and the loads
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool vin = (vinB >> t) & 1u;
+                const uint32_t code = cw[t] & (vin ? 3u : 0u);
+                float ub, lb;
+                pk_bound_decode(be[t], sb[t], ub, lb);
+                const double z = zB[t], zc = zc_of(izB[t]);
+                const bool k1 = zc < (double)lb, k0 = zc >= (double)ub;
+                // a one-value block: the exact term; every in-volume waypoint's z - lb bounds M
+                E = (vin & (lb == ub)) ? fmin(E, z - (double)ub) : E;
+                Ub = vin ? fmin(Ub, z - (double)lb) : Ub;
+                const double clo = z - (double)ub;
+                const bool fetch =
+                    vin & (code != 3u) & (!(k1 | k0) | (!(clo >= E) & !(clo > Ub)));
+                const uint32_t it = vt4_index(vs, ix[t], iy[t]);
+                const uint32_t a4 = it + __umul24((uint32_t)izB[t], layer);
+                const uint32_t ab = a4 << (code + 1u);
+                const uint32_t base = (code & 2u) ? ((code & 1u) ? o16 : o8) : o4;
+                const uint32_t voff = base + (code ? (ab & ~15u) : 0u);
+                kcB[t] = code | (ab & 12u) | ((uint32_t)izB[t] << 8);
+                rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
+                tvB[t] = *reinterpret_cast<const float*>(pk + (ot4 + (fetch ? it * 4u : 0u)));
+                tkB |= (uint32_t)fetch << t;
+                bvB |= (uint32_t)k1 << t;
+            }
+            nvB = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
         }
+        if (c >= 0) {
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool vl = t < nvA, in = (vinA >> t) & 1u;
+                uint32_t risk, psi, hit;
+                float rter;
+                pk_terms_k(rA[t], kcA[t], risk, psi, hit, rter);
+                const bool c3 = (kcA[t] & 3u) == 3u;
+                gc = gc + over_n((double)__uint_as_float(risk));
+                gn = gn + (double)__uint_as_float(psi);
+                nh += hit;
+                off += (vl && !in) ? 1u : 0u;
+                // the exact terrain, where taken: v16's (code 3) or the fetched one
+                const bool ex = in & (c3 | ((tkA >> t) & 1u));
+                const float ter = c3 ? rter : tvA[t];
+                const double z = vz_at(za, zb, s_jw[jcA + t]);
+                const uint32_t below =
+                    ex ? (zc_of((int32_t)(kcA[t] >> 8)) < (double)ter ? 1u : 0u) : ((bvA >> t) & 1u);
+                bel += in ? below : 0u;
+                E = ex ? fmin(E, z - (double)ter) : E;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+        vinA = vinB, tkA = tkB, bvA = bvB, nvA = nvB, jcA = jc;
     }
     VSlot o;
     o.cost = gc;
@@ -6349,7 +6536,7 @@ __global__ __launch_bounds__(256, CH >= 16 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     o.cm = E;
     o.cnt = nh | (off << 8) | (bel << 16);
     o.pad = 0;
-    reinterpret_cast<VSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
+    if (live) reinterpret_cast<VSlot*>(kg.slot)[(int64_t)s * kg.P + path] = o;
 }
 
 // outputs of every path (block = 64 pairs x D): the similarity-form geometry (oracle sim_geo on
@@ -7576,13 +7763,16 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (nsb > 4096) return 0;
     // K2h (the similarity form) unless disabled or maxratio_smooth (its turn rows are not
     // scale-free): 24-B slots, the geometry in the output launch
-    const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth;
+    // and its 32-bit offsets reach the whole packed copy; N <= 4096 (Phi / N by the reciprocal)
+    const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth && kr.pk && ctx->kp.N <= 4096;
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
                  b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot))),
-                 b_ug = al((size_t)D * sizeof(UGeo)), b_err = 256;
+                 b_ug = al((size_t)D * sizeof(UGeo)), b_err = 256,
+                 b_lbp = sim ? al((size_t)P * 4) : 0;
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_err, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_err + b_lbp, s,
+                           &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs;
@@ -7614,32 +7804,28 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
+    kg.lbp = sim ? (float*)(w + o) : nullptr, o += b_lbp;
     kg.key = (uint16_t*)(w + o);
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
+    using HEvalFn = void (*)(KParams, KRaster, KGrp);
     // gathers in flight per lane (K2g, profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351; K2h: 7, groups of 21 = three full chunks)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : sim ? 7 : 8;
     size_t lds;
     int bs;
-    EvalFn ev;
+    EvalFn ev = nullptr;
+    HEvalFn hev = nullptr;
     if (sim) {  // K2h: H_BS-item workgroups, the packed header in LDS
-        static const EvalFn hevals[4] = {k_h_eval<6, false>, k_h_eval<7, false>,
-                                         k_h_eval<8, false>, k_h_eval<11, false>};
-        static const EvalFn hevals_cells[1] = {k_h_eval<7, true>};
-        constexpr int CH_CELLS = 7;
-        ev = ko.cells ? hevals_cells[0]
-                      : hevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3];
+        static const HEvalFn hevals[4] = {k_h_eval<6>, k_h_eval<7>, k_h_eval<8>, k_h_eval<11>};
+        hev = hevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3];
         bs = H_BS;
-        const size_t need = (size_t)kr.hwords * 4 + ubytes + 16 +  // + the junk slot
-                            (ko.cells ? (size_t)(H_BS / 64) * CH_CELLS * 64 * 4 : 0);
+        const size_t need = (size_t)kr.hwords * 4 + ubytes + (size_t)16 * (G + 16);  // + padding
         lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
         if (lds > 160 * 1024) return 0;
         if (!ctx->k2h_attrs) {  // per context = per device (DeviceGuard active)
-            for (EvalFn f : hevals)
+            for (HEvalFn f : hevals)
                 HIP_TRY(hipFuncSetAttribute((const void*)f,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            HIP_TRY(hipFuncSetAttribute((const void*)hevals_cells[0],
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             ctx->k2h_attrs = true;
         }
     } else {  // K2g: 256-item workgroups, the code map in LDS
@@ -7651,22 +7837,14 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8),
                                          UAM_G_EVALS(11), UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
-        // with waypoint cells requested: the CH = 8 form that also writes them
-        static const EvalFn evals_cells[4] = {k_g_eval<8, false, false, true>,
-                                              k_g_eval<8, false, true, true>,
-                                              k_g_eval<8, true, false, true>,
-                                              k_g_eval<8, true, true, true>};
         const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                        (ctx->kp.length_smooth ? 2 : 0) + (ctx->kp.maxratio_smooth ? 1 : 0);
-        ev = ko.cells ? evals_cells[ch & 3] : evals[ch];
+        ev = evals[ch];
         bs = 256;
         const size_t need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16;
         lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
         if (lds > 64 * 1024 && !ctx->k2g_attrs) {
             for (EvalFn f : evals)
-                HIP_TRY(hipFuncSetAttribute((const void*)f,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            for (EvalFn f : evals_cells)
                 HIP_TRY(hipFuncSetAttribute((const void*)f,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             ctx->k2g_attrs = true;
@@ -7682,8 +7860,15 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (!kg.nsb_raw)
         hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
-    hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s, ctx->kp,
-                       kr, kg, (const uint4*)rec);
+    if (hev)
+        hipLaunchKernelGGL(hev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
+                           ctx->kp, kr, kg);
+    else
+        hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
+                           ctx->kp, kr, kg, (const uint4*)rec);
+    if (ko.cells)
+        hipLaunchKernelGGL(k_cells, dim3((unsigned)((P * W + 255) / 256)), dim3(256), 0, s,
+                           ctx->kp, kr, kg, ko.cells);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
@@ -7706,7 +7891,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
                             int32_t* best_l, hipStream_t s) {
     const int G = ctx->k2g_group;
     if (G < 1 || G > G_MAXLEN || ko.cells || ko.g_rows || D > 16 || ctx->kp.maxratio_smooth ||
-        !ctx->k2g_sim)
+        !ctx->k2g_sim || !kv.pk || ctx->kp.N > 4096)
         return 0;
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
@@ -7716,8 +7901,9 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     // sets another): fewer items resident per XCD, so fewer of their lines miss L2 -- cfg5
     // 0.415 ms at 2 with 11 gathers in flight, 0.418 at 3, 0.453 at the 6 the LDS allows with 6
     // (profiles/r04/sweep7)
-    const size_t lds = std::max((size_t)D * ctx->kp.N * 16 + (size_t)((W + 1) & ~1) * 8 +
-                                    (size_t)kv.hwords * 4,
+    const int64_t npad = G + 16;  // k_v_eval's padding slots
+    const size_t lds = std::max((size_t)(D * ctx->kp.N + npad) * 16 +
+                                    (size_t)((W + npad + 1) & ~1) * 8 + (size_t)kv.hwords * 4,
                                 (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 60000, 160 * 1024));
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
@@ -7738,9 +7924,11 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     if (nsb > 4096) return 0;
     const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
                  b_ord = al((size_t)n_items * 4), b_slot = al((size_t)n_items * sizeof(VSlot)),
-                 b_ug = al((size_t)D * sizeof(UGeo)), b_tot = al(4096 * 4), b_err = 256;
+                 b_ug = al((size_t)D * sizeof(UGeo)), b_tot = al(4096 * 4), b_err = 256,
+                 b_ubp = al((size_t)P * 8);
     char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug + b_tot + b_err, s, &w);
+    int st = order_scratch(ctx, b_key + b_cnt + b_ord + b_slot + b_ug + b_tot + b_err + b_ubp, s,
+                           &w);
     if (st) return st;
     KGrp kg{};
     kg.pairs = pairs6;
@@ -7772,6 +7960,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
+    kg.ubp = (double*)(w + o), o += b_ubp;
     kg.key = (uint16_t*)(w + o);
     st = ktime_begin(ctx, s);
     if (st) return st;
@@ -7838,14 +8027,15 @@ static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shi
 //   cells square, the smallest with at most PK_BOUND_MAX of them and at least 8 cells wide), the
 //   superblock table (nsb float2, 4 x 4 bound blocks each);
 //   scratch (nbb float2: the bound blocks' {min, max} while packing);
-//   p4 (4-B phi) and t4 (4-B terrain) in 4 x 8-cell blocks, e8 (8 B) in 4 x 4-cell blocks.
+//   p4 (4-B phi), t4 (4-B terrain), e8 (8 B) and r16 (the 16-B records) in 4 x 8-cell blocks,
+//   all at one index.
 struct PackDims {
     int32_t sh, nbx, nby, words;           // summary blocks, code-map words
     int32_t bsh, bnbx, bnby, nbb;          // bound blocks
     int32_t sbnbx, sbnby, nsb;             // superblocks
     int32_t hwords, bnd_off, sbt_off;      // header words, word offsets
-    int32_t nb8, nb4, lnby;                // blocks per row (4 x 8, 4 x 4), block rows
-    int64_t off_scr, off_p4, off_t4, off_e8, bytes;
+    int32_t nb8, lnby;                     // 4 x 8-cell blocks per row, block rows
+    int64_t off_scr, off_p4, off_t4, off_e8, off_r16, bytes;
 };
 
 static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
@@ -7868,17 +8058,17 @@ static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
     d->sbt_off = d->bnd_off + w16((int64_t)d->nbb * 2);
     d->hwords = d->sbt_off + w16((int64_t)d->nsb * 8);
     d->nb8 = (desc->nx + 7) >> 3;
-    d->nb4 = (desc->nx + 3) >> 2;
     d->lnby = (desc->ny + 3) >> 2;
-    const int64_t c4 = (int64_t)d->lnby * d->nb8 * 32, c8 = (int64_t)d->lnby * d->nb4 * 16;
-    if (c4 >= ((int64_t)1 << 31) || c8 >= ((int64_t)1 << 31))
+    const int64_t c4 = (int64_t)d->lnby * d->nb8 * 32;
+    if (c4 >= ((int64_t)1 << 31) || desc->nx >= (1 << 24) || desc->ny >= (1 << 24))
         return fail(UAM_E_INVALID, "packed raster too large");
     auto a256 = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
     d->off_scr = a256((int64_t)d->hwords * 4);
     d->off_p4 = d->off_scr + a256((int64_t)d->nbb * 8);
     d->off_t4 = d->off_p4 + a256(c4 * 4);
     d->off_e8 = d->off_t4 + a256(c4 * 4);
-    d->bytes = d->off_e8 + a256(c8 * 8);
+    d->off_r16 = d->off_e8 + a256(c4 * 8);
+    d->bytes = d->off_r16 + a256(c4 * 16);
     return UAM_OK;
 }
 
@@ -7893,10 +8083,15 @@ static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
     kr->bnbx = d.bnbx;
     kr->sbnbx = d.sbnbx;
     kr->nb8 = d.nb8;
-    kr->nb4 = d.nb4;
     kr->p4 = (const uint32_t*)(b + d.off_p4);
     kr->t4 = (const float*)(b + d.off_t4);
     kr->e8 = (const uint2*)(b + d.off_e8);
+    const bool o32 = d.bytes <= (int64_t)UINT32_MAX;  // K2h's 32-bit offsets reach every byte
+    kr->pk = o32 ? b : nullptr;
+    kr->o4 = (uint32_t)d.off_p4;
+    kr->o8 = (uint32_t)d.off_e8;
+    kr->o16 = (uint32_t)d.off_r16;
+    kr->ot4 = (uint32_t)d.off_t4;
 }
 
 static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
@@ -8109,7 +8304,7 @@ int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, 
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, r4,
                        kr, (uint32_t*)(b + d.off_p4), (float*)(b + d.off_t4),
-                       (uint2*)(b + d.off_e8));
+                       (uint2*)(b + d.off_e8), (uint4*)(b + d.off_r16));
     hipLaunchKernelGGL(k_t4_bminmax, dim3((unsigned)((d.nbb + 3) / 4)), dim3(256), 0, s,
                        (const float*)(b + d.off_t4), kr.nx, kr.ny, d.nb8, d.bsh, d.bnbx, d.nbb,
                        (float2*)(b + d.off_scr));
@@ -8229,18 +8424,17 @@ namespace {
 // words padded to 16 B; the column terrain's bound table, u16 per bound block of 2^bsh columns,
 // at most PK_BOUND_MAX, padded to 16 B; the superblock table, float2 per 4 x 4 bound blocks) |
 // scratch (float2 per bound block) | 16-B voxels in 4 x 2-column blocks | 4-B risk in 4 x 8-
-// column blocks | 8-B {risk, |psi| | nfz} in 4 x 4-column blocks | the 4-B column terrain in
+// column blocks | 8-B {risk, |psi| | nfz} in the same blocks | the 4-B column terrain in
 // 4 x 8-column blocks (one plane)
 struct VpkDims {
-    int32_t nbx4, nby2, cnbx, cnby, cwords;
+    int32_t cnbx, cnby, cwords;
     int32_t bsh, bnbx, bnby, nbb, sbnbx, sbnby;
     int32_t hwords, bnd_off, sbt_off;
-    int32_t nb8, nb4, lnby4;
-    int64_t off_scr, off_vp, off_r4, off_e8, off_t4, bytes;
+    int32_t nb8, lnby4;
+    int64_t layer;  // i4 entries per layer plane
+    int64_t off_scr, off_r4, off_t4, off_e8, off_v16, bytes;
 };
 void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
-    v->nbx4 = (d->nx + 3) >> 2;
-    v->nby2 = (d->ny + 1) >> 1;
     v->cnbx = (d->nx + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
     v->cnby = (d->ny + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
     v->cwords = (v->cnbx * v->cnby + 15) / 16;
@@ -8259,30 +8453,35 @@ void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
     v->sbt_off = v->bnd_off + w16((int64_t)v->nbb * 2);
     v->hwords = v->sbt_off + w16((int64_t)v->sbnbx * v->sbnby * 8);
     v->nb8 = (d->nx + 7) >> 3;
-    v->nb4 = (d->nx + 3) >> 2;
     v->lnby4 = (d->ny + 3) >> 2;
+    v->layer = (int64_t)v->lnby4 * v->nb8 * 32;
     v->off_scr = al256((int64_t)v->hwords * 4);
-    v->off_vp = v->off_scr + al256((int64_t)v->nbb * 8);
-    v->off_r4 = v->off_vp + al256((int64_t)v->nbx4 * v->nby2 * 8 * d->nz * 16);
-    v->off_e8 = v->off_r4 + al256((int64_t)v->lnby4 * v->nb8 * 32 * d->nz * 4);
-    v->off_t4 = v->off_e8 + al256((int64_t)v->lnby4 * v->nb4 * 16 * d->nz * 8);
-    v->bytes = v->off_t4 + al256((int64_t)v->lnby4 * v->nb8 * 32 * 4);
+    v->off_r4 = v->off_scr + al256((int64_t)v->nbb * 8);
+    v->off_t4 = v->off_r4 + al256(v->layer * d->nz * 4);
+    v->off_e8 = v->off_t4 + al256(v->layer * 4);
+    v->off_v16 = v->off_e8 + al256(v->layer * d->nz * 8);
+    v->bytes = v->off_v16 + al256(v->layer * d->nz * 16);
 }
 // the packed volume's view for K4h
 void vpk_kvol(const uam_volume_desc* vd, const VpkDims& v, const void* packed, KVol4* kv) {
     const char* b = (const char*)packed;
     kv->nx = vd->nx, kv->ny = vd->ny, kv->nz = vd->nz;
-    kv->nbx4 = v.nbx4, kv->nby2 = v.nby2;
     kv->x0 = vd->x0, kv->y_top = vd->y_top, kv->z0 = vd->z0, kv->dz = vd->dz;
     kv->inv_dx = 1.0 / vd->dx, kv->inv_dy = 1.0 / vd->dy, kv->inv_dz = 1.0 / vd->dz;
-    kv->vp = (const uint4*)(b + v.off_vp);
     kv->hdr = (const uint32_t*)b;
     kv->hwords = v.hwords, kv->cnbx = v.cnbx, kv->bnd_off = v.bnd_off, kv->sbt_off = v.sbt_off;
     kv->bshift = v.bsh, kv->bnbx = v.bnbx, kv->sbnbx = v.sbnbx;
-    kv->nb8 = v.nb8, kv->nb4 = v.nb4, kv->lnby4 = v.lnby4;
-    kv->r4 = (const uint32_t*)(b + v.off_r4);
-    kv->e8 = (const uint2*)(b + v.off_e8);
-    kv->t4 = (const float*)(b + v.off_t4);
+    kv->nb8 = v.nb8, kv->lnby4 = v.lnby4;
+    kv->layer = (uint32_t)std::min(v.layer, (int64_t)UINT32_MAX);
+    // K4h's 32-bit offsets and 24-bit products: a copy under 4 GiB, layers under 2^24 entries,
+    // columns under 2^24 a side
+    const bool o32 = v.bytes <= (int64_t)UINT32_MAX && v.layer < ((int64_t)1 << 24) &&
+                     vd->nx < (1 << 24) && vd->ny < (1 << 24) && vd->nz < (1 << 24);
+    kv->pk = o32 ? b : nullptr;
+    kv->o4 = (uint32_t)v.off_r4;
+    kv->o8 = (uint32_t)v.off_e8;
+    kv->o16 = (uint32_t)v.off_v16;
+    kv->ot4 = (uint32_t)v.off_t4;
 }
 }  // namespace
 
@@ -8316,11 +8515,9 @@ int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, vo
     hipStream_t s = (hipStream_t)stream;
     char* b = (char*)packed;
     HIP_TRY(hipMemsetAsync(b, 0, (size_t)v.off_scr, s));  // header padding
-    hipLaunchKernelGGL(k_volume_pack, dim3(grid_for((v.off_r4 - v.off_vp) / 16, 256)), dim3(256),
-                       0, s, vx, cl, vd->nx, vd->ny, vd->nz, v.nbx4, v.nby2,
-                       (uint4*)(b + v.off_vp));
-    hipLaunchKernelGGL(k_volume_pack_re, dim3(grid_for((v.off_e8 - v.off_r4) / 4, 256)), dim3(256),
-                       0, s, vx, cl, kv, (uint32_t*)(b + v.off_r4), (uint2*)(b + v.off_e8));
+    hipLaunchKernelGGL(k_volume_pack_planes, dim3(grid_for(v.layer * vd->nz, 256)), dim3(256), 0,
+                       s, vx, cl, kv, (uint32_t*)(b + v.off_r4), (uint2*)(b + v.off_e8),
+                       (uint4*)(b + v.off_v16));
     const int64_t nt4 = (int64_t)v.lnby4 * v.nb8 * 32;
     hipLaunchKernelGGL(k_volume_pack_t4, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s, cl,
                        kv, (float*)(b + v.off_t4));

@@ -119,8 +119,8 @@ class RiskVolume:
     vox: object = field(repr=False)     # [ny, nx, nz, 2] int32 view: 8-B voxels {risk, psi}
     cols: object = field(repr=False)    # [ny, nx, 2] int32 view: columns {terrain, flags}
     cbits: object = field(repr=False, default=None)  # int32 view: the column bitmap words
-    # the packed copy K4h reads (Engine.volume_pack: 16-B voxels {risk, psi, terrain, flags} in
-    # 4 x 2-cell blocks per layer), or None; rebuild it after buf changes
+    # the packed copy K4h reads (Engine.volume_pack: 4-B / 8-B / 16-B voxel planes in 4 x 8-
+    # column blocks per layer, codes, terrain bounds), or None; rebuild it after buf changes
     packed: object = field(repr=False, default=None)
 
 
