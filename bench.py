@@ -305,18 +305,21 @@ def main():
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
+    te = eng.get_option("k2h_terrain") == 1  # UAM_OPT_K2H_TERRAIN: the form K2h / K4h ran
     if last.startswith("K4h"):
-        ktag = last.lower()
+        ktag = last.lower() + ("" if te else ":bounds")
         kernel_name = ("K4h sequence (k_v_hist / k_scan / k_g_scatter (+ the unit-arc sums), k_v_eval "
-                       "over every (path, group) item: points, one 16-B packed voxel per "
-                       "waypoint; k_v_final: the similarity-form geometry, grouped sums, "
-                       "selection)")
+                       "over every (path, group) item: points, one packed voxel per waypoint"
+                       + (" with its column's terrain" if te else
+                          ", the column terrain where it could still decide an output") +
+                       "; k_v_final: the similarity-form geometry, grouped sums, selection)")
     elif last.startswith("K2h"):
-        ktag = last.lower()
+        ktag = last.lower() + ("" if te else ":bounds")
         kernel_name = ("K2h sequence (k_g_hist / k_scan / k_g_scatter (+ the unit-arc sums), "
-                       "k_h_eval over every (path, group) item: points, cells, packed entries "
-                       "and the terrain where its bound could be the path maximum; "
-                       "k_h_final: the similarity-form geometry, grouped sums, selection)")
+                       "k_h_eval over every (path, group) item: points, cells, packed entries"
+                       + (" with the terrain" if te else
+                          " and the terrain where its bound could be the path maximum") +
+                       "; k_h_final: the similarity-form geometry, grouped sums, selection)")
     elif last.startswith("K2g"):
         ktag = last.lower()
         kernel_name = ("K2g sequence (k_g_hist / k_scan / k_g_scatter, k_g_eval over every "
@@ -344,7 +347,8 @@ def main():
                                    packed=last in ("K2s+pack", "K2g+pack", "K2h+pack"),
                                    kernel_tag=last,
                                    volume=volume_mode,
-                                   cells=args.cells and not volume_mode)
+                                   cells=args.cells and not volume_mode,
+                                   terrain_entry=eng.get_option("k2h_terrain") == 1)
     roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "
                                     "stream) around the K timed steps / K: the whole launch "
                                     "sequence of every step (sorts, evaluation, output "
@@ -503,7 +507,7 @@ def main():
 
 
 def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False, cells=False,
-                    kernel_tag=""):
+                    kernel_tag="", terrain_entry=True):
     """HBM roofline of the raster / volume kernel.  Algorithmic bytes (the one
     definition used in SURVEY, DESIGN §4 and here): raster, one 16-B record gather per waypoint
     + 16 B of outputs per path = 16 W + 16 B/path; volume, one 8-B voxel {risk, psi_nfz} + a
@@ -534,19 +538,36 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
          "l2_hit_rate": prof.get("l2_hit_rate"),
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
-         "record_source": ("packed volume (uam_volume_pack): 8-B {risk, terrain} voxels "
-                           "outside the no-fly columns, 16-B voxels inside them" if volume
-                           else "packed (uam_raster_pack): 4-B phi entries (32 cells per line) "
-                           "and 8-B {phi, psi|nfz} entries (16 per line) by block code, 16-B "
-                           "records where a psi is negative, the 4-B terrain plane where a "
-                           "waypoint's bound could be the path maximum; the algorithmic bytes "
-                           "keep SURVEY's 16 B per waypoint, the information each waypoint "
-                           "consumes" if packed else "16-B records"),
-         "note": roofline_note(kernel_tag, prof, P, W)}
+         "record_source": record_source(volume, packed, terrain_entry),
+         "note": roofline_note(kernel_tag, prof, P, W, terrain_entry)}
     return r
 
 
-def roofline_note(kernel, prof, P, W):
+def record_source(volume, packed, terrain_entry):
+    """The entries the evaluation that ran reads (UAM_OPT_K2H_TERRAIN picks the form)."""
+    if volume:
+        if terrain_entry:
+            return ("packed volume (uam_volume_pack): 8-B {risk, column terrain} voxels in 4 x "
+                    "4-column blocks per layer outside the no-fly / psi columns, 16-B voxels "
+                    "inside them")
+        return ("packed volume (uam_volume_pack): 4-B risk and 8-B {risk, psi|nfz} voxels by "
+                "column-block code, 16-B voxels where a psi is negative, the 4-B column terrain "
+                "only where a waypoint could still decide an output")
+    if not packed:
+        return "16-B records"
+    tail = ("; the algorithmic bytes keep SURVEY's 16 B per waypoint, the information each "
+            "waypoint consumes")
+    if terrain_entry:
+        return ("packed (uam_raster_pack): 8-B {phi, terrain} entries in 4 x 4-cell blocks (16 "
+                "cells per line) outside the no-fly / psi blocks, 16-B records inside them, "
+                "nothing in blocks of phi, psi +-0 and terrain +0.0" + tail)
+    return ("packed (uam_raster_pack): 4-B phi entries (32 cells per line) and 8-B {phi, "
+            "psi|nfz} entries (16 per line) by block code, 16-B records where a psi is "
+            "negative, the 4-B terrain plane where a waypoint's bound could be the path "
+            "maximum" + tail)
+
+
+def roofline_note(kernel, prof, P, W, terrain_entry=True):
     """What bounds the kernel that ran, from this build's own PMC key when there is one."""
     miss = prof.get("tcc_miss")
     hits = prof.get("tcc_hit")
@@ -556,11 +577,13 @@ def roofline_note(kernel, prof, P, W):
                 f"{(miss + hits) / 1e6:.1f}M L2 requests per step for {P * W / 1e6:.1f}M "
                 f"waypoints, {miss / 1e6:.2f}M of them misses.")
     if kernel.startswith("K2h"):
-        return ("K2h: one 128-B line request per waypoint's packed entry (none in code-0 "
-                "blocks) plus one per terrain fetch (only where the waypoint's bound could "
-                "still be the path maximum); hits come from L2, misses from the Infinity "
-                "Cache / HBM at <= 55-59 G lines/s (tools/gather_ceiling.hip); DESIGN.md §4-5."
-                + tail)
+        what = ("one 128-B line request per waypoint's packed entry, terrain included (none "
+                "in code-0 blocks)" if terrain_entry else
+                "one 128-B line request per waypoint's packed entry (none in code-0 blocks) "
+                "plus one per terrain fetch (only where the waypoint's bound could still be the "
+                "path maximum)")
+        return ("K2h: " + what + "; hits come from L2, misses from the Infinity Cache / HBM "
+                "at <= 55-59 G lines/s (tools/gather_ceiling.hip); DESIGN.md §4-5." + tail)
     if kernel.startswith("K4h"):
         return ("K4h: one 128-B line request per waypoint's packed voxel; misses from the "
                 "Infinity Cache / HBM at <= 55-59 G lines/s; DESIGN.md §4-5." + tail)

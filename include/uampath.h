@@ -250,9 +250,10 @@ int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* re
 /* Packed raster (build-defined; no reference counterpart; results unchanged).  A derived copy
  * of rec for the sorted evaluations (K2h / K2g / K2s), 256-B aligned sections:
  *   header  the 2-bit code per summary block (16 per 32-bit word): 0 = every cell has
- *           phi == +-0, psi_nfz == +-0 and no no-fly flag (nothing to read but the terrain);
- *           1 = psi_nfz == +-0 and no flag (phi from the 4-B plane); 2 = no psi_nfz below
- *           zero (phi, |psi_nfz| and the flag from the 8-B plane); 3 = the 16-B record from rec;
+ *           phi == +-0, psi_nfz == +-0, no no-fly flag and terrain +0.0 as read (nothing to
+ *           read); 1 = psi_nfz == +-0 and no flag (phi from the 4-B plane, or phi and terrain
+ *           from the 8-B {phi, terrain} plane); 2 = no psi_nfz below zero (phi, |psi_nfz| and
+ *           the flag from the 8-B plane); 3 = the 16-B record;
  *           then the terrain bounds: one u16 {ub code, lb code << 8} per bound block (the
  *           smallest power-of-two square of >= 8 cells giving <= 16384 blocks), and one float2
  *           {base, step} per superblock of 4 x 4 bound blocks; a bound decodes as
@@ -487,10 +488,15 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                (default 0: the fewest giving at most 16 bands); tiles from
  *                                UAM_OPT_K2G_TILE_BITS (default 3: 8 x 8 tiles), at most
  *                                4096 (tile, band) bins
- *   UAM_OPT_K2H_LB_STRIDE        K2h terrain bounds: every item takes the maximum lower bound
- *                                over every n-th waypoint of its path as the path's lower bound
- *                                (1..1024; default 8); fewer terrain fetches at smaller n, more
- *                                arithmetic per item.  Same outputs. */
+ *   UAM_OPT_K2H_LB_STRIDE        K2h / K4h terrain bounds: the histogram launch samples every
+ *                                n-th waypoint of each path and seeds the path's items with the
+ *                                exact terrain (clearance) of the sample with the best bound
+ *                                (1..1024; default 8; 0: no seed); fewer terrain fetches at
+ *                                smaller n, more arithmetic in that launch.  Same outputs.
+ *   UAM_OPT_K2H_TERRAIN          K2h's terrain: 0 by bounds (the 4-B phi entries, the terrain
+ *                                plane read only where a waypoint could hold the path
+ *                                maximum), 1 in the entry (8-B {phi, terrain} entries, the
+ *                                16-B records in no-fly blocks).  Same outputs. */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -508,7 +514,8 @@ enum {
     UAM_OPT_K2G_CURVE = 14,
     UAM_OPT_K2G_SIM = 15,
     UAM_OPT_K4H_BAND = 17,
-    UAM_OPT_K2H_LB_STRIDE = 19
+    UAM_OPT_K2H_LB_STRIDE = 19,
+    UAM_OPT_K2H_TERRAIN = 20
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

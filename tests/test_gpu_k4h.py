@@ -74,9 +74,10 @@ def _check(gpu, ref, oracle_mod, D):
                                   oracle_mod.argmin(ref["length"], D, False))
 
 
+@pytest.mark.parametrize("terrain", [1, 0])
 @pytest.mark.parametrize("R,nz,group", [(256, 16, 21), (256, 64, 8), (512, 7, 21),
                                         (300, 33, 64), (256, 16, 1)])
-def test_k4h_vs_oracle(oracle_mod, R, nz, group):
+def test_k4h_vs_oracle(oracle_mod, R, nz, group, terrain):
     """Volumes with nx not a multiple of the block width (300), odd layer counts (7, 33: the
     altitude bands' last band partial), groups of 1-64; every output equals orc_eval_generated_h
     bit for bit; against the sequential K4 form: exact for the order-free outputs, rounding
@@ -85,6 +86,7 @@ def test_k4h_vs_oracle(oracle_mod, R, nz, group):
     from uam_path_planning_amd.scenario import displacements
 
     e, orc, vol, vd, host = _case(oracle_mod, R, nz, 80, group)
+    e.set_option("k2h_terrain", terrain)  # 1 (default): the terrain in the entry; 0: bounds
     D = 5
     ut = arc_table(80, displacements(D))
     pairs = _pairs3d(3000, 17)
@@ -100,9 +102,10 @@ def test_k4h_vs_oracle(oracle_mod, R, nz, group):
     np.testing.assert_allclose(ref["cost"][ok], seq["cost"][ok], rtol=1e-12)
 
 
+@pytest.mark.parametrize("terrain", [1, 0])
 @pytest.mark.parametrize("chunk,floor", [(6, 0), (7, 0), (8, 0), (11, 0), (0, 0), (6, 28000),
                                          (11, 41000), (8, 90000), (16, 0), (21, 90000)])
-def test_k4h_chunks(oracle_mod, chunk, floor):
+def test_k4h_chunks(oracle_mod, chunk, floor, terrain):
     """Gathers in flight (chunk; 0 = the default 11) and workgroups per CU (the LDS floor; 0 =
     the default 60 000 B, 90 000 needs the raised dynamic-LDS attribute) only move work."""
     from uam_path_planning_amd.arcs import arc_table
@@ -111,6 +114,7 @@ def test_k4h_chunks(oracle_mod, chunk, floor):
     e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21, maxalpha=0.015)
     e.set_option("k2g_chunk", chunk)
     e.set_option("k2g_lds_floor", floor)
+    e.set_option("k2h_terrain", terrain)
     D = 5
     ut = arc_table(80, displacements(D))
     pairs = _pairs3d(2000, 23)
@@ -153,9 +157,10 @@ def _vary_psi(e, vol):
 
 
 def test_k4h_pack_layout(oracle_mod):
-    """uam_volume_pack against its definition (uampath.hip VpkDims / KVol4): the 4-B risk, 8-B
-    {risk, |psi| | nfz << 31} and 16-B voxel ({risk, psi} of the voxel, {terrain, flags} of the
-    column) planes per layer (4 x 8-column blocks, one index), the column terrain (4 x 8), zero
+    """uam_volume_pack against its definition (uampath.hip VpkDims / KVol4): the 4-B risk and
+    8-B {risk, |psi| | nfz << 31} planes per layer (4 x 8-column blocks, one index), the 16-B
+    voxels ({risk, psi} of the voxel, {terrain, flags} of the column; 4 x 2-column blocks), the
+    8-B {risk, terrain} plane (4 x 4-column blocks), the column terrain (4 x 8), zero
     padding, the 2-bit code per 8 x 8 columns (3: a psi below zero in any
     layer; 2: another nonzero psi or the no-fly flag; 1: a nonzero risk; 0: none), and terrain
     bounds that hold every column."""
@@ -174,20 +179,30 @@ def test_k4h_pack_layout(oracle_mod):
     r4 = b[off[2]:off[2] + layer * nz * 4].view(np.uint32)
     t4 = b[off[3]:off[3] + layer * 4].view(np.float32)
     e8 = b[off[4]:off[4] + layer * nz * 8].view(np.uint32).reshape(-1, 2)
-    t16 = b[off[5]:off[5] + layer * nz * 16].view(np.int32).reshape(-1, 4)
+    nbx4, nby2 = (nx + 3) // 4, (ny + 1) // 2
+    layer42 = nby2 * nbx4 * 8
+    t16 = b[off[5]:off[5] + layer42 * nz * 16].view(np.int32).reshape(-1, 4)
+    nb4 = (nx + 3) // 4
+    layer44 = lnby4 * nb4 * 16
+    q8 = b[off[6]:off[6] + layer44 * nz * 8].view(np.uint32).reshape(-1, 2)
     iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     vox = vol.vox.cpu().numpy()            # [ny, nx, nz, 2]
     cols = vol.cols.cpu().numpy()          # [ny, nx, 2]
     vz = vox.transpose(2, 0, 1, 3).reshape(-1, 2)
     cz = np.broadcast_to(cols, (nz, ny, nx, 2)).reshape(-1, 2)
     i4 = (((iz * lnby4 + iy // 4) * nb8 + ix // 8) * 32 + (iy % 4) * 8 + ix % 8).reshape(-1)
-    np.testing.assert_array_equal(t16[i4], np.concatenate([vz, cz], axis=1))
+    i42 = ((iz * layer42) + ((iy // 2) * nbx4 + ix // 4) * 8 + (iy % 2) * 4 + ix % 4).reshape(-1)
+    np.testing.assert_array_equal(t16[i42], np.concatenate([vz, cz], axis=1))
     np.testing.assert_array_equal(r4[i4], vz[:, 0].view(np.uint32))
     pz = (vz[:, 1].view(np.uint32) & 0x7fffffff) | ((cz[:, 1].view(np.uint32) & 1) << 31)
     np.testing.assert_array_equal(e8[i4], np.stack([vz[:, 0].view(np.uint32), pz], axis=1))
     it = (((iy[0] // 4) * nb8 + ix[0] // 8) * 32 + (iy[0] % 4) * 8 + ix[0] % 8)
     np.testing.assert_array_equal(t4[it].view(np.uint32), cols[:, :, 0].view(np.uint32))
-    for t, idx in ((t16, i4), (r4, i4), (e8, i4), (t4.view(np.uint32), it.reshape(-1))):
+    i44 = ((iz * layer44) + ((iy // 4) * nb4 + ix // 4) * 16 + (iy % 4) * 4 + ix % 4).reshape(-1)
+    np.testing.assert_array_equal(q8[i44], np.stack([vz[:, 0].view(np.uint32),
+                                                     cz[:, 0].view(np.uint32)], axis=1))
+    for t, idx in ((t16, i42), (r4, i4), (e8, i4), (t4.view(np.uint32), it.reshape(-1)),
+                   (q8, i44)):
         mask = np.ones(len(t), bool)
         mask[idx] = False
         assert (t[mask] == 0).all()

@@ -38,8 +38,9 @@ def test_header_symbols_exported(lib):
 
 def _vpk_sections(nx, ny, nz):
     """The packed volume's sections (uampath.hip VpkDims): header (codes, bounds, superblocks),
-    bound scratch, then in 4 x 8-column blocks the 4-B risk layers, the 4-B column terrain, the
-    8-B risk/psi layers and the 16-B voxel layers, each 256-B aligned."""
+    bound scratch, then in 4 x 8-column blocks the 4-B risk layers, the 4-B column terrain and
+    the 8-B risk/psi layers, the 16-B voxel layers in 4 x 2-column blocks and the 8-B
+    {risk, terrain} layers in 4 x 4-column blocks, each 256-B aligned."""
     al = lambda v: (v + 255) // 256 * 256
     w16 = lambda v: -(-v // 16) * 16
     cw = (((nx + 7) // 8) * ((ny + 7) // 8) + 15) // 16
@@ -49,8 +50,10 @@ def _vpk_sections(nx, ny, nz):
     bnbx, bnby = -(-nx // (1 << bsh)), -(-ny // (1 << bsh))
     hdr = w16(cw * 4) + w16(bnbx * bnby * 2) + w16(-(-bnbx // 4) * -(-bnby // 4) * 8)
     layer = ((ny + 3) // 4) * ((nx + 7) // 8) * 32
+    layer44 = ((ny + 3) // 4) * ((nx + 3) // 4) * 16   # q8: 4 x 4-column blocks
+    layer42 = ((ny + 1) // 2) * ((nx + 3) // 4) * 8    # v16: 4 x 2-column blocks
     return [al(hdr), al(bnbx * bnby * 8), al(layer * nz * 4), al(layer * 4), al(layer * nz * 8),
-            al(layer * nz * 16)]
+            al(layer42 * nz * 16), al(layer44 * nz * 8)]
 
 
 def test_volume_packed_bytes(lib):
@@ -65,9 +68,10 @@ def test_volume_packed_bytes(lib):
         assert n.value == sum(_vpk_sections(nx, ny, nz)), (nx, ny, nz)
     vd = _lib.VolumeDesc(1024, 1024, 64, 0.0, 20.0, 60.0 / 1024, 60.0 / 1024, 0.0, 10.0)
     assert lib.uam_volume_packed_bytes(ctypes.byref(vd), ctypes.byref(n)) == _lib.UAM_OK
-    # 1024^2 x 64: 1 GiB of 16-B voxels, 256 MiB of risk, 512 MiB of risk/psi, 4 MiB of terrain,
-    # a 44 KiB header (4 KiB of codes, 32 KiB of 8-column bound blocks, 8 KiB of superblocks)
-    assert n.value == (1024 + 256 + 512 + 4) * 2**20 + 45056 + 131072
+    # 1024^2 x 64: 1 GiB of 16-B voxels, 256 MiB of risk, 512 MiB of risk/psi, 512 MiB of
+    # risk/terrain, 4 MiB of terrain, a 44 KiB header (4 KiB of codes, 32 KiB of 8-column bound
+    # blocks, 8 KiB of superblocks)
+    assert n.value == (1024 + 256 + 512 + 512 + 4) * 2**20 + 45056 + 131072
     assert lib.uam_volume_packed_bytes(ctypes.byref(vd), None) == _lib.UAM_E_INVALID
     bad = _lib.VolumeDesc(0, 1024, 64, 0.0, 20.0, 1.0, 1.0, 0.0, 10.0)
     assert lib.uam_volume_packed_bytes(ctypes.byref(bad), ctypes.byref(n)) == _lib.UAM_E_INVALID
@@ -95,10 +99,10 @@ def test_invalid_calls_fail_loudly(lib):
                                      ctypes.byref(nbytes)) == _lib.UAM_OK
     # header: 2-bit codes of 65536 blocks (16 KiB), 128^2 bound blocks of 32^2 cells (u16,
     # 32 KiB), 32^2 superblocks (float2, 8 KiB); the bound scratch (float2 per bound block);
-    # the 4-B phi and terrain planes, the 8-B {phi, psi | nfz} plane and the 16-B record plane
-    # of 4096^2 cells
+    # the 4-B phi and terrain planes, the 8-B {phi, psi | nfz} plane, the 16-B record plane and
+    # the 8-B {phi, terrain} plane (4 x 4-cell blocks) of 4096^2 cells
     assert (b.value, nbytes.value) == (16, 16384 + 32768 + 8192 + 8 * 16384 +
-                                       (4 + 4 + 8 + 16) * 4096 * 4096)
+                                       (4 + 4 + 8 + 16 + 8) * 4096 * 4096)
     # a raster that is no multiple of the blocks: every section padded to whole blocks
     rd2 = _lib.RasterDesc(1000, 700, 0.0, 20.0, 0.05, 0.05, -9999.0, 0.0)
     assert lib.uam_raster_pack_shape(ctypes.byref(rd2), 4, ctypes.byref(b),
@@ -107,7 +111,8 @@ def test_invalid_calls_fail_loudly(lib):
     nbb = 125 * 88                                     # 8-cell bound blocks (11000 <= 16384)
     hdr = -(-words * 4 // 16) * 16 + -(-nbb * 2 // 16) * 16 + 32 * 22 * 8
     a256 = lambda v: -(-v // 256) * 256
-    planes = 2 * a256(175 * 125 * 32 * 4) + a256(175 * 250 * 16 * 8) + a256(175 * 500 * 8 * 16)
+    planes = (2 * a256(175 * 125 * 32 * 4) + a256(175 * 250 * 16 * 8) +
+              a256(175 * 500 * 8 * 16) + a256(175 * 250 * 16 * 8))  # (p8: 175 x 250 blocks)
     assert (b.value, nbytes.value) == (4, a256(hdr) + a256(nbb * 8) + planes)
     assert lib.uam_raster_pack(None, None, None, 0, None, None) == _lib.UAM_E_INVALID
     assert lib.uam_eval_generated(None, 1, None, None, None, 0, None, None, 0, None, 5, None,

@@ -77,6 +77,9 @@ def main():
                          "instead of 16-B records; their terrain through the bounds too")
     ap.add_argument("--quant", default="exact,u8")
     ap.add_argument("--samples", default="", help="path lower-bound sample strides, e.g. 8,4,0")
+    ap.add_argument("--lag", type=int, default=0,
+                    help="chunks between a chunk's issue and its consume (1: the one-ahead "
+                         "pipeline: chunk c's fetch rule sees E up to chunk c - 2)")
     ap.add_argument("--use-sampled", action="store_true",
                     help="the L2 model uses the last --samples rule's fetches")
     a = ap.parse_args()
@@ -197,6 +200,7 @@ def main():
                 Lrun = np.broadcast_to(lbp[:, None, None], (P, nseg, 1)).copy()
                 Erun = np.full((P, nseg, 1), -np.inf)
                 fs = np.zeros_like(K)
+                pend = []  # fetched maxima not yet consumed (the pipeline's lag)
                 for c0 in range(0, G, CH):
                     sl = slice(c0, min(G, c0 + CH))
                     Lrun = np.maximum(Lrun, L[:, :, sl].max(axis=2, keepdims=True))
@@ -204,8 +208,10 @@ def main():
                                     .max(axis=2, keepdims=True))
                     f = (~K[:, :, sl]) & (U[:, :, sl] > Ec) & (U[:, :, sl] >= Lrun)
                     fs[:, :, sl] = f
-                    Erun = np.maximum(Ec, np.where(f, TT[:, :, sl], -np.inf)
-                                      .max(axis=2, keepdims=True))
+                    Erun = Ec
+                    pend.append(np.where(f, TT[:, :, sl], -np.inf).max(axis=2, keepdims=True))
+                    while len(pend) > a.lag:
+                        Erun = np.maximum(Erun, pend.pop(0))
                 print(f"    + path lower bound from every {s_ if s_ else 1}th waypoint: "
                       f"chunked fetches per waypoint {fs.reshape(P, Wp)[:, :W].mean():.4f}",
                       flush=True)

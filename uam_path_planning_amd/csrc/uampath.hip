@@ -142,7 +142,7 @@ struct KRaster {
     // all four at one index.
     const uint32_t* __restrict__ pmap;
     int32_t pwords, hwords, bnd_off, sbt_off;
-    int32_t bshift, bnbx, sbnbx, nb8;
+    int32_t bshift, bnbx, sbnbx, nb8, nb4;  // (nb4: p8's 4 x 4-cell blocks per row)
     const uint32_t* __restrict__ p4;
     const float* __restrict__ t4;
     const uint2* __restrict__ e8;
@@ -150,7 +150,7 @@ struct KRaster {
     // p4 / e8 / r16 (the 16-B records, same blocks and index) and t4 at o4 / o8 / o16 / ot4);
     // null when the copy is 4 GiB or larger (K2h then stands aside)
     const char* __restrict__ pk;
-    uint32_t o4, o8, o16, ot4;
+    uint32_t o4, o8, o16, ot4, op8;  // (op8: the 8-B {phi, terrain} plane p8, p44_addr)
 };
 
 // volume (config 5): 8-B voxels {risk, psi_nfz} [ny][nx][nz], the 8-B column plane
@@ -682,8 +682,9 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
 // The sorted forms are bound by 128-B lines; a 16-B record uses one eighth of its line, and most
 // waypoints need less of it.  The packed copy (layout: PackDims) keeps what each block needs in
 // the narrowest entry, with a 2-bit code per summary block saying which one a waypoint reads:
-//   0  nothing: every cell has phi == +-0, psi == +-0 and no no-fly flag (the phi and psi terms
-//      are exact no-ops on accumulators that are never -0, the hit count adds 0);
+//   0  nothing: every cell has phi == +-0, psi == +-0, no no-fly flag and a terrain that reads
+//      +0.0 (the phi and psi terms are exact no-ops on accumulators that are never -0, the hit
+//      count adds 0, the terrain is exactly +0.0);
 //   1  the 4-B phi plane p4 (psi == +-0 and no flag over the block), 32 cells per line;
 //   2  the 8-B plane e8 {phi, |psi| with the no-fly flag in the sign bit}, 16 cells per line:
 //      every psi of the block is >= +0 or -0 (its decoded +0 adds exactly what -0 adds);
@@ -704,6 +705,12 @@ constexpr int PK_BOUND_MAX = 16384;  // bound blocks at most (32 KiB of u16 in L
 __device__ __forceinline__ int32_t p4_addr(const KRaster& rs, int32_t ix, int32_t iy) {
     return (int32_t)(((__umul24((uint32_t)(iy >> 2), (uint32_t)rs.nb8) + (uint32_t)(ix >> 3)) << 5) |
                      (((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u));
+}
+
+// p8's index: 4 x 4-cell blocks (16 entries of 8 B, one 128-B line, a square of cells)
+__device__ __forceinline__ int32_t p44_addr(const KRaster& rs, int32_t ix, int32_t iy) {
+    return (int32_t)(((__umul24((uint32_t)(iy >> 2), (uint32_t)rs.nb4) + (uint32_t)(ix >> 2)) << 4) |
+                     (((uint32_t)iy & 3u) << 2) | ((uint32_t)ix & 3u));
 }
 
 // the summary-block index of cell (ix, iy) (its 2-bit code: word b >> 4, bits 2 (b & 15))
@@ -825,13 +832,15 @@ __device__ __forceinline__ void pk_terms_k(const uint4& r, uint32_t k, uint32_t&
     pk_terms(r, s, 0, phi, psi, hit, rter);
 }
 
-// one thread per cell, rows coalesced: the four planes at their blocked addresses (e8 and r16
-// are written everywhere, read only in code-2 / code-3 blocks)
+// one thread per cell, rows coalesced: the five planes at their blocked addresses (e8 and r16
+// are written everywhere, read only in code-2 / code-3 blocks; p8 {phi, terrain as read} only
+// by K2h's terrain-in-entry form)
 __global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ rec, KRaster rs,
                                                      uint32_t* __restrict__ p4,
                                                      float* __restrict__ t4,
                                                      uint2* __restrict__ e8,
-                                                     uint4* __restrict__ r16) {
+                                                     uint4* __restrict__ r16,
+                                                     uint2* __restrict__ p8) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= (int64_t)rs.nx * rs.ny) return;
     const int32_t iy = (int32_t)(c / rs.nx), ix = (int32_t)(c - (int64_t)iy * rs.nx);
@@ -842,6 +851,7 @@ __global__ __launch_bounds__(256) void k_raster_pack(const uint4* __restrict__ r
     e8[a4] =
         make_uint2(r.x, (r.y & 0x7fffffffu) | ((r.w & UAM_FLAG_NFZ) ? 0x80000000u : 0u));
     r16[a4] = r;
+    p8[p44_addr(rs, ix, iy)] = make_uint2(r.x, (r.w & UAM_FLAG_NODATA) ? 0u : r.z);
 }
 
 // one thread per summary block: its 2-bit code; lanes 0/16/32/48 write the wave's 4 words
@@ -862,7 +872,8 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
                 const uint4 r = rec[(int64_t)iy * nx + ix];
                 if ((r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ)) need = true;
                 if ((r.y >> 31) && r.y != 0x80000000u) neg = true;  // negative, or a -NaN
-                if (r.x & 0x7fffffffu) nz = true;
+                // a phi to add, or a terrain other than +0.0 as read
+                if ((r.x & 0x7fffffffu) || ((r.w & UAM_FLAG_NODATA) ? 0u : r.z)) nz = true;
             }
         code = need ? (neg ? 3u : 2u) : nz ? 1u : 0u;
     }
@@ -4977,6 +4988,7 @@ constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles o
 // tile bins twice over (a ragged last group's items have their own) + one for off-raster / NaN
 constexpr int G_BINS_MAX = (2 << (2 * G_TBITS_MAX)) + 1;
 constexpr int G_NBK = 256;                              // partitions of the counting sort
+constexpr int G_HIST_DYN_MAX = 119 * 1024;  // k_g_hist's dynamic LDS (K2h seeds) beside its 40 KiB
 constexpr int G_MAXLEN = 64;                            // longest group
 constexpr int G_UTAB_LDS = 48 * 1024;                   // K2g: unit-arc table (in LDS) up to this
 
@@ -5048,9 +5060,10 @@ struct KGrp {
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_cells), or null
     UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's block 0
     int32_t lb_stride;             // K2h: the path lower bound's sample stride (>= 1)
-    float* __restrict__ lbp;       // K2h: [P] each path's sampled terrain lower bound (formed by
+    float* __restrict__ lbp;       // K2h: [P] each path's terrain seed (h_path_seed, formed by
                                    // the histogram launch), or null
-    double* __restrict__ ubp;      // K4h: [P] each path's sampled clearance upper bound, likewise
+    int32_t seed_lds;              // K2h: the histogram launch stages header + unit arcs in LDS
+    double* __restrict__ ubp;      // K4h: [P] each path's clearance seed (v_path_seed), likewise
     int32_t* __restrict__ err;     // the sort's check word: zeroed by the histogram launch, set
                                    // by the scatter on a position outside the order (keys of the
                                    // two launches disagreeing); the output launch then writes
@@ -5161,28 +5174,44 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t a, uint64_t m, int sh) {
     return (uint32_t)(((uint64_t)a * m) >> sh);
 }
 
-// K2h: a path's sampled terrain lower bound Lb (h_item): the maximum decoded lb over its
-// waypoints j = 0, s, 2s, ... (s = kg.lb_stride) and j = W - 1, each at its own cell by the
-// evaluation's operations (the pair's points, arc_point's), +0.0 for one off the raster (its
-// exact terrain); -inf without the packed header.  Every sample is a real waypoint, so Lb is at
-// most the path's maximum terrain.
-__device__ __forceinline__ float h_path_lb(const KParams& p, const KRaster& rs, const KGrp& kg,
-                                           int32_t path) {
+// K2h: a path's terrain seed E0 (h_item): the exact terrain (t4; +0.0 off the raster) of the
+// sampled waypoint with the largest decoded lb, over j = 0, s, 2s, ... (s = kg.lb_stride) and
+// j = W - 1, each at its own cell by the evaluation's operations (the pair's points,
+// arc_point's); -inf when no sample has a bound.  E0 is an exact terrain value of the path, so
+// it is at most the path's maximum M, and every item of the path may start its running maximum
+// E (and its lower bound Lb) there.  hdr / u: the packed header and the unit-arc table (LDS
+// copies when the launch staged them).
+__device__ __forceinline__ float h_path_seed(const KParams& p, const KRaster& rs, const KGrp& kg,
+                                            int32_t path, const uint32_t* __restrict__ hdr,
+                                            const double2* __restrict__ utab) {
     if (!rs.pmap) return -INFINITY;
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
     const int32_t d = path - q * kg.D;
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-    const double2* u = reinterpret_cast<const double2*>(kg.utab) + (int64_t)d * p.N - 1;
+    const double2* u = utab + d * p.N - 1;
     const int W = kg.W;
+    constexpr uint32_t NONE = 0xffffffffu, OFF = 0xfffffffeu;
     float Lb = -INFINITY;
-    auto take = [&](bool in, int32_t ix, int32_t iy) {
+    uint32_t best = NONE;  // the t4 index of the sample holding Lb (OFF: off the raster)
+    auto take = [&](bool in, int32_t ix, int32_t iy, uint32_t e, float2 sb) {
         float ub, lb;
-        pk_bounds(rs, rs.pmap, ix, iy, ub, lb);
-        Lb = fmaxf(Lb, in ? lb : 0.0f);
+        pk_bound_decode(e, sb, ub, lb);
+        const float v = in ? lb : 0.0f;
+        const bool up = v > Lb;  // (a NaN bound: no)
+        Lb = up ? v : Lb;
+        best = up ? (in ? (uint32_t)p4_addr(rs, ix, iy) : OFF) : best;
     };
-    int32_t ix, iy;
-    take(gen_cell(rs, pr.x, pr.y, ix, iy), ix, iy);
-    take(gen_cell(rs, pr.z, pr.w, ix, iy), ix, iy);
+    {
+        int32_t ix, iy;
+        uint32_t e;
+        float2 sb;
+        bool in = gen_cell(rs, pr.x, pr.y, ix, iy);
+        pk_bound_raw(rs, hdr, ix, iy, e, sb);
+        take(in, ix, iy, e, sb);
+        in = gen_cell(rs, pr.z, pr.w, ix, iy);
+        pk_bound_raw(rs, hdr, ix, iy, e, sb);
+        take(in, ix, iy, e, sb);
+    }
     // four samples at a time, every load of the four issued together (a sample past the last
     // interior waypoint repeats it)
     constexpr int K = 4;
@@ -5192,22 +5221,19 @@ __device__ __forceinline__ float h_path_lb(const KParams& p, const KRaster& rs, 
         for (int k = 0; k < K; ++k) uu[k] = u[min(j0 + k * kg.lb_stride, W - 2)];
         uint32_t e[K];
         float2 sb[K];
+        int32_t ix[K], iy[K];
         bool in[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double x0, x1;
             arc_point(pr.x, pr.y, pr.z, pr.w, uu[k].x, uu[k].y, x0, x1);
-            in[k] = gen_cell(rs, x0, x1, ix, iy);
-            pk_bound_raw(rs, rs.pmap, ix, iy, e[k], sb[k]);
+            in[k] = gen_cell(rs, x0, x1, ix[k], iy[k]);
+            pk_bound_raw(rs, hdr, ix[k], iy[k], e[k], sb[k]);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float ub, lb;
-            pk_bound_decode(e[k], sb[k], ub, lb);
-            Lb = fmaxf(Lb, in[k] ? lb : 0.0f);
-        }
+        for (int k = 0; k < K; ++k) take(in[k], ix[k], iy[k], e[k], sb[k]);
     }
-    return Lb;
+    return best == NONE ? -INFINITY : best == OFF ? 0.0f : rs.t4[best];
 }
 
 // counting sort, launch 1: partition b = paths [P b / NBK, P (b+1) / NBK); keys of all their
@@ -5216,10 +5242,23 @@ __device__ __forceinline__ float h_path_lb(const KParams& p, const KRaster& rs, 
 __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];  // the tile-key table (curve order)
+    // K2h with kg.seed_lds: the packed header and the unit-arc table staged for the seeds
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_hist_dyn[];
     const int t = threadIdx.x, b = blockIdx.x;
     if (b == 0 && t == 0) *kg.err = 0;
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
+    const uint32_t* s_hdr = rs.pmap;
+    const double2* s_ut = reinterpret_cast<const double2*>(kg.utab);
+    if (kg.lbp && kg.seed_lds) {
+        uint4* dh = reinterpret_cast<uint4*>(s_hist_dyn);
+        const uint4* gh = reinterpret_cast<const uint4*>(rs.pmap);
+        for (int k = t; k < (rs.hwords >> 2); k += 1024) dh[k] = gh[k];
+        double2* du = reinterpret_cast<double2*>(s_hist_dyn + rs.hwords);
+        for (int k = t; k < kg.D * p.N; k += 1024) du[k] = s_ut[k];
+        s_hdr = s_hist_dyn;
+        s_ut = du;
+    }
     __syncthreads();
     // thread = item (consecutive threads: the groups of one path, then the next path's), so
     // the key stores are coalesced and a path's pair is one broadcast load; U items per thread
@@ -5273,10 +5312,10 @@ __global__ __launch_bounds__(1024) void k_g_hist(KParams p, KRaster rs, KGrp kg)
             atomicAdd(&h[key], 1);
         }
     }
-    if (kg.lbp) {  // K2h: the partition's paths' sampled lower bounds, one thread per path
+    if (kg.lbp) {  // K2h: the partition's paths' terrain seeds, one thread per path
         const int64_t plo = (int64_t)kg.P * b / G_NBK, phi = (int64_t)kg.P * (b + 1) / G_NBK;
         for (int64_t pth = plo + t; pth < phi; pth += 1024)
-            kg.lbp[pth] = h_path_lb(p, rs, kg, (int32_t)pth);
+            kg.lbp[pth] = h_path_seed(p, rs, kg, (int32_t)pth, s_hdr, s_ut);
     }
     __syncthreads();
     // the partition's count per bin, bin-major ([bin][partition]): k_scan_local's exclusive
@@ -5747,28 +5786,45 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // maximum's): min_clearance needs only the path's maximum terrain M, an order-free maximum, so
 // a waypoint's exact terrain is fetched (t4) only when it could still be M.  Every in-raster
 // waypoint w has decoded bounds lb_w <= terrain_w <= ub_w (pk_bounds, from LDS).  The item keeps
-//   Lb: the path's sampled lower bound (h_path_lb, formed once per path by the histogram
-//       launch: lb of real waypoints, so Lb <= M) raised by its own waypoints' lb as it goes;
-//       off-raster waypoints count +0.0, their exact value;
-//   E:  the maximum of the exact terrain values it has taken (fetched, code-3 records,
-//       off-raster +0.0, blocks whose bounds coincide).
+//   Lb: a lower bound of M: the path's seed (below), raised by its own waypoints' lb as it
+//       goes; off-raster waypoints count +0.0, their exact value;
+//   E:  the maximum of exact terrain values of the path: the seed E0 (h_path_seed, formed once
+//       per path by the histogram launch: the exact terrain of the sampled waypoint with the
+//       largest lb) and those the item takes (fetched, code-3 records, off-raster +0.0, blocks
+//       whose bounds coincide).
 // It fetches w iff !(ub_w <= E) && !(ub_w < Lb) (NaN bounds: "no bound", always fetched).
 // Exactness: let w* hold M, in this item's group.  If w* was not taken exactly, then either
 // ub_w* <= E, so M <= E and E -- an exact terrain value of the path -- is M; or ub_w* < Lb <= M,
 // impossible since M <= ub_w*.  So the group holding M reports M, every group reports at most
 // its own maximum (E holds exact values), and the output launch's maximum over the groups is M.
 // (A group without M may report less than its own maximum: only the path's is an output.)
-// The slot's hmax is that E.  tools/sim_terrain_bound.py models the fetches (0.17 per waypoint
-// at cfg3, sample stride 8).
+// The slot's hmax is that E.  (Measured, cfg3: 0.19 fetches per waypoint with the sampled lb
+// alone and chunks issued one ahead, tools/k2h_counts.py.)
+#ifdef UAM_K2H_COUNT  // measurement builds only: K2h's slot classes (tools/k2h_counts.py)
+__device__ unsigned long long g_k2h_cnt[8];  // valid, in-raster, fetched, code 1, 2, 3, Lb -inf
+extern "C" int uam_debug_k2h_counts(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2h_cnt), sizeof(g_k2h_cnt)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2h_cnt), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 #ifndef UAM_K2H_MINW  // waves per SIMD the register budget allows (measurement builds)
 #define UAM_K2H_MINW 4
 #endif
-constexpr int H_BS = 512;  // K2h workgroup (2 per CU at 4 waves per SIMD; LDS <= 80 KiB each)
-template <int CH>
+#ifndef UAM_K2H_BS  // (measurement builds)
+#define UAM_K2H_BS 256
+#endif
+// K2h workgroup: 256 items (cfg3 0.297 ms against 0.306 at 512, profiles/r05/k2h12)
+constexpr int H_BS = UAM_K2H_BS;
+template <int CH, bool TE>  // TE: the terrain in the entry (UAM_OPT_K2H_TERRAIN 1)
 __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, const KGrp& kg,
                                        const uint32_t* __restrict__ s_hdr,
                                        const double2* __restrict__ s_u, bool live, int32_t item,
-                                       int32_t path, int32_t q, const double4& pr, float Lb) {
+                                       int32_t path, int32_t q, const double4& pr,
+                                       float seed) {
     // a lane past the last item evaluates nothing and writes nothing
     const int s = item - path * kg.nseg;
     const int32_t d = path - q * kg.D;
@@ -5802,8 +5858,9 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
     const uint32_t o8 = __builtin_amdgcn_readfirstlane(rs.o8);
     const uint32_t o16 = __builtin_amdgcn_readfirstlane(rs.o16);
     const uint32_t ot4 = __builtin_amdgcn_readfirstlane(rs.ot4);
+    const uint32_t op8 = __builtin_amdgcn_readfirstlane(rs.op8);
     double gc = 0.0, gn = 0.0;
-    float E = -INFINITY;
+    float Lb = seed, E = seed;  // the path's seed: an exact terrain value of the path
     uint32_t nh = 0, off = 0;
     // one chunk ahead: chunk c + 1's loads are issued before chunk c is consumed (the fetch
     // rule then sees E without chunk c's fetched values: valid, E only holds exact values).
@@ -5812,13 +5869,18 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
     float tvA[CH];
     uint32_t kcA[CH], vinA = 0, tkA = 0;
     int nvA = 0;
-    for (int c = -1; c < nch; ++c) {  // (nch wave-uniform)
+#ifndef UAM_K2H_AHEAD  // (measurement builds: 1 issues chunk c + 1 before consuming chunk c;
+#define UAM_K2H_AHEAD 0  // the same at cfg3 with 256-item workgroups, profiles/r05/k2h12)
+#endif
+    constexpr bool ahead = UAM_K2H_AHEAD != 0;
+    for (int c = ahead ? -1 : 0; c < nch; ++c) {  // (nch wave-uniform)
+        const int ci = ahead ? c + 1 : c;  // the chunk issued by this iteration
         uint4 rB[CH];
         float tvB[CH];
         uint32_t kcB[CH], vinB = 0, tkB = 0;
         int nvB = 0;
-        if (c + 1 < nch) {
-            const int jc = j0 + (c + 1) * CH;
+        if (ci < nch) {
+            const int jc = j0 + ci * CH;
             const double2* uc = urow + jc;
             // phase 1: the cells (in-raster and in-group bits per slot)
             int32_t ix[CH], iy[CH];
@@ -5851,23 +5913,38 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
             for (int t = 0; t < CH; ++t) {
                 const int32_t b = pk_block(rs, ix[t], iy[t]);
                 cw[t] = s_hdr[b >> 4] >> ((b & 15) * 2);
-                const uint32_t bx = (uint32_t)(ix[t] >> rs.bshift);
-                const uint32_t by = (uint32_t)(iy[t] >> rs.bshift);
-                be[t] = bnd[__umul24(by, (uint32_t)rs.bnbx) + bx];
-                sb[t] = sbt[__umul24(by >> 2, (uint32_t)rs.sbnbx) + (bx >> 2)];
+                if constexpr (!TE) {
+                    const uint32_t bx = (uint32_t)(ix[t] >> rs.bshift);
+                    const uint32_t by = (uint32_t)(iy[t] >> rs.bshift);
+                    be[t] = bnd[__umul24(by, (uint32_t)rs.bnbx) + bx];
+                    sb[t] = sbt[__umul24(by >> 2, (uint32_t)rs.sbnbx) + (bx >> 2)];
+                }
             }
             // phase 3: the decisions and the loads
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const bool vin = (vinB >> t) & 1u, vj = (vjb >> t) & 1u;
                 const uint32_t code = cw[t] & (vin ? 3u : 0u);
+                if constexpr (TE) {
+                    // code 1: the 8-B {phi, terrain} entry; 2 / 3: the 16-B record (both carry
+                    // the exact terrain); code 0: nothing to read (phi, psi +-0, terrain +0.0)
+                    const bool rec = code & 2u;
+                    const uint32_t a4 = (uint32_t)p4_addr(rs, ix[t], iy[t]);
+                    const uint32_t ab = (uint32_t)p44_addr(rs, ix[t], iy[t]) << 3;
+                    const uint32_t voff = rec ? o16 + (a4 << 4) : code ? op8 + (ab & ~15u) : o4;
+                    kcB[t] = code | (rec ? 0u : (ab & 8u));
+                    rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
+                    (void)vj;
+                    continue;
+                }
                 float ub, lb;
                 pk_bound_decode(be[t], sb[t], ub, lb);
-                // off the raster: +0.0, an exact value and a lower bound; a block of one
-                // value: ub
-                Lb = fmaxf(Lb, vin ? lb : vj ? 0.0f : -INFINITY);
-                E = fmaxf(E, vin ? (lb == ub ? ub : -INFINITY) : vj ? 0.0f : -INFINITY);
-                const bool fetch = vin & (code != 3u) & !(ub <= E) & !(ub < Lb);
+                // off the raster or code 0: +0.0, an exact value and a lower bound; a block
+                // of one value: ub
+                const bool zero = !vin | (code == 0u);
+                Lb = fmaxf(Lb, vj ? (zero ? 0.0f : lb) : -INFINITY);
+                E = fmaxf(E, vj ? (zero ? 0.0f : lb == ub ? ub : -INFINITY) : -INFINITY);
+                const bool fetch = !zero & (code != 3u) & !(ub <= E) & !(ub < Lb);
                 const uint32_t a4 = (uint32_t)p4_addr(rs, ix[t], iy[t]);
                 // the entry's byte offset in its plane: a4 * 4 / 8 / 16 for codes 1 / 2 / 3;
                 // its aligned 16 B and the cell's word in them
@@ -5878,14 +5955,44 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
                 rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
                 tvB[t] = *reinterpret_cast<const float*>(pk + (ot4 + (fetch ? a4 * 4u : 0u)));
                 tkB |= (uint32_t)fetch << t;
+#ifdef UAM_K2H_COUNT
+                {
+                    const uint64_t m[6] = {__ballot(vj), __ballot(vin), __ballot(fetch),
+                                           __ballot(code == 1u), __ballot(code == 2u),
+                                           __ballot(code == 3u)};
+                    if ((threadIdx.x & 63) == 0)
+                        for (int q = 0; q < 6; ++q)
+                            atomicAdd(&g_k2h_cnt[q], (unsigned long long)__popcll(m[q]));
+                }
+#endif
             }
             nvB = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
+        }
+        if (!ahead) {
+#pragma unroll
+            for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+            vinA = vinB, tkA = tkB, nvA = nvB;
         }
         if (c >= 0) {
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const bool vl = t < nvA;
                 const bool in = (vinA >> t) & 1u;
+                if constexpr (TE) {
+                    const uint4 r = rA[t];
+                    const uint32_t code = kcA[t] & 3u;  // (0 off the raster)
+                    const bool rec = code & 2u, s1 = kcA[t] & 8u;
+                    const uint32_t lo = s1 ? r.z : r.x, hi = s1 ? r.w : r.y;
+                    const uint32_t phi = code ? (rec ? r.x : lo) : 0u;
+                    const uint32_t tb = rec ? ((r.w & UAM_FLAG_NODATA) ? 0u : r.z) : hi;
+                    nh += (rec && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+                    off += (vl && !in) ? 1u : 0u;
+                    gc = gc + over_n((double)__uint_as_float(phi));
+                    gn = gn + (rec ? (double)__uint_as_float(r.y) : 0.0);
+                    // (off the raster, or code 0: +0.0 exactly)
+                    E = fmaxf(E, code ? __uint_as_float(tb) : vl ? 0.0f : -INFINITY);
+                    continue;
+                }
                 uint32_t phi, psi, hit;
                 float rter;
                 pk_terms_k(rA[t], kcA[t], phi, psi, hit, rter);
@@ -5897,9 +6004,11 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
                 E = fmaxf(E, ter);
             }
         }
+        if (ahead) {
 #pragma unroll
-        for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
-        vinA = vinB, tkA = tkB, nvA = nvB;
+            for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+            vinA = vinB, tkA = tkB, nvA = nvB;
+        }
     }
     HSlot o;
     o.cost = gc;
@@ -5912,12 +6021,14 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
 // K2h evaluation: workgroups of H_BS items (xcd_chunk), the packed raster's header (codes,
 // bounds, superblocks) and the unit-arc rows (+ G + CH padding slots) staged in LDS, then one item
 // per lane (h_item)
-template <int CH>
+template <int CH, bool TE>
 __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaster rs, KGrp kg) {
     PK_CODES_CHECK(CH);
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_hdr = s_dyn;
-    double2* s_u = reinterpret_cast<double2*>(s_dyn + rs.hwords);
+    // the header in LDS: codes, bounds and superblocks; the code map alone with TE
+    const int hw = TE ? rs.bnd_off : rs.hwords;
+    double2* s_u = reinterpret_cast<double2*>(s_dyn + hw);
     // the item's order entry, pair and path bound first: their dependent round trips overlap
     // the staging below instead of following it
     const int64_t pos = xcd_chunk(blockIdx.x, gridDim.x) * H_BS + threadIdx.x;
@@ -5926,11 +6037,17 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
     const int32_t path = (int32_t)div_magic((uint32_t)item, kg.m_nseg, kg.sh_nseg);
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-    const float Lb = kg.lbp[path];
+    const float seed = kg.lbp ? kg.lbp[path] : -INFINITY;
+#ifdef UAM_K2H_COUNT
+    {
+        const uint64_t m = __ballot(live && seed == -INFINITY);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_k2h_cnt[6], (unsigned long long)__popcll(m));
+    }
+#endif
     const int nu = kg.D * p.N;
-    {  // staging: every load of a thread issued before its first LDS store (hwords % 4 == 0)
+    {  // staging: every load of a thread issued before its first LDS store (hw % 4 == 0)
         constexpr int U = 4;
-        const int nv = rs.hwords >> 2;
+        const int nv = hw >> 2;
         const uint4* src = reinterpret_cast<const uint4*>(rs.pmap);
         uint4* dst = reinterpret_cast<uint4*>(s_hdr);
         const uint4* gu = reinterpret_cast<const uint4*>(kg.utab);
@@ -5954,7 +6071,7 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
     // waypoint in a wave of full ones)
     if ((int)threadIdx.x < kg.G + CH) s_u[nu + threadIdx.x] = make_double2(0.0, 0.0);
     __syncthreads();
-    h_item<CH>(p, rs, kg, s_hdr, s_u, live, item, path, q, pr, Lb);
+    h_item<CH, TE>(p, rs, kg, s_hdr, s_u, live, item, path, q, pr, seed);
 }
 
 // The waypoint cells (the reference's returned waypoints as raster cells, solver.py:49,
@@ -6105,6 +6222,14 @@ struct KVol4 {
     // t4); null when the copy is 4 GiB or larger or a layer holds 2^24 entries (K4h stands aside)
     const char* __restrict__ pk;
     uint32_t o4, o8, o16, ot4;
+    // the terrain-in-entry form's plane q8 {risk, column terrain} in 4 x 4-column blocks per
+    // layer (nb4 blocks a row, layer44 entries a layer) at byte offset oq8
+    uint32_t oq8, layer44;
+    int32_t nb4;
+    // v16 in 4 x 2-column blocks per layer (8 entries, one 128-B line): nbx4 blocks a row,
+    // layer42 entries a layer
+    uint32_t layer42;
+    int32_t nbx4;
 };
 
 constexpr int VPK_CSHIFT = 3;           // code blocks of 8 x 8 columns
@@ -6116,13 +6241,26 @@ __device__ __forceinline__ uint32_t vt4_index(const KVol4& v, int32_t ix, int32_
            (((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u);
 }
 
-// the layer planes r4, e8 and v16: one thread per i4 entry, which writes all three (padding:
-// zero)
+// v16's in-layer index of column (ix, iy): 4 x 2-column blocks (8 entries of 16 B, one line)
+__device__ __forceinline__ uint32_t vv16_index(const KVol4& v, int32_t ix, int32_t iy) {
+    return ((__umul24((uint32_t)(iy >> 1), (uint32_t)v.nbx4) + (uint32_t)(ix >> 2)) << 3) |
+           (((uint32_t)iy & 1u) << 2) | ((uint32_t)ix & 3u);
+}
+
+// q8's in-layer index of column (ix, iy): 4 x 4-column blocks (16 entries of 8 B, one line)
+__device__ __forceinline__ uint32_t vq8_index(const KVol4& v, int32_t ix, int32_t iy) {
+    return ((__umul24((uint32_t)(iy >> 2), (uint32_t)v.nb4) + (uint32_t)(ix >> 2)) << 4) |
+           (((uint32_t)iy & 3u) << 2) | ((uint32_t)ix & 3u);
+}
+
+// the layer planes r4, e8, v16 and q8: one thread per i4 entry (r4 / e8 at i4, v16 and q8 at
+// their own block indices), which writes all four (padding: zero)
 __global__ __launch_bounds__(256) void k_volume_pack_planes(const uint2* __restrict__ vox,
                                                             const uint2* __restrict__ col,
                                                             KVol4 v, uint32_t* __restrict__ r4,
                                                             uint2* __restrict__ e8,
-                                                            uint4* __restrict__ v16) {
+                                                            uint4* __restrict__ v16,
+                                                            uint2* __restrict__ q8) {
     const int64_t total = (int64_t)v.nz * v.layer;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -6140,7 +6278,10 @@ __global__ __launch_bounds__(256) void k_volume_pack_planes(const uint2* __restr
         }
         r4[i] = a.x;
         e8[i] = make_uint2(a.x, (a.y & 0x7fffffffu) | ((cl.y & UAM_FLAG_NFZ) ? 0x80000000u : 0u));
-        v16[i] = make_uint4(a.x, a.y, cl.x, cl.y);
+        if (ix < v.nbx4 * 4 && iy < ((v.ny + 1) >> 1) * 2)  // (v16's padded extent)
+            v16[(int64_t)iz * v.layer42 + vv16_index(v, ix, iy)] = make_uint4(a.x, a.y, cl.x, cl.y);
+        if (ix < v.nb4 * 4 && iy < v.lnby4 * 4)  // (q8 is narrower: nb4 4-column blocks)
+            q8[(int64_t)iz * v.layer44 + vq8_index(v, ix, iy)] = make_uint2(a.x, cl.x);
     }
 }
 
@@ -6206,31 +6347,39 @@ __device__ __forceinline__ bool vol_voxel(const KVol4& vs, double x0, double x1,
     return in;
 }
 
-// K4h: a path's sampled upper bound of its minimum clearance (k_v_eval's Ub): the minimum of
-// z - lb over its in-volume waypoints j = 0, s, 2s, ... (s = kg.lb_stride) and j = W - 1, at
-// their own voxels and altitudes by the evaluation's operations (+inf: none)
-__device__ __forceinline__ double v_path_ub(const KParams& p, const KVol4& vs, const KGrp& kg,
-                                            int32_t path) {
+// K4h: a path's clearance seed (k_v_eval's E and Ub): the exact clearance z - T (T the column's
+// terrain, t4) of the in-volume sampled waypoint with the smallest z - lb, over j = 0, s, 2s,
+// ... (s = kg.lb_stride) and j = W - 1, at their own voxels and altitudes by the evaluation's
+// operations (+inf: none).  It is an exact clearance of the path, so at least the path's
+// minimum M.  hdr / u: the packed header and the unit-arc table (LDS copies when staged).
+__device__ __forceinline__ double v_path_seed(const KParams& p, const KVol4& vs, const KGrp& kg,
+                                             int32_t path, const uint32_t* __restrict__ hdr,
+                                             const double2* __restrict__ utab) {
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d), d = path - q * kg.D;
     const double* pr = kg.pairs + (int64_t)q * 6;
     const double ax = pr[0], ay = pr[1], za = pr[2], bx = pr[3], by = pr[4], zb = pr[5];
-    const double2* u = reinterpret_cast<const double2*>(kg.utab) + (int64_t)d * p.N - 1;
+    const double2* u = utab + d * p.N - 1;
     const int W = kg.W;
-    double Ub = INFINITY;
-    auto take = [&](double x0, double x1, int j) {
-        const double z = vz_at(za, zb, (double)j / (double)(W - 1));
+    constexpr uint32_t NONE = 0xffffffffu;
+    double Ub = INFINITY, zbest = 0.0;
+    uint32_t best = NONE;  // the t4 index of the sample holding Ub
+    auto take = [&](double x0, double x1, double z) {
         int32_t ix, iy, iz;
         const bool in = vol_voxel(vs, x0, x1, z, ix, iy, iz);
         const uint32_t bx2 = (uint32_t)(ix >> vs.bshift), by2 = (uint32_t)(iy >> vs.bshift);
-        const uint32_t e = reinterpret_cast<const uint16_t*>(vs.hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
+        const uint32_t e = reinterpret_cast<const uint16_t*>(hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
         const float2 sb =
-            reinterpret_cast<const float2*>(vs.hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx + (bx2 >> 2)];
+            reinterpret_cast<const float2*>(hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx + (bx2 >> 2)];
         float ub, lb;
         pk_bound_decode(e, sb, ub, lb);
-        if (in) Ub = fmin(Ub, z - (double)lb);
+        const double v = z - (double)lb;
+        const bool dn = in && v < Ub;  // (a NaN bound: no)
+        Ub = dn ? v : Ub;
+        zbest = dn ? z : zbest;
+        best = dn ? vt4_index(vs, ix, iy) : best;
     };
-    take(ax, ay, 0);
-    take(bx, by, W - 1);
+    take(ax, ay, vz_at(za, zb, 0.0 / (double)(W - 1)));
+    take(bx, by, vz_at(za, zb, (double)(W - 1) / (double)(W - 1)));
     // four samples at a time, every load of the four issued together (a sample past the last
     // interior waypoint repeats it)
     constexpr int K = 4;
@@ -6242,40 +6391,38 @@ __device__ __forceinline__ double v_path_ub(const KParams& p, const KVol4& vs, c
             jj[k] = min(j0 + k * kg.lb_stride, W - 2);
             uu[k] = u[jj[k]];
         }
-        uint32_t e[K];
-        float2 sb[K];
-        double z[K];
-        bool in[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double x0, x1;
             arc_point(ax, ay, bx, by, uu[k].x, uu[k].y, x0, x1);
-            z[k] = vz_at(za, zb, (double)jj[k] / (double)(W - 1));
-            int32_t ix, iy, iz;
-            in[k] = vol_voxel(vs, x0, x1, z[k], ix, iy, iz);
-            const uint32_t bx2 = (uint32_t)(ix >> vs.bshift), by2 = (uint32_t)(iy >> vs.bshift);
-            e[k] = reinterpret_cast<const uint16_t*>(vs.hdr + vs.bnd_off)[by2 * vs.bnbx + bx2];
-            sb[k] = reinterpret_cast<const float2*>(vs.hdr + vs.sbt_off)[(by2 >> 2) * vs.sbnbx +
-                                                                         (bx2 >> 2)];
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float ub, lb;
-            pk_bound_decode(e[k], sb[k], ub, lb);
-            if (in[k]) Ub = fmin(Ub, z[k] - (double)lb);
+            take(x0, x1, vz_at(za, zb, (double)jj[k] / (double)(W - 1)));
         }
     }
-    return Ub;
+    return best == NONE ? INFINITY
+                        : zbest - (double)reinterpret_cast<const float*>(vs.pk + vs.ot4)[best];
 }
 
 // sort, launch 1 (K4h): keys on (altitude band, tile) of each item's middle waypoint
 __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
     __shared__ __attribute__((aligned(16))) int32_t h[G_BINS_MAX];
     __shared__ uint16_t tk[1 << (2 * G_TBITS_MAX)];
+    // with kg.seed_lds: the packed header and the unit-arc table staged for the seeds
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_vhist_dyn[];
     const int t = threadIdx.x, b = blockIdx.x;
     if (b == 0 && t == 0) *kg.err = 0;
     for (int k = t; k < kg.bins; k += 1024) h[k] = 0;
     for (int k = t; k < (1 << (2 * kg.tbits)); k += 1024) tk[k] = kg.tkey[k];
+    const uint32_t* s_hdr = vs.hdr;
+    const double2* s_ut = reinterpret_cast<const double2*>(kg.utab);
+    if (kg.ubp && kg.seed_lds) {
+        uint4* dh = reinterpret_cast<uint4*>(s_vhist_dyn);
+        const uint4* gh = reinterpret_cast<const uint4*>(vs.hdr);
+        for (int k = t; k < (vs.hwords >> 2); k += 1024) dh[k] = gh[k];
+        double2* du = reinterpret_cast<double2*>(s_vhist_dyn + vs.hwords);
+        for (int k = t; k < kg.D * p.N; k += 1024) du[k] = s_ut[k];
+        s_hdr = s_vhist_dyn;
+        s_ut = du;
+    }
     __syncthreads();
     const int64_t lo = ((int64_t)kg.P * b / G_NBK) * kg.nseg;
     const int64_t hi = ((int64_t)kg.P * (b + 1) / G_NBK) * kg.nseg;
@@ -6330,10 +6477,10 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
             atomicAdd(&h[key], 1);
         }
     }
-    if (kg.ubp) {  // the partition's paths' sampled clearance upper bounds, one thread per path
+    if (kg.ubp) {  // the partition's paths' clearance seeds, one thread per path
         const int64_t plo = (int64_t)kg.P * b / G_NBK, phi = (int64_t)kg.P * (b + 1) / G_NBK;
         for (int64_t pth = plo + t; pth < phi; pth += 1024)
-            kg.ubp[pth] = v_path_ub(p, vs, kg, (int32_t)pth);
+            kg.ubp[pth] = v_path_seed(p, vs, kg, (int32_t)pth, s_hdr, s_ut);
     }
     __syncthreads();
     for (int k = t; k < kg.bins; k += 1024) kg.cnt[(int64_t)k * G_NBK + b] = h[k];
@@ -6351,12 +6498,14 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 //       (0), else its terrain is fetched;
 //   c_j = z_j - T_j, whose path minimum is min_clearance: z_j - ub_j <= c_j <= z_j - lb_j (the
 //       float64 subtraction is monotone).  The item keeps Ub, an upper bound of the path minimum
-//       M (v_path_ub's samples, then its own waypoints' z - lb), and E, the minimum of the c_j
-//       it has taken exactly (fetched, v16's, one-value blocks); it fetches w iff it is
-//       undecided or !(z_w - ub_w >= E) && !(z_w - ub_w > Ub).  If w* holds M and is not
-//       taken: z - ub >= E gives M >= E >= M, and z - ub > Ub >= M is impossible.  NaN bounds
-//       (no bound) always fetch.
-template <int CH>
+//       M (the path's seed, then its own waypoints' z - lb), and E, the minimum of exact c_j of
+//       the path: the seed (v_path_seed: the exact clearance of the sampled waypoint with the
+//       smallest z - lb, formed once per path by the histogram launch) and those it takes
+//       (fetched, v16's, one-value blocks); it fetches w iff it is undecided or
+//       !(z_w - ub_w >= E) && !(z_w - ub_w > Ub).  If w* holds M and is not taken: z - ub >= E
+//       gives M >= E >= M, and z - ub > Ub >= M is impossible.  NaN bounds (no bound) always
+//       fetch.
+template <int CH, bool TE>  // TE: the terrain in the entry (UAM_OPT_K2H_TERRAIN 1)
 __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
                                                                               KGrp kg) {
     PK_CODES_CHECK(CH);
@@ -6379,7 +6528,8 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     const double2 pa = *reinterpret_cast<const double2*>(prp);
     const double2 pb = *reinterpret_cast<const double2*>(prp + 2);
     const double2 pc = *reinterpret_cast<const double2*>(prp + 4);
-    double Ub = kg.ubp[path];
+    const double seed = kg.ubp ? kg.ubp[path] : INFINITY;  // an exact clearance of the path
+    double Ub = seed;
     for (int i = threadIdx.x; i < nu + npad; i += 256)
         s_u[i] = i < nu ? reinterpret_cast<const double2*>(kg.utab)[i] : make_double2(0.0, 0.0);
     for (int j = threadIdx.x; j < njw; j += 256)
@@ -6387,7 +6537,8 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     {
         const uint4* src = reinterpret_cast<const uint4*>(vs.hdr);
         uint4* dst = reinterpret_cast<uint4*>(s_hdr);
-        for (int i = threadIdx.x; i < (vs.hwords >> 2); i += 256) dst[i] = src[i];
+        const int hw = TE ? vs.bnd_off : vs.hwords;  // (TE: the code map alone)
+        for (int i = threadIdx.x; i < (hw >> 2); i += 256) dst[i] = src[i];
     }
     __syncthreads();
     const double ax = pa.x, ay = pa.y, za = pb.x, bx = pb.y, by = pc.x, zb = pc.y;
@@ -6419,7 +6570,10 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     const uint32_t o16 = __builtin_amdgcn_readfirstlane(vs.o16);
     const uint32_t ot4 = __builtin_amdgcn_readfirstlane(vs.ot4);
     const uint32_t layer = __builtin_amdgcn_readfirstlane(vs.layer);
-    double gc = 0.0, gn = 0.0, E = INFINITY;
+    const uint32_t oq8 = __builtin_amdgcn_readfirstlane(vs.oq8);
+    const uint32_t layer44 = __builtin_amdgcn_readfirstlane(vs.layer44);
+    const uint32_t layer42 = __builtin_amdgcn_readfirstlane(vs.layer42);
+    double gc = 0.0, gn = 0.0, E = seed;
     uint32_t nh = 0, off = 0, bel = 0;
     // one chunk ahead, as h_item: iteration c issues chunk c + 1 (B arrays) and consumes chunk
     // c (A arrays)
@@ -6428,13 +6582,15 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     float tvA[CH];
     uint32_t kcA[CH], vinA = 0, tkA = 0, bvA = 0;
     int nvA = 0, jcA = 0;
-    for (int c = -1; c < nch; ++c) {  // (nch wave-uniform)
+    constexpr bool ahead = UAM_K2H_AHEAD != 0;  // (h_item's switch)
+    for (int c = ahead ? -1 : 0; c < nch; ++c) {  // (nch wave-uniform)
+        const int ci = ahead ? c + 1 : c;  // the chunk issued by this iteration
         uint4 rB[CH];
         float tvB[CH];
         uint32_t kcB[CH], vinB = 0, tkB = 0, bvB = 0;
         int nvB = 0;
-        const int jc = j0 + (c + 1) * CH;
-        if (c + 1 < nch) {
+        const int jc = j0 + ci * CH;
+        if (ci < nch) {
             double zB[CH];
             int32_t izB[CH];
             const double2* uc = urow + jc;
@@ -6471,16 +6627,29 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
                 const uint32_t b = __umul24((uint32_t)(iy[t] >> VPK_CSHIFT), (uint32_t)vs.cnbx) +
                                    (uint32_t)(ix[t] >> VPK_CSHIFT);
                 cw[t] = s_hdr[b >> 4] >> ((b & 15u) * 2u);
-                const uint32_t bx2 = (uint32_t)(ix[t] >> vs.bshift);
-                const uint32_t by2 = (uint32_t)(iy[t] >> vs.bshift);
-                be[t] = bnd[__umul24(by2, (uint32_t)vs.bnbx) + bx2];
-                sb[t] = sbt[__umul24(by2 >> 2, (uint32_t)vs.sbnbx) + (bx2 >> 2)];
+                if constexpr (!TE) {
+                    const uint32_t bx2 = (uint32_t)(ix[t] >> vs.bshift);
+                    const uint32_t by2 = (uint32_t)(iy[t] >> vs.bshift);
+                    be[t] = bnd[__umul24(by2, (uint32_t)vs.bnbx) + bx2];
+                    sb[t] = sbt[__umul24(by2 >> 2, (uint32_t)vs.sbnbx) + (bx2 >> 2)];
+                }
             }
             // phase 3: the decisions and the loads
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const bool vin = (vinB >> t) & 1u;
                 const uint32_t code = cw[t] & (vin ? 3u : 0u);
+                if constexpr (TE) {
+                    // codes 0 / 1: the 8-B {risk, column terrain} entry (q8); 2 / 3: v16
+                    const bool rec = code & 2u;
+                    const uint32_t iz = (uint32_t)izB[t];
+                    const uint32_t a16 = vv16_index(vs, ix[t], iy[t]) + __umul24(iz, layer42);
+                    const uint32_t ab = (vq8_index(vs, ix[t], iy[t]) + __umul24(iz, layer44)) << 3;
+                    const uint32_t voff = rec ? o16 + (a16 << 4) : oq8 + (ab & ~15u);
+                    kcB[t] = code | (rec ? 0u : (ab & 8u)) | (iz << 8);
+                    rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
+                    continue;
+                }
                 float ub, lb;
                 pk_bound_decode(be[t], sb[t], ub, lb);
                 const double z = zB[t], zc = zc_of(izB[t]);
@@ -6493,10 +6662,12 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
                     vin & (code != 3u) & (!(k1 | k0) | (!(clo >= E) & !(clo > Ub)));
                 const uint32_t it = vt4_index(vs, ix[t], iy[t]);
                 const uint32_t a4 = it + __umul24((uint32_t)izB[t], layer);
+                // codes 1 / 2: the r4 / e8 entry's aligned 16 B and word; 3: v16 (its own index)
                 const uint32_t ab = a4 << (code + 1u);
-                const uint32_t base = (code & 2u) ? ((code & 1u) ? o16 : o8) : o4;
-                const uint32_t voff = base + (code ? (ab & ~15u) : 0u);
-                kcB[t] = code | (ab & 12u) | ((uint32_t)izB[t] << 8);
+                const uint32_t a16 = vv16_index(vs, ix[t], iy[t]) + __umul24((uint32_t)izB[t], layer42);
+                const uint32_t voff = code == 3u ? o16 + (a16 << 4)
+                                                 : (code == 2u ? o8 : o4) + (code ? (ab & ~15u) : 0u);
+                kcB[t] = code | (code == 3u ? 0u : (ab & 12u)) | ((uint32_t)izB[t] << 8);
                 rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
                 tvB[t] = *reinterpret_cast<const float*>(pk + (ot4 + (fetch ? it * 4u : 0u)));
                 tkB |= (uint32_t)fetch << t;
@@ -6504,10 +6675,30 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
             }
             nvB = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
         }
+        if (!ahead) {
+#pragma unroll
+            for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+            vinA = vinB, tkA = tkB, bvA = bvB, nvA = nvB, jcA = jc;
+        }
         if (c >= 0) {
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const bool vl = t < nvA, in = (vinA >> t) & 1u;
+                if constexpr (TE) {
+                    const uint4 r = rA[t];
+                    const bool rec = kcA[t] & 2u, s1 = kcA[t] & 8u;
+                    const uint32_t lo = s1 ? r.z : r.x, hi = s1 ? r.w : r.y;
+                    const uint32_t risk = in ? (rec ? r.x : lo) : 0u;
+                    const float ter = __uint_as_float(rec ? r.z : hi);  // (+0 on nodata)
+                    nh += (rec && (r.w & UAM_FLAG_NFZ)) ? 1u : 0u;
+                    off += (vl && !in) ? 1u : 0u;
+                    gc = gc + over_n((double)__uint_as_float(risk));
+                    gn = gn + (rec ? (double)__uint_as_float(r.y) : 0.0);
+                    const double z = vz_at(za, zb, s_jw[jcA + t]);
+                    bel += (in && zc_of((int32_t)(kcA[t] >> 8)) < (double)ter) ? 1u : 0u;
+                    E = in ? fmin(E, z - (double)ter) : E;
+                    continue;
+                }
                 uint32_t risk, psi, hit;
                 float rter;
                 pk_terms_k(rA[t], kcA[t], risk, psi, hit, rter);
@@ -6526,9 +6717,11 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
                 E = ex ? fmin(E, z - (double)ter) : E;
             }
         }
+        if (ahead) {
 #pragma unroll
-        for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
-        vinA = vinB, tkA = tkB, bvA = bvB, nvA = nvB, jcA = jc;
+            for (int t = 0; t < CH; ++t) rA[t] = rB[t], tvA[t] = tvB[t], kcA[t] = kcB[t];
+            vinA = vinB, tkA = tkB, bvA = bvB, nvA = nvB, jcA = jc;
+        }
     }
     VSlot o;
     o.cost = gc;
@@ -6656,6 +6849,7 @@ struct uam_ctx {
     int64_t k2s_min = 65536;    // K2g / K2s: smallest batch in paths (UAM_OPT_SORTED_MIN_PATHS)
     bool k2s_attrs = false;     // K2s dynamic-LDS attributes raised on this context's device
     bool k2h_attrs = false;     // K2h's dynamic-LDS attributes raised on this context's device
+    bool k4h_hist_attr = false;  // k_v_hist's, likewise
     bool k2g_attrs = false;     // K2g dynamic-LDS attributes raised on this context's device
     bool k4h_attrs = false;     // the same for K4h
     void* d_ord = nullptr;      // pair_order scratch (grow-only)
@@ -6684,6 +6878,7 @@ struct uam_ctx {
     int k2g_curve = 1;          // K2g tile order: 1 Hilbert, 0 Morton (UAM_OPT_K2G_CURVE)
     int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
                                 // 0 = the fewest giving <= 16 bands)
+    int k2h_te = 1;             // K2h: terrain in the entry (UAM_OPT_K2H_TERRAIN)
     int k2h_lbs = 8;            // K2h: the path lower bound's sample stride (UAM_OPT_K2H_LB_STRIDE;
                                 // tools/sim_terrain_bound.py at cfg3: fetches per waypoint 0.17
                                 // at 8, 0.15 at 4, 0.37 without the path bound)
@@ -7399,9 +7594,15 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             (long long)value);
             ctx->k4h_band = (int)value;
             return UAM_OK;
+        case UAM_OPT_K2H_TERRAIN:
+            if (value != 0 && value != 1)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2H_TERRAIN %lld is not 0 or 1",
+                            (long long)value);
+            ctx->k2h_te = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2H_LB_STRIDE:
-            if (value < 1 || value > 1024)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2H_LB_STRIDE %lld outside [1, 1024]",
+            if (value < 0 || value > 1024)
+                return fail(UAM_E_INVALID, "UAM_OPT_K2H_LB_STRIDE %lld outside [0, 1024]",
                             (long long)value);
             ctx->k2h_lbs = (int)value;
             return UAM_OK;
@@ -7439,6 +7640,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_CHUNK: *value = ctx->k2g_chunk; return UAM_OK;
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
         case UAM_OPT_K2H_LB_STRIDE: *value = ctx->k2h_lbs; return UAM_OK;
+        case UAM_OPT_K2H_TERRAIN: *value = ctx->k2h_te; return UAM_OK;
         case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
@@ -7804,28 +8006,42 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
-    kg.lbp = sim ? (float*)(w + o) : nullptr, o += b_lbp;
+    kg.lbp = sim && !ctx->k2h_te && ctx->k2h_lbs > 0 ? (float*)(w + o) : nullptr, o += b_lbp;
+    // the seeds' header and unit-arc reads from LDS when both fit beside the histogram's own
+    const size_t hist_dyn = kg.lbp ? (size_t)kr.hwords * 4 + ubytes : 0;
+    kg.seed_lds = kg.lbp && hist_dyn <= (size_t)G_HIST_DYN_MAX;
     kg.key = (uint16_t*)(w + o);
     using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
     using HEvalFn = void (*)(KParams, KRaster, KGrp);
     // gathers in flight per lane (K2g, profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
-    // 10 0.369, 6 0.351; K2h: 7, groups of 21 = three full chunks)
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : sim ? 7 : 8;
+    // 10 0.369, 6 0.351; K2h: 7, groups of 21 = three full chunks).  A raster far beyond the
+    // L2s (over 2^25 cells: cfg4's 8192^2) misses more: fewer items resident per XCD (3
+    // workgroups per CU through an LDS floor of 54 000 B) with 11 gathers in flight (cfg4
+    // 0.886 against 0.936 ms, profiles/r04/sweep7)
+    const bool big = sim && (int64_t)kr.nx * kr.ny > ((int64_t)1 << 25);
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : big ? 11 : sim ? 7 : 8;
     size_t lds;
     int bs;
     EvalFn ev = nullptr;
     HEvalFn hev = nullptr;
     if (sim) {  // K2h: H_BS-item workgroups, the packed header in LDS
-        static const HEvalFn hevals[4] = {k_h_eval<6>, k_h_eval<7>, k_h_eval<8>, k_h_eval<11>};
-        hev = hevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3];
+        static const HEvalFn hevals[8] = {k_h_eval<6, false>, k_h_eval<7, false>,
+                                          k_h_eval<8, false>, k_h_eval<11, false>,
+                                          k_h_eval<6, true>,  k_h_eval<7, true>,
+                                          k_h_eval<8, true>,  k_h_eval<11, true>};
+        hev = hevals[(chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3) + (ctx->k2h_te ? 4 : 0)];
         bs = H_BS;
-        const size_t need = (size_t)kr.hwords * 4 + ubytes + (size_t)16 * (G + 16);  // + padding
-        lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+        const size_t hw = ctx->k2h_te ? (size_t)kr.bnd_off : (size_t)kr.hwords;
+        const size_t need = hw * 4 + ubytes + (size_t)16 * (G + 16);  // + padding
+        const int floor_lds = ctx->k2g_lds ? ctx->k2g_lds : big ? 54000 : 0;
+        lds = std::max(need, (size_t)std::min(floor_lds, 160 * 1024));
         if (lds > 160 * 1024) return 0;
         if (!ctx->k2h_attrs) {  // per context = per device (DeviceGuard active)
             for (HEvalFn f : hevals)
                 HIP_TRY(hipFuncSetAttribute((const void*)f,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            HIP_TRY(hipFuncSetAttribute((const void*)k_g_hist,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, G_HIST_DYN_MAX));
             ctx->k2h_attrs = true;
         }
     } else {  // K2g: 256-item workgroups, the code map in LDS
@@ -7853,7 +8069,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cells = ko.cells;
     st = ktime_begin(ctx, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? hist_dyn : 0, s,
+                       ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     kg.nsb_raw = nsb <= 1024 ? (int32_t)nsb : 0;  // up to 1024 totals: scanned by the scatter
@@ -7903,7 +8120,8 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     // (profiles/r04/sweep7)
     const int64_t npad = G + 16;  // k_v_eval's padding slots
     const size_t lds = std::max((size_t)(D * ctx->kp.N + npad) * 16 +
-                                    (size_t)((W + npad + 1) & ~1) * 8 + (size_t)kv.hwords * 4,
+                                    (size_t)((W + npad + 1) & ~1) * 8 +
+                                    (size_t)(ctx->k2h_te ? kv.bnd_off : kv.hwords) * 4,
                                 (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 60000, 160 * 1024));
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
@@ -7960,11 +8178,19 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
-    kg.ubp = (double*)(w + o), o += b_ubp;
+    kg.ubp = ctx->k2h_lbs > 0 && !ctx->k2h_te ? (double*)(w + o) : nullptr, o += b_ubp;
+    const size_t hist_dyn = (size_t)kv.hwords * 4 + (size_t)D * ctx->kp.N * 16;
+    kg.seed_lds = kg.ubp && hist_dyn <= (size_t)G_HIST_DYN_MAX;
     kg.key = (uint16_t*)(w + o);
     st = ktime_begin(ctx, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_v_hist, dim3(G_NBK), dim3(1024), 0, s, ctx->kp, kv, kg);
+    if (kg.seed_lds && !ctx->k4h_hist_attr) {
+        HIP_TRY(hipFuncSetAttribute((const void*)k_v_hist,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, G_HIST_DYN_MAX));
+        ctx->k4h_hist_attr = true;
+    }
+    hipLaunchKernelGGL(k_v_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? hist_dyn : 0, s,
+                       ctx->kp, kv, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
                        kg.tot);
     kg.nsb_raw = nsb <= 1024 ? (int32_t)nsb : 0;  // up to 1024 totals: scanned by the scatter
@@ -7977,9 +8203,13 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     // 11 are built for 3, 16 and 21 for 2)
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 11;
     // (21 runs as 16: a chunk's per-slot codes take 4 bits each of 64)
-    static const VEvalFn vevals[5] = {k_v_eval<6>, k_v_eval<7>, k_v_eval<8>, k_v_eval<11>,
-                                      k_v_eval<16>};
-    const VEvalFn ev = vevals[chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3 : 4];
+    static const VEvalFn vevals[10] = {k_v_eval<6, false>, k_v_eval<7, false>,
+                                       k_v_eval<8, false>,  k_v_eval<11, false>,
+                                       k_v_eval<16, false>, k_v_eval<6, true>,
+                                       k_v_eval<7, true>,   k_v_eval<8, true>,
+                                       k_v_eval<11, true>,  k_v_eval<16, true>};
+    const VEvalFn ev = vevals[(chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3 : 4) +
+                              (ctx->k2h_te ? 5 : 0)];
     if (lds > 64 * 1024 && !ctx->k4h_attrs) {
         for (VEvalFn f : vevals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -8028,14 +8258,15 @@ static int summary_dims(const uam_raster_desc* desc, int32_t block, int32_t* shi
 //   superblock table (nsb float2, 4 x 4 bound blocks each);
 //   scratch (nbb float2: the bound blocks' {min, max} while packing);
 //   p4 (4-B phi), t4 (4-B terrain), e8 (8 B) and r16 (the 16-B records) in 4 x 8-cell blocks,
-//   all at one index.
+//   all at one index; p8 ({phi, terrain}) in 4 x 4-cell blocks (p44_addr).
 struct PackDims {
     int32_t sh, nbx, nby, words;           // summary blocks, code-map words
     int32_t bsh, bnbx, bnby, nbb;          // bound blocks
     int32_t sbnbx, sbnby, nsb;             // superblocks
     int32_t hwords, bnd_off, sbt_off;      // header words, word offsets
     int32_t nb8, lnby;                     // 4 x 8-cell blocks per row, block rows
-    int64_t off_scr, off_p4, off_t4, off_e8, off_r16, bytes;
+    int32_t nb4;                           // p8's 4 x 4-cell blocks per row
+    int64_t off_scr, off_p4, off_t4, off_e8, off_r16, off_p8, bytes;
 };
 
 static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
@@ -8068,7 +8299,9 @@ static int pack_dims(const uam_raster_desc* desc, int32_t block, PackDims* d) {
     d->off_t4 = d->off_p4 + a256(c4 * 4);
     d->off_e8 = d->off_t4 + a256(c4 * 4);
     d->off_r16 = d->off_e8 + a256(c4 * 8);
-    d->bytes = d->off_r16 + a256(c4 * 16);
+    d->off_p8 = d->off_r16 + a256(c4 * 16);
+    d->nb4 = (desc->nx + 3) >> 2;
+    d->bytes = d->off_p8 + a256((int64_t)d->lnby * d->nb4 * 16 * 8);
     return UAM_OK;
 }
 
@@ -8083,6 +8316,7 @@ static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
     kr->bnbx = d.bnbx;
     kr->sbnbx = d.sbnbx;
     kr->nb8 = d.nb8;
+    kr->nb4 = d.nb4;
     kr->p4 = (const uint32_t*)(b + d.off_p4);
     kr->t4 = (const float*)(b + d.off_t4);
     kr->e8 = (const uint2*)(b + d.off_e8);
@@ -8092,6 +8326,7 @@ static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
     kr->o8 = (uint32_t)d.off_e8;
     kr->o16 = (uint32_t)d.off_r16;
     kr->ot4 = (uint32_t)d.off_t4;
+    kr->op8 = (uint32_t)d.off_p8;
 }
 
 static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
@@ -8304,7 +8539,8 @@ int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, 
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, r4,
                        kr, (uint32_t*)(b + d.off_p4), (float*)(b + d.off_t4),
-                       (uint2*)(b + d.off_e8), (uint4*)(b + d.off_r16));
+                       (uint2*)(b + d.off_e8), (uint4*)(b + d.off_r16),
+                       (uint2*)(b + d.off_p8));
     hipLaunchKernelGGL(k_t4_bminmax, dim3((unsigned)((d.nbb + 3) / 4)), dim3(256), 0, s,
                        (const float*)(b + d.off_t4), kr.nx, kr.ny, d.nb8, d.bsh, d.bnbx, d.nbb,
                        (float2*)(b + d.off_scr));
@@ -8432,7 +8668,11 @@ struct VpkDims {
     int32_t hwords, bnd_off, sbt_off;
     int32_t nb8, lnby4;
     int64_t layer;  // i4 entries per layer plane
-    int64_t off_scr, off_r4, off_t4, off_e8, off_v16, bytes;
+    int32_t nb4;    // q8: 4 x 4-column blocks per row
+    int64_t layer44;
+    int32_t nbx4;   // v16: 4 x 2-column blocks per row
+    int64_t layer42;
+    int64_t off_scr, off_r4, off_t4, off_e8, off_v16, off_q8, bytes;
 };
 void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
     v->cnbx = (d->nx + (1 << VPK_CSHIFT) - 1) >> VPK_CSHIFT;
@@ -8460,7 +8700,12 @@ void vpk_dims(const uam_volume_desc* d, VpkDims* v) {
     v->off_t4 = v->off_r4 + al256(v->layer * d->nz * 4);
     v->off_e8 = v->off_t4 + al256(v->layer * 4);
     v->off_v16 = v->off_e8 + al256(v->layer * d->nz * 8);
-    v->bytes = v->off_v16 + al256(v->layer * d->nz * 16);
+    v->nb4 = (d->nx + 3) >> 2;
+    v->layer44 = (int64_t)v->lnby4 * v->nb4 * 16;
+    v->nbx4 = (d->nx + 3) >> 2;
+    v->layer42 = (int64_t)((d->ny + 1) >> 1) * v->nbx4 * 8;
+    v->off_q8 = v->off_v16 + al256(v->layer42 * d->nz * 16);
+    v->bytes = v->off_q8 + al256(v->layer44 * d->nz * 8);
 }
 // the packed volume's view for K4h
 void vpk_kvol(const uam_volume_desc* vd, const VpkDims& v, const void* packed, KVol4* kv) {
@@ -8476,12 +8721,18 @@ void vpk_kvol(const uam_volume_desc* vd, const VpkDims& v, const void* packed, K
     // K4h's 32-bit offsets and 24-bit products: a copy under 4 GiB, layers under 2^24 entries,
     // columns under 2^24 a side
     const bool o32 = v.bytes <= (int64_t)UINT32_MAX && v.layer < ((int64_t)1 << 24) &&
+                     v.layer44 < ((int64_t)1 << 24) && v.layer42 < ((int64_t)1 << 24) &&
                      vd->nx < (1 << 24) && vd->ny < (1 << 24) && vd->nz < (1 << 24);
     kv->pk = o32 ? b : nullptr;
     kv->o4 = (uint32_t)v.off_r4;
     kv->o8 = (uint32_t)v.off_e8;
     kv->o16 = (uint32_t)v.off_v16;
     kv->ot4 = (uint32_t)v.off_t4;
+    kv->oq8 = (uint32_t)v.off_q8;
+    kv->nbx4 = v.nbx4;
+    kv->layer42 = (uint32_t)std::min(v.layer42, (int64_t)UINT32_MAX);
+    kv->nb4 = v.nb4;
+    kv->layer44 = (uint32_t)std::min(v.layer44, (int64_t)UINT32_MAX);
 }
 }  // namespace
 
@@ -8517,7 +8768,7 @@ int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* vd, const void* vol, vo
     HIP_TRY(hipMemsetAsync(b, 0, (size_t)v.off_scr, s));  // header padding
     hipLaunchKernelGGL(k_volume_pack_planes, dim3(grid_for(v.layer * vd->nz, 256)), dim3(256), 0,
                        s, vx, cl, kv, (uint32_t*)(b + v.off_r4), (uint2*)(b + v.off_e8),
-                       (uint4*)(b + v.off_v16));
+                       (uint4*)(b + v.off_v16), (uint2*)(b + v.off_q8));
     const int64_t nt4 = (int64_t)v.lnby4 * v.nb8 * 32;
     hipLaunchKernelGGL(k_volume_pack_t4, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s, cl,
                        kv, (float*)(b + v.off_t4));
