@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--workload", default="cfg3", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--mode", default=None, choices=["raster", "analytic", "volume"],
                     help="default: the workload's mode (raster; volume for cfg5)")
+    ap.add_argument("--shard", choices=("spatial", "index"), default="spatial",
+                    help="cfg4's strong-scaling shards: by space (Hilbert order of the pairs' "
+                         "midpoints) or by index")
+    ap.add_argument("--share", default=None,
+                    help="cfg4 rehearsal on one process: R/N = rank R's shard of N ranks")
     ap.add_argument("--pairs", type=int, default=None,
                     help="override the pair count (per GPU, or in total for cfg4)")
     ap.add_argument("--R", type=int, default=None, help="override raster size")
@@ -246,8 +251,16 @@ def main():
     gen = random_pairs3d if volume_mode else random_pairs
     all_pairs = gen(Q_total, seed=0)
     if strong:
-        lo, hi = udist.shard_range(Q_total, rank, world)
-        pairs_host = all_pairs[lo:hi]
+        # by space (distributed.spatial_shard): each rank's paths cover a compact part of the
+        # raster; --share R/N rehearses rank R of an N-rank run on this one process
+        srank, sworld = rank, world
+        if args.share:
+            srank, sworld = (int(v) for v in args.share.split("/"))
+        if args.shard == "spatial":
+            pairs_host, _ = udist.spatial_shard(all_pairs, srank, sworld)
+        else:
+            lo, hi = udist.shard_range(Q_total, srank, sworld)
+            pairs_host = all_pairs[lo:hi]
     else:
         pairs_host = udist.weak_shard(all_pairs, cfg["pairs"], rank, world)
     del all_pairs
@@ -300,12 +313,14 @@ def main():
     if world > 1:
         elapsed, kern_ms = udist.max_over_ranks([elapsed, kern_ms], device=eng.torch_device)
 
-    total_paths = Q_total * D * args.steps
+    # (a --share rehearsal processes one rank's shard only: its own paths)
+    total_paths = (Q if args.share else Q_total) * D * args.steps
     value = total_paths / elapsed
     last = eng.last_kernel()   # which evaluation the library ran (uam_last_kernel)
     wave = last in ("K2w", "K4w")
     skip = raster_mode and not args.no_skip and raster.summary is not None
-    te = eng.get_option("k2h_terrain") == 1  # UAM_OPT_K2H_TERRAIN: the form K2h / K4h ran
+    # UAM_OPT_K2H_TERRAIN / UAM_OPT_K4H_TERRAIN: the terrain form K2h / K4h ran
+    te = eng.get_option("k4h_terrain" if volume_mode else "k2h_terrain") == 1
     if last.startswith("K4h"):
         ktag = last.lower() + ("" if te else ":bounds")
         kernel_name = ("K4h sequence (k_v_hist / k_scan / k_g_scatter (+ the unit-arc sums), k_v_eval "
@@ -348,7 +363,7 @@ def main():
                                    kernel_tag=last,
                                    volume=volume_mode,
                                    cells=args.cells and not volume_mode,
-                                   terrain_entry=eng.get_option("k2h_terrain") == 1)
+                                   terrain_entry=te)
     roofline["kernel_ms_source"] = ("one HIP event pair (torch.cuda.Event on the launch "
                                     "stream) around the K timed steps / K: the whole launch "
                                     "sequence of every step (sorts, evaluation, output "
@@ -380,8 +395,11 @@ def main():
                    "mode": mode, "no_fly_shapes": geom.n_obstacles,
                    "region_shapes": int(geom.region_first[-1] - geom.region_first[0]),
                    "parallelism": (f"pair-sharded dp{world}, raster broadcast once" +
+                                   (f", {args.shard} shards" if strong else "") +
                                    (f" ({world} ranks on {n_gpus} GPU(s), rehearsal)"
-                                    if world != n_gpus else ""))},
+                                    if world != n_gpus else "") +
+                                   (f"; rank share {args.share} rehearsed on one process "
+                                    f"(value: this shard's paths)" if args.share else ""))},
         "waypoint_evals_per_s": round(value * W, 1),
         "roofline": roofline,
         "setup": setup,

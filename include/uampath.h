@@ -493,10 +493,14 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *                                exact terrain (clearance) of the sample with the best bound
  *                                (1..1024; default 8; 0: no seed); fewer terrain fetches at
  *                                smaller n, more arithmetic in that launch.  Same outputs.
- *   UAM_OPT_K2H_TERRAIN          K2h's terrain: 0 by bounds (the 4-B phi entries, the terrain
- *                                plane read only where a waypoint could hold the path
- *                                maximum), 1 in the entry (8-B {phi, terrain} entries, the
- *                                16-B records in no-fly blocks).  Same outputs. */
+ *   UAM_OPT_K2H_TERRAIN          K2h's terrain: 1 (default) in the entry (8-B {phi, terrain}
+ *                                entries, the 16-B records in no-fly / psi blocks), 0 by bounds
+ *                                (4-B phi entries, the terrain plane read only where a waypoint
+ *                                could still hold the path maximum).  Same outputs.
+ *   UAM_OPT_K4H_TERRAIN          K4h's likewise: 0 (default) by bounds (4-B risk / 8-B
+ *                                {risk, psi|nfz} voxels, the column terrain only where it could
+ *                                still decide an output), 1 in the entry (8-B {risk, terrain}
+ *                                voxels, 16-B voxels in no-fly / psi columns).  Same outputs. */
 enum {
     UAM_OPT_GROUP = 1,
     UAM_OPT_SORTED_MIN_PATHS = 2,
@@ -515,7 +519,8 @@ enum {
     UAM_OPT_K2G_SIM = 15,
     UAM_OPT_K4H_BAND = 17,
     UAM_OPT_K2H_LB_STRIDE = 19,
-    UAM_OPT_K2H_TERRAIN = 20
+    UAM_OPT_K2H_TERRAIN = 20,
+    UAM_OPT_K4H_TERRAIN = 21
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

@@ -162,3 +162,32 @@ def test_shard_ranges_cover():
             assert max(h - lo for lo, h in got) - min(h - lo for lo, h in got) <= 1
     with pytest.raises(ValueError):
         shard_range(10, 2, 2)
+
+
+def test_spatial_shard():
+    """cfg4's strong-scaling shards by space: every pair in exactly one shard, sizes within 1,
+    and each shard's midpoints compact (a Hilbert-order cut: a shard's bounding box is far
+    smaller than the whole set's); NaN pairs sort last; 6-column (3-D) pairs use x/y."""
+    import numpy as np
+
+    from uam_path_planning_amd import distributed as udist
+    from uam_path_planning_amd.synthetic import random_pairs
+
+    pr = random_pairs(20000, seed=3)
+    pr[5] = np.nan
+    world = 8
+    idx = [udist.spatial_shard(pr, r, world)[1] for r in range(world)]
+    allidx = np.concatenate(idx)
+    assert len(allidx) == len(pr) and len(np.unique(allidx)) == len(pr)
+    assert max(map(len, idx)) - min(map(len, idx)) <= 1
+    assert 5 in idx[-1]
+    mid = 0.5 * (pr[:, :2] + pr[:, 2:4])
+    whole = np.nanmax(mid, 0) - np.nanmin(mid, 0)
+    for r in range(world - 1):
+        m = mid[idx[r]]
+        box = m.max(0) - m.min(0)
+        assert (box[0] * box[1]) < 0.5 * whole[0] * whole[1]
+    p6 = np.concatenate([pr[:, :2], np.zeros((len(pr), 1)), pr[:, 2:4], np.ones((len(pr), 1))], 1)
+    np.testing.assert_array_equal(udist.spatial_shard(p6, 2, world)[1], idx[2])
+    sh, ix = udist.spatial_shard(pr, 1, world)
+    np.testing.assert_array_equal(sh, pr[ix])

@@ -86,7 +86,7 @@ def test_k4h_vs_oracle(oracle_mod, R, nz, group, terrain):
     from uam_path_planning_amd.scenario import displacements
 
     e, orc, vol, vd, host = _case(oracle_mod, R, nz, 80, group)
-    e.set_option("k2h_terrain", terrain)  # 1 (default): the terrain in the entry; 0: bounds
+    e.set_option("k4h_terrain", terrain)  # 0 (default): bounds; 1: the terrain in the entry
     D = 5
     ut = arc_table(80, displacements(D))
     pairs = _pairs3d(3000, 17)
@@ -114,7 +114,7 @@ def test_k4h_chunks(oracle_mod, chunk, floor, terrain):
     e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21, maxalpha=0.015)
     e.set_option("k2g_chunk", chunk)
     e.set_option("k2g_lds_floor", floor)
-    e.set_option("k2h_terrain", terrain)
+    e.set_option("k4h_terrain", terrain)
     D = 5
     ut = arc_table(80, displacements(D))
     pairs = _pairs3d(2000, 23)

@@ -23,7 +23,7 @@ OPTIONS = {"group": 1, "sorted_min_paths": 2, "k2s_segments": 3, "wave_max_paths
            "pair_order": 5, "k1_rows": 6, "k3b_segment": 7, "k3b_points_per_lane": 8,
            "k8_tiled": 9, "k8_streams": 10, "k2g_tile_bits": 11, "k2g_lds_floor": 12,
            "k2g_chunk": 13, "k2g_curve": 14, "k2g_sim": 15, "k4h_band": 17,
-           "k2h_lb_stride": 19, "k2h_terrain": 20}
+           "k2h_lb_stride": 19, "k2h_terrain": 20, "k4h_terrain": 21}
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
 MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
 FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4

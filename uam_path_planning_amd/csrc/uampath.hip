@@ -6083,26 +6083,35 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
 // profiles/r04/final2/cells.)
 __global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
                                                int32_t* __restrict__ cells) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // workgroup = 64 consecutive paths, their 64 W cells contiguous in cells
     const int W = kg.W, N = p.N;
-    if (i >= (int64_t)kg.P * W) return;
-    const int32_t path = (int32_t)(i / W);
-    const int j = (int)(i - (int64_t)path * W);
-    const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-    const int32_t d = path - q * kg.D;
-    const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-    const double2 u = reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(j - 1, 0), N - 1)];
-    const double vx = pr.x - pr.z, vy = pr.y - pr.w;
-    const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
-    double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
-    double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-    x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
-    x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
-    int32_t ix, iy;
-    const bool in = gen_cell(rs, x0, x1, ix, iy);
-    // plain stores: a wave writes 256 contiguous bytes, whole lines the L2 writes back once
-    // (streaming stores of such runs measured ~3.7x slower, tools/write_runs.hip)
-    cells[i] = in ? iy * rs.nx + ix : -1;
+    const int64_t path0 = (int64_t)blockIdx.x * 64;
+    const int np = (int)min((int64_t)64, (int64_t)kg.P - path0);
+    int32_t* out = cells + path0 * W;
+    for (int i = threadIdx.x; i < np * W; i += 256) {
+        const int lp = i / W, j = i - lp * W;  // (32-bit: np W < 2^13)
+        const int32_t path = (int32_t)(path0 + lp);
+        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+        const int32_t d = path - q * kg.D;
+        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+        const double2 u =
+            reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(j - 1, 0), N - 1)];
+        const double vx = pr.x - pr.z, vy = pr.y - pr.w;
+        const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
+        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
+        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
+        x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
+        x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
+        int32_t ix, iy;
+        const bool in = gen_cell(rs, x0, x1, ix, iy);
+        // plain stores: a wave writes 256 contiguous bytes, whole lines the L2 writes back once
+        // (streaming stores of such runs measured ~3.7x slower, tools/write_runs.hip)
+#ifdef UAM_CELLS_NT  // (measurement builds)
+        __builtin_nontemporal_store(in ? iy * rs.nx + ix : -1, out + i);
+#else
+        out[i] = in ? iy * rs.nx + ix : -1;
+#endif
+    }
 }
 
 // outputs of every path (block = 64 pairs x D, k_g_final's layout): the geometry terms from
@@ -6879,6 +6888,7 @@ struct uam_ctx {
     int k4h_band = 0;           // K4h sort key: layers per altitude band (UAM_OPT_K4H_BAND;
                                 // 0 = the fewest giving <= 16 bands)
     int k2h_te = 1;             // K2h: terrain in the entry (UAM_OPT_K2H_TERRAIN)
+    int k4h_te = 0;             // K4h: likewise (UAM_OPT_K4H_TERRAIN)
     int k2h_lbs = 8;            // K2h: the path lower bound's sample stride (UAM_OPT_K2H_LB_STRIDE;
                                 // tools/sim_terrain_bound.py at cfg3: fetches per waypoint 0.17
                                 // at 8, 0.15 at 4, 0.37 without the path bound)
@@ -7595,10 +7605,11 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
             ctx->k4h_band = (int)value;
             return UAM_OK;
         case UAM_OPT_K2H_TERRAIN:
+        case UAM_OPT_K4H_TERRAIN:
             if (value != 0 && value != 1)
-                return fail(UAM_E_INVALID, "UAM_OPT_K2H_TERRAIN %lld is not 0 or 1",
-                            (long long)value);
-            ctx->k2h_te = (int)value;
+                return fail(UAM_E_INVALID, "UAM_OPT_K%cH_TERRAIN %lld is not 0 or 1",
+                            option == UAM_OPT_K2H_TERRAIN ? '2' : '4', (long long)value);
+            (option == UAM_OPT_K2H_TERRAIN ? ctx->k2h_te : ctx->k4h_te) = (int)value;
             return UAM_OK;
         case UAM_OPT_K2H_LB_STRIDE:
             if (value < 0 || value > 1024)
@@ -7641,6 +7652,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2G_SIM: *value = ctx->k2g_sim; return UAM_OK;
         case UAM_OPT_K2H_LB_STRIDE: *value = ctx->k2h_lbs; return UAM_OK;
         case UAM_OPT_K2H_TERRAIN: *value = ctx->k2h_te; return UAM_OK;
+        case UAM_OPT_K4H_TERRAIN: *value = ctx->k4h_te; return UAM_OK;
         case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
@@ -8084,7 +8096,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
                            ctx->kp, kr, kg, (const uint4*)rec);
     if (ko.cells)
-        hipLaunchKernelGGL(k_cells, dim3((unsigned)((P * W + 255) / 256)), dim3(256), 0, s,
+        hipLaunchKernelGGL(k_cells, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, s,
                            ctx->kp, kr, kg, ko.cells);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
@@ -8114,15 +8126,15 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     if (P < ctx->k2s_min || n_pairs > INT32_MAX / D) return 0;
     if ((size_t)D * ctx->kp.N * 16 > (size_t)G_UTAB_LDS) return 0;
     if ((size_t)kv.hwords * 4 > (size_t)VPK_HDR_LDS) return 0;
-    // workgroups per CU: 2 by default through an LDS floor of 60 000 B (UAM_OPT_K2G_LDS_FLOOR
-    // sets another): fewer items resident per XCD, so fewer of their lines miss L2 -- cfg5
-    // 0.415 ms at 2 with 11 gathers in flight, 0.418 at 3, 0.453 at the 6 the LDS allows with 6
-    // (profiles/r04/sweep7)
+    // workgroups per CU: 3 by default through an LDS floor of 40 000 B (UAM_OPT_K2G_LDS_FLOOR
+    // sets another): fewer items resident per XCD, so fewer of their lines miss L2 -- round 5's
+    // bound form, cfg5: 0.394 ms at 3 with 7 in flight, 0.397 at 5 (28 000 B), 0.428 at 2
+    // (60 000 B), 0.448 at 2 with 11 (profiles/r05/k4h2, cc)
     const int64_t npad = G + 16;  // k_v_eval's padding slots
     const size_t lds = std::max((size_t)(D * ctx->kp.N + npad) * 16 +
                                     (size_t)((W + npad + 1) & ~1) * 8 +
-                                    (size_t)(ctx->k2h_te ? kv.bnd_off : kv.hwords) * 4,
-                                (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 60000, 160 * 1024));
+                                    (size_t)(ctx->k4h_te ? kv.bnd_off : kv.hwords) * 4,
+                                (size_t)std::min(ctx->k2g_lds ? ctx->k2g_lds : 40000, 160 * 1024));
     const int nseg = (int)((W + G - 1) / G);
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
@@ -8178,7 +8190,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
-    kg.ubp = ctx->k2h_lbs > 0 && !ctx->k2h_te ? (double*)(w + o) : nullptr, o += b_ubp;
+    kg.ubp = ctx->k2h_lbs > 0 && !ctx->k4h_te ? (double*)(w + o) : nullptr, o += b_ubp;
     const size_t hist_dyn = (size_t)kv.hwords * 4 + (size_t)D * ctx->kp.N * 16;
     kg.seed_lds = kg.ubp && hist_dyn <= (size_t)G_HIST_DYN_MAX;
     kg.key = (uint16_t*)(w + o);
@@ -8199,9 +8211,9 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
     const dim3 ge((unsigned)((n_items + 255) / 256));
     using VEvalFn = void (*)(KParams, KVol4, KGrp);
-    // gathers in flight per lane: 11 by default (k_v_eval<8> spills at 4 waves per SIMD, so 8 and
-    // 11 are built for 3, 16 and 21 for 2)
-    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 11;
+    // gathers in flight per lane: 7 by default (the bound form at 3 workgroups per CU; 8 and 11
+    // are built for 3 / 2 waves per SIMD)
+    const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : 7;
     // (21 runs as 16: a chunk's per-slot codes take 4 bits each of 64)
     static const VEvalFn vevals[10] = {k_v_eval<6, false>, k_v_eval<7, false>,
                                        k_v_eval<8, false>,  k_v_eval<11, false>,
@@ -8209,7 +8221,7 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
                                        k_v_eval<7, true>,   k_v_eval<8, true>,
                                        k_v_eval<11, true>,  k_v_eval<16, true>};
     const VEvalFn ev = vevals[(chl <= 6 ? 0 : chl == 7 ? 1 : chl <= 8 ? 2 : chl == 11 ? 3 : 4) +
-                              (ctx->k2h_te ? 5 : 0)];
+                              (ctx->k4h_te ? 5 : 0)];
     if (lds > 64 * 1024 && !ctx->k4h_attrs) {
         for (VEvalFn f : vevals)
             HIP_TRY(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -29,6 +29,54 @@ def shard_range(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
+def hilbert_keys(x, y, bits=10):
+    """Hilbert-curve index of points (x, y) on a 2^bits x 2^bits grid over their bounding box
+    (host numpy; NaN coordinates sort last)."""
+    import numpy as np
+
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    ok = np.isfinite(x) & np.isfinite(y)
+    n = 1 << bits
+    if ok.any():
+        x0, x1, y0, y1 = x[ok].min(), x[ok].max(), y[ok].min(), y[ok].max()
+    else:
+        x0 = x1 = y0 = y1 = 0.0
+    sx = (n - 1) / (x1 - x0) if x1 > x0 else 0.0
+    sy = (n - 1) / (y1 - y0) if y1 > y0 else 0.0
+    xi = np.where(ok, np.clip((x - x0) * sx, 0, n - 1), 0).astype(np.int64)
+    yi = np.where(ok, np.clip((y - y0) * sy, 0, n - 1), 0).astype(np.int64)
+    d = np.zeros(len(x), np.int64)
+    s = n >> 1
+    while s > 0:  # the classic xy -> d walk, vectorised
+        rx = (xi & s) > 0
+        ry = (yi & s) > 0
+        d += s * s * ((3 * rx) ^ ry)
+        flip = ~ry
+        swap_x = np.where(flip & rx, s - 1 - xi, xi)
+        swap_y = np.where(flip & rx, s - 1 - yi, yi)
+        xi, yi = np.where(flip, swap_y, xi), np.where(flip, swap_x, yi)
+        s >>= 1
+    return np.where(ok, d, np.int64(1) << (2 * bits))
+
+
+def spatial_shard(global_pairs, rank, world, bits=10):
+    """Strong scaling by space: the pairs in the order of their midpoints on a Hilbert curve,
+    cut into world contiguous shards (sizes differ by <= 1), so a rank's paths cover a compact
+    part of the raster and its sorted evaluation keeps the single-GPU problem's density of
+    paths per raster line.  Returns (this rank's pairs, their indices in global_pairs)."""
+    import numpy as np
+
+    pr = np.asarray(global_pairs)
+    ex = 3 if pr.shape[1] == 6 else 2  # (pairs3d: x0 y0 z0 xf yf zf)
+    mx = 0.5 * (pr[:, 0] + pr[:, ex])
+    my = 0.5 * (pr[:, 1] + pr[:, ex + 1])
+    order = np.argsort(hilbert_keys(mx, my, bits), kind="stable")
+    lo, hi = shard_range(len(pr), rank, world)
+    idx = order[lo:hi]
+    return pr[idx], idx
+
+
 def weak_shard(global_pairs, per_rank, rank, world):
     """Weak scaling: every rank owns per_rank consecutive pairs of one seeded global set."""
     if len(global_pairs) < per_rank * world:
