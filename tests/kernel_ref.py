@@ -5,7 +5,7 @@ other form -> the reference's sequential order (orc_eval_paths)."""
 
 
 def raster_ref(oracle_mod, orc, kernel, group, pairs, ut, rd, rec, want_cells=False):
-    if kernel == "K2h+pack":
+    if kernel.startswith("K2h"):
         return orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=group,
                                     want_cells=want_cells)
     return orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd, rec=rec,

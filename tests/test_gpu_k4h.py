@@ -262,3 +262,25 @@ def test_k4h_layer_varying_psi(oracle_mod, group):
     gpu = e.eval_generated3d(pairs, ut, vol)
     assert e.last_kernel() == "K4h+pack"
     _check(gpu, ref, oracle_mod, D)
+
+
+def test_k4h_stale_pack_rebuilt(oracle_mod):
+    """Voxels written in place after volume_pack (no explicit repack): eval_generated3d sees
+    the buffer's version change and rebuilds the packed copy, so K4h evaluates the new voxels
+    (every output equals orc_eval_generated_h on them)."""
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21, maxalpha=0.015)
+    old = vol.packed
+    vol.vox[::7, 3::11, :, 0] = int(np.float32(2.5).view(np.int32))   # risk, every layer
+    vol.vox[::13, 5::37, 3, 1] = int(np.float32(0.25).view(np.int32))
+    torch.cuda.synchronize()
+    host = (vol.vox.cpu().numpy().view(np.float32), vol.cols.cpu().numpy().view(np.float32))
+    D = 5
+    ut = arc_table(80, displacements(D))
+    pairs = _pairs3d(2000, 31)
+    ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=21)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack" and vol.packed is not old
+    _check(gpu, ref, oracle_mod, D)

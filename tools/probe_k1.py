@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--cases", default="cfg3,cfg3-obstacles,canonical,regions,obstacles,empty")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--cpl", type=int, default=0, help="k1_rows option (0: the default)")
     args = ap.parse_args()
     from uam_path_planning_amd.engine import Engine
     from uam_path_planning_amd.geometry import compile_map
@@ -42,6 +43,8 @@ def main():
 
     geo = raster_geo(args.R)
     eng = Engine(0)
+    if args.cpl:
+        eng.set_option("k1_rows", args.cpl)
     dem = eng.tensor(synthetic_dem(args.R), torch.float32)
     out = eng.empty((geo.ny, geo.nx, 4), torch.int32)
     for case in args.cases.split(","):
@@ -59,9 +62,11 @@ def main():
             print(json.dumps({"probe": "k1", "case": case, "error": repr(e)}), flush=True)
             continue
         eng.set_params(canonical_params(spec, N=80, altitude=320.0))
-        ms = timed(lambda: eng.raster_build(geo, dem, out=out), reps=args.reps)
+        # K1 alone (no gather-skip summary, no packed copy)
+        ms = timed(lambda: eng.raster_build(geo, dem, out=out, summary=False), reps=args.reps)
         cells = geo.nx * geo.ny
-        print(json.dumps({"probe": "k1", "case": case, "R": args.R, "ms": round(ms, 4),
+        print(json.dumps({"probe": "k1", "case": case, "R": args.R, "cpl": args.cpl,
+                          "ms": round(ms, 4),
                           "cells_per_s": round(cells / (ms * 1e-3), 1),
                           "GBps_algorithmic": round(cells * 20 / (ms * 1e-3) / 1e9, 1)}),
               flush=True)

@@ -735,15 +735,6 @@ __device__ __forceinline__ void pk_bound_decode(uint32_t e, float2 sb, float& ub
     lb = fmaf((float)(e >> 8), sb.y, sb.x);
 }
 
-// the decoded bounds of cell (ix, iy) from a header copy (LDS or global)
-__device__ __forceinline__ void pk_bounds(const KRaster& rs, const uint32_t* __restrict__ hdr,
-                                          int32_t ix, int32_t iy, float& ub, float& lb) {
-    uint32_t e;
-    float2 sb;
-    pk_bound_raw(rs, hdr, ix, iy, e, sb);
-    pk_bound_decode(e, sb, ub, lb);
-}
-
 // the raster cell of a generated point (arc_point's or the pair's coordinates; uampath.h's float64
 // floor): false off the raster or NaN, with (ix, iy) = (0, 0) then (a valid header index)
 __device__ __forceinline__ bool gen_cell(const KRaster& rs, double x0, double x1, int32_t& ix,
@@ -5785,7 +5776,7 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // The terrain maximum by bounds (build-defined; the outputs are exactly the per-waypoint
 // maximum's): min_clearance needs only the path's maximum terrain M, an order-free maximum, so
 // a waypoint's exact terrain is fetched (t4) only when it could still be M.  Every in-raster
-// waypoint w has decoded bounds lb_w <= terrain_w <= ub_w (pk_bounds, from LDS).  The item keeps
+// waypoint w has decoded bounds lb_w <= terrain_w <= ub_w (pk_bound_raw + pk_bound_decode).  The item keeps
 //   Lb: a lower bound of M: the path's seed (below), raised by its own waypoints' lb as it
 //       goes; off-raster waypoints count +0.0, their exact value;
 //   E:  the maximum of exact terrain values of the path: the seed E0 (h_path_seed, formed once
@@ -6083,34 +6074,73 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
 // profiles/r04/final2/cells.)
 __global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
                                                int32_t* __restrict__ cells) {
-    // workgroup = 64 consecutive paths, their 64 W cells contiguous in cells
-    const int W = kg.W, N = p.N;
+    // workgroup = 64 consecutive paths, their 64 W cells contiguous in cells; each lane forms
+    // 4 consecutive cells and writes them as one 16-B store (a wave: 1 KiB contiguous)
+    constexpr int kUtabLds = 1024;  // unit-arc entries staged in LDS (D N <= 1024: 16 KiB)
+    __shared__ double4 s_pr[64];    // the path's pair (x0, y0, xf, yf)
+    __shared__ double4 s_cv[64];    // its centre and chord (cx, cy, vx, vy): arc_point's terms
+    __shared__ int32_t s_d[64];
+    __shared__ double2 s_u[kUtabLds];
+    const int W = kg.W, N = p.N, t = threadIdx.x;
     const int64_t path0 = (int64_t)blockIdx.x * 64;
     const int np = (int)min((int64_t)64, (int64_t)kg.P - path0);
-    int32_t* out = cells + path0 * W;
-    for (int i = threadIdx.x; i < np * W; i += 256) {
-        const int lp = i / W, j = i - lp * W;  // (32-bit: np W < 2^13)
-        const int32_t path = (int32_t)(path0 + lp);
+    const int nu = kg.D * N;
+    const bool ulds = nu <= kUtabLds;
+    const double2* __restrict__ gu = reinterpret_cast<const double2*>(kg.utab);
+    if (t < np) {
+        const int32_t path = (int32_t)(path0 + t);
         const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-        const int32_t d = path - q * kg.D;
         const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-        const double2 u =
-            reinterpret_cast<const double2*>(kg.utab)[d * N + min(max(j - 1, 0), N - 1)];
-        const double vx = pr.x - pr.z, vy = pr.y - pr.w;
-        const double cx = (pr.z + pr.x) * 0.5, cy = (pr.w + pr.y) * 0.5;
-        double x0 = cx + 0.5 * (vx * u.x - vy * u.y);  // arc_point's operations
-        double x1 = cy + 0.5 * (vy * u.x + vx * u.y);
-        x0 = j == 0 ? pr.x : j == W - 1 ? pr.z : x0;
-        x1 = j == 0 ? pr.y : j == W - 1 ? pr.w : x1;
-        int32_t ix, iy;
-        const bool in = gen_cell(rs, x0, x1, ix, iy);
-        // plain stores: a wave writes 256 contiguous bytes, whole lines the L2 writes back once
-        // (streaming stores of such runs measured ~3.7x slower, tools/write_runs.hip)
+        s_pr[t] = pr;
+        s_cv[t] = make_double4((pr.z + pr.x) * 0.5, (pr.w + pr.y) * 0.5, pr.x - pr.z,
+                               pr.y - pr.w);
+        s_d[t] = path - q * kg.D;
+    }
+    if (ulds)
+        for (int k = t; k < nu; k += 256) s_u[k] = gu[k];
+    __syncthreads();
+    const double2* __restrict__ ut = ulds ? s_u : gu;
+    int32_t* out = cells + path0 * W;
+    const int total = np * W;  // (32-bit: 64 W < 2^13)
+    // (lp, j) of the lane's first cell 4t, then advanced by 1024 cells a step (step < W after
+    // the whole paths are taken out, so one conditional subtraction)
+    int lp = (4 * t) / W, j = 4 * t - lp * W;
+    const int lstep = 1024 / W, jstep = 1024 - lstep * W;
+    for (int i = 4 * t; i < total; i += 1024) {
+        int32_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            int jj = j + c, l = lp;
+            if (jj >= W) jj -= W, ++l;  // (W >= 3: one wrap at most)
+            l = min(l, np - 1);         // (a tail cell past the block: computed, not stored)
+            const double4 pr = s_pr[l];
+            const double4 cv = s_cv[l];
+            const double2 u = ut[s_d[l] * N + min(max(jj - 1, 0), N - 1)];
+            double x0 = cv.x + 0.5 * (cv.z * u.x - cv.w * u.y);  // arc_point's operations
+            double x1 = cv.y + 0.5 * (cv.w * u.x + cv.z * u.y);
+            x0 = jj == 0 ? pr.x : jj == W - 1 ? pr.z : x0;
+            x1 = jj == 0 ? pr.y : jj == W - 1 ? pr.w : x1;
+            int32_t ix, iy;
+            const bool in = gen_cell(rs, x0, x1, ix, iy);
+            v[c] = in ? iy * rs.nx + ix : -1;
+        }
+        // plain stores: whole lines the L2 writes back once (streaming stores of such runs
+        // measured ~3.7x slower, tools/write_runs.hip)
+        if (i + 3 < total) {
 #ifdef UAM_CELLS_NT  // (measurement builds)
-        __builtin_nontemporal_store(in ? iy * rs.nx + ix : -1, out + i);
+            typedef int32_t v4i __attribute__((ext_vector_type(4)));
+            const v4i w = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(w, reinterpret_cast<v4i*>(out + i));
 #else
-        out[i] = in ? iy * rs.nx + ix : -1;
+            *reinterpret_cast<int4*>(out + i) = make_int4(v[0], v[1], v[2], v[3]);
 #endif
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (i + c < total) out[i + c] = v[c];
+        }
+        lp += lstep, j += jstep;
+        if (j >= W) j -= W, ++lp;
     }
 }
 
@@ -7139,7 +7169,45 @@ int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
 // 1 = obstacles by box_obs for psi (SHAPE_CULL_PSI), 2 = obstacles by box_obs for contains
 // (SHAPE_CULL_HIT); a shape without its cull flag is listed in every cell and in the off-grid
 // slot.  The grid spans the union of the flagged boxes.
-static constexpr int kShapeGridN = 64;
+#ifndef UAM_SHAPE_GRID_N
+#define UAM_SHAPE_GRID_N 64  // (a build knob for measurement)
+#endif
+static constexpr int kShapeGridN = UAM_SHAPE_GRID_N;
+#ifndef UAM_GRID_REFINE
+#define UAM_GRID_REFINE 1  // measurement switch: 0 lists every cell a shape's box meets
+#endif
+
+// true when inequality q's h exceeds thr over the whole rectangle [rx0, rx1] x [ry0, ry1] by a
+// margin far above any evaluation's rounding (h affine in a half-plane or square side: its
+// minimum is at a corner; an ellipse's at the rectangle's point nearest its centre), so every
+// point a kernel places there computes h > thr: the shape's psi has a zero factor (h >= e in
+// the smooth forms) and contains() is false (h > 1e-14)
+static bool ineq_above(const DevIneq& q, double rx0, double rx1, double ry0, double ry1,
+                       double thr) {
+    const double* p = q.p;
+    double hmin, mag;
+    if (q.kind == UAM_INEQ_HALFPLANE) {
+        auto h = [&](double x, double y) { return p[4] * (p[3] * (x - p[0]) - p[2] * (y - p[1])); };
+        hmin = std::min(std::min(h(rx0, ry0), h(rx0, ry1)), std::min(h(rx1, ry0), h(rx1, ry1)));
+        mag = std::fabs(p[4]) * (std::fabs(p[3]) * (std::max(std::fabs(rx0), std::fabs(rx1)) +
+                                                    std::fabs(p[0])) +
+                                 std::fabs(p[2]) * (std::max(std::fabs(ry0), std::fabs(ry1)) +
+                                                    std::fabs(p[1])));
+    } else if (q.kind == UAM_INEQ_ELLIPSE) {
+        const double xs = std::min(std::max(p[0], rx0), rx1), ys = std::min(std::max(p[1], ry0), ry1);
+        const double a = (xs - p[0]) / p[2], b = (ys - p[1]) / p[3];
+        hmin = a * a + b * b - 1.0;
+        mag = a * a + b * b + 1.0;
+    } else {
+        const bool onx = p[0] == 0.0;
+        const double v0 = onx ? rx0 : ry0, v1 = onx ? rx1 : ry1;
+        hmin = std::min(p[3] * (v0 - p[1]) - p[2], p[3] * (v1 - p[1]) - p[2]);
+        mag = std::fabs(p[3]) * (std::max(std::fabs(v0), std::fabs(v1)) + std::fabs(p[1])) +
+              std::fabs(p[2]);
+    }
+    const double need = thr + 1e-9 * (mag + std::fabs(thr)) + 1e-300;
+    return std::isfinite(hmin) && std::isfinite(mag) && hmin > need;
+}
 
 static int build_shape_grid(uam_ctx* ctx) {
     if (ctx->d_grid) (void)hipFree(ctx->d_grid);
@@ -7193,8 +7261,23 @@ static int build_shape_grid(uam_ctx* ctx) {
             if (b[1] < x0 || b[0] > x1 || b[3] < y0 || b[2] > y1) continue;
             const int cx0 = cell_of(b[0], x0, gr.inv_dx), cx1 = cell_of(b[1], x0, gr.inv_dx);
             const int cy0 = cell_of(b[2], y0, gr.inv_dy), cy1 = cell_of(b[3], y0, gr.inv_dy);
+            // a grid cell the shape's support misses entirely (one of its inequalities above
+            // the threshold over the whole cell, grown by a relative 1e-6 for the kernels'
+            // rounding of the slot index) does not list it: the per-point box test would have
+            // let its points through to an exact +0 (or a false contains)
+            const double thr = l == 0 ? ctx->kp.enlargement : l == 1 ? 0.0 : 1e-14;
+            const DevIneq* qi = ctx->h_ineq.data() + d.first;
+            const double cw = (x1 - x0) / G, chh = (y1 - y0) / G;
             for (int cy = cy0; cy <= cy1; ++cy)
-                for (int cx = cx0; cx <= cx1; ++cx) lists[cy * G + cx].push_back(sh);
+                for (int cx = cx0; cx <= cx1; ++cx) {
+                    const double rx0 = x0 + cx * cw - 1e-6 * cw, rx1 = x0 + (cx + 1) * cw + 1e-6 * cw;
+                    const double ry0 = y0 + cy * chh - 1e-6 * chh;
+                    const double ry1 = y0 + (cy + 1) * chh + 1e-6 * chh;
+                    bool out = false;
+                    for (int k = 0; UAM_GRID_REFINE && k < d.count && !out; ++k)
+                        out = ineq_above(qi[k], rx0, rx1, ry0, ry1, thr);
+                    if (!out) lists[cy * G + cx].push_back(sh);
+                }
         }
         offs[l][0] = all.size();
         int32_t run = 0;

@@ -120,8 +120,10 @@ class RiskVolume:
     cols: object = field(repr=False)    # [ny, nx, 2] int32 view: columns {terrain, flags}
     cbits: object = field(repr=False, default=None)  # int32 view: the column bitmap words
     # the packed copy K4h reads (Engine.volume_pack: 4-B / 8-B / 16-B voxel planes in 4 x 8-
-    # column blocks per layer, codes, terrain bounds), or None; rebuild it after buf changes
+    # column blocks per layer, codes, terrain bounds), or None; eval_generated3d rebuilds it
+    # when buf (or a view of it: vox, cols) was written in place since (torch's version counter)
     packed: object = field(repr=False, default=None)
+    packed_version: int = field(repr=False, default=-1)
 
 
 def _ptr(t):
@@ -450,6 +452,7 @@ class Engine:
                                             _ptr(volume.buf), _ptr(packed), self.stream),
                    "uam_volume_pack")
         volume.packed = packed
+        volume.packed_version = volume.buf._version
         return packed
 
     def eval_generated3d(self, pairs6, utab, volume, outputs=None):
@@ -467,6 +470,8 @@ class Engine:
         else:
             o, s = self._outputs(Q * D, self.params.N + 2, _lib.MODE_VOLUME, False, False,
                                  n_pairs=Q)
+        if volume.packed is not None and volume.buf._version != volume.packed_version:
+            self.volume_pack(volume)   # the voxels changed since the copy: K4h reads only it
         _lib.check(self.lib.uam_eval_generated3d(
             self._ctx, ctypes.byref(volume.geo.as_struct()), _ptr(volume.buf),
             _ptr(volume.packed), _ptr(pr), Q, _ptr(ut), D, ctypes.byref(s), self.stream),
