@@ -6072,75 +6072,84 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
 // evaluation's lanes through LDS instead, the 21-cell runs of scattered items cost K2h ~120 us
 // of partial-line writes per cfg3 step: 402 MB of WRITE_SIZE for 164 MB of cells,
 // profiles/r04/final2/cells.)
+template <bool ULDS>  // the unit-arc rows staged in LDS (D N <= 1024) or read from global
 __global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
                                                int32_t* __restrict__ cells) {
     // workgroup = 64 consecutive paths, their 64 W cells contiguous in cells; each lane forms
-    // 4 consecutive cells and writes them as one 16-B store (a wave: 1 KiB contiguous)
-    constexpr int kUtabLds = 1024;  // unit-arc entries staged in LDS (D N <= 1024: 16 KiB)
-    __shared__ double4 s_pr[64];    // the path's pair (x0, y0, xf, yf)
-    __shared__ double4 s_cv[64];    // its centre and chord (cx, cy, vx, vy): arc_point's terms
-    __shared__ int32_t s_d[64];
-    __shared__ double2 s_u[kUtabLds];
+    // runs of 4 consecutive cells of one path and writes them by 8-B stores
+    constexpr int kUtabLds = 1024;  // (16 KiB)
+    __shared__ double4 s_cv[64];    // the path's centre and chord (cx, cy, vx, vy): arc_point's
+    __shared__ int4 s_e[64];        // {its unit-arc row offset d N, start cell, goal cell, 0}
+    __shared__ double2 s_u[ULDS ? kUtabLds : 1];
     const int W = kg.W, N = p.N, t = threadIdx.x;
-    const int64_t path0 = (int64_t)blockIdx.x * 64;
-    const int np = (int)min((int64_t)64, (int64_t)kg.P - path0);
-    const int nu = kg.D * N;
-    const bool ulds = nu <= kUtabLds;
     const double2* __restrict__ gu = reinterpret_cast<const double2*>(kg.utab);
-    if (t < np) {
-        const int32_t path = (int32_t)(path0 + t);
-        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-        s_pr[t] = pr;
-        s_cv[t] = make_double4((pr.z + pr.x) * 0.5, (pr.w + pr.y) * 0.5, pr.x - pr.z,
-                               pr.y - pr.w);
-        s_d[t] = path - q * kg.D;
-    }
-    if (ulds)
-        for (int k = t; k < nu; k += 256) s_u[k] = gu[k];
-    __syncthreads();
-    const double2* __restrict__ ut = ulds ? s_u : gu;
-    int32_t* out = cells + path0 * W;
-    const int total = np * W;  // (32-bit: 64 W < 2^13)
-    // (lp, j) of the lane's first cell 4t, then advanced by 1024 cells a step (step < W after
-    // the whole paths are taken out, so one conditional subtraction)
-    int lp = (4 * t) / W, j = 4 * t - lp * W;
-    const int lstep = 1024 / W, jstep = 1024 - lstep * W;
-    for (int i = 4 * t; i < total; i += 1024) {
-        int32_t v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            int jj = j + c, l = lp;
-            if (jj >= W) jj -= W, ++l;  // (W >= 3: one wrap at most)
-            l = min(l, np - 1);         // (a tail cell past the block: computed, not stored)
-            const double4 pr = s_pr[l];
-            const double4 cv = s_cv[l];
-            const double2 u = ut[s_d[l] * N + min(max(jj - 1, 0), N - 1)];
-            double x0 = cv.x + 0.5 * (cv.z * u.x - cv.w * u.y);  // arc_point's operations
-            double x1 = cv.y + 0.5 * (cv.w * u.x + cv.z * u.y);
-            x0 = jj == 0 ? pr.x : jj == W - 1 ? pr.z : x0;
-            x1 = jj == 0 ? pr.y : jj == W - 1 ? pr.w : x1;
-            int32_t ix, iy;
-            const bool in = gen_cell(rs, x0, x1, ix, iy);
-            v[c] = in ? iy * rs.nx + ix : -1;
+    if (ULDS)
+        for (int k = t; k < kg.D * N; k += 256) s_u[k] = gu[k];
+    const int64_t nblk = ((int64_t)kg.P + 63) / 64;
+    // (a grid smaller than nblk loops over the blocks: the side-stream launch's share of CUs)
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int64_t path0 = blk * 64;
+        const int np = (int)min((int64_t)64, (int64_t)kg.P - path0);
+        __syncthreads();  // (the previous block's reads of s_cv / s_e are done)
+        if (t < np) {
+            const int32_t path = (int32_t)(path0 + t);
+            const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+            const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+            s_cv[t] = make_double4((pr.z + pr.x) * 0.5, (pr.w + pr.y) * 0.5, pr.x - pr.z,
+                                   pr.y - pr.w);
+            int32_t ix, iy;  // the end points: the pair's own coordinates
+            const int32_t c0 = gen_cell(rs, pr.x, pr.y, ix, iy) ? iy * rs.nx + ix : -1;
+            const int32_t c1 = gen_cell(rs, pr.z, pr.w, ix, iy) ? iy * rs.nx + ix : -1;
+            s_e[t] = make_int4((path - q * kg.D) * N, c0, c1, 0);
         }
-        // plain stores: whole lines the L2 writes back once (streaming stores of such runs
-        // measured ~3.7x slower, tools/write_runs.hip)
-        if (i + 3 < total) {
-#ifdef UAM_CELLS_NT  // (measurement builds)
-            typedef int32_t v4i __attribute__((ext_vector_type(4)));
-            const v4i w = {v[0], v[1], v[2], v[3]};
-            __builtin_nontemporal_store(w, reinterpret_cast<v4i*>(out + i));
+        __syncthreads();
+        int32_t* out = cells + path0 * W;
+        // work item w = (path lp = w / R, run k = w % R): the run's 4 cells j = 4k ... 4k + 3
+        // of one path (R = ceil(W / 4) runs a path; cells past W are not stored), so a lane
+        // reads its path's terms once and selects nothing per cell; items advance by 256 a
+        // step (256 = lstep R + kstep, one conditional subtraction)
+        const int R = (W + 3) >> 2, items = np * R;
+        int lp = t / R, k = t - lp * R;
+        const int lstep = 256 / R, kstep = 256 - lstep * R;
+        for (int w = t; w < items; w += 256) {
+            const double4 cv = s_cv[lp];
+            const int4 e = s_e[lp];
+            const int j0 = 4 * k;
+            int32_t v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int jj = j0 + c;
+                const double2 u = ULDS ? s_u[e.x + min(max(jj - 1, 0), N - 1)]
+                                       : gu[e.x + min(max(jj - 1, 0), N - 1)];
+                const double x0 = cv.x + 0.5 * (cv.z * u.x - cv.w * u.y);  // arc_point's ops
+                const double x1 = cv.y + 0.5 * (cv.w * u.x + cv.z * u.y);
+                int32_t ix, iy;
+                const bool in = gen_cell(rs, x0, x1, ix, iy);
+                v[c] = jj == 0 ? e.y : jj == W - 1 ? e.z : in ? iy * rs.nx + ix : -1;
+            }
+            // streaming stores: the 164 MB of cfg3's cells do not stay in L2 / the Infinity
+            // Cache as dirty lines whose write-back the next step's gathers would meet (plain
+            // stores: cfg3 with cells 0.399 against 0.374 ms, profiles/r05/cc6); a wave's runs
+            // cover ~3 paths' contiguous rows
+            int32_t* o = out + (int64_t)lp * W + j0;
+            if (j0 + 3 < W && !(((uintptr_t)o) & 7)) {
+                typedef int32_t v2i __attribute__((ext_vector_type(2)));
+                const v2i w0 = {v[0], v[1]}, w1 = {v[2], v[3]};
+#ifndef UAM_CELLS_PLAIN  // (plain: a measurement build)
+                __builtin_nontemporal_store(w0, reinterpret_cast<v2i*>(o));
+                __builtin_nontemporal_store(w1, reinterpret_cast<v2i*>(o) + 1);
 #else
-            *reinterpret_cast<int4*>(out + i) = make_int4(v[0], v[1], v[2], v[3]);
+                reinterpret_cast<v2i*>(o)[0] = w0;
+                reinterpret_cast<v2i*>(o)[1] = w1;
 #endif
-        } else {
+            } else {
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (i + c < total) out[i + c] = v[c];
+                for (int c = 0; c < 4; ++c)
+                    if (j0 + c < W) o[c] = v[c];
+            }
+            lp += lstep, k += kstep;
+            if (k >= R) k -= R, ++lp;
         }
-        lp += lstep, j += jstep;
-        if (j >= W) j -= W, ++lp;
     }
 }
 
@@ -7760,6 +7769,15 @@ int uam_kernel_time(uam_ctx* ctx, double* ms_total, int64_t* launches) {
 // The pair-order scratch (ctx->d_ord, grow-only) on stream s: waits for the last launch that
 // read it (possibly on another stream), so two streams sharing a context cannot overwrite each
 // other's order; the caller records ctx->ev_ord after the launch that reads the order.
+// the context's side stream and its fork / join events (created on first use)
+static int side_stream(uam_ctx* ctx) {
+    if (ctx->s2) return UAM_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    return UAM_OK;
+}
+
 static int order_scratch(uam_ctx* ctx, size_t need, hipStream_t s, char** w) {
     if (!ctx->ev_ord) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_ord, hipEventDisableTiming));
     // another stream's launches that read the scratch must finish first (the caller's own
@@ -7909,11 +7927,8 @@ static int launch_segmented(uam_ctx* ctx, const KRaster& kr, const void* rec, co
                                         160 * 1024));
         ctx->k2s_attrs = true;
     }
-    if (!ctx->s2) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
+    st = side_stream(ctx);
+    if (st) return st;
     // kernel timing brackets the whole sequence (sorts included)
     st = ktime_begin(ctx, s);
     if (st) return st;
@@ -8162,8 +8177,46 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         }
     }
     kg.cells = ko.cells;
+    // the waypoint cells depend on the pairs and arc rows only: k_cells (VALU and store bound)
+    // runs on the side stream beside the sort and the gathers (miss bound), joined before the
+    // end of the call (UAM_CELLS_SIDE 0: after the evaluation on the caller's stream; 2: forked
+    // after the scatter, beside the evaluation only -- 0.363 ms, profiles/r05/cc9)
+#ifndef UAM_CELLS_SIDE
+#define UAM_CELLS_SIDE 1
+#endif
+    const bool cells_side = ko.cells && UAM_CELLS_SIDE;
+    if (cells_side) {
+        st = side_stream(ctx);
+        if (st) return st;
+    }
     st = ktime_begin(ctx, s);
     if (st) return st;
+#ifndef UAM_CELLS_GRID
+// workgroups of the cells launch, looping over the 64-path blocks (0: one per block).  On the
+// side stream a capped grid takes a share of the CUs beside the sort and the gathers instead
+// of holding them all first (cfg3 with cells: 0.357 ms at 256-512, 0.372 uncapped, 0.362
+// inline after the evaluation; profiles/r05/cc9, cc10)
+#define UAM_CELLS_GRID 512
+#endif
+    const unsigned cells_wg = (unsigned)std::min<int64_t>(
+        (P + 63) / 64, UAM_CELLS_GRID > 0 ? UAM_CELLS_GRID : INT32_MAX);
+#ifndef UAM_CELLS_ULDS
+#define UAM_CELLS_ULDS 1  // (0: the arc rows from global memory, 3 KiB of LDS per workgroup)
+#endif
+    void (*const cells_fn)(KParams, KRaster, KGrp, int32_t*) =
+        UAM_CELLS_ULDS && (int64_t)D * ctx->kp.N <= 1024 ? k_cells<true> : k_cells<false>;
+    auto fork_cells = [&]() -> int {
+        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
+        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, ctx->s2, ctx->kp, kr, kg,
+                           ko.cells);
+        HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+        return UAM_OK;
+    };
+    if (cells_side && UAM_CELLS_SIDE == 1) {
+        st = fork_cells();
+        if (st) return st;
+    }
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? hist_dyn : 0, s,
                        ctx->kp, kr, kg);
     hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
@@ -8172,15 +8225,18 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (!kg.nsb_raw)
         hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
     hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
+    if (cells_side && UAM_CELLS_SIDE == 2) {  // (beside the evaluation only)
+        st = fork_cells();
+        if (st) return st;
+    }
     if (hev)
         hipLaunchKernelGGL(hev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
                            ctx->kp, kr, kg);
     else
         hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
                            ctx->kp, kr, kg, (const uint4*)rec);
-    if (ko.cells)
-        hipLaunchKernelGGL(k_cells, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, s,
-                           ctx->kp, kr, kg, ko.cells);
+    if (ko.cells && !cells_side)
+        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, s, ctx->kp, kr, kg, ko.cells);
     // the output launch holds a path's slots in registers up to 8 groups
     using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
     const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
@@ -8188,6 +8244,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
     if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
+    if (cells_side) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
