@@ -2052,20 +2052,42 @@ __device__ __forceinline__ void wave_walk_obs_cells(const KGeom& g, const int (&
     wave_walk_cells<2, CPL>(g, slot, [&](int s, uint32_t m) { body(s, 0u, m); });
 }
 
+#ifndef UAM_K1_TILE_ROWS
+// raster rows per column of K1's strip order (0: row-major).  cfg3 map at 4096^2: row-major
+// 0.225 ms, columns of 16 / 32 / 64 / 128 / 256 / 512 / 4096 rows 0.196 / 0.196 / 0.195 /
+// 0.190 / 0.188 / 0.189 / 0.231 ms (the shape-free build 0.108 -> 0.118-0.130: the record
+// rows' DRAM pages); profiles/r05/cc13, cc14
+#define UAM_K1_TILE_ROWS 128
+#endif
 template <int CPL>
 __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
                                                             const float* __restrict__ dem,
                                                             float nodata, float thr,
                                                             uint4* __restrict__ rec) {
-    const int sxn = (rs.nx + 63) / 64;
-    const int64_t n_strips = (int64_t)sxn * ((rs.ny + CPL - 1) / CPL);
+    constexpr int K1_SPT = UAM_K1_TILE_ROWS / CPL;  // strips per column of the strip order
+    const int sxn = (rs.nx + 63) / 64, sny = (rs.ny + CPL - 1) / CPL;
     const int lane = threadIdx.x & 63;
-    const int64_t w0 = __builtin_amdgcn_readfirstlane(
-        (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    // strip order: row-major, or (K1_SPT > 0) down columns of K1_SPT strips so that a
+    // workgroup's waves and the workgroups an XCD runs in a row cover one 64-column tile of the
+    // shape grid (the same shape lists: scalar-cache hits), the 8 XCDs taking contiguous ranges
+    const int64_t n_virt = K1_SPT ? (int64_t)sxn * ((sny + K1_SPT - 1) / K1_SPT) * K1_SPT
+                                  : (int64_t)sxn * sny;
+    int64_t blk = blockIdx.x;
+    if (K1_SPT) blk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int64_t w0 = __builtin_amdgcn_readfirstlane((int)((blk * blockDim.x + threadIdx.x) >> 6));
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool pen_smooth = p.penalty_smooth != 0, obs_smooth = p.obstacle_smooth != 0;
-    for (int64_t st = w0; st < n_strips; st += nw) {  // wave-uniform strip index
-        const int sy = (int)(st / sxn), sx = (int)(st - (int64_t)sy * sxn);
+    for (int64_t st = w0; st < n_virt; st += nw) {  // wave-uniform strip index
+        int sy, sx;
+        if (K1_SPT) {
+            const int64_t tile = st / K1_SPT;
+            const int ty = (int)(tile / sxn);
+            sx = (int)(tile - (int64_t)ty * sxn);
+            sy = ty * K1_SPT + (int)(st - tile * K1_SPT);
+            if (sy >= sny) continue;  // (the last tile row's strips past the raster)
+        } else {
+            sy = (int)(st / sxn), sx = (int)(st - (int64_t)sy * sxn);
+        }
         const int ix = sx * 64 + lane;
         const double xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
         double yc[CPL];
@@ -7409,8 +7431,11 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     const hipStream_t s = (hipStream_t)stream;
     const int cpl = ctx->k1_cpl;  // cells (rows) per lane
-    const int64_t strips = (int64_t)((kr.nx + 63) / 64) * ((kr.ny + cpl - 1) / cpl);
-    const dim3 gs(grid_for(strips * 64, 256, 1 << 20));
+    const int sny = (kr.ny + cpl - 1) / cpl, spt = UAM_K1_TILE_ROWS / cpl;
+    const int64_t strips = (int64_t)((kr.nx + 63) / 64) *
+                           (spt > 0 ? (int64_t)((sny + spt - 1) / spt) * spt : sny);
+    // (the column order's XCD mapping wants a multiple of 8 workgroups)
+    const dim3 gs((grid_for(strips * 64, 256, 1 << 20) + 7) & ~7);
     switch (cpl) {
         case 1:  // the single-cell kernel
             hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0, s,
