@@ -2077,29 +2077,53 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
     const int64_t w0 = __builtin_amdgcn_readfirstlane((int)((blk * blockDim.x + threadIdx.x) >> 6));
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool pen_smooth = p.penalty_smooth != 0, obs_smooth = p.obstacle_smooth != 0;
-    for (int64_t st = w0; st < n_virt; st += nw) {  // wave-uniform strip index
-        int sy, sx;
+    // the strip's first row and column block (a strip of the last tile row past the raster
+    // gets rows >= ny: every cell invalid, nothing walked or stored)
+    auto strip_of = [&](int64_t st, int& sy, int& sx) {
         if (K1_SPT) {
             const int64_t tile = st / K1_SPT;
             const int ty = (int)(tile / sxn);
             sx = (int)(tile - (int64_t)ty * sxn);
             sy = ty * K1_SPT + (int)(st - tile * K1_SPT);
-            if (sy >= sny) continue;  // (the last tile row's strips past the raster)
         } else {
             sy = (int)(st / sxn), sx = (int)(st - (int64_t)sy * sxn);
+        }
+    };
+    auto load_z = [&](int sy, int sx, float (&zz)[CPL]) {
+        const int ix = sx * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int iy = sy * CPL + k;
+            zz[k] = (ix < rs.nx && iy < rs.ny && dem) ? dem[(int64_t)iy * rs.nx + ix] : 0.0f;
+        }
+    };
+    int sy = 0, sx = 0;
+    float z[CPL];
+    if (w0 < n_virt) {
+        strip_of(w0, sy, sx);
+        load_z(sy, sx, z);
+    }
+    for (int64_t st = w0; st < n_virt; st += nw) {  // wave-uniform strip index
+        // the next strip's DEM loads issued before this strip's walks (a grid smaller than
+        // the strip count: each wave loops)
+        int nsy = 0, nsx = 0;
+        float zn[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) zn[k] = 0.0f;
+        if (st + nw < n_virt) {
+            strip_of(st + nw, nsy, nsx);
+            load_z(nsy, nsx, zn);
         }
         const int ix = sx * 64 + lane;
         const double xc = rs.x0 + ((double)ix + 0.5) * rs.dx;
         double yc[CPL];
         int slot[CPL];
         bool valid[CPL];
-        float z[CPL];
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int iy = sy * CPL + k;
             valid[k] = ix < rs.nx && iy < rs.ny;
             yc[k] = rs.y_top - ((double)iy + 0.5) * rs.dy;
-            z[k] = (valid[k] && dem) ? dem[(int64_t)iy * rs.nx + ix] : 0.0f;
             slot[k] = valid[k] ? (g.grid.gx ? grid_slot(g.grid, xc, yc[k]) : -1) : -2;
         }
         // Φ: total_penalty's region loop, per cell
@@ -2207,6 +2231,9 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
                                __float_as_uint(z[k]), fl);
             }
         }
+        sy = nsy, sx = nsx;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) z[k] = zn[k];
     }
 }
 
@@ -7434,8 +7461,14 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
     const int sny = (kr.ny + cpl - 1) / cpl, spt = UAM_K1_TILE_ROWS / cpl;
     const int64_t strips = (int64_t)((kr.nx + 63) / 64) *
                            (spt > 0 ? (int64_t)((sny + spt - 1) / spt) * spt : sny);
-    // (the column order's XCD mapping wants a multiple of 8 workgroups)
-    const dim3 gs((grid_for(strips * 64, 256, 1 << 20) + 7) & ~7);
+    // (the column order's XCD mapping wants a multiple of 8 workgroups; a capped grid loops,
+    // each wave prefetching its next strip's DEM)
+#ifndef UAM_K1_GRID_CAP
+// cfg3 map at 4096^2 (32 768 strip workgroups): uncapped 0.185 ms, 16 384 0.179, 12 288
+// 0.197, 8192 0.176, 6144 0.205, 4096 0.193, 2048 0.254 (profiles/r05/cc15, cc16)
+#define UAM_K1_GRID_CAP 8192
+#endif
+    const dim3 gs((grid_for(strips * 64, 256, UAM_K1_GRID_CAP) + 7) & ~7);
     switch (cpl) {
         case 1:  // the single-cell kernel
             hipLaunchKernelGGL(k_raster_build, dim3(grid_for(cells, 256)), dim3(256), 0, s,
