@@ -5027,7 +5027,10 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
 constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles over the raster
 // tile bins twice over (a ragged last group's items have their own) + one for off-raster / NaN
 constexpr int G_BINS_MAX = (2 << (2 * G_TBITS_MAX)) + 1;
-constexpr int G_NBK = 256;                              // partitions of the counting sort
+#ifndef UAM_G_NBK
+#define UAM_G_NBK 256  // (a build knob for measurement)
+#endif
+constexpr int G_NBK = UAM_G_NBK;                        // partitions of the counting sort
 constexpr int G_HIST_DYN_MAX = 119 * 1024;  // k_g_hist's dynamic LDS (K2h seeds) beside its 40 KiB
 constexpr int G_MAXLEN = 64;                            // longest group
 constexpr int G_UTAB_LDS = 48 * 1024;                   // K2g: unit-arc table (in LDS) up to this
