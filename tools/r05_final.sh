@@ -2,7 +2,7 @@
 # GPU box, round 5 final: the whole GPU suite, smoke, the default bench and the other configs'
 # bench lines with the CPU baseline and parity, a kernel trace + PMC of the default bench.
 cd "$GRAFT_REPO_ROOT"
-o=r05/final
+o=r05/final2
 mkdir -p gpurun_out/$o
 export TMPDIR=/tmp
 tools/gpu_session.sh \
