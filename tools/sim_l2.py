@@ -126,12 +126,24 @@ def main():
           mid = (j0 + j1 - 1) // 2
           mx, my, mi = ix[items_p, mid], iy[items_p, mid], inr[items_p, mid]
           last = (items_s == nseg - 1) & (W % G != 0)
+          # the item's direction (its first to last waypoint) in 2^db bins, a minor key
+          ex, ey = ix[items_p, j1 - 1] - ix[items_p, j0], iy[items_p, j1 - 1] - iy[items_p, j0]
+          ang = (np.arctan2(ey, ex) + np.pi) / (2 * np.pi)
           for order in a.orders.split(","):
-              kind, tb = order[:-1], int(order[-1])
+              db = 0
+              if "d" in order:
+                  order_t, db = order.split("d")
+                  db = int(db)
+              else:
+                  order_t = order
+              kind, tb = order_t[:-1], int(order_t[-1])
               sh = int(np.log2(R)) - tb
               tx_, ty_ = mx >> sh, my >> sh
               k = hilbert_index(tb, tx_, ty_) if kind == "hilbert" else morton_index(tb, tx_, ty_)
               k = np.where(mi, k + (last << (2 * tb)), 1 << (2 * tb + 1))
+              if db:
+                  dirb = np.minimum((ang * (1 << db)).astype(np.int64), (1 << db) - 1)
+                  k = (k << db) | dirb
               perm = np.argsort(k, kind="stable")
               n = perm.size
               nb = (n + 255) // 256
