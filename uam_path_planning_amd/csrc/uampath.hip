@@ -6924,6 +6924,7 @@ struct uam_ctx {
     int k1_cpl = 2;             // K1 cells (rows) per lane: 1 = single-cell kernel, 2, 4, 8
                                 // (UAM_OPT_K1_ROWS)
     hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
+    hipStream_t s_lo = nullptr; // low-priority side stream (the waypoint cells beside K2h)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     // uam_load_tiles: two page-locked chunk buffers, each reused once its copy has completed
@@ -7135,6 +7136,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
         (void)hipEventDestroy(e.second);
     }
     if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
+    if (ctx->s_lo) (void)hipStreamDestroy(ctx->s_lo);
     for (hipStream_t k : ctx->k8s)
         if (k) (void)hipStreamDestroy(k);
     if (ctx->pinned) pinned_arena_free(ctx->pinned);
@@ -7839,6 +7841,17 @@ static int side_stream(uam_ctx* ctx) {
     return UAM_OK;
 }
 
+// the side stream at the device's lowest priority (created on first use; the fork / join
+// events are side_stream's)
+static int side_stream_lo(uam_ctx* ctx) {
+    int st = side_stream(ctx);
+    if (st || ctx->s_lo) return st;
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&ctx->s_lo, hipStreamNonBlocking, least));
+    return UAM_OK;
+}
+
 static int order_scratch(uam_ctx* ctx, size_t need, hipStream_t s, char** w) {
     if (!ctx->ev_ord) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_ord, hipEventDisableTiming));
     // another stream's launches that read the scratch must finish first (the caller's own
@@ -8246,10 +8259,17 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
 #define UAM_CELLS_SIDE 1
 #endif
     const bool cells_side = ko.cells && UAM_CELLS_SIDE;
+#ifndef UAM_CELLS_PRIO_LOW
+// the cells on a side stream of the device's lowest priority, so the sort's and the
+// evaluation's workgroups dispatch first and the cells fill what they leave (cfg3 with cells
+// 0.353 against 0.358 ms at normal priority; profiles/r05/cc20)
+#define UAM_CELLS_PRIO_LOW 1
+#endif
     if (cells_side) {
-        st = side_stream(ctx);
+        st = UAM_CELLS_PRIO_LOW ? side_stream_lo(ctx) : side_stream(ctx);
         if (st) return st;
     }
+    const hipStream_t s_cells = UAM_CELLS_PRIO_LOW ? ctx->s_lo : ctx->s2;
     st = ktime_begin(ctx, s);
     if (st) return st;
 #ifndef UAM_CELLS_GRID
@@ -8268,10 +8288,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         UAM_CELLS_ULDS && (int64_t)D * ctx->kp.N <= 1024 ? k_cells<true> : k_cells<false>;
     auto fork_cells = [&]() -> int {
         HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(ctx->s2, ctx->ev_fork, 0));
-        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, ctx->s2, ctx->kp, kr, kg,
+        HIP_TRY(hipStreamWaitEvent(s_cells, ctx->ev_fork, 0));
+        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, s_cells, ctx->kp, kr, kg,
                            ko.cells);
-        HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s2));
+        HIP_TRY(hipEventRecord(ctx->ev_join, s_cells));
         return UAM_OK;
     };
     if (cells_side && UAM_CELLS_SIDE == 1) {
