@@ -2,7 +2,7 @@
 # GPU box, round 5 final: the whole GPU suite, smoke, the default bench and the other configs'
 # bench lines with the CPU baseline and parity, a kernel trace + PMC of the default bench.
 cd "$GRAFT_REPO_ROOT"
-o=r05/final2
+o=r05/final3
 mkdir -p gpurun_out/$o
 export TMPDIR=/tmp
 tools/gpu_session.sh \
@@ -10,6 +10,7 @@ tools/gpu_session.sh \
   "300|$o/smoke|python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
   "300|$o/bench|python -u bench.py" \
   "300|$o/bench_cells|python -u bench.py --cells" \
+  "300|$o/prof_cells|PASSES='trace fetch write tcc sq' bash tools/profile_bench.sh gpurun_out/$o/cellsp --cells --steps 5 --warmup 1" \
   "300|$o/bench_cfg5|python -u bench.py --workload cfg5" \
   "400|$o/bench_cfg4|python -u bench.py --workload cfg4" \
   "300|$o/bench_cfg4_s3|python -u bench.py --workload cfg4 --share 3/8" \
