@@ -557,7 +557,7 @@ def gather_roofline(prof, P, W, kern_ms, kernel_name, packed=False, volume=False
          "gathers_per_s": round(P * W / (kern_ms * 1e-3), 1),
          "random_gather_ceiling_per_s": RANDOM_GATHER_CEILING,
          "record_source": record_source(volume, packed, terrain_entry),
-         "note": roofline_note(kernel_tag, prof, P, W, terrain_entry)}
+         "note": roofline_note(kernel_tag, prof, P, W, terrain_entry, cells)}
     return r
 
 
@@ -585,7 +585,7 @@ def record_source(volume, packed, terrain_entry):
             "maximum" + tail)
 
 
-def roofline_note(kernel, prof, P, W, terrain_entry=True):
+def roofline_note(kernel, prof, P, W, terrain_entry=True, cells=False):
     """What bounds the kernel that ran, from this build's own PMC key when there is one."""
     miss = prof.get("tcc_miss")
     hits = prof.get("tcc_hit")
@@ -600,8 +600,12 @@ def roofline_note(kernel, prof, P, W, terrain_entry=True):
                 "one 128-B line request per waypoint's packed entry (none in code-0 blocks) "
                 "plus one per terrain fetch (only where the waypoint's bound could still be the "
                 "path maximum)")
+        cells = (" The waypoint cells come from k_cells beside the evaluation (a lowest-"
+                 "priority side stream; runs of 4 cells per path by 8-B streaming stores)."
+                 if cells else "")
         return ("K2h: " + what + "; hits come from L2, misses from the Infinity Cache / HBM "
-                "at <= 55-59 G lines/s (tools/gather_ceiling.hip); DESIGN.md §4-5." + tail)
+                "at <= 55-59 G lines/s (tools/gather_ceiling.hip); DESIGN.md §4-5." + cells +
+                tail)
     if kernel.startswith("K4h"):
         return ("K4h: one 128-B line request per waypoint's packed voxel; misses from the "
                 "Infinity Cache / HBM at <= 55-59 G lines/s; DESIGN.md §4-5." + tail)
