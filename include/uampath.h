@@ -45,7 +45,9 @@
 extern "C" {
 #endif
 
-#define UAM_ABI_VERSION 1
+/* 2 (round 5): uam_eval_generated gained summary_dev / block / packed_dev and
+ * uam_eval_generated3d packed_dev, and the _s / _p entry points were folded into them */
+#define UAM_ABI_VERSION 2
 #define UAM_MAX_REGIONS 16
 #define UAM_RECORD_BYTES 16
 
@@ -55,7 +57,9 @@ enum {
     UAM_E_HIP = -2,     /* HIP runtime failure */
     UAM_E_NOMEM = -3,
     UAM_E_STATE = -4,   /* call order: e.g. eval before set_geometry / set_params */
-    UAM_E_VERSION = -5  /* abi_version field does not match UAM_ABI_VERSION */
+    UAM_E_VERSION = -5, /* abi_version field does not match UAM_ABI_VERSION */
+    UAM_E_DEVICE = -6   /* a device-side consistency check of an earlier call failed: that
+                           call's outputs were poisoned (uam_device_status) */
 };
 
 /* inequality kinds h(x) <= 0 (parameters p[0..5]) */
@@ -262,12 +266,15 @@ int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* re
  *   scratch the bound blocks' {min, max} (float2 each) while packing;
  *   planes  phi (4 B) and the terrain as read (4 B) in 4 x 8-cell blocks (one 128-B line),
  *           {phi, |psi_nfz| | nfz << 31} (8 B) in the same blocks (two 128-B lines) and the
- *           16-B records (four lines), at one index for all four.
+ *           16-B records (four lines), at one index for all four; then {phi, terrain} (8 B) in
+ *           4 x 4-cell blocks (one line; K2h's code-1 entry): 40 B per cell in all.
  * K2h reads a waypoint's terrain only where its bound could still be the path's maximum (the
  * maximum is order-free, so min_clearance is unchanged bit for bit); K2g and K2s read it for
- * every waypoint.  K2h addresses the copy by 32-bit offsets (it stands aside for a copy of
- * 4 GiB or more); packing needs nx, ny < 2^24.  uam_raster_pack_shape gives the bytes of the
- * caller's buffer (4096^2: 56 KiB of header + 128 KiB of scratch + 512 MiB of planes); block as
+ * every waypoint.  K2h addresses the copy by 32-bit offsets: for a copy of 4 GiB or more (about
+ * 10^4 x 10^4 cells) it stands aside and the batch runs K2g / K2s on the same copy (slower, same
+ * outputs in their documented sum order); packing needs nx, ny < 2^24.  uam_raster_pack_shape
+ * gives the bytes of the caller's buffer (4096^2: 640.2 MiB = 56 KiB of header + 128 KiB of
+ * scratch + 640 MiB of planes; 8192^2: 2.5 GiB); block as
  * uam_raster_summary
  * (0 = automatic), and the same block must be passed to uam_eval_generated.  Rebuild the copy
  * whenever rec changes. */
@@ -285,7 +292,17 @@ int uam_argmin(uam_ctx* ctx, const double* values_dev, int64_t groups, int32_t G
 int uam_path_length(uam_ctx* ctx, const double* pts_dev, int64_t n_paths, int32_t n_points,
                     int32_t n_segments, int32_t smooth, double* out_dev, uam_stream stream);
 
+/* Waits for stream, then reports uam_device_status (below). */
 int uam_synchronize(uam_ctx* ctx, uam_stream stream);
+/* Device-side errors.  The sorted forms (K2h / K2g / K4h) check on the device that their
+ * counting sort is consistent (every item lands on one position of the order).  A call whose
+ * check fails writes NaN to every floating-point output and -1 to every count and selection of
+ * the whole batch, and sets a word in page-locked host memory (no copy is issued otherwise).
+ * Once the failing call has completed on its stream, uam_device_status returns UAM_E_DEVICE
+ * with the text in uam_last_error() and clears the word; UAM_OK otherwise.  uam_synchronize
+ * and the next uam_eval_generated* call on ctx report it too (the reference's convention of
+ * raising on a failed solve, path_generation/solver.py:22-38, 53-55). */
+int uam_device_status(uam_ctx* ctx);
 
 /* Bytes of the volume buffer (256-B aligned sections) and the column plane's byte offset. */
 int uam_volume_shape(const uam_volume_desc* desc, int64_t* bytes, int64_t* col_offset);
@@ -317,13 +334,17 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* desc, const void* 
  *   4-B risk per voxel in 4 x 8-column blocks of one layer, layer-major (code 1; index i4);
  *   the 4-B column terrain (+0 on nodata) in the same blocks (one layer);
  *   8-B {risk, |psi_nfz| | nfz << 31} per voxel at i4 (code 2);
- *   16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} at i4 (code 3).
- * K4h addresses the copy by 32-bit offsets: it stands aside (the batch runs on vol_dev) for a
+ *   16-B voxels {float risk, float psi_nfz, float terrain, uint32 flags} in 4 x 2-column
+ *   blocks of one layer (one 128-B line; code 3);
+ *   8-B {risk, column terrain} voxels in 4 x 4-column blocks of one layer (the
+ *   UAM_OPT_K4H_TERRAIN = 1 form's entry): 36 B per voxel + 4 B per column in all.
+ * K4h addresses the copy by 32-bit offsets: it stands aside (the batch runs K4 on vol_dev) for a
  * copy of 4 GiB or more or a layer of 2^24 or more entries.
  * K4h reads a waypoint's terrain only where it could still decide min_clearance or
  * below_terrain (the outputs are unchanged bit for bit).  uam_volume_pack derives it from a
- * built volume (vol_dev); packed_dev holds uam_volume_packed_bytes bytes (1.75 GiB at
- * 1024^2 x 64), 256-B aligned. */
+ * built volume (vol_dev); packed_dev holds uam_volume_packed_bytes bytes (2.25 GiB at
+ * 1024^2 x 64), 256-B aligned.  The copy is not tracked: rebuild it (uam_volume_pack) after
+ * any write to vol_dev, including uam_volume_build into the same buffer and uam_bcast_raster. */
 int uam_volume_packed_bytes(const uam_volume_desc* desc, int64_t* bytes);
 int uam_volume_pack(uam_ctx* ctx, const uam_volume_desc* desc, const void* vol_dev,
                     void* packed_dev, uam_stream stream);
@@ -520,7 +541,9 @@ enum {
     UAM_OPT_K4H_BAND = 17,
     UAM_OPT_K2H_LB_STRIDE = 19,
     UAM_OPT_K2H_TERRAIN = 20,
-    UAM_OPT_K4H_TERRAIN = 21
+    UAM_OPT_K4H_TERRAIN = 21,
+    UAM_OPT_TEST_SORT_FAULT = 22  /* tests only: 1 makes the next sorted calls flag their sort as
+                                     inconsistent (the uam_device_status path); 0 (default) off */
 };
 int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value);
 int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value);

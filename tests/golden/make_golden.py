@@ -13,6 +13,8 @@ it on fixed inputs, and writes small fixtures next to this file:
                                      option combinations, random waypoints, random params
   arcs.npz                          -- Solver.create_x_init (solver.py:103-136) for several N, d
   grid.npz                          -- reference Φ / ψ at raster cell centres (raster mode pin)
+  waypoint_cells.npz                -- raster cells (4096^2, 8192^2) of Solver.create_x_init's
+                                     own waypoints for the first 2000 cfg3 pairs x 5 d, N=80
   errors.json                       -- reference exception types + messages for bad inputs
 
 Nothing here is copied reference source: the fixtures are inputs and the reference's outputs.
@@ -394,13 +396,69 @@ def gen_errors():
         json.dump(cases, f, indent=1)
 
 
+# cfg3's pairs (uam_path_planning_amd/synthetic.py random_pairs(100_000, seed=0): uniform in
+# the land bbox) and raster extent (x in [0, 60] km, y in [-40, 20] km)
+LAND_BBOX = (11.673387096774192, 46.75403225806451, -37.53246753246754, 19.204545454545457)
+
+
+def cfg3_pairs(Q_total=100_000, take=2000):
+    rng = np.random.default_rng(0)
+    x = rng.uniform(LAND_BBOX[0], LAND_BBOX[1], size=(Q_total, 2))
+    y = rng.uniform(LAND_BBOX[2], LAND_BBOX[3], size=(Q_total, 2))
+    return np.stack([x[:, 0], y[:, 0], x[:, 1], y[:, 1]], axis=1)[:take].astype(np.float64)
+
+
+def raster_cells(wp, R):
+    """The raster cell of every waypoint (include/uampath.h uam_raster_desc): ix =
+    floor((x - x0) * (1/dx)), iy = floor((y_top - y) * (1/dy)) in float64, ix = iy = -1 off
+    the raster; x0 = 0, y_top = 20, dx = dy = 60 / R.  Stored as int16 differences along each
+    path (the first waypoint's ix / iy as is), which compress: tests/golden_io.py
+    waypoint_cells() rebuilds iy * R + ix."""
+    inv = 1.0 / (60.0 / R)
+    fx = np.floor((wp[..., 0] - 0.0) * inv)
+    fy = np.floor((20.0 - wp[..., 1]) * inv)
+    ok = (fx >= 0) & (fx < R) & (fy >= 0) & (fy < R)
+    ix = np.where(ok, fx, -1.0).astype(np.int16)
+    iy = np.where(ok, fy, -1.0).astype(np.int16)
+    d = lambda a: np.concatenate([a[:, :1], np.diff(a, axis=1)], axis=1).astype(np.int16)
+    return d(ix), d(iy)
+
+
+def gen_waypoint_cells(take=2000, N=80):
+    """Verdict r5 item 1: the reference's own waypoints (create_x_init, solver.py:103-136, with
+    the pair's start and goal, main.py:160-171) as raster cells at 4096^2 and 8192^2, for the
+    first `take` pairs of cfg3 x the 5 displacements of main.py:160.  Paths are pair-major
+    (path = q * 5 + d), W = N + 2 cells each."""
+    pairs = cfg3_pairs(take=take)
+    m = RegionMap()
+    wp = np.empty((take * len(DISPLACEMENTS), N + 2, 2))
+    for q, pr in enumerate(pairs):
+        m.x_start, m.x_goal = [pr[0], pr[1]], [pr[2], pr[3]]
+        s = Solver(Problem(m, N), {})
+        for di, d in enumerate(DISPLACEMENTS):
+            x = np.asarray(s.create_x_init(d), dtype=np.float64).reshape(N, 2)
+            p = q * len(DISPLACEMENTS) + di
+            wp[p, 0] = pr[:2]
+            wp[p, 1:N + 1] = x
+            wp[p, N + 1] = pr[2:]
+    res = {"pairs": pairs, "displacements": np.asarray(DISPLACEMENTS), "N": np.asarray(N)}
+    for R in (4096, 8192):
+        res[f"dix{R}"], res[f"diy{R}"] = raster_cells(wp, R)
+    np.savez_compressed(os.path.join(HERE, "waypoint_cells.npz"), **res)
+    print(f"waypoint cells: {wp.shape[0]} paths x {N + 2}")
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF_PG):
         sys.exit("reference not mounted; golden fixtures are generated in the build container only")
+    if sys.argv[1:] == ["cells"]:   # round 6: only the waypoint-cell fixture
+        gen_waypoint_cells()
+        sys.exit(0)
     spec, _ = gen_canonical()
     gen_variants(spec)
     gen_random_cases()
     gen_arcs()
     gen_grid(spec)
     gen_errors()
+    gen_waypoint_cells()
     print("done")

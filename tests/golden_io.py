@@ -40,3 +40,16 @@ def grid():
 def errors():
     with open(os.path.join(GOLDEN, "errors.json")) as f:
         return {c["case"]: c for c in json.load(f)}
+
+
+def waypoint_cells():
+    """waypoint_cells.npz: pairs [Q, 4], displacements [D], N, and for R in (4096, 8192) the
+    raster cell (iy * R + ix, -1 off the raster) of every waypoint of Solver.create_x_init's
+    own paths, [Q * D, N + 2] int32 (stored as int16 differences of ix / iy along each path)."""
+    a = dict(np.load(os.path.join(GOLDEN, "waypoint_cells.npz")))
+    out = {"pairs": a["pairs"], "displacements": a["displacements"], "N": int(a["N"])}
+    for R in (4096, 8192):
+        ix = np.cumsum(a[f"dix{R}"].astype(np.int32), axis=1)
+        iy = np.cumsum(a[f"diy{R}"].astype(np.int32), axis=1)
+        out[f"cells{R}"] = np.where(ix >= 0, iy * R + ix, -1).astype(np.int32)
+    return out

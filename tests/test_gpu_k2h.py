@@ -442,3 +442,96 @@ def test_k2h_maxratio_smooth_runs_k2g(oracle_mod):
     _check(gpu, ref, oracle_mod, D)
     with pytest.raises(ValueError):
         orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=21)
+
+
+@pytest.mark.parametrize("sim", [1, 0])
+def test_sorted_device_check_surfaces(oracle_mod, sim):
+    """A failed sort check on the device (forced by the test-only UAM_OPT_TEST_SORT_FAULT)
+    poisons every output of the batch -- NaN in the f64 outputs, -1 in the counts and both
+    selections -- and surfaces on the host: Engine.synchronize (uam_synchronize) raises
+    DeviceCheckError once, and the next call runs clean (K2h and, with k2g_sim 0, K2g)."""
+    from uam_path_planning_amd import _lib
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 40)
+    e.set_option("k2g_sim", sim)
+    D = 5
+    ut = arc_table(40, displacements(D))
+    pairs = _pairs(1500, 51)
+    e.set_option("test_sort_fault", 1)
+    bad = e.eval_generated(pairs, ut, raster=raster)
+    assert e.last_kernel() == ("K2h+pack" if sim else "K2g+pack")
+    with pytest.raises(_lib.DeviceCheckError):
+        e.synchronize()
+    for k in ("cost", "length_q", "length", "kin_sum", "nfz_sum", "min_clearance"):
+        assert np.isnan(bad[k].cpu().numpy()).all(), k
+    for k in ("nfz_hits", "offmap", "best_fval_idx", "best_length_idx"):
+        assert (bad[k].cpu().numpy() == -1).all(), k
+    e.synchronize()   # reported once
+    e.set_option("test_sort_fault", 0)
+    gpu = e.eval_generated(pairs, ut, raster=raster)
+    e.synchronize()
+    if sim:
+        _check(gpu, orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=21), oracle_mod, D)
+    else:
+        _check(gpu, orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd,
+                                   rec=rec, group=21), oracle_mod, D)
+
+
+def test_device_check_reported_by_next_call(oracle_mod):
+    """Without a synchronize in between, the next uam_eval_generated on the context reports
+    the earlier call's failed check (once the failing call has completed)."""
+    from uam_path_planning_amd import _lib
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, raster, rd, rec = _case(oracle_mod, 21, 40)
+    ut = arc_table(40, displacements(5))
+    pairs = _pairs(800, 52)
+    e.set_option("test_sort_fault", 1)
+    e.eval_generated(pairs, ut, raster=raster)
+    torch.cuda.synchronize()
+    e.set_option("test_sort_fault", 0)
+    with pytest.raises(_lib.DeviceCheckError):
+        e.eval_generated(pairs, ut, raster=raster)
+    e.eval_generated(pairs, ut, raster=raster)
+    e.synchronize()
+
+
+@pytest.mark.parametrize("R", [4096, 8192])
+@pytest.mark.parametrize("sorted_min", [0, 65536])
+def test_k2h_cells_vs_create_x_init(oracle_mod, R, sorted_min):
+    """Verdict r5 item 1: the returned waypoint cells of eval_generated(want_cells=True) equal
+    the cells of the reference's own create_x_init waypoints (solver.py:103-136; fixture
+    tests/golden/waypoint_cells.npz, first 2000 cfg3 pairs x 5 d, N = 80) at 4096^2 and 8192^2:
+    0 mismatches over 820 000 waypoints, through K2h + k_cells (sorted_min 0) and through the
+    lane-per-path form the default picks for a batch this small."""
+    import golden_io as G
+    from uam_path_planning_amd import build
+    from uam_path_planning_amd.engine import Engine, PathParams
+    from uam_path_planning_amd.geometry import compile_map
+    from uam_path_planning_amd.scenario import build_region_map, canonical_spec, raster_geo
+    from uam_path_planning_amd.arcs import arc_table
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    build.build_library()
+    w = G.waypoint_cells()
+    e = Engine(0)
+    e.set_option("sorted_min_paths", sorted_min)
+    spec = canonical_spec(nfz_polygons=16)
+    e.set_geometry(compile_map(build_region_map(spec)))
+    e.set_params(PathParams(N=w["N"], **spec["options"], maxratio=spec["maxratio"],
+                            maxalpha=spec["maxalpha"], enlargement=spec["enlargement"],
+                            weights=tuple(spec["weights"]), altitude=320.0))
+    raster = e.raster_build(raster_geo(R), None)
+    g = e.eval_generated(w["pairs"], arc_table(w["N"], w["displacements"]), raster=raster,
+                         want_cells=True)
+    e.synchronize()
+    if sorted_min == 0:
+        assert e.last_kernel() == "K2h+pack"
+    cells = g["cells"].cpu().numpy().reshape(w[f"cells{R}"].shape)
+    assert int((cells != w[f"cells{R}"]).sum()) == 0
+    del raster
+    torch.cuda.empty_cache()

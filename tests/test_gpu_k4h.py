@@ -284,3 +284,29 @@ def test_k4h_stale_pack_rebuilt(oracle_mod):
     gpu = e.eval_generated3d(pairs, ut, vol)
     assert e.last_kernel() == "K4h+pack" and vol.packed is not old
     _check(gpu, ref, oracle_mod, D)
+
+
+def test_k4h_device_check_surfaces(oracle_mod):
+    """K4h's failed sort check (forced, UAM_OPT_TEST_SORT_FAULT) poisons every output, the
+    below-terrain count included, and raises DeviceCheckError at the next synchronize."""
+    from uam_path_planning_amd import _lib
+    from uam_path_planning_amd.arcs import arc_table
+    from uam_path_planning_amd.scenario import displacements
+
+    e, orc, vol, vd, host = _case(oracle_mod, 256, 16, 80, 21)
+    ut = arc_table(80, displacements(5))
+    pairs = _pairs3d(1000, 61)
+    e.set_option("test_sort_fault", 1)
+    bad = e.eval_generated3d(pairs, ut, vol)
+    assert e.last_kernel() == "K4h+pack"
+    with pytest.raises(_lib.DeviceCheckError):
+        e.synchronize()
+    for k in ("cost", "length_q", "length", "kin_sum", "nfz_sum", "min_clearance"):
+        assert np.isnan(bad[k].cpu().numpy()).all(), k
+    for k in ("nfz_hits", "offmap", "below_terrain", "best_fval_idx", "best_length_idx"):
+        assert (bad[k].cpu().numpy() == -1).all(), k
+    e.set_option("test_sort_fault", 0)
+    gpu = e.eval_generated3d(pairs, ut, vol)
+    e.synchronize()
+    _check(gpu, orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=21),
+           oracle_mod, 5)

@@ -33,7 +33,7 @@ def test_header_symbols_exported(lib):
     for name in declared:
         assert hasattr(lib, name), name
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert lib.uam_abi_version() == 1
+    assert lib.uam_abi_version() == _lib.ABI_VERSION == 2
 
 
 def _vpk_sections(nx, ny, nz):

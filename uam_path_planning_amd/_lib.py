@@ -12,18 +12,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # with different compile-time knobs); the default is the in-tree build
 LIB_PATH = os.environ.get("UAM_LIB_PATH") or os.path.join(HERE, "lib", "libuampath.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/uampath.h UAM_ABI_VERSION
 MAX_REGIONS = 16
 RECORD_BYTES = 16
 COMM_ID_BYTES = 128
 
 UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
+UAM_E_DEVICE = -6  # a device-side check of an earlier call failed (uam_device_status)
 # uam_set_option keys (include/uampath.h)
 OPTIONS = {"group": 1, "sorted_min_paths": 2, "k2s_segments": 3, "wave_max_paths": 4,
            "pair_order": 5, "k1_rows": 6, "k3b_segment": 7, "k3b_points_per_lane": 8,
            "k8_tiled": 9, "k8_streams": 10, "k2g_tile_bits": 11, "k2g_lds_floor": 12,
            "k2g_chunk": 13, "k2g_curve": 14, "k2g_sim": 15, "k4h_band": 17,
-           "k2h_lb_stride": 19, "k2h_terrain": 20, "k4h_terrain": 21}
+           "k2h_lb_stride": 19, "k2h_terrain": 20, "k4h_terrain": 21,
+           "test_sort_fault": 22}
 INEQ_HALFPLANE, INEQ_ELLIPSE, INEQ_AXIS = 0, 1, 2
 MODE_ANALYTIC, MODE_RASTER, MODE_VOLUME = 0, 1, 2
 FLAG_NFZ, FLAG_MASK, FLAG_NODATA = 1, 2, 4
@@ -130,6 +132,7 @@ SIGNATURES = {
     "uam_path_length": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _vp, _vp]),
     "uam_synchronize": (ctypes.c_int, [_vp, _vp]),
+    "uam_device_status": (ctypes.c_int, [_vp]),
     "uam_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "uam_kernel_time": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_int64)]),
@@ -183,6 +186,11 @@ class UamError(RuntimeError):
     pass
 
 
+class DeviceCheckError(UamError):
+    """UAM_E_DEVICE: a device-side consistency check of an earlier call failed; that call's
+    outputs hold NaN / -1 (include/uampath.h uam_device_status)."""
+
+
 def load():
     """Load libuampath.so (no fallback: raises if it was not built).
 
@@ -222,4 +230,6 @@ def check(status, what=""):
     text = f"{what}: {msg}" if what else msg
     if status == UAM_E_INVALID:
         raise ValueError(text)
+    if status == UAM_E_DEVICE:
+        raise DeviceCheckError(f"[status {status}] {text}")
     raise UamError(f"[status {status}] {text}")

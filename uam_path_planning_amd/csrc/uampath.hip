@@ -5110,8 +5110,39 @@ struct KGrp {
     int32_t* __restrict__ err;     // the sort's check word: zeroed by the histogram launch, set
                                    // by the scatter on a position outside the order (keys of the
                                    // two launches disagreeing); the output launch then writes
-                                   // NaN costs and -1 selections for the whole batch
+                                   // NaN / -1 in every output of the whole batch
+    int32_t* herr;                 // page-locked host word the output launch sets on err
+                                   // (uam_device_status), or null
+    int32_t test_fault;            // UAM_OPT_TEST_SORT_FAULT: the scatter flags err (tests)
 };
+
+// a path's outputs from the output launches (k_g_final / k_h_final / k_v_final); with the
+// sort's check word set (bad), NaN in every f64 output and -1 in every count
+__device__ __forceinline__ void put_outputs(const KOut& out, int64_t gp, bool bad, double cost,
+                                            double L, double len, double ksum, double nsum,
+                                            double clear, int32_t nh, int32_t off, int32_t bel) {
+    const double nan = __builtin_nan("");
+    if (out.cost) out.cost[gp] = bad ? nan : cost;
+    if (out.length_q) out.length_q[gp] = bad ? nan : L;
+    if (out.length) out.length[gp] = bad ? nan : len;
+    if (out.kin_sum) out.kin_sum[gp] = bad ? nan : ksum;
+    if (out.nfz_sum) out.nfz_sum[gp] = bad ? nan : nsum;
+    if (out.min_clearance) out.min_clearance[gp] = bad ? nan : clear;
+    if (out.nfz_hits) out.nfz_hits[gp] = bad ? -1 : nh;
+    if (out.offmap) out.offmap[gp] = bad ? -1 : off;
+    if (out.below_terrain) out.below_terrain[gp] = bad ? -1 : bel;
+}
+
+// the output launches' selections and, on a failed sort check, the host word (one lane)
+__device__ __forceinline__ void put_selection(const KGrp& kg, bool bad, int64_t q0, int t,
+                                              const double* s_cost, const double* s_len,
+                                              int32_t* best_f, int32_t* best_l) {
+    if (bad && blockIdx.x == 0 && t == 0 && kg.herr) *kg.herr = 1;
+    if (t < 64 && q0 + t < kg.n_pairs) {
+        if (best_f) best_f[q0 + t] = bad ? -1 : select_best(s_cost + t, 64, kg.D, true);
+        if (best_l) best_l[q0 + t] = bad ? -1 : select_best(s_len + t, 64, kg.D, false);
+    }
+}
 
 // K2h / K4h: the D rows' unit sums by one block (block 0 of the scatter launch, one more than
 // its partitions, so the step has no launch for them).
@@ -5386,6 +5417,7 @@ __global__ __launch_bounds__(1024) void k_g_scatter(KParams p, KGrp kg) {
         return;
     }
     const int b = blockIdx.x - (kg.ugeo ? 1 : 0);
+    if (kg.test_fault && b == 0 && t == 0) atomicOr(kg.err, 1);  // (UAM_OPT_TEST_SORT_FAULT)
     const int nsb = kg.nsb_raw;
     if (nsb > 0) {  // the scan's block totals, scanned here (replaces k_scan_totals' launch)
         const int32_t v = t < nsb ? kg.tot[t] : 0;
@@ -5733,6 +5765,7 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
     double* s_len = smem + 64 * D;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
+    const bool bad = *kg.err != 0;  // an inconsistent sort (k_g_scatter / k_v_hist)
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
         double L = 0.0, len = 0.0, ksum = 0.0, nsum = 0.0, hmax = -INFINITY;
@@ -5776,24 +5809,12 @@ __global__ __launch_bounds__(1024) void k_g_final(KParams p, KGrp kg, KOut out,
             cost = (double)(p.N + 1) * L;
             for (int s = 0; s < kg.nseg; ++s) cost = cost + kg.slot[(int64_t)s * kg.P + gp].cost;
         }
-        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
-        if (out.cost) out.cost[gp] = cost;
-        if (out.length_q) out.length_q[gp] = L;
-        if (out.length) out.length[gp] = len;
-        if (out.kin_sum) out.kin_sum[gp] = ksum;
-        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
-        if (out.min_clearance) out.min_clearance[gp] = p.altitude - hmax;
-        if (out.nfz_hits) out.nfz_hits[gp] = nh;
-        if (out.offmap) out.offmap[gp] = off;
-        if (out.below_terrain) out.below_terrain[gp] = 0;
+        put_outputs(out, gp, bad, cost, L, len, ksum, nsum, p.altitude - hmax, nh, off, 0);
         s_cost[di * 64 + qi] = cost;
         s_len[di * 64 + qi] = len;
     }
     __syncthreads();
-    if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
-    }
+    put_selection(kg, bad, q0, t, s_cost, s_len, best_f, best_l);
 }
 
 // ---- K2h: generated candidates in the similarity form (oracle orc_eval_generated_h) --------
@@ -6218,6 +6239,7 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
     double* s_len = smem + 64 * D;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
+    const bool bad = *kg.err != 0;  // an inconsistent sort (k_g_scatter / k_v_hist)
     const HSlot* slot = reinterpret_cast<const HSlot*>(kg.slot);
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
@@ -6268,24 +6290,12 @@ __global__ __launch_bounds__(1024) void k_h_final(KParams p, KGrp kg, KOut out,
                 off += (int32_t)((gs.cnt >> 8) & 255u);
             }
         }
-        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
-        if (out.cost) out.cost[gp] = cost;
-        if (out.length_q) out.length_q[gp] = L;
-        if (out.length) out.length[gp] = len;
-        if (out.kin_sum) out.kin_sum[gp] = ksum;
-        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
-        if (out.min_clearance) out.min_clearance[gp] = p.altitude - hmax;
-        if (out.nfz_hits) out.nfz_hits[gp] = nh;
-        if (out.offmap) out.offmap[gp] = off;
-        if (out.below_terrain) out.below_terrain[gp] = 0;
+        put_outputs(out, gp, bad, cost, L, len, ksum, nsum, p.altitude - hmax, nh, off, 0);
         s_cost[di * 64 + qi] = cost;
         s_len[di * 64 + qi] = len;
     }
     __syncthreads();
-    if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
-    }
+    put_selection(kg, bad, q0, t, s_cost, s_len, best_f, best_l);
 }
 
 // ---- K4h: the volume (config 5) in K2h's form -------------------------------------------------
@@ -6844,6 +6854,7 @@ __global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
     double* s_len = smem + 64 * D;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int qi = t / D, di = t - qi * D;
+    const bool bad = *kg.err != 0;  // an inconsistent sort (k_g_scatter / k_v_hist)
     const VSlot* slot = reinterpret_cast<const VSlot*>(kg.slot);
     if (q0 + qi < kg.n_pairs) {
         const int64_t gp = (q0 + qi) * D + di;
@@ -6877,24 +6888,12 @@ __global__ __launch_bounds__(1024) void k_v_final(KParams p, KGrp kg, KOut out,
             off += (int32_t)((g.cnt >> 8) & 255u);
             bel += (int32_t)((g.cnt >> 16) & 255u);
         }
-        if (*kg.err) cost = __builtin_nan("");  // an inconsistent sort (k_g_scatter)
-        if (out.cost) out.cost[gp] = cost;
-        if (out.length_q) out.length_q[gp] = L;
-        if (out.length) out.length[gp] = len;
-        if (out.kin_sum) out.kin_sum[gp] = ksum;
-        if (out.nfz_sum) out.nfz_sum[gp] = nsum;
-        if (out.min_clearance) out.min_clearance[gp] = cm;
-        if (out.nfz_hits) out.nfz_hits[gp] = nh;
-        if (out.offmap) out.offmap[gp] = off;
-        if (out.below_terrain) out.below_terrain[gp] = bel;
+        put_outputs(out, gp, bad, cost, L, len, ksum, nsum, cm, nh, off, bel);
         s_cost[di * 64 + qi] = cost;
         s_len[di * 64 + qi] = len;
     }
     __syncthreads();
-    if (t < 64 && q0 + t < kg.n_pairs) {
-        if (best_f) best_f[q0 + t] = *kg.err ? -1 : select_best(s_cost + t, 64, D, true);
-        if (best_l) best_l[q0 + t] = *kg.err ? -1 : select_best(s_len + t, 64, D, false);
-    }
+    put_selection(kg, bad, q0, t, s_cost, s_len, best_f, best_l);
 }
 
 }  // namespace
@@ -6988,6 +6987,9 @@ struct uam_ctx {
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
     int k2g_chunk = 0;          // K2g / K2h / K4h gathers in flight per lane (UAM_OPT_K2G_CHUNK:
                                 // 6, 7, 8, 11, 16, 21; 0 = the launchers' defaults)
+    int32_t* h_err = nullptr;   // page-locked, device-mapped word the sorted forms' output
+    int32_t* d_err = nullptr;   // launches set on a failed sort check (uam_device_status)
+    int test_sort_fault = 0;    // UAM_OPT_TEST_SORT_FAULT (tests only)
 
 };
 
@@ -7040,6 +7042,29 @@ int ktime_end(uam_ctx* ctx, hipStream_t s) {
     HIP_TRY(hipEventRecord(ctx->ktime_ev[ctx->ktime_n].second, s));
     ++ctx->ktime_n;
     return UAM_OK;
+}
+
+// the device-error word (uam_device_status), created on the first sorted call; the output
+// launches write it only when the sort check fails, so a good call issues no copy for it
+int err_word(uam_ctx* ctx, KGrp* kg) {
+    if (!ctx->h_err) {
+        HIP_TRY(hipHostMalloc((void**)&ctx->h_err, 64, hipHostMallocMapped));
+        *ctx->h_err = 0;
+        void* d = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&d, ctx->h_err, 0));
+        ctx->d_err = (int32_t*)d;
+    }
+    kg->herr = ctx->d_err;
+    kg->test_fault = ctx->test_sort_fault;
+    return UAM_OK;
+}
+
+int device_status(uam_ctx* ctx) {
+    if (!ctx->h_err || !*(volatile int32_t*)ctx->h_err) return UAM_OK;
+    *(volatile int32_t*)ctx->h_err = 0;
+    return fail(UAM_E_DEVICE,
+                "a sorted evaluation (K2h / K2g / K4h) found its counting sort inconsistent on "
+                "the device; that call wrote NaN / -1 to every output of its batch");
 }
 
 int make_kraster(const uam_raster_desc* d, KRaster* k) {
@@ -7149,6 +7174,7 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     }
     if (ctx->devarena) dev_arena_free(ctx->devarena);
     if (ctx->d_tmtab) (void)hipFree(ctx->d_tmtab);
+    if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     delete ctx;
 }
 
@@ -7766,6 +7792,12 @@ int uam_set_option(uam_ctx* ctx, int32_t option, int64_t value) {
                             option == UAM_OPT_K2H_TERRAIN ? '2' : '4', (long long)value);
             (option == UAM_OPT_K2H_TERRAIN ? ctx->k2h_te : ctx->k4h_te) = (int)value;
             return UAM_OK;
+        case UAM_OPT_TEST_SORT_FAULT:
+            if (value != 0 && value != 1)
+                return fail(UAM_E_INVALID, "UAM_OPT_TEST_SORT_FAULT %lld is not 0 or 1",
+                            (long long)value);
+            ctx->test_sort_fault = (int)value;
+            return UAM_OK;
         case UAM_OPT_K2H_LB_STRIDE:
             if (value < 0 || value > 1024)
                 return fail(UAM_E_INVALID, "UAM_OPT_K2H_LB_STRIDE %lld outside [0, 1024]",
@@ -7808,6 +7840,7 @@ int uam_get_option(const uam_ctx* ctx, int32_t option, int64_t* value) {
         case UAM_OPT_K2H_LB_STRIDE: *value = ctx->k2h_lbs; return UAM_OK;
         case UAM_OPT_K2H_TERRAIN: *value = ctx->k2h_te; return UAM_OK;
         case UAM_OPT_K4H_TERRAIN: *value = ctx->k4h_te; return UAM_OK;
+        case UAM_OPT_TEST_SORT_FAULT: *value = ctx->test_sort_fault; return UAM_OK;
         case UAM_OPT_K4H_BAND: *value = ctx->k4h_band; return UAM_OK;
         case UAM_OPT_K2G_CURVE: *value = ctx->k2g_curve; return UAM_OK;
 
@@ -8190,6 +8223,8 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
+    st = err_word(ctx, &kg);
+    if (st) return st;
     kg.lbp = sim && !ctx->k2h_te && ctx->k2h_lbs > 0 ? (float*)(w + o) : nullptr, o += b_lbp;
     // the seeds' header and unit-arc reads from LDS when both fit beside the histogram's own
     const size_t hist_dyn = kg.lbp ? (size_t)kr.hwords * 4 + ubytes : 0;
@@ -8294,9 +8329,21 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         HIP_TRY(hipEventRecord(ctx->ev_join, s_cells));
         return UAM_OK;
     };
+    // once the cells are forked, every exit makes the caller's stream wait for them (an error
+    // return must not leave k_cells writing the caller's buffer behind the call)
+    bool forked = false;
+    auto join = [&](int r) -> int {
+        if (forked) {
+            forked = false;
+            const hipError_t e = hipStreamWaitEvent(s, ctx->ev_join, 0);
+            if (e != hipSuccess && r >= 0) return fail(UAM_E_HIP, "cells join: %s", hipGetErrorString(e));
+        }
+        return r;
+    };
     if (cells_side && UAM_CELLS_SIDE == 1) {
         st = fork_cells();
         if (st) return st;
+        forked = true;
     }
     hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? hist_dyn : 0, s,
                        ctx->kp, kr, kg);
@@ -8309,6 +8356,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (cells_side && UAM_CELLS_SIDE == 2) {  // (beside the evaluation only)
         st = fork_cells();
         if (st) return st;
+        forked = true;
     }
     if (hev)
         hipLaunchKernelGGL(hev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
@@ -8324,8 +8372,9 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
                             : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
     hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
                        (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
-    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "grouped evaluation launch");
-    if (cells_side) HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    if (hipGetLastError() != hipSuccess) return join(fail(UAM_E_HIP, "grouped evaluation launch"));
+    st = join(UAM_OK);
+    if (st) return st;
     st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = G;
@@ -8411,6 +8460,8 @@ static int launch_grouped3d(uam_ctx* ctx, const KVol4& kv, const double* pairs6,
     kg.cnt = (int32_t*)(w + o), o += b_cnt;
     kg.tot = (int32_t*)(w + o), o += b_tot;
     kg.err = (int32_t*)(w + o), o += b_err;
+    st = err_word(ctx, &kg);
+    if (st) return st;
     kg.ubp = ctx->k2h_lbs > 0 && !ctx->k4h_te ? (double*)(w + o) : nullptr, o += b_ubp;
     const size_t hist_dyn = (size_t)kv.hwords * 4 + (size_t)D * ctx->kp.N * 16;
     kg.seed_lds = kg.ubp && hist_dyn <= (size_t)G_HIST_DYN_MAX;
@@ -8733,6 +8784,10 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const void* packed, const double* pairs, int64_t n_pairs,
                        const double* utab, int32_t D, const uam_path_outputs* out,
                        uam_stream stream) {
+    if (ctx) {  // an earlier call's failed device check, reported once (uam_device_status)
+        const int st = device_status(ctx);
+        if (st) return st;
+    }
     return eval_generated(ctx, mode, desc, rec, summary, block, pairs, n_pairs, utab, D, out,
                           stream, packed);
 }
@@ -9025,6 +9080,10 @@ int uam_eval_generated3d(uam_ctx* ctx, const uam_volume_desc* vd, const void* vo
                          const void* packed, const double* pairs6, int64_t n_pairs,
                          const double* utab, int32_t D, const uam_path_outputs* out,
                          uam_stream stream) {
+    if (ctx) {  // an earlier call's failed device check, reported once (uam_device_status)
+        const int st = device_status(ctx);
+        if (st) return st;
+    }
     if (packed) {
         int st = check_ctx(ctx, true);
         if (st) return st;
@@ -9952,7 +10011,12 @@ int uam_synchronize(uam_ctx* ctx, uam_stream stream) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
     DeviceGuard dg(ctx->device);
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    return UAM_OK;
+    return device_status(ctx);
+}
+
+int uam_device_status(uam_ctx* ctx) {
+    if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
+    return device_status(ctx);
 }
 
 }  // extern "C"

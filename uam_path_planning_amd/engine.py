@@ -640,7 +640,13 @@ class Engine:
         return t
 
     def synchronize(self):
+        """Wait for this engine's stream; raises DeviceCheckError when a call's device-side
+        check failed (its outputs then hold NaN / -1)."""
         _lib.check(self.lib.uam_synchronize(self._ctx, self.stream), "uam_synchronize")
+
+    def device_status(self):
+        """Raise DeviceCheckError if a completed call's device-side check failed (no wait)."""
+        _lib.check(self.lib.uam_device_status(self._ctx), "uam_device_status")
 
 
 _default = {}
