@@ -90,6 +90,11 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="libuampath context option (uam_set_option; names in _lib.OPTIONS), "
                          "repeatable: measurement sweeps of forms that give the same outputs")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="steps submitted per library call (uam_eval_generated_batches, raster "
+                         "K2h only: batch k + 1's sort and batch k - 1's output launch beside "
+                         "batch k's evaluation; every step keeps its own sort, evaluation and "
+                         "output set); 1 = one uam_eval_generated per step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -283,8 +288,22 @@ def main():
         else:
             eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
 
-    for _ in range(args.warmup):
-        step()
+    # --batches B: B steps per call, each with its own output set (outsets[0] = outs)
+    nb = max(1, args.batches) if raster_mode and not args.cells else 1
+    outsets = [outs] + [eng.outputs(P, W, n_pairs=Q) for _ in range(nb - 1)]
+
+    def run_steps(n):
+        if nb == 1:
+            for _ in range(n):
+                step()
+            return
+        done = 0
+        while done < n:
+            b = min(nb, n - done)
+            eng.eval_generated_batches([pairs] * b, ut, raster, outputs=outsets[:b])
+            done += b
+
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     # the timed region: ONE HIP event pair on the launch stream (libuampath enqueues on torch's
     # current stream) around all K steps, so no per-step marker perturbs the launches
@@ -294,8 +313,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
-    for i in range(args.steps):
-        step()
+    run_steps(args.steps)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -305,8 +323,7 @@ def main():
     # cross-check after the timed region: the library's own HIP-event pair around each call's
     # launch sequence (uam_kernel_timing), same steps
     eng.kernel_timing(True)
-    for i in range(args.steps):
-        step()
+    run_steps(args.steps)
     k_total, k_launches = eng.kernel_time()
     eng.kernel_timing(False)
     seq_ms = k_total / k_launches if k_launches == args.steps else None
@@ -375,6 +392,8 @@ def main():
     roofline["profile_key"] = pkey
     if args.opt:
         roofline["options"] = list(args.opt)
+    if nb > 1:
+        roofline["batches_per_call"] = nb
     result = {
         "metric": METRIC,
         "value": round(value, 1),

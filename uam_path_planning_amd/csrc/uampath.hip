@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -40,6 +39,48 @@
 
 #include "../../include/uampath.h"
 #include "polyproc.h"
+
+// ---- Measurement-build knobs -------------------------------------------------------------
+// Tuning experiments only (tools/build_variant.sh passes -D overrides into a separate .so that
+// UAM_LIB_PATH loads); the shipped library is built with exactly these defaults, and no knob
+// changes what any kernel computes.
+#ifndef UAM_K1_TILE_ROWS
+// raster rows per column of K1's strip order (0: row-major).  cfg3 map at 4096^2: row-major
+// 0.225 ms, columns of 16 / 32 / 64 / 128 / 256 / 512 / 4096 rows 0.196 / 0.196 / 0.195 /
+// 0.190 / 0.188 / 0.189 / 0.231 ms (the shape-free build 0.108 -> 0.118-0.130: the record
+// rows' DRAM pages); profiles/r05/cc13, cc14
+#define UAM_K1_TILE_ROWS 128
+#endif
+#ifndef UAM_K1_GRID_CAP
+// K1's strip workgroups, cfg3 map at 4096^2 (32 768 strips): uncapped 0.185 ms, 16 384 0.179,
+// 12 288 0.197, 8192 0.176, 6144 0.205, 4096 0.193, 2048 0.254 (profiles/r05/cc15, cc16)
+#define UAM_K1_GRID_CAP 8192
+#endif
+#ifndef UAM_RF_PREFETCH  // K6 refinement: 0 reads the L-BFGS pairs without prefetch
+#define UAM_RF_PREFETCH 1
+#endif
+#ifndef UAM_RF_WAVES  // K6 refinement: waves per SIMD of k_refine's register budget
+#define UAM_RF_WAVES 4
+#endif
+#ifndef UAM_RORD_BITS  // K2's raster pair order: 4^bits bins per key level
+#define UAM_RORD_BITS 2
+#endif
+#ifndef UAM_G_NBK  // K2g / K2h / K4h counting sort: partitions (one 1024-thread block each)
+#define UAM_G_NBK 256
+#endif
+#ifndef UAM_K2H_MINW  // K2h evaluation: waves per SIMD the register budget allows
+#define UAM_K2H_MINW 4
+#endif
+#ifndef UAM_K2H_BS  // K2h evaluation: items per workgroup
+#define UAM_K2H_BS 256
+#endif
+#ifndef UAM_SHAPE_GRID_N  // shape-grid index: cells per side
+#define UAM_SHAPE_GRID_N 64
+#endif
+#ifndef UAM_GRID_REFINE  // shape-grid index: 0 lists every cell a shape's box meets
+#define UAM_GRID_REFINE 1
+#endif
+// ---- end of the measurement-build knobs ---------------------------------------------------
 
 
 namespace {
@@ -2052,13 +2093,6 @@ __device__ __forceinline__ void wave_walk_obs_cells(const KGeom& g, const int (&
     wave_walk_cells<2, CPL>(g, slot, [&](int s, uint32_t m) { body(s, 0u, m); });
 }
 
-#ifndef UAM_K1_TILE_ROWS
-// raster rows per column of K1's strip order (0: row-major).  cfg3 map at 4096^2: row-major
-// 0.225 ms, columns of 16 / 32 / 64 / 128 / 256 / 512 / 4096 rows 0.196 / 0.196 / 0.195 /
-// 0.190 / 0.188 / 0.189 / 0.231 ms (the shape-free build 0.108 -> 0.118-0.130: the record
-// rows' DRAM pages); profiles/r05/cc13, cc14
-#define UAM_K1_TILE_ROWS 128
-#endif
 template <int CPL>
 __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
                                                             const float* __restrict__ dem,
@@ -2269,16 +2303,6 @@ __device__ __forceinline__ void for_ineqs_u(const KGeom& g, const DevShape& sh, 
 // accumulator that is never -0), the hit count.  A point with more than K3B_KT terms, or whose
 // terms do not fit the segment's term list, is re-walked by its lane (eval_path's own loop).
 // Outputs are bit-identical to k_eval_pairs.
-#ifdef UAM_K3B_DIAG
-// diagnostics build only (tools/probe_k3b.py): [0] chunks, [1] distinct grid slots per chunk,
-// [2] union walk steps (table 0), [3] lane list entries (table 0), [4] / [5] the same for the
-// obstacle walk, [6] points re-walked by their lane; [8..13] s_memtime cycles of workgroup
-// phases (thread 0): pass 1, zero + keys, scan + scatter, evaluation, ordered sums, output
-__device__ unsigned long long g_k3b_diag[16];
-__device__ unsigned long long g_k3b_ev[8];  // eval-phase sub-stamps (lane 0 of each wave)
-__constant__ int g_k3b_skip;  // bit 0: skip the evaluation phase (timing of the rest); bit 1:
-                              // no coherence counters (clean phase timing)
-#endif
 constexpr int K3B_BINS = 1024 + 2;  // grid cell mod 1024, off-grid, no slot
 constexpr int K3B_KT = 3;           // psi terms a point keeps in registers (more: re-walk)
 constexpr uint8_t K3B_HIT = 1, K3B_REWALK = 7;  // flags: bit 0 hit, bits 1-3 term count
@@ -2331,9 +2355,6 @@ struct K3bRes {
     double tm[CPL][K3B_KT];  // the first nonzero obstacle psi terms, list order
     int cnt[CPL];            // nonzero terms (may exceed K3B_KT)
     bool hit[CPL];
-#ifdef UAM_K3B_DIAG
-    unsigned long long cyc0, cyc1;  // s_memtime cycles of the two walks
-#endif
 };
 
 // Phi, the nonzero obstacle psi terms and the collision bit of each lane's CPL points (whole
@@ -2348,27 +2369,8 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
     int rc[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) R.pen[k] = t[k] = wc[k] = 0.0, rc[k] = -1;
-#ifdef UAM_K3B_DIAG
-    unsigned long long dg[4] = {0, 0, 0, 0};
-#endif
-#ifdef UAM_K3B_DIAG
-    unsigned long long e0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef UAM_K3B_DIAG
-    int slot0[CPL];  // bit 2: skip the table-0 walk; bit 3: skip the obstacle walk
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) slot0[k] = (g_k3b_skip & 4) ? -2 : slot[k];
-#else
     const int(&slot0)[CPL] = slot;
-#endif
-#ifdef UAM_K3B_DIAG
-    int slot1[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) slot1[k] = (g_k3b_skip & 8) ? -2 : slot[k];
-    unsigned long long e1 = 0;
-#else
     const int(&slot1)[CPL] = slot;
-#endif
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         R.cnt[k] = 0;
@@ -2388,10 +2390,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
         ++R.cnt[k];
     };
     auto body0 = [&](int s, uint32_t mine) {
-#ifdef UAM_K3B_DIAG
-        dg[0] += 1;
-        dg[1] += __builtin_popcount(mine);
-#endif
         if (!mine) return;
         const DevShape sh = uload(g.shape, s);
         uint32_t need = 0;
@@ -2430,10 +2428,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
     };
 
     auto body1 = [&](int s, uint32_t m1, uint32_t m2) {
-#ifdef UAM_K3B_DIAG
-        dg[2] += 1;
-        dg[3] += __builtin_popcount(m1 | m2);
-#endif
         if (!(m1 | m2)) return;
         const DevShape sh = uload(g.shape, s);
         uint32_t n1 = 0, n2 = 0;
@@ -2504,9 +2498,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
                 body0(gr.mbase[0] + 64 * w + bit, mine);
             }
         k3b_finish_pen();
-#ifdef UAM_K3B_DIAG
-        e1 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
         for (int w = 0; w < 2; ++w)
             for (uint64_t bb = w ? u11 : u10; bb; bb &= bb - 1) {
@@ -2522,9 +2513,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
     } else {
         wave_walk_cells<0, CPL>(g, slot0, body0);
         k3b_finish_pen();
-#ifdef UAM_K3B_DIAG
-        e1 = __builtin_amdgcn_s_memtime();
-#endif
         wave_walk_obs_cells<CPL>(g, slot1, body1);
     }
 #pragma unroll
@@ -2539,35 +2527,6 @@ __device__ __forceinline__ void k3b_points(const KGeom& g, const KParams& p,
             R.hit[k] = collides(g, x[k], y[k]);
         }
     }
-#ifdef UAM_K3B_DIAG
-    {
-        const unsigned long long e2 = __builtin_amdgcn_s_memtime();
-        R.cyc0 = e1 - e0;
-        R.cyc1 = e2 - e1;
-    }
-    if (g_k3b_skip & 2) return;  // timing run: no counters
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-        int nd = 0;  // distinct slots of the wave's valid points k (whole wave active here)
-        uint64_t act = __ballot(slot[k] != -2);
-        while (act) {
-            const int l0 = __builtin_ctzll(act);
-            const int s0 = __shfl(slot[k], l0, 64);
-            act &= ~__ballot(slot[k] == s0);
-            ++nd;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&g_k3b_diag[0], 1ull);
-            atomicAdd(&g_k3b_diag[1], (unsigned long long)nd);
-        }
-    }
-    atomicAdd(&g_k3b_diag[3], dg[1]);
-    atomicAdd(&g_k3b_diag[5], dg[3]);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&g_k3b_diag[2], dg[0] * CPL);
-        atomicAdd(&g_k3b_diag[4], dg[2] * CPL);
-    }
-#endif
 }
 
 // eval_path's no-fly terms of one point, added in its order (a point K3b could not park)
@@ -2650,22 +2609,7 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
     src.u = utab + (int64_t)d * N * 2;
     PathAcc a;
     a.L = a.len = a.ksum = 0.0;
-#ifdef UAM_K3B_DIAG
-    unsigned long long evc[6] = {0, 0, 0, 0, 0, 0};
-    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime();
-#define K3B_STAMP(k)                                                \
-    do {                                                            \
-        const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
-        ph[k] += tn - tp;                                           \
-        tp = tn;                                                    \
-    } while (0)
-#else
-#define K3B_STAMP(k) \
-    do {             \
-    } while (0)
-#endif
     if (in) path_pass1<true>(p, src, nullptr, a);
-    K3B_STAMP(0);
     a.cost = (double)(N + 1) * a.L;
     a.nsum = 0.0;
     a.nh = 0;
@@ -2716,7 +2660,6 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
             }
         }
         __syncthreads();
-        K3B_STAMP(1);
         const int npts = block_excl_scan(s_hist, K3B_BINS, s_part);
         int pos[S];  // sorted position of each of this lane's points (rank reused)
 #pragma unroll
@@ -2725,19 +2668,9 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
             if (key[t] >= 0) s_ord[pos[t]] = (uint16_t)(tid * S + t);
         }
         __syncthreads();
-        K3B_STAMP(2);
         // B: evaluate 64 CPL consecutive sorted points per wave step (wave-uniform trip count)
-#ifdef UAM_K3B_DIAG
-        const int npts_b = (g_k3b_skip & 1) ? 0 : npts;
-        if (g_k3b_skip & 1)
-            for (int i = tid; i < NPT; i += nt) s_fl[i] = 0, s_phi[i] = 0.0;
-#else
         const int npts_b = npts;
-#endif
         for (int c0 = wave * 64 * CPL; c0 < npts_b; c0 += nwaves * 64 * CPL) {
-#ifdef UAM_K3B_DIAG
-            const unsigned long long b0 = __builtin_amdgcn_s_memtime();
-#endif
             double x[CPL], y[CPL];
             int slot[CPL], id[CPL];
 #pragma unroll
@@ -2754,25 +2687,12 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
                 }
             }
             K3bRes<CPL> R;
-#ifdef UAM_K3B_DIAG
-            const unsigned long long b1 = __builtin_amdgcn_s_memtime();
-#endif
             k3b_points<CPL>(g, p, x, y, slot, R);
-#ifdef UAM_K3B_DIAG
-            const unsigned long long b2 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 if (id[k] < 0) continue;
                 const int ps = c0 + k * 64 + lane;  // results at the sorted position
                 int c = R.cnt[k];
-#ifdef UAM_K3B_DIAG
-                if (!(g_k3b_skip & 2)) {
-                    if (c > 0) atomicAdd(&g_k3b_diag[14], 1ull);
-                    atomicAdd(&g_k3b_diag[15], (unsigned long long)c);
-                    if (c > K3B_KT) atomicAdd(&g_k3b_diag[7], 1ull);
-                }
-#endif
                 if (c > K3B_KT) {
                     c = K3B_REWALK;
                 } else if (c > 1) {  // terms 2..c go to the segment's list
@@ -2790,18 +2710,8 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
                 s_phi[ps] = R.pen[k];
                 s_fl[ps] = (uint8_t)((R.hit[k] ? K3B_HIT : 0) | (c << 1));
             }
-#ifdef UAM_K3B_DIAG
-            const unsigned long long b3 = __builtin_amdgcn_s_memtime();
-            evc[0] += R.cyc0;
-            evc[1] += R.cyc1;
-            evc[2] += b1 - b0;
-            evc[3] += b2 - b1;
-            evc[4] += b3 - b2;
-            evc[5] += 1;
-#endif
         }
         __syncthreads();
-        K3B_STAMP(3);
         // C: the path's lane adds its points in waypoint order (eval_path's chains)
         if (in) {
 #pragma unroll
@@ -2815,9 +2725,6 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
                     double x, y;
                     seg_point(tid, t, x, y);
                     a.nsum = k3b_psi_chain(g, p, x, y, a.nsum);
-#ifdef UAM_K3B_DIAG
-                    atomicAdd(&g_k3b_diag[6], 1ull);
-#endif
                 } else if (c) {
                     a.nsum = a.nsum + s_psi[id];
                     if (c > 1) {
@@ -2829,7 +2736,6 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
             }
         }
         __syncthreads();
-        K3B_STAMP(4);
     }
     // outputs staged through LDS exactly as k_eval_pairs does (the segment arrays are dead)
     double* s_cost = smem;
@@ -2872,14 +2778,6 @@ __global__ __launch_bounds__(1024) void k_eval_pairs_k3b(KGeom g, KParams p,
         if (best_f) best_f[q] = select_best(s_cost + lane, 64, D, true);
         if (best_l) best_l[q] = select_best(s_len + lane, 64, D, false);
     }
-#ifdef UAM_K3B_DIAG
-    K3B_STAMP(5);
-    if (tid == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&g_k3b_diag[8 + k], ph[k]);
-    if (lane == 0 && (g_k3b_skip & 2))
-        for (int k = 0; k < 6; ++k) atomicAdd(&g_k3b_ev[k], evc[k]);
-#endif
-#undef K3B_STAMP
 }
 
 // L(z + a dr); want (a = 0): gradient into gr and |gr|^2 into gn2.  Per-waypoint terms and
@@ -3086,9 +2984,6 @@ __device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const do
                                           const double* hy, const double* rho, double* ai,
                                           double gamma, int m, int cnt, int head, int N, int W,
                                           int lane) {
-#ifndef UAM_RF_PREFETCH
-#define UAM_RF_PREFETCH 1
-#endif
     if (W > 128 || !UAM_RF_PREFETCH) {
         lbfgs_dir_loops(gr, dr, hs, hy, rho, gamma, m, cnt, head, N, W, lane);
         return;
@@ -3154,9 +3049,6 @@ __device__ __forceinline__ void lbfgs_dir(const double* gr, double* dr, const do
 
 // register budget: <= 128 VGPRs keeps 4 waves per SIMD (rf_L inlined at every call site; an
 // out-of-line call spills around s_swappc)
-#ifndef UAM_RF_WAVES
-#define UAM_RF_WAVES 4
-#endif
 // distance along the unit direction (ux, uy) from a point inside shape sh (every h_i < 0) to
 // its boundary: the smallest positive root over its inequalities (oracle exit_dist, op for op)
 __device__ double rf_exit_dist(const KGeom& g, const DevShape& sh, double x0, double x1,
@@ -3514,19 +3406,6 @@ __device__ __forceinline__ int wave_compact_nonzero(double* a, int n, int lane) 
     return cnt;
 }
 
-// UAM_EW_PROF builds (tuning experiments only): lane 0 of each of the first 1024 paths stamps
-// s_memtime at the phase boundaries of k_eval_wave; uam_debug_ew_prof copies the stamps out.
-#ifdef UAM_EW_PROF
-__device__ uint64_t g_ew_prof[1024 * 8];
-#define EW_STAMP(k)                                                                      \
-    do {                                                                                 \
-        if (lane == 0 && path < 1024) g_ew_prof[path * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define EW_STAMP(k) \
-    do {            \
-    } while (0)
-#endif
 
 template <int MODE, bool GEN>
 __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster rs, KVolume vs,
@@ -3539,7 +3418,6 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int64_t path = (int64_t)blockIdx.x * wpb + wave;
     if (path >= n_paths) return;  // whole wave
-    EW_STAMP(0);
     const int N = p.N, W = N + 2;
     const bool ls = p.length_smooth != 0, ms = p.maxratio_smooth != 0;
     double* px = ew_lds + (int64_t)wave * ewave_doubles(N);
@@ -3577,7 +3455,6 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
         py[j] = y;
     }
     wave_sync();
-    EW_STAMP(1);
     // geometry terms: lq = get_cost length term of the segment ending at j (anchor segment
     // for j = 0; +0.0 where eval_path adds nothing), sg = true segment norm, kinematic rows
     for (int j = lane; j < W; j += 64) {
@@ -3622,7 +3499,6 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
             }
         }
     }
-    EW_STAMP(2);
     wave_sync();
     // eval_path's sequential sums, same order, on four lanes at once.  Every accumulator
     // starts at +0.0 and so is never -0.0, which makes a ±0.0 term an exact no-op: the
@@ -3705,14 +3581,12 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
         issue(jb);
         consume(jb);
     }
-    EW_STAMP(3);
     hmax = wave_fmax(hmax);
     cmin = wave_fmin(cmin);
     nh = wave_isum(nh);
     off = wave_isum(off);
     below = wave_isum(below);
     wave_sync();
-    EW_STAMP(4);
     const int nps = wave_compact_nonzero(ps, W, lane);
     const int nph = wave_compact_nonzero(ph, W, lane);
     // chains B
@@ -3725,10 +3599,8 @@ __global__ __launch_bounds__(256) void k_eval_wave(KGeom g, KParams p, KRaster r
     L = __shfl(L, 0, 64);
     const double len = __shfl(acc, 1, 64), nsum = __shfl(acc, 2, 64);
     const double ksum = __shfl(acc, 3, 64);
-    EW_STAMP(5);
     if (lane == 0) {
         const double cost = acc;
-        EW_STAMP(6);
         if (out.cost) out.cost[path] = cost;
         if (out.length_q) out.length_q[path] = L;
         if (out.length) out.length[path] = len;
@@ -4588,9 +4460,6 @@ __global__ __launch_bounds__(256) void k_pair_scatter(const uint16_t* __restrict
 // per-partition LDS histogram, stored bin-major; (2) every partition scans the 256 x RORD_NB
 // counts (thread t owns bin t across all partitions) and scatters its pairs through LDS cursors.
 // cfg3: the order takes the raster kernel from 0.765 to 0.718 ms (profiles/r02).
-#ifndef UAM_RORD_BITS
-#define UAM_RORD_BITS 2
-#endif
 constexpr int RORD_BITS = UAM_RORD_BITS, RORD_BINS = 1 << (4 * RORD_BITS);
 constexpr int RORD_BPT = RORD_BINS / 256;          // bins per thread of the order kernels
 constexpr int RORD_NB = RORD_BPT > 1 ? 16 : 64;    // partitions of the pairs
@@ -5027,9 +4896,6 @@ __global__ __launch_bounds__(1024) void k_seg_final(KParams p, KSeg ks, KOut out
 constexpr int G_TBITS_MAX = 6;                          // up to 64 x 64 tiles over the raster
 // tile bins twice over (a ragged last group's items have their own) + one for off-raster / NaN
 constexpr int G_BINS_MAX = (2 << (2 * G_TBITS_MAX)) + 1;
-#ifndef UAM_G_NBK
-#define UAM_G_NBK 256  // (a build knob for measurement)
-#endif
 constexpr int G_NBK = UAM_G_NBK;                        // partitions of the counting sort
 constexpr int G_HIST_DYN_MAX = 119 * 1024;  // k_g_hist's dynamic LDS (K2h seeds) beside its 40 KiB
 constexpr int G_MAXLEN = 64;                            // longest group
@@ -5641,10 +5507,6 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
             const int32_t ix = (int32_t)tx, iy = (int32_t)ty;
             cs.set(t, pk_locate(rs, rec, s_map, ix, iy, vp, tp));
         }
-#ifdef UAM_K2G_DIAG_NOGATHER  // measurement build: every load reads the planes' first line
-        vp = vdummy;
-        tp = rs.t4;
-#endif
         return vp;
     };
     // the consume step, branch-free: a lane with nothing gathered adds +0.0 (an exact no-op on
@@ -5683,17 +5545,12 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 }
                 // the rows of waypoints j0 and (group 0) j0 + 1 belong elsewhere / do not exist
                 const bool rv = !(first && (t == 0 || (t == 1 && j0 == 0)));
-#ifdef UAM_K2G_DIAG_NOGEO  // measurement build: no segment / kinematic work
-                (void)rv;
-                px = x0, py = x1;
-#else
                 if (t == 0 && first && j == 0) {
                     // p_0 of group 0: no segment ends here (the anchor term stands for it)
                     px = x0, py = x1;
                 } else {
                     segment_fast(x0, x1, rv);
                 }
-#endif
                 const float* tp;
                 r[t] = *locate(x0, x1, t, inb, cs, tp);
                 tv[t] = *tp;
@@ -5707,9 +5564,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
                 double x0 = px, x1 = py;  // j = 0: p_0, generated above
                 if (j > 0) {
                     point(j, x0, x1);
-#ifndef UAM_K2G_DIAG_NOGEO
                     segment(j, x0, x1);
-#endif
                 }
                 uint32_t inb = 0;
                 PkSlots cs;
@@ -5719,11 +5574,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
             }
         }
     }
-#ifdef UAM_K2G_DIAG_NOGEO
-    if (false) {
-#else
     if (j1 <= W - 1) {  // the point after the group: its last kinematic row only
-#endif
         double x0, x1;
         point(j1, x0, x1);
         segment(j1, x0, x1);
@@ -5736,20 +5587,7 @@ __global__ __launch_bounds__(256, CH > 11 ? 2 : 4) void k_g_eval(KParams p, KRas
     o.ksum = gk;
     o.hmax = hmax;
     o.cnt = nh | (off << 8);
-#if defined(UAM_K2G_DIAG_NOSLOT)  // measurement build: slots written only when a NaN shows up
-    if (!(gc == gc) || !(gL == gL)) kg.slot[(int64_t)s * kg.P + path] = o;
-#elif defined(UAM_K2G_SLOT_NT)
-    GSlot* dst = kg.slot + (int64_t)s * kg.P + path;
-    __builtin_nontemporal_store(o.cost, &dst->cost);
-    __builtin_nontemporal_store(o.psi, &dst->psi);
-    __builtin_nontemporal_store(o.L, &dst->L);
-    __builtin_nontemporal_store(o.len, &dst->len);
-    __builtin_nontemporal_store(o.ksum, &dst->ksum);
-    __builtin_nontemporal_store(o.hmax, &dst->hmax);
-    __builtin_nontemporal_store(o.cnt, &dst->cnt);
-#else
     kg.slot[(int64_t)s * kg.P + path] = o;
-#endif
 }
 
 // outputs of every path (block = 64 pairs x D, k_eval_pairs's store layout): the partials
@@ -5864,23 +5702,6 @@ struct alignas(8) HSlot {  // 24 B per (path, group), written by one lane
 // (A group without M may report less than its own maximum: only the path's is an output.)
 // The slot's hmax is that E.  (Measured, cfg3: 0.19 fetches per waypoint with the sampled lb
 // alone and chunks issued one ahead, tools/k2h_counts.py.)
-#ifdef UAM_K2H_COUNT  // measurement builds only: K2h's slot classes (tools/k2h_counts.py)
-__device__ unsigned long long g_k2h_cnt[8];  // valid, in-raster, fetched, code 1, 2, 3, Lb -inf
-extern "C" int uam_debug_k2h_counts(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2h_cnt), sizeof(g_k2h_cnt)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long z[8] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2h_cnt), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif
-#ifndef UAM_K2H_MINW  // waves per SIMD the register budget allows (measurement builds)
-#define UAM_K2H_MINW 4
-#endif
-#ifndef UAM_K2H_BS  // (measurement builds)
-#define UAM_K2H_BS 256
-#endif
 // K2h workgroup: 256 items (cfg3 0.297 ms against 0.306 at 512, profiles/r05/k2h12)
 constexpr int H_BS = UAM_K2H_BS;
 template <int CH, bool TE>  // TE: the terrain in the entry (UAM_OPT_K2H_TERRAIN 1)
@@ -5933,10 +5754,9 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
     float tvA[CH];
     uint32_t kcA[CH], vinA = 0, tkA = 0;
     int nvA = 0;
-#ifndef UAM_K2H_AHEAD  // (measurement builds: 1 issues chunk c + 1 before consuming chunk c;
-#define UAM_K2H_AHEAD 0  // the same at cfg3 with 256-item workgroups, profiles/r05/k2h12)
-#endif
-    constexpr bool ahead = UAM_K2H_AHEAD != 0;
+    // (ahead: chunk c + 1 issued before chunk c is consumed -- the same at cfg3 with 256-item
+    // workgroups, profiles/r05/k2h12)
+    constexpr bool ahead = false;
     for (int c = ahead ? -1 : 0; c < nch; ++c) {  // (nch wave-uniform)
         const int ci = ahead ? c + 1 : c;  // the chunk issued by this iteration
         uint4 rB[CH];
@@ -6019,16 +5839,6 @@ __device__ __forceinline__ void h_item(const KParams& p, const KRaster& rs, cons
                 rB[t] = *reinterpret_cast<const uint4*>(pk + voff);
                 tvB[t] = *reinterpret_cast<const float*>(pk + (ot4 + (fetch ? a4 * 4u : 0u)));
                 tkB |= (uint32_t)fetch << t;
-#ifdef UAM_K2H_COUNT
-                {
-                    const uint64_t m[6] = {__ballot(vj), __ballot(vin), __ballot(fetch),
-                                           __ballot(code == 1u), __ballot(code == 2u),
-                                           __ballot(code == 3u)};
-                    if ((threadIdx.x & 63) == 0)
-                        for (int q = 0; q < 6; ++q)
-                            atomicAdd(&g_k2h_cnt[q], (unsigned long long)__popcll(m[q]));
-                }
-#endif
             }
             nvB = max(0, min(CH, j1 - jc));  // slots past the group's end: no waypoint
         }
@@ -6102,12 +5912,6 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
     const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
     const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
     const float seed = kg.lbp ? kg.lbp[path] : -INFINITY;
-#ifdef UAM_K2H_COUNT
-    {
-        const uint64_t m = __ballot(live && seed == -INFINITY);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&g_k2h_cnt[6], (unsigned long long)__popcll(m));
-    }
-#endif
     const int nu = kg.D * p.N;
     {  // staging: every load of a thread issued before its first LDS store (hw % 4 == 0)
         constexpr int U = 4;
@@ -6208,13 +6012,8 @@ __global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
             if (j0 + 3 < W && !(((uintptr_t)o) & 7)) {
                 typedef int32_t v2i __attribute__((ext_vector_type(2)));
                 const v2i w0 = {v[0], v[1]}, w1 = {v[2], v[3]};
-#ifndef UAM_CELLS_PLAIN  // (plain: a measurement build)
                 __builtin_nontemporal_store(w0, reinterpret_cast<v2i*>(o));
                 __builtin_nontemporal_store(w1, reinterpret_cast<v2i*>(o) + 1);
-#else
-                reinterpret_cast<v2i*>(o)[0] = w0;
-                reinterpret_cast<v2i*>(o)[1] = w1;
-#endif
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
@@ -6692,7 +6491,7 @@ __global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(
     float tvA[CH];
     uint32_t kcA[CH], vinA = 0, tkA = 0, bvA = 0;
     int nvA = 0, jcA = 0;
-    constexpr bool ahead = UAM_K2H_AHEAD != 0;  // (h_item's switch)
+    constexpr bool ahead = false;  // (h_item's)
     for (int c = ahead ? -1 : 0; c < nch; ++c) {  // (nch wave-uniform)
         const int ci = ahead ? c + 1 : c;  // the chunk issued by this iteration
         uint4 rB[CH];
@@ -6925,6 +6724,7 @@ struct uam_ctx {
     hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
     hipStream_t s_lo = nullptr; // low-priority side stream (the waypoint cells beside K2h)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_bs[2] = {}, ev_be[2] = {};  // uam_eval_generated_batches: sorted / evaluated
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     // uam_load_tiles: two page-locked chunk buffers, each reused once its copy has completed
     char* tring[2] = {nullptr, nullptr};
@@ -7037,10 +6837,12 @@ int ktime_begin(uam_ctx* ctx, hipStream_t s) {
     return UAM_OK;
 }
 
-int ktime_end(uam_ctx* ctx, hipStream_t s) {
+// n: the evaluations the pair covers (uam_eval_generated_batches: its batches)
+int ktime_end(uam_ctx* ctx, hipStream_t s, int n = 1) {
     if (!ctx->ktime_on) return UAM_OK;
     HIP_TRY(hipEventRecord(ctx->ktime_ev[ctx->ktime_n].second, s));
     ++ctx->ktime_n;
+    ctx->ktime_acc_n += n - 1;
     return UAM_OK;
 }
 
@@ -7155,6 +6957,8 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    for (hipEvent_t e : {ctx->ev_bs[0], ctx->ev_bs[1], ctx->ev_be[0], ctx->ev_be[1]})
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ktime_ev) {
         (void)hipEventSynchronize(e.second);
         (void)hipEventDestroy(e.first);
@@ -7258,13 +7062,7 @@ int uam_set_geometry(uam_ctx* ctx, const uam_geometry* geom) {
 // 1 = obstacles by box_obs for psi (SHAPE_CULL_PSI), 2 = obstacles by box_obs for contains
 // (SHAPE_CULL_HIT); a shape without its cull flag is listed in every cell and in the off-grid
 // slot.  The grid spans the union of the flagged boxes.
-#ifndef UAM_SHAPE_GRID_N
-#define UAM_SHAPE_GRID_N 64  // (a build knob for measurement)
-#endif
 static constexpr int kShapeGridN = UAM_SHAPE_GRID_N;
-#ifndef UAM_GRID_REFINE
-#define UAM_GRID_REFINE 1  // measurement switch: 0 lists every cell a shape's box meets
-#endif
 
 // true when inequality q's h exceeds thr over the whole rectangle [rx0, rx1] x [ry0, ry1] by a
 // margin far above any evaluation's rounding (h affine in a half-plane or square side: its
@@ -7494,11 +7292,6 @@ int uam_raster_build(uam_ctx* ctx, const uam_raster_desc* desc, const float* dem
                            (spt > 0 ? (int64_t)((sny + spt - 1) / spt) * spt : sny);
     // (the column order's XCD mapping wants a multiple of 8 workgroups; a capped grid loops,
     // each wave prefetching its next strip's DEM)
-#ifndef UAM_K1_GRID_CAP
-// cfg3 map at 4096^2 (32 768 strip workgroups): uncapped 0.185 ms, 16 384 0.179, 12 288
-// 0.197, 8192 0.176, 6144 0.205, 4096 0.193, 2048 0.254 (profiles/r05/cc15, cc16)
-#define UAM_K1_GRID_CAP 8192
-#endif
     const dim3 gs((grid_for(strips * 64, 256, UAM_K1_GRID_CAP) + 7) & ~7);
     switch (cpl) {
         case 1:  // the single-cell kernel
@@ -7683,18 +7476,6 @@ int uam_eval_waypoints(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     return UAM_OK;
 }
 
-#ifdef UAM_K3B_DIAG
-// diagnostics build only: read and clear the K3b counters; set the phase-skip mask
-int uam_k3b_diag(uint64_t* out8, int32_t skip) {
-    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_k3b_diag), 16 * sizeof(uint64_t)));
-    HIP_TRY(hipMemcpyFromSymbol(out8 + 16, HIP_SYMBOL(g_k3b_ev), 8 * sizeof(uint64_t)));
-    const uint64_t z[16] = {};
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_ev), z, 8 * sizeof(uint64_t)));
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_diag), z, sizeof(z)));
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_k3b_skip), &skip, sizeof(skip)));
-    return UAM_OK;
-}
-#endif
 
 int uam_kernel_timing(uam_ctx* ctx, int32_t enable) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
@@ -8149,12 +7930,28 @@ static void magic_div(uint32_t D, uint64_t* m, int32_t* sh) {
     *m = (uint64_t)(((one << *sh) + D - 1) / D);
 }
 
-// K2g launch (segment-grouped raster evaluation); returns 1 if launched, 0 if the batch is not
-// one it takes (the caller runs K2s / K2).  Needs the packed raster.  Scratch: the pair-order
-// scratch (order_scratch), so two streams sharing the context serialise on it.
-static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
-                          int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
-                          int32_t* best_f, int32_t* best_l, hipStream_t s) {
+// One K2g / K2h launch sequence (segment-grouped raster evaluation): what grouped_plan decides
+// for a batch, then its scratch carved by grouped_carve, then the launches (grouped_sort: the
+// counting sort's histogram, scan and scatter; grouped_eval; grouped_final: the output launch)
+using GEvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
+using HEvalFn = void (*)(KParams, KRaster, KGrp);
+using GFinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
+struct GPlan {
+    KGrp kg;
+    bool sim;                 // K2h (the similarity form); K2g otherwise
+    int64_t ncnt, nsb;        // counts ([bins][G_NBK]) and scan blocks
+    size_t lds, hist_dyn, ubytes, bytes;  // eval / histogram dynamic LDS, arc rows, scratch
+    size_t b_key, b_cnt, b_tot, b_ord, b_slot, b_ug, b_err, b_lbp;
+    int bs;                   // evaluation workgroup
+    GEvalFn ev;
+    HEvalFn hev;
+    GFinalFn fin;
+};
+
+// the sequence a batch takes: 1 (pl filled, scratch not yet carved), 0 when the batch is not
+// one K2g / K2h takes, < 0 on error
+static int grouped_plan(uam_ctx* ctx, const KRaster& kr, const double* pairs, int64_t n_pairs,
+                        const double* utab, int32_t D, const KOut& ko, GPlan* pl) {
     const int G = ctx->k2g_group;
     if (G < 1 || G > G_MAXLEN || !kr.pmap || ko.g_rows || D > 16) return 0;
     const int64_t W = ctx->kp.N + 2, P = n_pairs * D;
@@ -8170,30 +7967,27 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         while (tbits < G_TBITS_MAX && (std::max(kr.nx, kr.ny) >> tbits) > 256) ++tbits;
     }
     const int tiles = 1 << (2 * tbits);
-#ifndef UAM_K2G_NO_LASTBIN  // (measurement builds: mixed group lengths in one key space)
     const int last_bin = (W % G) ? tiles : 0;  // a ragged last group gets its own bins
-#else
-    const int last_bin = 0;
-#endif
     const int bins = tiles + last_bin + 1;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const int64_t ncnt = (int64_t)bins * G_NBK;
-    const int64_t nsb = (ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
-    if (nsb > 4096) return 0;
+    pl->ncnt = (int64_t)bins * G_NBK;
+    pl->nsb = (pl->ncnt + 256 * SCAN_ITEMS - 1) / (256 * SCAN_ITEMS);
+    if (pl->nsb > 4096) return 0;
     // K2h (the similarity form) unless disabled or maxratio_smooth (its turn rows are not
     // scale-free): 24-B slots, the geometry in the output launch
     // and its 32-bit offsets reach the whole packed copy; N <= 4096 (Phi / N by the reciprocal)
     const bool sim = ctx->k2g_sim && !ctx->kp.maxratio_smooth && kr.pk && ctx->kp.N <= 4096;
-    const size_t b_key = al((size_t)n_items * 2), b_cnt = al((size_t)ncnt * 4),
-                 b_tot = al(4096 * 4), b_ord = al((size_t)n_items * 4),
-                 b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot))),
-                 b_ug = al((size_t)D * sizeof(UGeo)), b_err = 256,
-                 b_lbp = sim ? al((size_t)P * 4) : 0;
-    char* w = nullptr;
-    int st = order_scratch(ctx, b_key + b_cnt + b_tot + b_ord + b_slot + b_ug + b_err + b_lbp, s,
-                           &w);
-    if (st) return st;
-    KGrp kg{};
+    pl->sim = sim;
+    pl->ubytes = ubytes;
+    pl->b_key = al((size_t)n_items * 2), pl->b_cnt = al((size_t)pl->ncnt * 4);
+    pl->b_tot = al(4096 * 4), pl->b_ord = al((size_t)n_items * 4);
+    pl->b_slot = al((size_t)n_items * (sim ? sizeof(HSlot) : sizeof(GSlot)));
+    pl->b_ug = al((size_t)D * sizeof(UGeo)), pl->b_err = 256;
+    pl->b_lbp = sim ? al((size_t)P * 4) : 0;
+    pl->bytes = pl->b_key + pl->b_cnt + pl->b_tot + pl->b_ord + pl->b_slot + pl->b_ug +
+                pl->b_err + pl->b_lbp;
+    KGrp& kg = pl->kg;
+    kg = KGrp{};
     kg.pairs = pairs;
     kg.utab = utab;
     kg.n_pairs = n_pairs;
@@ -8208,30 +8002,13 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     kg.tbits = tbits;
     kg.bins = bins;
     kg.last_bin = last_bin;
-    st = tile_keys(ctx, tbits, ctx->k2g_curve, s);
-    if (st) return st;
-    kg.tkey = ctx->d_tkey;
     magic_div((uint32_t)nseg, &kg.m_nseg, &kg.sh_nseg);
     magic_div((uint32_t)D, &kg.m_d, &kg.sh_d);
     kg.inv_n = ctx->kp.N <= 4096 ? 1.0 / (double)ctx->kp.N : 0.0;
     kg.n_items = n_items;
     kg.lb_stride = ctx->k2h_lbs;
-    size_t o = 0;
-    kg.slot = (GSlot*)(w + o), o += b_slot;  // 256-B aligned slots first (HSlot for K2h)
-    kg.ugeo = sim ? (UGeo*)(w + o) : nullptr, o += b_ug;
-    kg.order = (int32_t*)(w + o), o += b_ord;
-    kg.cnt = (int32_t*)(w + o), o += b_cnt;
-    kg.tot = (int32_t*)(w + o), o += b_tot;
-    kg.err = (int32_t*)(w + o), o += b_err;
-    st = err_word(ctx, &kg);
-    if (st) return st;
-    kg.lbp = sim && !ctx->k2h_te && ctx->k2h_lbs > 0 ? (float*)(w + o) : nullptr, o += b_lbp;
-    // the seeds' header and unit-arc reads from LDS when both fit beside the histogram's own
-    const size_t hist_dyn = kg.lbp ? (size_t)kr.hwords * 4 + ubytes : 0;
-    kg.seed_lds = kg.lbp && hist_dyn <= (size_t)G_HIST_DYN_MAX;
-    kg.key = (uint16_t*)(w + o);
-    using EvalFn = void (*)(KParams, KRaster, KGrp, const uint4*);
-    using HEvalFn = void (*)(KParams, KRaster, KGrp);
+    kg.nsb_raw = pl->nsb <= 1024 ? (int32_t)pl->nsb : 0;  // up to 1024 totals: scanned by the
+                                                          // scatter
     // gathers in flight per lane (K2g, profiles/r03/k2g9, cfg3: 8 at G = 21 0.337 ms, 11 0.350,
     // 10 0.369, 6 0.351; K2h: 7, groups of 21 = three full chunks).  A raster far beyond the
     // L2s (over 2^25 cells: cfg4's 8192^2) misses more: fewer items resident per XCD (3
@@ -8239,22 +8016,23 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     // 0.886 against 0.936 ms, profiles/r04/sweep7)
     const bool big = sim && (int64_t)kr.nx * kr.ny > ((int64_t)1 << 25);
     const int chl = ctx->k2g_chunk ? ctx->k2g_chunk : big ? 11 : sim ? 7 : 8;
-    size_t lds;
-    int bs;
-    EvalFn ev = nullptr;
-    HEvalFn hev = nullptr;
+    pl->ev = nullptr;
+    pl->hev = nullptr;
+    const bool lbp = sim && !ctx->k2h_te && ctx->k2h_lbs > 0;
+    // the seeds' header and unit-arc reads from LDS when both fit beside the histogram's own
+    pl->hist_dyn = lbp ? (size_t)kr.hwords * 4 + ubytes : 0;
     if (sim) {  // K2h: H_BS-item workgroups, the packed header in LDS
         static const HEvalFn hevals[8] = {k_h_eval<6, false>, k_h_eval<7, false>,
                                           k_h_eval<8, false>, k_h_eval<11, false>,
                                           k_h_eval<6, true>,  k_h_eval<7, true>,
                                           k_h_eval<8, true>,  k_h_eval<11, true>};
-        hev = hevals[(chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3) + (ctx->k2h_te ? 4 : 0)];
-        bs = H_BS;
+        pl->hev = hevals[(chl <= 6 ? 0 : chl == 7 ? 1 : chl == 8 ? 2 : 3) + (ctx->k2h_te ? 4 : 0)];
+        pl->bs = H_BS;
         const size_t hw = ctx->k2h_te ? (size_t)kr.bnd_off : (size_t)kr.hwords;
         const size_t need = hw * 4 + ubytes + (size_t)16 * (G + 16);  // + padding
         const int floor_lds = ctx->k2g_lds ? ctx->k2g_lds : big ? 54000 : 0;
-        lds = std::max(need, (size_t)std::min(floor_lds, 160 * 1024));
-        if (lds > 160 * 1024) return 0;
+        pl->lds = std::max(need, (size_t)std::min(floor_lds, 160 * 1024));
+        if (pl->lds > 160 * 1024) return 0;
         if (!ctx->k2h_attrs) {  // per context = per device (DeviceGuard active)
             for (HEvalFn f : hevals)
                 HIP_TRY(hipFuncSetAttribute((const void*)f,
@@ -8266,69 +8044,110 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     } else {  // K2g: 256-item workgroups, the code map in LDS
 #define UAM_G_EVALS(CH) k_g_eval<CH, false, false>, k_g_eval<CH, false, true>, \
                         k_g_eval<CH, true, false>, k_g_eval<CH, true, true>
-#ifndef UAM_K2G_CH6
-#define UAM_K2G_CH6 6
-#endif
-        static const EvalFn evals[16] = {UAM_G_EVALS(UAM_K2G_CH6), UAM_G_EVALS(8),
-                                         UAM_G_EVALS(11), UAM_G_EVALS(16)};
+        static const GEvalFn evals[16] = {UAM_G_EVALS(6), UAM_G_EVALS(8), UAM_G_EVALS(11),
+                                          UAM_G_EVALS(16)};
 #undef UAM_G_EVALS
         const int ch = (chl == 6 || chl == 7 ? 0 : chl == 8 ? 1 : chl == 11 ? 2 : 3) * 4 +
                        (ctx->kp.length_smooth ? 2 : 0) + (ctx->kp.maxratio_smooth ? 1 : 0);
-        ev = evals[ch];
-        bs = 256;
+        pl->ev = evals[ch];
+        pl->bs = 256;
         const size_t need = (size_t)((kr.pwords + 3) & ~3) * 4 + ubytes + 16;
-        lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
-        if (lds > 64 * 1024 && !ctx->k2g_attrs) {
-            for (EvalFn f : evals)
+        pl->lds = std::max(need, (size_t)std::min(ctx->k2g_lds, 160 * 1024));
+        if (pl->lds > 64 * 1024 && !ctx->k2g_attrs) {
+            for (GEvalFn f : evals)
                 HIP_TRY(hipFuncSetAttribute((const void*)f,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             ctx->k2g_attrs = true;
         }
     }
+    // the output launch holds a path's slots in registers up to 8 groups
+    pl->fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
+                  : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
+    const int st = err_word(ctx, &kg);  // (kg.tkey: the launchers, after tile_keys)
+    return st ? st : 1;
+}
+
+// the plan's scratch at w (pl->bytes, 256-B aligned)
+static void grouped_carve(uam_ctx* ctx, GPlan* pl, char* w) {
+    KGrp& kg = pl->kg;
+    size_t o = 0;
+    kg.slot = (GSlot*)(w + o), o += pl->b_slot;  // 256-B aligned slots first (HSlot for K2h)
+    kg.ugeo = pl->sim ? (UGeo*)(w + o) : nullptr, o += pl->b_ug;
+    kg.order = (int32_t*)(w + o), o += pl->b_ord;
+    kg.cnt = (int32_t*)(w + o), o += pl->b_cnt;
+    kg.tot = (int32_t*)(w + o), o += pl->b_tot;
+    kg.err = (int32_t*)(w + o), o += pl->b_err;
+    kg.lbp = pl->sim && !ctx->k2h_te && ctx->k2h_lbs > 0 ? (float*)(w + o) : nullptr;
+    o += pl->b_lbp;
+    kg.seed_lds = kg.lbp && pl->hist_dyn <= (size_t)G_HIST_DYN_MAX;
+    kg.key = (uint16_t*)(w + o);
+}
+
+static void grouped_sort(uam_ctx* ctx, const GPlan& pl, const KRaster& kr, hipStream_t s) {
+    const KGrp& kg = pl.kg;
+    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? pl.hist_dyn : 0, s,
+                       ctx->kp, kr, kg);
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)pl.nsb), dim3(256), 0, s, kg.cnt, pl.ncnt,
+                       kg.cnt, kg.tot);
+    if (!kg.nsb_raw)
+        hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)pl.nsb);
+    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp,
+                       kg);
+}
+
+static void grouped_eval(uam_ctx* ctx, const GPlan& pl, const KRaster& kr, const void* rec,
+                         hipStream_t s) {
+    const dim3 grid((unsigned)((pl.kg.n_items + pl.bs - 1) / pl.bs));
+    if (pl.hev)
+        hipLaunchKernelGGL(pl.hev, grid, dim3(pl.bs), pl.lds, s, ctx->kp, kr, pl.kg);
+    else
+        hipLaunchKernelGGL(pl.ev, grid, dim3(pl.bs), pl.lds, s, ctx->kp, kr, pl.kg,
+                           (const uint4*)rec);
+}
+
+static void grouped_final(uam_ctx* ctx, const GPlan& pl, const KOut& ko, int32_t* best_f,
+                          int32_t* best_l, hipStream_t s) {
+    const int D = pl.kg.D;
+    hipLaunchKernelGGL(pl.fin, dim3((unsigned)((pl.kg.n_pairs + 63) / 64)), dim3(64 * D),
+                       (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, pl.kg, ko, best_f,
+                       best_l);
+}
+
+// K2g launch (segment-grouped raster evaluation); returns 1 if launched, 0 if the batch is not
+// one it takes (the caller runs K2s / K2).  Needs the packed raster.  Scratch: the pair-order
+// scratch (order_scratch), so two streams sharing the context serialise on it.
+static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, const double* pairs,
+                          int64_t n_pairs, const double* utab, int32_t D, const KOut& ko,
+                          int32_t* best_f, int32_t* best_l, hipStream_t s) {
+    GPlan pl;
+    int st = grouped_plan(ctx, kr, pairs, n_pairs, utab, D, ko, &pl);
+    if (st <= 0) return st;
+    char* w = nullptr;
+    st = order_scratch(ctx, pl.bytes, s, &w);
+    if (st) return st;
+    st = tile_keys(ctx, pl.kg.tbits, ctx->k2g_curve, s);  // (enqueued only when they change)
+    if (st) return st;
+    pl.kg.tkey = ctx->d_tkey;
+    grouped_carve(ctx, &pl, w);
+    KGrp& kg = pl.kg;
     kg.cells = ko.cells;
     // the waypoint cells depend on the pairs and arc rows only: k_cells (VALU and store bound)
-    // runs on the side stream beside the sort and the gathers (miss bound), joined before the
-    // end of the call (UAM_CELLS_SIDE 0: after the evaluation on the caller's stream; 2: forked
-    // after the scatter, beside the evaluation only -- 0.363 ms, profiles/r05/cc9)
-#ifndef UAM_CELLS_SIDE
-#define UAM_CELLS_SIDE 1
-#endif
-    const bool cells_side = ko.cells && UAM_CELLS_SIDE;
-#ifndef UAM_CELLS_PRIO_LOW
-// the cells on a side stream of the device's lowest priority, so the sort's and the
-// evaluation's workgroups dispatch first and the cells fill what they leave (cfg3 with cells
-// 0.353 against 0.358 ms at normal priority; profiles/r05/cc20)
-#define UAM_CELLS_PRIO_LOW 1
-#endif
-    if (cells_side) {
-        st = UAM_CELLS_PRIO_LOW ? side_stream_lo(ctx) : side_stream(ctx);
+    // runs beside the sort and the gathers (miss bound) on a side stream of the device's lowest
+    // priority, so their workgroups dispatch first and the cells fill what they leave, on a
+    // grid capped at 512 workgroups looping over the 64-path blocks; joined before the call
+    // returns.  cfg3 with cells (profiles/r05/cc9, cc10, cc20): 0.350-0.353 ms; at normal
+    // priority 0.355-0.358; forked after the scatter 0.363; inline after the evaluation 0.362;
+    // uncapped 0.372; the arc rows from global memory instead of LDS 0.005-0.02 ms more
+    if (ko.cells) {
+        st = side_stream_lo(ctx);
         if (st) return st;
     }
-    const hipStream_t s_cells = UAM_CELLS_PRIO_LOW ? ctx->s_lo : ctx->s2;
     st = ktime_begin(ctx, s);
     if (st) return st;
-#ifndef UAM_CELLS_GRID
-// workgroups of the cells launch, looping over the 64-path blocks (0: one per block).  On the
-// side stream a capped grid takes a share of the CUs beside the sort and the gathers instead
-// of holding them all first (cfg3 with cells: 0.357 ms at 256-512, 0.372 uncapped, 0.362
-// inline after the evaluation; profiles/r05/cc9, cc10)
-#define UAM_CELLS_GRID 512
-#endif
-    const unsigned cells_wg = (unsigned)std::min<int64_t>(
-        (P + 63) / 64, UAM_CELLS_GRID > 0 ? UAM_CELLS_GRID : INT32_MAX);
-#ifndef UAM_CELLS_ULDS
-#define UAM_CELLS_ULDS 1  // (0: the arc rows from global memory, 3 KiB of LDS per workgroup)
-#endif
+    const int64_t P = kg.P;
+    const unsigned cells_wg = (unsigned)std::min<int64_t>((P + 63) / 64, 512);
     void (*const cells_fn)(KParams, KRaster, KGrp, int32_t*) =
-        UAM_CELLS_ULDS && (int64_t)D * ctx->kp.N <= 1024 ? k_cells<true> : k_cells<false>;
-    auto fork_cells = [&]() -> int {
-        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(s_cells, ctx->ev_fork, 0));
-        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, s_cells, ctx->kp, kr, kg,
-                           ko.cells);
-        HIP_TRY(hipEventRecord(ctx->ev_join, s_cells));
-        return UAM_OK;
-    };
+        (int64_t)D * ctx->kp.N <= 1024 ? k_cells<true> : k_cells<false>;
     // once the cells are forked, every exit makes the caller's stream wait for them (an error
     // return must not leave k_cells writing the caller's buffer behind the call)
     bool forked = false;
@@ -8340,45 +8159,99 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         }
         return r;
     };
-    if (cells_side && UAM_CELLS_SIDE == 1) {
-        st = fork_cells();
-        if (st) return st;
+    if (ko.cells) {
+        HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->s_lo, ctx->ev_fork, 0));
+        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, ctx->s_lo, ctx->kp, kr, kg,
+                           ko.cells);
+        HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s_lo));
         forked = true;
     }
-    hipLaunchKernelGGL(k_g_hist, dim3(G_NBK), dim3(1024), kg.seed_lds ? hist_dyn : 0, s,
-                       ctx->kp, kr, kg);
-    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nsb), dim3(256), 0, s, kg.cnt, ncnt, kg.cnt,
-                       kg.tot);
-    kg.nsb_raw = nsb <= 1024 ? (int32_t)nsb : 0;  // up to 1024 totals: scanned by the scatter
-    if (!kg.nsb_raw)
-        hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(1024), 0, s, kg.tot, (int)nsb);
-    hipLaunchKernelGGL(k_g_scatter, dim3(G_NBK + (kg.ugeo ? 1 : 0)), dim3(1024), 0, s, ctx->kp, kg);
-    if (cells_side && UAM_CELLS_SIDE == 2) {  // (beside the evaluation only)
-        st = fork_cells();
-        if (st) return st;
-        forked = true;
-    }
-    if (hev)
-        hipLaunchKernelGGL(hev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
-                           ctx->kp, kr, kg);
-    else
-        hipLaunchKernelGGL(ev, dim3((unsigned)((n_items + bs - 1) / bs)), dim3(bs), lds, s,
-                           ctx->kp, kr, kg, (const uint4*)rec);
-    if (ko.cells && !cells_side)
-        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, s, ctx->kp, kr, kg, ko.cells);
-    // the output launch holds a path's slots in registers up to 8 groups
-    using FinalFn = void (*)(KParams, KGrp, KOut, int32_t*, int32_t*);
-    const FinalFn fin = sim ? (nseg <= 4 ? k_h_final<4> : nseg <= 8 ? k_h_final<8> : k_h_final<0>)
-                            : nseg <= 4 ? k_g_final<4> : nseg <= 8 ? k_g_final<8> : k_g_final<0>;
-    hipLaunchKernelGGL(fin, dim3((unsigned)((n_pairs + 63) / 64)), dim3(64 * D),
-                       (size_t)2 * 64 * D * sizeof(double), s, ctx->kp, kg, ko, best_f, best_l);
+    grouped_sort(ctx, pl, kr, s);
+    grouped_eval(ctx, pl, kr, rec, s);
+    grouped_final(ctx, pl, ko, best_f, best_l, s);
     if (hipGetLastError() != hipSuccess) return join(fail(UAM_E_HIP, "grouped evaluation launch"));
     st = join(UAM_OK);
     if (st) return st;
-    st = ktime_end(ctx, s);
+    st = ktime_end(ctx, s, 1);
     if (st) return st;
-    ctx->last_group = G;
-    ctx->last_kernel = sim ? "K2h+pack" : "K2g+pack";
+    ctx->last_group = pl.kg.G;
+    ctx->last_kernel = pl.sim ? "K2h+pack" : "K2g+pack";
+    st = order_done(ctx, s);
+    return st ? st : 1;
+}
+
+// K2h over a list of batches (uam_eval_generated_batches): batch k's counting sort and the
+// output launch of batch k - 1 run on the context's side stream while batch k - 1 / k
+// evaluates on the caller's stream.  Two scratch sets (batch k uses set k % 2):
+//   side:   sort 0, sort 1, [eval 0 done] final 0, sort 2, [eval 1 done] final 1, sort 3, ...
+//   caller: [sort 0 done] eval 0, [sort 1 done] eval 1, [sort 2 done] eval 2, ...
+// so sort k + 2 (which rewrites set k % 2's keys, order and check word) follows eval k and
+// final k, and eval k + 2 (which rewrites its slots) follows final k.  Every batch does its own
+// sort and its own evaluation -- nothing is shared between batches but the raster and the
+// arc rows.  Returns 1 if launched; 0 if some batch is not one K2h takes (the caller then runs
+// the batches one call at a time).
+static int launch_grouped_batches(uam_ctx* ctx, const KRaster& kr, int32_t n_batches,
+                                  const double* const* pairs, const int64_t* n_pairs,
+                                  const double* utab, int32_t D, const KOut* ko,
+                                  int32_t* const* best_f, int32_t* const* best_l, hipStream_t s) {
+    if (n_batches < 2 || n_batches > UAM_MAX_BATCHES) return 0;
+    std::vector<GPlan> pl((size_t)n_batches);
+    size_t half = 0;
+    for (int k = 0; k < n_batches; ++k) {
+        if (ko[k].cells) return 0;
+        const int st = grouped_plan(ctx, kr, pairs[k], n_pairs[k], utab, D, ko[k], &pl[k]);
+        if (st <= 0) return st;
+        if (!pl[k].sim) return 0;
+        half = std::max(half, pl[k].bytes);
+    }
+    int st = side_stream(ctx);
+    if (st) return st;
+    for (hipEvent_t* e : {&ctx->ev_bs[0], &ctx->ev_bs[1], &ctx->ev_be[0], &ctx->ev_be[1]})
+        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    char* w = nullptr;
+    st = order_scratch(ctx, 2 * half, s, &w);
+    if (st) return st;
+    st = tile_keys(ctx, pl[0].kg.tbits, ctx->k2g_curve, s);  // (one raster: one tile grid)
+    if (st) return st;
+    for (int k = 0; k < n_batches; ++k) {
+        pl[k].kg.tkey = ctx->d_tkey;
+        grouped_carve(ctx, &pl[k], w + (k & 1) * half);
+    }
+    const hipStream_t b = ctx->s2;
+    st = ktime_begin(ctx, s);
+    if (st) return st;
+    // the side stream starts behind everything enqueued on the caller's stream so far
+    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(b, ctx->ev_fork, 0));
+    grouped_sort(ctx, pl[0], kr, b);
+    HIP_TRY(hipEventRecord(ctx->ev_bs[0], b));
+    grouped_sort(ctx, pl[1], kr, b);
+    HIP_TRY(hipEventRecord(ctx->ev_bs[1], b));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_bs[0], 0));
+    grouped_eval(ctx, pl[0], kr, nullptr, s);
+    HIP_TRY(hipEventRecord(ctx->ev_be[0], s));
+    for (int k = 0; k < n_batches; ++k) {
+        const int c = k & 1;
+        HIP_TRY(hipStreamWaitEvent(b, ctx->ev_be[c], 0));
+        grouped_final(ctx, pl[k], ko[k], best_f[k], best_l[k], b);
+        if (k + 2 < n_batches) {
+            grouped_sort(ctx, pl[k + 2], kr, b);
+            HIP_TRY(hipEventRecord(ctx->ev_bs[c], b));
+        }
+        if (k + 1 < n_batches) {
+            HIP_TRY(hipStreamWaitEvent(s, ctx->ev_bs[c ^ 1], 0));
+            grouped_eval(ctx, pl[k + 1], kr, nullptr, s);
+            HIP_TRY(hipEventRecord(ctx->ev_be[c ^ 1], s));
+        }
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_join, b));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "batched evaluation launch");
+    st = ktime_end(ctx, s, n_batches);
+    if (st) return st;
+    ctx->last_group = pl[0].kg.G;
+    ctx->last_kernel = "K2h+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -8613,6 +8486,32 @@ static void set_kpack(KRaster* kr, const PackDims& d, const void* packed) {
     kr->op8 = (uint32_t)d.off_p8;
 }
 
+// the raster's descriptor and its derived copies as the evaluations read them
+static int raster_inputs(const uam_raster_desc* desc, const void* rec, const uint32_t* summary,
+                         int32_t sblock, const void* packed, KRaster* kr) {
+    int st = make_kraster(desc, kr);
+    if (st) return st;
+    if (!rec) return fail(UAM_E_INVALID, "raster mode needs rec");
+    if (summary) {
+        int32_t sh, nbx, nby;
+        st = summary_dims(desc, sblock, &sh, &nbx, &nby);
+        if (st) return st;
+        kr->sum = summary;
+        kr->sshift = sh;
+        kr->snbx = nbx;
+        kr->swords = (nbx * nby + 31) / 32;
+    }
+    if (packed) {
+        PackDims pd;
+        st = pack_dims(desc, sblock, &pd);
+        if (st) return st;
+        kr->sshift = pd.sh;  // the block codes use the summary's block grid
+        kr->snbx = pd.nbx;
+        set_kpack(kr, pd, packed);
+    }
+    return UAM_OK;
+}
+
 static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                           const void* rec, const uint32_t* summary, int32_t sblock,
                           const double* pairs, int64_t n_pairs, const double* utab, int32_t D,
@@ -8625,26 +8524,8 @@ static int eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* des
     if (!pairs || !utab) return fail(UAM_E_INVALID, "pairs/utab is NULL");
     KRaster kr{};
     if (mode == UAM_MODE_RASTER) {
-        st = make_kraster(desc, &kr);
+        st = raster_inputs(desc, rec, summary, sblock, packed, &kr);
         if (st) return st;
-        if (!rec) return fail(UAM_E_INVALID, "raster mode needs rec");
-        if (summary) {
-            int32_t sh, nbx, nby;
-            st = summary_dims(desc, sblock, &sh, &nbx, &nby);
-            if (st) return st;
-            kr.sum = summary;
-            kr.sshift = sh;
-            kr.snbx = nbx;
-            kr.swords = (nbx * nby + 31) / 32;
-        }
-        if (packed) {
-            PackDims pd;
-            st = pack_dims(desc, sblock, &pd);
-            if (st) return st;
-            kr.sshift = pd.sh;  // the block codes use the summary's block grid
-            kr.snbx = pd.nbx;
-            set_kpack(&kr, pd, packed);
-        }
     } else if (mode != UAM_MODE_ANALYTIC) {
         return fail(UAM_E_INVALID, "unknown mode %d", mode);
     }
@@ -8790,6 +8671,54 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     }
     return eval_generated(ctx, mode, desc, rec, summary, block, pairs, n_pairs, utab, D, out,
                           stream, packed);
+}
+
+int uam_eval_generated_batches(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
+                               const uint32_t* summary, int32_t block, const void* packed,
+                               int32_t n_batches, const double* const* pairs,
+                               const int64_t* n_pairs, const double* utab, int32_t D,
+                               const uam_path_outputs* outs, uam_stream stream) {
+    int st = check_ctx(ctx, true);
+    if (st) return st;
+    st = device_status(ctx);  // an earlier call's failed device check, reported once
+    if (st) return st;
+    if (n_batches < 0 || n_batches > UAM_MAX_BATCHES)
+        return fail(UAM_E_INVALID, "n_batches %d outside [0, %d]", n_batches, UAM_MAX_BATCHES);
+    if (n_batches == 0) return UAM_OK;
+    if (!pairs || !n_pairs || !outs || !utab)
+        return fail(UAM_E_INVALID, "pairs / n_pairs / outs / utab is NULL");
+    if (D < 1) return fail(UAM_E_INVALID, "D < 1");
+    for (int k = 0; k < n_batches; ++k)
+        if (n_pairs[k] < 1 || !pairs[k])
+            return fail(UAM_E_INVALID, "batch %d: n_pairs %lld < 1 or pairs NULL", k,
+                        (long long)n_pairs[k]);
+    KRaster kr{};
+    st = raster_inputs(desc, rec, summary, block, packed, &kr);
+    if (st) return st;
+    std::vector<KOut> ko((size_t)n_batches);
+    std::vector<int32_t*> bf((size_t)n_batches), bl((size_t)n_batches);
+    for (int k = 0; k < n_batches; ++k) {
+        ko[k] = make_kout(&outs[k]);
+        bf[k] = outs[k].best_fval_idx;
+        bl[k] = outs[k].best_length_idx;
+    }
+    {
+        DeviceGuard dg(ctx->device);
+        ctx->last_group = 0;
+        if (ctx->k2g_group > 0) {
+            st = launch_grouped_batches(ctx, kr, n_batches, pairs, n_pairs, utab, D, ko.data(),
+                                        bf.data(), bl.data(), (hipStream_t)stream);
+            if (st < 0) return st;
+            if (st == 1) return UAM_OK;
+        }
+    }
+    // not a K2h batch list: one call per batch, in order
+    for (int k = 0; k < n_batches; ++k) {
+        st = eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs[k], n_pairs[k],
+                            utab, D, &outs[k], stream, packed);
+        if (st) return st;
+    }
+    return UAM_OK;
 }
 
 int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,
@@ -9734,24 +9663,6 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     g_pinned->reset();
     g_devarena = (DevArena*)ctx->devarena;
     g_devarena->reset();
-    // -DUAM_K8_PROF (diagnostics build): host timestamps of the phases (at the existing
-    // synchronisation points)
-#ifdef UAM_K8_PROF
-    constexpr bool prof = true;
-#else
-    constexpr bool prof = false;
-#endif
-    const auto t_start = std::chrono::steady_clock::now();
-    auto stamp = [&](const char* what) {
-        if (prof)
-            std::fprintf(stderr, "[k8] %-28s %9.3f ms\n", what,
-                         std::chrono::duration<double, std::milli>(
-                             std::chrono::steady_clock::now() - t_start).count());
-    };
-    struct AtExit {  // stamps after every scratch buffer below has been released
-        std::function<void()> f;
-        ~AtExit() { f(); }
-    } at_exit{[&] { stamp("returned (scratch released)"); }};
     DevBuf<int32_t> L;
     HIP_TRY2(L.alloc(n));
     const bool tiled = ctx->k8_tiled;
@@ -9773,7 +9684,6 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
     mj.nx = nx, mj.ny = ny, mj.L = L.p;
     int rc = label_grid(mj, nullptr, nullptr, true, s, tiled);
     if (rc) return rc;
-    stamp("labelled + stats");
     const CompStats& st = mj.st;
     const int32_t ncomp = (int32_t)st.cnt.size();
     const double cell = std::fabs(DX * DY);
@@ -9903,7 +9813,6 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         }
         small_at[c + 1] = (int64_t)small_out.size();
     }
-    stamp("small rectangles (host)");
     HIP_TRY2(sync_all());  // every region's component stats
     for (size_t ri = 0; ri < regs.size(); ++ri) {
         Region& r = regs[ri];
@@ -9914,7 +9823,6 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
         if (rc) return rc;
     }
     HIP_TRY2(sync_all());  // every region's row extents
-    stamp("large regions labelled");
     // rectangles in component order (small: the region; large: its pieces, boxes j (x) outer,
     // k (y) inner -- the reference's order)
     // a large region's pieces are independent host work: up to 8 worker threads take regions
@@ -9960,8 +9868,6 @@ int uam_dem_polygons(uam_ctx* ctx, const float* dem, const uam_raster_desc* rd, 
             ++ri;
         }
     }
-    stamp("all rectangles");
-    if (prof) std::fprintf(stderr, "[k8] components %d, large regions %zu\n", ncomp, regs.size());
     const int64_t nr = (int64_t)out.size() / 8;
     *n_rects = (int32_t)nr;
     if (rect_xy)
@@ -9998,14 +9904,6 @@ int uam_path_length(uam_ctx* ctx, const double* pts, int64_t n_paths, int32_t n_
     return UAM_OK;
 }
 
-#ifdef UAM_EW_PROF
-int uam_debug_ew_prof(uint64_t* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ew_prof), (size_t)std::min(n, 1024 * 8) * 8) ==
-                   hipSuccess
-               ? UAM_OK
-               : UAM_E_HIP;
-}
-#endif
 
 int uam_synchronize(uam_ctx* ctx, uam_stream stream) {
     if (!ctx) return fail(UAM_E_INVALID, "ctx is NULL");
