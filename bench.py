@@ -90,11 +90,6 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="libuampath context option (uam_set_option; names in _lib.OPTIONS), "
                          "repeatable: measurement sweeps of forms that give the same outputs")
-    ap.add_argument("--batches", type=int, default=1,
-                    help="steps submitted per library call (uam_eval_generated_batches, raster "
-                         "K2h only: batch k + 1's sort and batch k - 1's output launch beside "
-                         "batch k's evaluation; every step keeps its own sort, evaluation and "
-                         "output set); 1 = one uam_eval_generated per step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived L2->fabric bytes per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -288,20 +283,9 @@ def main():
         else:
             eng.eval_generated(pairs, ut, raster=raster, outputs=outs)
 
-    # --batches B: B steps per call, each with its own output set (outsets[0] = outs)
-    nb = max(1, args.batches) if raster_mode and not args.cells else 1
-    outsets = [outs] + [eng.outputs(P, W, n_pairs=Q) for _ in range(nb - 1)]
-
     def run_steps(n):
-        if nb == 1:
-            for _ in range(n):
-                step()
-            return
-        done = 0
-        while done < n:
-            b = min(nb, n - done)
-            eng.eval_generated_batches([pairs] * b, ut, raster, outputs=outsets[:b])
-            done += b
+        for _ in range(n):
+            step()
 
     run_steps(args.warmup)
     torch.cuda.synchronize()
@@ -392,8 +376,6 @@ def main():
     roofline["profile_key"] = pkey
     if args.opt:
         roofline["options"] = list(args.opt)
-    if nb > 1:
-        roofline["batches_per_call"] = nb
     result = {
         "metric": METRIC,
         "value": round(value, 1),

@@ -238,23 +238,6 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
                        const double* utab_dev, int32_t D, const uam_path_outputs* out,
                        uam_stream stream);
 
-/* uam_eval_generated (raster mode) over a list of batches, as if called once per batch in
- * order on stream: batch k = pairs_dev[k] [n_pairs[k]][4] (device pointers in a host array),
- * outputs outs[k]; the raster, its copies and utab_dev are shared.  Batches that all run K2h
- * (the default for packed rasters and >= UAM_OPT_SORTED_MIN_PATHS paths; no cells) are
- * pipelined: the counting sort of batch k + 1 and the output launch of batch k - 1 run on the
- * context's side stream beside the evaluation of batch k, with two scratch sets.  Every batch
- * still gets its own sort, evaluation and outputs, bit-identical to uam_eval_generated's; the
- * list is only a throughput shape for a caller holding several batches at once (the candidate
- * loop of main.py:160-193 over many start/goal batches).  Any other list runs one
- * uam_eval_generated per batch.  1 <= n_batches <= UAM_MAX_BATCHES. */
-#define UAM_MAX_BATCHES 64
-int uam_eval_generated_batches(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec_dev,
-                               const uint32_t* summary_dev, int32_t block, const void* packed_dev,
-                               int32_t n_batches, const double* const* pairs_dev,
-                               const int64_t* n_pairs, const double* utab_dev, int32_t D,
-                               const uam_path_outputs* outs, uam_stream stream);
-
 /* K2 gather skip (build-defined; no reference counterpart; results unchanged).  A bitmap
  * summary of a record raster: one bit per block x block cells (blocks row-major, nby x nbx;
  * bit b in 32-bit word b / 32), set when every cell of the block has phi == +-0,

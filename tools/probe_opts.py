@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--R", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cells", action="store_true")
+    ap.add_argument("--share", default=None,
+                    help="R/N: rank R's spatial shard (distributed.spatial_shard) of the --pairs "
+                         "pairs over N ranks (cfg4: --R 8192 --pairs 200000 --share 3/8)")
     ap.add_argument("--volume", action="store_true",
                     help="cfg5: 1024^2 x 64 volume, packed copy, 100k pairs x 5 (K4h / K4)")
     ap.add_argument("--analytic", action="store_true",
@@ -61,7 +64,13 @@ def main():
             e.eval_generated(pairs, ut, raster=None, outputs=outs)
     else:
         raster = e.raster_build(raster_geo(a.R), synthetic_dem(a.R))
-        pairs = e.tensor(random_pairs(a.pairs, seed=0), torch.float64)
+        ph = random_pairs(a.pairs, seed=0)
+        if a.share:
+            from uam_path_planning_amd.distributed import spatial_shard
+            r, n = (int(v) for v in a.share.split("/"))
+            ph, _ = spatial_shard(ph, r, n)
+            a.pairs = len(ph)
+        pairs = e.tensor(ph, torch.float64)
 
         def run():
             e.eval_generated(pairs, ut, raster=raster, outputs=outs)

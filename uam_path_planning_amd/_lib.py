@@ -16,7 +16,6 @@ ABI_VERSION = 2  # include/uampath.h UAM_ABI_VERSION
 MAX_REGIONS = 16
 RECORD_BYTES = 16
 COMM_ID_BYTES = 128
-MAX_BATCHES = 64
 
 UAM_OK, UAM_E_INVALID, UAM_E_HIP, UAM_E_NOMEM, UAM_E_STATE, UAM_E_VERSION = 0, -1, -2, -3, -4, -5
 UAM_E_DEVICE = -6  # a device-side check of an earlier call failed (uam_device_status)
@@ -120,9 +119,6 @@ SIGNATURES = {
     "uam_eval_generated": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(RasterDesc), _vp,
                                           _vp, ctypes.c_int32, _vp, _vp, ctypes.c_int64, _vp,
                                           ctypes.c_int32, ctypes.POINTER(PathOutputs), _vp]),
-    "uam_eval_generated_batches": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, _vp,
-                                                  ctypes.c_int32, _vp, ctypes.c_int32, _vp, _vp,
-                                                  _vp, ctypes.c_int32, _vp, _vp]),
     "uam_raster_summary_shape": (ctypes.c_int, [ctypes.POINTER(RasterDesc), ctypes.c_int32,
                                                 _i32p, _i32p, _i32p]),
     "uam_raster_summary": (ctypes.c_int, [_vp, ctypes.POINTER(RasterDesc), _vp, ctypes.c_int32,

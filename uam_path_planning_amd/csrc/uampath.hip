@@ -6415,7 +6415,7 @@ __global__ __launch_bounds__(1024) void k_v_hist(KParams p, KVol4 vs, KGrp kg) {
 //       gives M >= E >= M, and z - ub > Ub >= M is impossible.  NaN bounds (no bound) always
 //       fetch.
 template <int CH, bool TE>  // TE: the terrain in the entry (UAM_OPT_K2H_TERRAIN 1)
-__global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 8 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
+__global__ __launch_bounds__(256, CH >= 11 ? 2 : CH >= 7 ? 3 : 4) void k_v_eval(KParams p, KVol4 vs,
                                                                               KGrp kg) {
     PK_CODES_CHECK(CH);
     // unit-arc rows + padding, then j / (W-1) (+ padding), then the header
@@ -6724,7 +6724,6 @@ struct uam_ctx {
     hipStream_t s2 = nullptr;   // side stream (K2s: the later segments' sorts beside segment 0)
     hipStream_t s_lo = nullptr; // low-priority side stream (the waypoint cells beside K2h)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipEvent_t ev_bs[2] = {}, ev_be[2] = {};  // uam_eval_generated_batches: sorted / evaluated
     void* pinned = nullptr;     // K8 page-locked host arena (PinnedArena), created on first use
     // uam_load_tiles: two page-locked chunk buffers, each reused once its copy has completed
     char* tring[2] = {nullptr, nullptr};
@@ -6837,12 +6836,10 @@ int ktime_begin(uam_ctx* ctx, hipStream_t s) {
     return UAM_OK;
 }
 
-// n: the evaluations the pair covers (uam_eval_generated_batches: its batches)
-int ktime_end(uam_ctx* ctx, hipStream_t s, int n = 1) {
+int ktime_end(uam_ctx* ctx, hipStream_t s) {
     if (!ctx->ktime_on) return UAM_OK;
     HIP_TRY(hipEventRecord(ctx->ktime_ev[ctx->ktime_n].second, s));
     ++ctx->ktime_n;
-    ctx->ktime_acc_n += n - 1;
     return UAM_OK;
 }
 
@@ -6957,8 +6954,6 @@ void uam_ctx_destroy(uam_ctx* ctx) {
     if (ctx->ev_ord) (void)hipEventDestroy(ctx->ev_ord);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    for (hipEvent_t e : {ctx->ev_bs[0], ctx->ev_bs[1], ctx->ev_be[0], ctx->ev_be[1]})
-        if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ktime_ev) {
         (void)hipEventSynchronize(e.second);
         (void)hipEventDestroy(e.first);
@@ -8173,85 +8168,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (hipGetLastError() != hipSuccess) return join(fail(UAM_E_HIP, "grouped evaluation launch"));
     st = join(UAM_OK);
     if (st) return st;
-    st = ktime_end(ctx, s, 1);
+    st = ktime_end(ctx, s);
     if (st) return st;
     ctx->last_group = pl.kg.G;
     ctx->last_kernel = pl.sim ? "K2h+pack" : "K2g+pack";
-    st = order_done(ctx, s);
-    return st ? st : 1;
-}
-
-// K2h over a list of batches (uam_eval_generated_batches): batch k's counting sort and the
-// output launch of batch k - 1 run on the context's side stream while batch k - 1 / k
-// evaluates on the caller's stream.  Two scratch sets (batch k uses set k % 2):
-//   side:   sort 0, sort 1, [eval 0 done] final 0, sort 2, [eval 1 done] final 1, sort 3, ...
-//   caller: [sort 0 done] eval 0, [sort 1 done] eval 1, [sort 2 done] eval 2, ...
-// so sort k + 2 (which rewrites set k % 2's keys, order and check word) follows eval k and
-// final k, and eval k + 2 (which rewrites its slots) follows final k.  Every batch does its own
-// sort and its own evaluation -- nothing is shared between batches but the raster and the
-// arc rows.  Returns 1 if launched; 0 if some batch is not one K2h takes (the caller then runs
-// the batches one call at a time).
-static int launch_grouped_batches(uam_ctx* ctx, const KRaster& kr, int32_t n_batches,
-                                  const double* const* pairs, const int64_t* n_pairs,
-                                  const double* utab, int32_t D, const KOut* ko,
-                                  int32_t* const* best_f, int32_t* const* best_l, hipStream_t s) {
-    if (n_batches < 2 || n_batches > UAM_MAX_BATCHES) return 0;
-    std::vector<GPlan> pl((size_t)n_batches);
-    size_t half = 0;
-    for (int k = 0; k < n_batches; ++k) {
-        if (ko[k].cells) return 0;
-        const int st = grouped_plan(ctx, kr, pairs[k], n_pairs[k], utab, D, ko[k], &pl[k]);
-        if (st <= 0) return st;
-        if (!pl[k].sim) return 0;
-        half = std::max(half, pl[k].bytes);
-    }
-    int st = side_stream(ctx);
-    if (st) return st;
-    for (hipEvent_t* e : {&ctx->ev_bs[0], &ctx->ev_bs[1], &ctx->ev_be[0], &ctx->ev_be[1]})
-        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    char* w = nullptr;
-    st = order_scratch(ctx, 2 * half, s, &w);
-    if (st) return st;
-    st = tile_keys(ctx, pl[0].kg.tbits, ctx->k2g_curve, s);  // (one raster: one tile grid)
-    if (st) return st;
-    for (int k = 0; k < n_batches; ++k) {
-        pl[k].kg.tkey = ctx->d_tkey;
-        grouped_carve(ctx, &pl[k], w + (k & 1) * half);
-    }
-    const hipStream_t b = ctx->s2;
-    st = ktime_begin(ctx, s);
-    if (st) return st;
-    // the side stream starts behind everything enqueued on the caller's stream so far
-    HIP_TRY(hipEventRecord(ctx->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(b, ctx->ev_fork, 0));
-    grouped_sort(ctx, pl[0], kr, b);
-    HIP_TRY(hipEventRecord(ctx->ev_bs[0], b));
-    grouped_sort(ctx, pl[1], kr, b);
-    HIP_TRY(hipEventRecord(ctx->ev_bs[1], b));
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_bs[0], 0));
-    grouped_eval(ctx, pl[0], kr, nullptr, s);
-    HIP_TRY(hipEventRecord(ctx->ev_be[0], s));
-    for (int k = 0; k < n_batches; ++k) {
-        const int c = k & 1;
-        HIP_TRY(hipStreamWaitEvent(b, ctx->ev_be[c], 0));
-        grouped_final(ctx, pl[k], ko[k], best_f[k], best_l[k], b);
-        if (k + 2 < n_batches) {
-            grouped_sort(ctx, pl[k + 2], kr, b);
-            HIP_TRY(hipEventRecord(ctx->ev_bs[c], b));
-        }
-        if (k + 1 < n_batches) {
-            HIP_TRY(hipStreamWaitEvent(s, ctx->ev_bs[c ^ 1], 0));
-            grouped_eval(ctx, pl[k + 1], kr, nullptr, s);
-            HIP_TRY(hipEventRecord(ctx->ev_be[c ^ 1], s));
-        }
-    }
-    HIP_TRY(hipEventRecord(ctx->ev_join, b));
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
-    if (hipGetLastError() != hipSuccess) return fail(UAM_E_HIP, "batched evaluation launch");
-    st = ktime_end(ctx, s, n_batches);
-    if (st) return st;
-    ctx->last_group = pl[0].kg.G;
-    ctx->last_kernel = "K2h+pack";
     st = order_done(ctx, s);
     return st ? st : 1;
 }
@@ -8671,54 +8591,6 @@ int uam_eval_generated(uam_ctx* ctx, int32_t mode, const uam_raster_desc* desc,
     }
     return eval_generated(ctx, mode, desc, rec, summary, block, pairs, n_pairs, utab, D, out,
                           stream, packed);
-}
-
-int uam_eval_generated_batches(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec,
-                               const uint32_t* summary, int32_t block, const void* packed,
-                               int32_t n_batches, const double* const* pairs,
-                               const int64_t* n_pairs, const double* utab, int32_t D,
-                               const uam_path_outputs* outs, uam_stream stream) {
-    int st = check_ctx(ctx, true);
-    if (st) return st;
-    st = device_status(ctx);  // an earlier call's failed device check, reported once
-    if (st) return st;
-    if (n_batches < 0 || n_batches > UAM_MAX_BATCHES)
-        return fail(UAM_E_INVALID, "n_batches %d outside [0, %d]", n_batches, UAM_MAX_BATCHES);
-    if (n_batches == 0) return UAM_OK;
-    if (!pairs || !n_pairs || !outs || !utab)
-        return fail(UAM_E_INVALID, "pairs / n_pairs / outs / utab is NULL");
-    if (D < 1) return fail(UAM_E_INVALID, "D < 1");
-    for (int k = 0; k < n_batches; ++k)
-        if (n_pairs[k] < 1 || !pairs[k])
-            return fail(UAM_E_INVALID, "batch %d: n_pairs %lld < 1 or pairs NULL", k,
-                        (long long)n_pairs[k]);
-    KRaster kr{};
-    st = raster_inputs(desc, rec, summary, block, packed, &kr);
-    if (st) return st;
-    std::vector<KOut> ko((size_t)n_batches);
-    std::vector<int32_t*> bf((size_t)n_batches), bl((size_t)n_batches);
-    for (int k = 0; k < n_batches; ++k) {
-        ko[k] = make_kout(&outs[k]);
-        bf[k] = outs[k].best_fval_idx;
-        bl[k] = outs[k].best_length_idx;
-    }
-    {
-        DeviceGuard dg(ctx->device);
-        ctx->last_group = 0;
-        if (ctx->k2g_group > 0) {
-            st = launch_grouped_batches(ctx, kr, n_batches, pairs, n_pairs, utab, D, ko.data(),
-                                        bf.data(), bl.data(), (hipStream_t)stream);
-            if (st < 0) return st;
-            if (st == 1) return UAM_OK;
-        }
-    }
-    // not a K2h batch list: one call per batch, in order
-    for (int k = 0; k < n_batches; ++k) {
-        st = eval_generated(ctx, UAM_MODE_RASTER, desc, rec, summary, block, pairs[k], n_pairs[k],
-                            utab, D, &outs[k], stream, packed);
-        if (st) return st;
-    }
-    return UAM_OK;
 }
 
 int uam_raster_pack_shape(const uam_raster_desc* desc, int32_t block, int32_t* block_out,

@@ -412,39 +412,6 @@ class Engine:
             "uam_eval_generated")
         return o
 
-    def eval_generated_batches(self, pairs_list, utab, raster, outputs=None):
-        """eval_generated over several batches in one call (uam_eval_generated_batches): the
-        K2h batches are pipelined -- batch k + 1's sort and batch k - 1's output launch beside
-        batch k's evaluation -- with every batch's outputs identical to its own
-        eval_generated call.  pairs_list: [Q_k, 4] each; returns one output dict per batch
-        (outputs: a list of (dict, struct) from Engine.outputs to reuse)."""
-        torch = _torch()
-        if raster is None:
-            raise ValueError("eval_generated_batches is raster mode: pass a raster")
-        ut = self.tensor(utab, torch.float64)
-        D = ut.shape[0]
-        if ut.shape[1] != self.params.N:
-            raise ValueError(f"arc table has N={ut.shape[1]}, params N={self.params.N}")
-        prs = [self.tensor(p, torch.float64).reshape(-1, 4) for p in pairs_list]
-        K = len(prs)
-        if not 1 <= K <= _lib.MAX_BATCHES:
-            raise ValueError(f"{K} batches: 1..{_lib.MAX_BATCHES} per call")
-        if outputs is None:
-            outputs = [self._outputs(p.shape[0] * D, self.params.N + 2, _lib.MODE_RASTER,
-                                     False, False, n_pairs=p.shape[0]) for p in prs]
-        elif len(outputs) != K:
-            raise ValueError(f"{len(outputs)} output sets for {K} batches")
-        for (o, _), p in zip(outputs, prs):
-            _check_outputs(o, p.shape[0] * D, p.shape[0], self.params.N + 2)
-        ptrs = (ctypes.c_void_p * K)(*[p.data_ptr() for p in prs])
-        nq = (ctypes.c_int64 * K)(*[p.shape[0] for p in prs])
-        structs = (_lib.PathOutputs * K)(*[s for _, s in outputs])
-        _lib.check(self.lib.uam_eval_generated_batches(
-            self._ctx, ctypes.byref(raster.geo.as_struct()), _ptr(raster.rec),
-            _ptr(raster.summary), int(raster.block or 0), _ptr(raster.packed), K, ptrs, nq,
-            _ptr(ut), D, structs, self.stream), "uam_eval_generated_batches")
-        return [o for o, _ in outputs]
-
     # -- volume (config 5) -------------------------------------------------------------
     def volume_alloc(self, vg):
         """An uninitialised volume buffer of VolumeGeo vg (uam_volume_shape), e.g. for a rank
