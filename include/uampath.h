@@ -512,7 +512,7 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K2H_LB_STRIDE        K2h / K4h terrain bounds: the histogram launch samples every
  *                                n-th waypoint of each path and seeds the path's items with the
  *                                exact terrain (clearance) of the sample with the best bound
- *                                (1..1024; default 8; 0: no seed); fewer terrain fetches at
+ *                                (1..1024; default 16; 0: no seed); fewer terrain fetches at
  *                                smaller n, more arithmetic in that launch.  Same outputs.
  *   UAM_OPT_K2H_TERRAIN          K2h's terrain: 1 (default) in the entry (8-B {phi, terrain}
  *                                entries, the 16-B records in no-fly / psi blocks), 0 by bounds

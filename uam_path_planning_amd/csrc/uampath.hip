@@ -4085,10 +4085,19 @@ __global__ __launch_bounds__(256) void k_scan_local(const int32_t* __restrict__ 
     __shared__ int32_t wsum[4];
     const int64_t base = (int64_t)blockIdx.x * 256 * SCAN_ITEMS + (int64_t)threadIdx.x * SCAN_ITEMS;
     int32_t v[SCAN_ITEMS], run = 0;
+    const bool full = base + SCAN_ITEMS <= n;  // a whole run: 16-B loads and stores
+    if (full) {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; k += 4) {
+            const int4 q = *reinterpret_cast<const int4*>(in + base + k);
+            v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = base + k < n ? in[base + k] : 0;
+    }
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const int64_t i = base + k;
-        v[k] = i < n ? in[i] : 0;
         const int32_t t = v[k];
         v[k] = run;
         run += t;
@@ -4106,10 +4115,15 @@ __global__ __launch_bounds__(256) void k_scan_local(const int32_t* __restrict__ 
     int32_t woff = 0;
     for (int k = 0; k < wv; ++k) woff += wsum[k];
     const int32_t excl = woff + x - run;
+    if (full) {
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const int64_t i = base + k;
-        if (i < n) out[i] = v[k] + excl;
+        for (int k = 0; k < SCAN_ITEMS; k += 4)
+            *reinterpret_cast<int4*>(out + base + k) =
+                make_int4(v[k] + excl, v[k + 1] + excl, v[k + 2] + excl, v[k + 3] + excl);
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k)
+            if (base + k < n) out[base + k] = v[k] + excl;
     }
     if (threadIdx.x == 255) totals[blockIdx.x] = woff + x;
 }
@@ -6779,9 +6793,12 @@ struct uam_ctx {
                                 // 0 = the fewest giving <= 16 bands)
     int k2h_te = 1;             // K2h: terrain in the entry (UAM_OPT_K2H_TERRAIN)
     int k4h_te = 0;             // K4h: likewise (UAM_OPT_K4H_TERRAIN)
-    int k2h_lbs = 8;            // K2h: the path lower bound's sample stride (UAM_OPT_K2H_LB_STRIDE;
+    int k2h_lbs = 16;           // K2h / K4h: the path seed's sample stride (UAM_OPT_K2H_LB_STRIDE;
                                 // tools/sim_terrain_bound.py at cfg3: fetches per waypoint 0.17
-                                // at 8, 0.15 at 4, 0.37 without the path bound)
+                                // at 8, 0.15 at 4, 0.37 without the path bound; cfg5 K4h step
+                                // 0.392 / 0.385 / 0.382 / 0.382 / 0.383 / 0.392 ms at 4 / 8 / 16
+                                // / 32 / 81 / none, profiles/r06/c7: the histogram launch's seeds
+                                // 35 -> 30 us at 16, the evaluation unchanged)
     int k2g_sim = 1;            // K2g: the similarity form K2h (UAM_OPT_K2G_SIM; 0 = per-waypoint
                                 // geometry, K2g proper; maxratio_smooth always runs K2g)
     int k2g_chunk = 0;          // K2g / K2h / K4h gathers in flight per lane (UAM_OPT_K2G_CHUNK:
