@@ -119,6 +119,25 @@ def test_invalid_calls_fail_loudly(lib):
                                   None) == _lib.UAM_E_INVALID
     assert lib.uam_eval_generated3d(None, None, None, None, None, 0, None, 5, None,
                                     None) == _lib.UAM_E_INVALID
+    assert lib.uam_device_status(None) == _lib.UAM_E_INVALID
+    assert lib.uam_synchronize(None, None) == _lib.UAM_E_INVALID
+
+
+def test_status_mapping():
+    """The wrapper's error convention: UAM_E_INVALID -> ValueError (the reference's argument
+    errors), UAM_E_DEVICE -> DeviceCheckError (a device-side check of an earlier call failed;
+    its outputs are poisoned), any other status -> UamError."""
+    from uam_path_planning_amd import _lib
+
+    _lib.check(_lib.UAM_OK, "ok")
+    with pytest.raises(ValueError):
+        _lib.check(_lib.UAM_E_INVALID, "x")
+    with pytest.raises(_lib.DeviceCheckError, match="status -6"):
+        _lib.check(_lib.UAM_E_DEVICE, "x")
+    assert issubclass(_lib.DeviceCheckError, _lib.UamError)
+    with pytest.raises(_lib.UamError):
+        _lib.check(_lib.UAM_E_HIP, "x")
+    assert _lib.OPTIONS["test_sort_fault"] == 22
 
 
 def _specs():

@@ -247,7 +247,9 @@ class Engine:
 
     def raster_summary(self, raster, block=0, packed=True):
         """(Re)build raster.summary (and raster.packed unless packed=False; else it is dropped)
-        from raster.rec (block 0 = automatic); returns raster."""
+        from raster.rec (block 0 = automatic); returns raster.  Both are derived copies that
+        are not tracked: call this again after any write to raster.rec (raster_build into it,
+        a broadcast, a raw-pointer writer) -- distributed.broadcast_raster does."""
         torch = _torch()
         g = raster.geo.as_struct()
         b, nbx, nby = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
@@ -442,7 +444,11 @@ class Engine:
         return vol
 
     def volume_pack(self, volume):
-        """Derive the packed copy K4h evaluates (uam_volume_pack) into volume.packed."""
+        """Derive the packed copy K4h evaluates (uam_volume_pack) into volume.packed.
+        eval_generated3d repacks by itself when torch's version counter of volume.buf moved;
+        a write that bypasses torch (uam_volume_build into the same buffer, an RCCL broadcast
+        through the C ABI, DLPack or ctypes writers) does not move it, so call this after
+        one (distributed.broadcast_raster does)."""
         torch = _torch()
         nb = ctypes.c_int64()
         _lib.check(self.lib.uam_volume_packed_bytes(ctypes.byref(volume.geo.as_struct()),
