@@ -778,15 +778,21 @@ __device__ __forceinline__ void pk_bound_decode(uint32_t e, float2 sb, float& ub
 
 // the raster cell of a generated point (arc_point's or the pair's coordinates; uampath.h's float64
 // floor): false off the raster or NaN, with (ix, iy) = (0, 0) then (a valid header index)
-__device__ __forceinline__ bool gen_cell(const KRaster& rs, double x0, double x1, int32_t& ix,
-                                         int32_t& iy) {
-    const double tx = (x0 - rs.x0) * rs.inv_dx;
-    const double ty = (rs.y_top - x1) * rs.inv_dy;
+__device__ __forceinline__ bool gen_cell_g(double gx0, double gy_top, double inv_dx,
+                                           double inv_dy, int32_t nx, int32_t ny, double x0,
+                                           double x1, int32_t& ix, int32_t& iy) {
+    const double tx = (x0 - gx0) * inv_dx;
+    const double ty = (gy_top - x1) * inv_dy;
     // (bitwise: no short-circuit branches)
-    const bool in = (tx >= 0.0) & (tx < (double)rs.nx) & (ty >= 0.0) & (ty < (double)rs.ny);
+    const bool in = (tx >= 0.0) & (tx < (double)nx) & (ty >= 0.0) & (ty < (double)ny);
     ix = in ? (int32_t)tx : 0;
     iy = in ? (int32_t)ty : 0;
     return in;
+}
+
+__device__ __forceinline__ bool gen_cell(const KRaster& rs, double x0, double x1, int32_t& ix,
+                                         int32_t& iy) {
+    return gen_cell_g(rs.x0, rs.y_top, rs.inv_dx, rs.inv_dy, rs.nx, rs.ny, x0, x1, ix, iy);
 }
 
 // a chunk's per-slot entry kinds: the code (2 bits) and the cell's first component in the
@@ -4981,6 +4987,8 @@ struct KGrp {
     GSlot* __restrict__ slot;      // [nseg][P]: group-major, so the output launch's lanes read
                                    // a group's slots of consecutive paths contiguously
     int32_t* __restrict__ cells;   // [P][W] waypoint cells (k_cells), or null
+    double cx0, cy_top, cinv_dx, cinv_dy;  // the raster's cell grid (gen_cell) for k_cells
+    int32_t cnx, cny;
     UGeo* __restrict__ ugeo;       // K2h / K4h: [D] unit sums, formed by k_g_scatter's block 0
     int32_t lb_stride;             // K2h: the path lower bound's sample stride (>= 1)
     float* __restrict__ lbp;       // K2h: [P] each path's terrain seed (h_path_seed, formed by
@@ -5963,79 +5971,95 @@ __global__ __launch_bounds__(H_BS, UAM_K2H_MINW) void k_h_eval(KParams p, KRaste
 // evaluation's lanes through LDS instead, the 21-cell runs of scattered items cost K2h ~120 us
 // of partial-line writes per cfg3 step: 402 MB of WRITE_SIZE for 164 MB of cells,
 // profiles/r04/final2/cells.)
+// The waypoint cells of paths [path0, path0 + np) by one workgroup of nt threads (np <= 1024):
+// each path's chord terms (cx, cy, vx, vy: arc_point's) and end-point cells go to s_cv / s_e
+// once, then work item w = (path lp = w / R, run k = w % R) forms the run's 4 cells
+// j = 4k ... 4k + 3 of one path (R = ceil(W / 4) runs a path; cells past W are not stored),
+// so a lane reads its path's terms once and selects nothing per cell; items advance by nt a
+// step (nt = lstep R + kstep, one conditional subtraction).  Every thread of the workgroup
+// calls it (it synchronises).  u_rows: the unit-arc rows (LDS when staged).
+__device__ __forceinline__ void cells_rows(const KParams& p, const KGrp& kg, int64_t path0,
+                                           int np, double4* s_cv, int4* s_e,
+                                           const double2* __restrict__ u_rows, int t, int nt) {
+    const int W = kg.W, N = p.N;
+    __syncthreads();  // (a previous block's reads of s_cv / s_e are done)
+    for (int i = t; i < np; i += nt) {
+        const int32_t path = (int32_t)(path0 + i);
+        const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
+        const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
+        s_cv[i] = make_double4((pr.z + pr.x) * 0.5, (pr.w + pr.y) * 0.5, pr.x - pr.z,
+                               pr.y - pr.w);
+        int32_t ix, iy;  // the end points: the pair's own coordinates
+        const int32_t c0 = gen_cell_g(kg.cx0, kg.cy_top, kg.cinv_dx, kg.cinv_dy, kg.cnx, kg.cny,
+                                      pr.x, pr.y, ix, iy) ? iy * kg.cnx + ix : -1;
+        const int32_t c1 = gen_cell_g(kg.cx0, kg.cy_top, kg.cinv_dx, kg.cinv_dy, kg.cnx, kg.cny,
+                                      pr.z, pr.w, ix, iy) ? iy * kg.cnx + ix : -1;
+        s_e[i] = make_int4((path - q * kg.D) * N, c0, c1, 0);
+    }
+    __syncthreads();
+    int32_t* out = kg.cells + path0 * W;
+    const int R = (W + 3) >> 2, items = np * R;
+    int lp = t / R, k = t - lp * R;
+    const int lstep = nt / R, kstep = nt - lstep * R;
+    for (int w = t; w < items; w += nt) {
+        const double4 cv = s_cv[lp];
+        const int4 e = s_e[lp];
+        const int j0 = 4 * k;
+        int32_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int jj = j0 + c;
+            const double2 u = u_rows[e.x + min(max(jj - 1, 0), N - 1)];
+            const double x0 = cv.x + 0.5 * (cv.z * u.x - cv.w * u.y);  // arc_point's ops
+            const double x1 = cv.y + 0.5 * (cv.w * u.x + cv.z * u.y);
+            int32_t ix, iy;
+            const bool in = gen_cell_g(kg.cx0, kg.cy_top, kg.cinv_dx, kg.cinv_dy, kg.cnx, kg.cny,
+                                       x0, x1, ix, iy);
+            v[c] = jj == 0 ? e.y : jj == W - 1 ? e.z : in ? iy * kg.cnx + ix : -1;
+        }
+        // streaming stores: the 164 MB of cfg3's cells do not stay in L2 / the Infinity Cache
+        // as dirty lines whose write-back the next step's gathers would meet (plain stores:
+        // cfg3 with cells 0.399 against 0.374 ms, profiles/r05/cc6); a wave's runs cover ~3
+        // paths' contiguous rows
+        int32_t* o = out + (int64_t)lp * W + j0;
+        if (j0 + 3 < W && !(((uintptr_t)o) & 7)) {
+            typedef int32_t v2i __attribute__((ext_vector_type(2)));
+            const v2i w0 = {v[0], v[1]}, w1 = {v[2], v[3]};
+            __builtin_nontemporal_store(w0, reinterpret_cast<v2i*>(o));
+            __builtin_nontemporal_store(w1, reinterpret_cast<v2i*>(o) + 1);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (j0 + c < W) o[c] = v[c];
+        }
+        lp += lstep, k += kstep;
+        if (k >= R) k -= R, ++lp;
+    }
+}
+
+// The waypoint cells (the reference's returned waypoints as raster cells, solver.py:49,
+// main.py:186-190) of the sorted forms that do not write them in their output launch (K2g):
+// cells[path][j] = iy nx + ix (-1 off the raster) by the evaluations' own point and cell
+// arithmetic, workgroups of 64 consecutive paths (cells_rows) looping over the path blocks.
+// (Written by the evaluation's lanes through LDS instead, the 21-cell runs of scattered items
+// cost K2h ~120 us of partial-line writes per cfg3 step: 402 MB of WRITE_SIZE for 164 MB of
+// cells, profiles/r04/final2/cells.)
 template <bool ULDS>  // the unit-arc rows staged in LDS (D N <= 1024) or read from global
-__global__ __launch_bounds__(256) void k_cells(KParams p, KRaster rs, KGrp kg,
-                                               int32_t* __restrict__ cells) {
-    // workgroup = 64 consecutive paths, their 64 W cells contiguous in cells; each lane forms
-    // runs of 4 consecutive cells of one path and writes them by 8-B stores
+__global__ __launch_bounds__(256) void k_cells(KParams p, KGrp kg) {
     constexpr int kUtabLds = 1024;  // (16 KiB)
-    __shared__ double4 s_cv[64];    // the path's centre and chord (cx, cy, vx, vy): arc_point's
-    __shared__ int4 s_e[64];        // {its unit-arc row offset d N, start cell, goal cell, 0}
+    __shared__ double4 s_cv[64];
+    __shared__ int4 s_e[64];
     __shared__ double2 s_u[ULDS ? kUtabLds : 1];
-    const int W = kg.W, N = p.N, t = threadIdx.x;
+    const int t = threadIdx.x;
     const double2* __restrict__ gu = reinterpret_cast<const double2*>(kg.utab);
     if (ULDS)
-        for (int k = t; k < kg.D * N; k += 256) s_u[k] = gu[k];
+        for (int k = t; k < kg.D * p.N; k += 256) s_u[k] = gu[k];
     const int64_t nblk = ((int64_t)kg.P + 63) / 64;
     // (a grid smaller than nblk loops over the blocks: the side-stream launch's share of CUs)
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const int64_t path0 = blk * 64;
         const int np = (int)min((int64_t)64, (int64_t)kg.P - path0);
-        __syncthreads();  // (the previous block's reads of s_cv / s_e are done)
-        if (t < np) {
-            const int32_t path = (int32_t)(path0 + t);
-            const int32_t q = (int32_t)div_magic((uint32_t)path, kg.m_d, kg.sh_d);
-            const double4 pr = reinterpret_cast<const double4*>(kg.pairs)[q];
-            s_cv[t] = make_double4((pr.z + pr.x) * 0.5, (pr.w + pr.y) * 0.5, pr.x - pr.z,
-                                   pr.y - pr.w);
-            int32_t ix, iy;  // the end points: the pair's own coordinates
-            const int32_t c0 = gen_cell(rs, pr.x, pr.y, ix, iy) ? iy * rs.nx + ix : -1;
-            const int32_t c1 = gen_cell(rs, pr.z, pr.w, ix, iy) ? iy * rs.nx + ix : -1;
-            s_e[t] = make_int4((path - q * kg.D) * N, c0, c1, 0);
-        }
-        __syncthreads();
-        int32_t* out = cells + path0 * W;
-        // work item w = (path lp = w / R, run k = w % R): the run's 4 cells j = 4k ... 4k + 3
-        // of one path (R = ceil(W / 4) runs a path; cells past W are not stored), so a lane
-        // reads its path's terms once and selects nothing per cell; items advance by 256 a
-        // step (256 = lstep R + kstep, one conditional subtraction)
-        const int R = (W + 3) >> 2, items = np * R;
-        int lp = t / R, k = t - lp * R;
-        const int lstep = 256 / R, kstep = 256 - lstep * R;
-        for (int w = t; w < items; w += 256) {
-            const double4 cv = s_cv[lp];
-            const int4 e = s_e[lp];
-            const int j0 = 4 * k;
-            int32_t v[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int jj = j0 + c;
-                const double2 u = ULDS ? s_u[e.x + min(max(jj - 1, 0), N - 1)]
-                                       : gu[e.x + min(max(jj - 1, 0), N - 1)];
-                const double x0 = cv.x + 0.5 * (cv.z * u.x - cv.w * u.y);  // arc_point's ops
-                const double x1 = cv.y + 0.5 * (cv.w * u.x + cv.z * u.y);
-                int32_t ix, iy;
-                const bool in = gen_cell(rs, x0, x1, ix, iy);
-                v[c] = jj == 0 ? e.y : jj == W - 1 ? e.z : in ? iy * rs.nx + ix : -1;
-            }
-            // streaming stores: the 164 MB of cfg3's cells do not stay in L2 / the Infinity
-            // Cache as dirty lines whose write-back the next step's gathers would meet (plain
-            // stores: cfg3 with cells 0.399 against 0.374 ms, profiles/r05/cc6); a wave's runs
-            // cover ~3 paths' contiguous rows
-            int32_t* o = out + (int64_t)lp * W + j0;
-            if (j0 + 3 < W && !(((uintptr_t)o) & 7)) {
-                typedef int32_t v2i __attribute__((ext_vector_type(2)));
-                const v2i w0 = {v[0], v[1]}, w1 = {v[2], v[3]};
-                __builtin_nontemporal_store(w0, reinterpret_cast<v2i*>(o));
-                __builtin_nontemporal_store(w1, reinterpret_cast<v2i*>(o) + 1);
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (j0 + c < W) o[c] = v[c];
-            }
-            lp += lstep, k += kstep;
-            if (k >= R) k -= R, ++lp;
-        }
+        cells_rows(p, kg, path0, np, s_cv, s_e, ULDS ? s_u : gu, t, 256);
     }
 }
 
@@ -8150,7 +8174,13 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     // returns.  cfg3 with cells (profiles/r05/cc9, cc10, cc20): 0.350-0.353 ms; at normal
     // priority 0.355-0.358; forked after the scatter 0.363; inline after the evaluation 0.362;
     // uncapped 0.372; the arc rows from global memory instead of LDS 0.005-0.02 ms more
-    if (ko.cells) {
+    kg.cx0 = kr.x0, kg.cy_top = kr.y_top, kg.cinv_dx = kr.inv_dx, kg.cinv_dy = kr.inv_dy;
+    kg.cnx = kr.nx, kg.cny = kr.ny;
+    // (the cells written by K2h's output launch instead, the block's 320 paths each: that
+    // launch 80.6 us against 15.1 + k_cells' 57.7, cfg3 with cells 0.365 against 0.350 ms;
+    // profiles/r06/final1)
+    const bool cells_side = ko.cells != nullptr;
+    if (cells_side) {
         st = side_stream_lo(ctx);
         if (st) return st;
     }
@@ -8158,7 +8188,7 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
     if (st) return st;
     const int64_t P = kg.P;
     const unsigned cells_wg = (unsigned)std::min<int64_t>((P + 63) / 64, 512);
-    void (*const cells_fn)(KParams, KRaster, KGrp, int32_t*) =
+    void (*const cells_fn)(KParams, KGrp) =
         (int64_t)D * ctx->kp.N <= 1024 ? k_cells<true> : k_cells<false>;
     // once the cells are forked, every exit makes the caller's stream wait for them (an error
     // return must not leave k_cells writing the caller's buffer behind the call)
@@ -8171,11 +8201,10 @@ static int launch_grouped(uam_ctx* ctx, const KRaster& kr, const void* rec, cons
         }
         return r;
     };
-    if (ko.cells) {
+    if (cells_side) {
         HIP_TRY(hipEventRecord(ctx->ev_fork, s));
         HIP_TRY(hipStreamWaitEvent(ctx->s_lo, ctx->ev_fork, 0));
-        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, ctx->s_lo, ctx->kp, kr, kg,
-                           ko.cells);
+        hipLaunchKernelGGL(cells_fn, dim3(cells_wg), dim3(256), 0, ctx->s_lo, ctx->kp, kg);
         HIP_TRY(hipEventRecord(ctx->ev_join, ctx->s_lo));
         forked = true;
     }
