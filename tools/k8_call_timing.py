@@ -1,4 +1,4 @@
-"""Per-call wall time of uam_dem_polygons (run with UAM_K8_PROF=1 for the phase stamps).
+"""Per-call wall time of uam_dem_polygons (the per-phase stamps of a -DUAM_K8_PROF build were removed in round 6).
 usage: python tools/k8_call_timing.py [size=8192] [calls=4]"""
 import sys, time, os
 sys.path.insert(0, os.getcwd())
