@@ -4,7 +4,8 @@ same slot t each) for the cfg3 batch at sort tiles of 2^tbits -- the L1 -> L2 re
 waypoint the TCP has to hold (profiles/r06: 0.983 / 0.983 / 0.978 at tile bits 4 / 5 / 6;
 measured 39.6M requests for 41.0M waypoints).  usage: python tools/sim_wave_lines.py [pairs]"""
 import sys, numpy as np
-sys.path.insert(0, '/root/repo')
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from uam_path_planning_amd.arcs import arc_table
 from uam_path_planning_amd.scenario import displacements
 from uam_path_planning_amd.synthetic import random_pairs
