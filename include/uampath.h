@@ -488,7 +488,8 @@ int32_t uam_last_group(const uam_ctx* ctx);
  *   UAM_OPT_K8_TILED             DEM polygons: 1 (default) tile labelling in LDS, 0 cell-parallel
  *   UAM_OPT_K8_STREAMS           DEM polygons: streams the large regions spread over, 1..8 (4)
  *   UAM_OPT_K2G_TILE_BITS        K2g sort key: 2^b x 2^b tiles over the raster, b = 3..6; 0
- *                                (default) = tiles of ~256 x 256 cells
+ *                                (default) = tiles of ~256 x 256 cells, coarser for batches
+ *                                whose sort counts would exceed half their (path, group) items
  *   UAM_OPT_K2G_LDS_FLOOR        K2g / K2h / K4h evaluation: dynamic-LDS floor per workgroup in
  *                                bytes, which caps the workgroups resident per CU; 0 (default):
  *                                none for K2g and K2h (512-item workgroups, 2 per CU by their

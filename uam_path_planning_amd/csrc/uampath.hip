@@ -7998,9 +7998,14 @@ static int grouped_plan(uam_ctx* ctx, const KRaster& kr, const double* pairs, in
     const int64_t n_items = P * nseg;
     if (n_items >= INT32_MAX) return 0;
     int tbits = ctx->k2g_tbits;
-    if (tbits == 0) {  // tiles of ~256 x 256 cells
+    if (tbits == 0) {  // tiles of ~256 x 256 cells ...
         tbits = 3;
         while (tbits < G_TBITS_MAX && (std::max(kr.nx, kr.ny) >> tbits) > 256) ++tbits;
+        // ... but coarser for a small batch, so the sort's counts (bins x partitions) stay
+        // within half its items (cfg4's rank share of 8, 500k items at 8192^2: tiles of 512^2
+        // 0.175 ms against 0.178-0.181 at 256^2; the whole 1M-path job keeps 256^2: 0.900
+        // against 0.958 ms; profiles/r06/c10)
+        while (tbits > 3 && ((int64_t)(2 << (2 * tbits)) + 1) * G_NBK > n_items / 2) --tbits;
     }
     const int tiles = 1 << (2 * tbits);
     const int last_bin = (W % G) ? tiles : 0;  // a ragged last group gets its own bins
