@@ -47,6 +47,10 @@ def main():
         eng.set_option("k1_rows", args.cpl)
     dem = eng.tensor(synthetic_dem(args.R), torch.float32)
     out = eng.empty((geo.ny, geo.nx, 4), torch.int32)
+    # the store floor: torch's fill of the same 16 B-per-cell records
+    ms = timed(lambda: out.fill_(0), reps=args.reps)
+    print(json.dumps({"probe": "k1", "case": "fill_records", "R": args.R, "ms": round(ms, 4),
+                      "GBps": round(out.numel() * 4 / (ms * 1e-3) / 1e9, 1)}), flush=True)
     for case in args.cases.split(","):
         spec = canonical_spec(nfz_polygons=64 if case.startswith("cfg3") else 0)
         if case == "regions":       # region shapes only (Φ table)

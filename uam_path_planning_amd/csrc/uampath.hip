@@ -56,6 +56,19 @@
 // 12 288 0.197, 8192 0.176, 6144 0.205, 4096 0.193, 2048 0.254 (profiles/r05/cc15, cc16)
 #define UAM_K1_GRID_CAP 8192
 #endif
+#ifndef UAM_K1_NT
+// K1's record stores: 1 nontemporal.  cfg3 map at 4096^2: 0.177 -> 0.158 ms, the shape-free
+// build 0.108 -> 0.081 ms; 8192^2 0.649 -> 0.571 ms (profiles/r06/c13, c14)
+#define UAM_K1_NT 1
+#endif
+#ifndef UAM_K1_NTLOAD  // K1: 1 reads the DEM nontemporally (0.158 -> 0.171 ms, c14)
+#define UAM_K1_NTLOAD 0
+#endif
+#ifdef UAM_K1_WAVES  // K1: waves per SIMD the strip kernel's register budget allows
+#define UAM_K1_ATTR __attribute__((amdgpu_waves_per_eu(UAM_K1_WAVES)))
+#else
+#define UAM_K1_ATTR
+#endif
 #ifndef UAM_RF_PREFETCH  // K6 refinement: 0 reads the L-BFGS pairs without prefetch
 #define UAM_RF_PREFETCH 1
 #endif
@@ -242,6 +255,39 @@ __device__ __forceinline__ double ineq_h(const DevIneq* __restrict__ q, double x
         // square.py right/left/top/bottom: s*(x_k - c) - r
         double xk = (q->p[0] == 0.0) ? x0 : x1;
         return q->p[3] * (xk - q->p[1]) - q->p[2];
+    }
+}
+
+// ineq_h at the CPL cells of one raster column (x0 shared, rows x1[k]), the same operations
+// in the same order per cell.  The kind branch is taken once for all rows: with ineq_h called
+// per row the compiler hoisted the ellipse's shared x division above the kind test, so every
+// half-plane paid it (K1's inequality loop: ~14 f64 VALU per inequality).
+template <int CPL>
+__device__ __forceinline__ void ineq_h_col(const DevIneq& q, double x0, const double (&x1)[CPL],
+                                           double (&h)[CPL]) {
+    if (q.kind == UAM_INEQ_HALFPLANE) {
+        const double ax = q.p[3] * (x0 - q.p[0]);
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const double line = ax - q.p[2] * (x1[k] - q.p[1]);
+            h[k] = q.p[4] * line;
+        }
+    } else if (q.kind == UAM_INEQ_ELLIPSE) {
+        const double a = (x0 - q.p[0]) / q.p[2];
+        const double sa = 0.0 + a * a;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const double b = (x1[k] - q.p[1]) / q.p[3];
+            const double s = sa + b * b;
+            h[k] = s - 1.0;
+        }
+    } else if (q.p[0] == 0.0) {
+        const double v = q.p[3] * (x0 - q.p[1]) - q.p[2];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) h[k] = v;
+    } else {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) h[k] = q.p[3] * (x1[k] - q.p[1]) - q.p[2];
     }
 }
 
@@ -2100,7 +2146,7 @@ __device__ __forceinline__ void wave_walk_obs_cells(const KGeom& g, const int (&
 }
 
 template <int CPL>
-__global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
+__global__ __launch_bounds__(256) UAM_K1_ATTR void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
                                                             const float* __restrict__ dem,
                                                             float nodata, float thr,
                                                             uint4* __restrict__ rec) {
@@ -2134,7 +2180,10 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int iy = sy * CPL + k;
-            zz[k] = (ix < rs.nx && iy < rs.ny && dem) ? dem[(int64_t)iy * rs.nx + ix] : 0.0f;
+            zz[k] = (ix < rs.nx && iy < rs.ny && dem)
+                        ? (UAM_K1_NTLOAD ? __builtin_nontemporal_load(dem + (int64_t)iy * rs.nx + ix)
+                                         : dem[(int64_t)iy * rs.nx + ix])
+                        : 0.0f;
         }
     };
     int sy = 0, sx = 0;
@@ -2194,9 +2243,11 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
             const int end = sh.first + sh.count;
             for (int i = sh.first; i < end; ++i) {  // psi_u, one record load for all cells
                 const DevIneq q = uload(g.ineq, i);
+                double hk[CPL];
+                ineq_h_col<CPL>(q, xc, yc, hk);
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) {
-                    const double h = ineq_h(&q, xc, yc[k]);
+                    const double h = hk[k];
                     if (pen_smooth) {
                         const double m = fmin(h - p.enlargement, 0.0);
                         r[k] = r[k] * (m * m);
@@ -2236,9 +2287,11 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
             const int end = sh.first + sh.count;
             for (int i = sh.first; i < end; ++i) {
                 const DevIneq q = uload(g.ineq, i);
+                double hk[CPL];
+                ineq_h_col<CPL>(q, xc, yc, hk);
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) {
-                    const double h = ineq_h(&q, xc, yc[k]);
+                    const double h = hk[k];
                     if (obs_smooth) {
                         const double m = fmin(h - 0.0, 0.0);
                         r[k] = r[k] * (m * m);
@@ -2266,9 +2319,16 @@ __global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, 
                 if (hit[k]) fl |= UAM_FLAG_NFZ;
                 if (thr == -9999.0f ? (z[k] == -9999.0f) : (z[k] > thr)) fl |= UAM_FLAG_MASK;
                 if (z[k] == nodata) fl |= UAM_FLAG_NODATA;
-                rec[(int64_t)(sy * CPL + k) * rs.nx + ix] =
-                    make_uint4(__float_as_uint((float)pen[k]), __float_as_uint((float)acc[k]),
-                               __float_as_uint(z[k]), fl);
+                uint4* dst = rec + (int64_t)(sy * CPL + k) * rs.nx + ix;
+                if (UAM_K1_NT) {
+                    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                    const v4u w = {__float_as_uint((float)pen[k]), __float_as_uint((float)acc[k]),
+                                   __float_as_uint(z[k]), fl};
+                    __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(dst));
+                } else {
+                    *dst = make_uint4(__float_as_uint((float)pen[k]),
+                                      __float_as_uint((float)acc[k]), __float_as_uint(z[k]), fl);
+                }
             }
         }
         sy = nsy, sx = nsx;
