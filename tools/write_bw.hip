@@ -33,8 +33,9 @@ __global__ __launch_bounds__(256) void k_fill(v4i* __restrict__ out, int64_t n4)
     }
 }
 
-int main() {
-    const int64_t bytes = 500000LL * 82 * 4, n4 = bytes / 16;
+int main(int argc, char** argv) {
+    // default: the waypoint-cells output; argv[1]: another size in bytes (a multiple of 16)
+    const int64_t bytes = argc > 1 ? atoll(argv[1]) : 500000LL * 82 * 4, n4 = bytes / 16;
     v4i* out;
     CHECK(hipMalloc(&out, bytes));
     hipEvent_t a, b;
