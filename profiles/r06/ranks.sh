@@ -3,7 +3,7 @@
 # sharing the GPU, gloo for the host collectives): cfg3 at 2 ranks, cfg4 at 8 ranks over
 # spatial shards (the driver's 8-GPU cfg4 layout); per-rank parity in each line.
 cd "$GRAFT_REPO_ROOT"
-o=r06/ranks
+o=r06/${1:-ranks}
 mkdir -p gpurun_out/$o
 export TMPDIR=/tmp
 r="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
