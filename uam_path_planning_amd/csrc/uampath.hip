@@ -58,16 +58,9 @@
 #endif
 #ifndef UAM_K1_NT
 // K1's record stores: 1 nontemporal.  cfg3 map at 4096^2: 0.177 -> 0.158 ms, the shape-free
-// build 0.108 -> 0.081 ms; 8192^2 0.649 -> 0.571 ms (profiles/r06/c13, c14)
+// build 0.108 -> 0.081 ms; 8192^2 0.649 -> 0.571 ms (profiles/r06/c13, c14; nontemporal DEM
+// loads 0.171 ms and 7-8 waves per SIMD, which spill, were measured and dropped)
 #define UAM_K1_NT 1
-#endif
-#ifndef UAM_K1_NTLOAD  // K1: 1 reads the DEM nontemporally (0.158 -> 0.171 ms, c14)
-#define UAM_K1_NTLOAD 0
-#endif
-#ifdef UAM_K1_WAVES  // K1: waves per SIMD the strip kernel's register budget allows
-#define UAM_K1_ATTR __attribute__((amdgpu_waves_per_eu(UAM_K1_WAVES)))
-#else
-#define UAM_K1_ATTR
 #endif
 #ifndef UAM_RF_PREFETCH  // K6 refinement: 0 reads the L-BFGS pairs without prefetch
 #define UAM_RF_PREFETCH 1
@@ -2146,7 +2139,7 @@ __device__ __forceinline__ void wave_walk_obs_cells(const KGeom& g, const int (&
 }
 
 template <int CPL>
-__global__ __launch_bounds__(256) UAM_K1_ATTR void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
+__global__ __launch_bounds__(256) void k_raster_build_cells(KGeom g, KParams p, KRaster rs,
                                                             const float* __restrict__ dem,
                                                             float nodata, float thr,
                                                             uint4* __restrict__ rec) {
@@ -2180,10 +2173,7 @@ __global__ __launch_bounds__(256) UAM_K1_ATTR void k_raster_build_cells(KGeom g,
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int iy = sy * CPL + k;
-            zz[k] = (ix < rs.nx && iy < rs.ny && dem)
-                        ? (UAM_K1_NTLOAD ? __builtin_nontemporal_load(dem + (int64_t)iy * rs.nx + ix)
-                                         : dem[(int64_t)iy * rs.nx + ix])
-                        : 0.0f;
+            zz[k] = (ix < rs.nx && iy < rs.ny && dem) ? dem[(int64_t)iy * rs.nx + ix] : 0.0f;
         }
     };
     int sy = 0, sx = 0;
