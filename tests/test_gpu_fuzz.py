@@ -6,9 +6,12 @@ sort tile bits, rows per lane) and the batch, then checks one of
 
   * K1, the raster build (a raster geometry of its own: non-square, offset, any cell size)
     against orc_raster_build -- records, flags and all;
-  * the generated raster evaluation (K2h, or K2g under maxratio_smooth) against
-    orc_eval_generated_h / orc_eval_paths in the same group order;
-  * the generated volume evaluation (K4h) against orc_eval_generated_h in volume mode;
+  * the generated raster evaluation -- the sorted forms (K2h, or K2g under maxratio_smooth),
+    the form the library picks for the batch size, or the reference's sequential order
+    (group 0: K2s / K2 / K2w), waypoint cells on some -- against orc_eval_generated_h /
+    orc_eval_paths in the same group order;
+  * the generated volume evaluation (K4h, or the sequential K4 when the form draw or the batch
+    size selects it) against orc_eval_generated_h in volume mode / orc_eval_paths3d;
   * analytic mode (K3b or the small-batch forms) against the sequential orc_eval_paths.
 
 The default run covers seeds 0-47; UAM_FUZZ_SEEDS=a:b widens it (profiles/r06 records a
@@ -58,6 +61,10 @@ def _draw(seed):
                 float(rng.uniform(0.02, 0.4)), float(rng.uniform(0.02, 0.4)))
     c["thr"] = float(rng.choice([0.0, 100.0, -9999.0]))
     c["pair_seed"] = int(rng.integers(0, 1 << 30))
+    # raster: the sorted forms forced, the library's own choice by batch size, or the
+    # reference's sequential order (group 0); waypoint cells on some
+    c["form"] = str(rng.choice(["sorted", "sorted", "auto", "seq"]))
+    c["cells"] = bool(rng.random() < 0.3)
     return c
 
 
@@ -71,9 +78,10 @@ def _setup(oracle_mod, c):
         pytest.fail("GPU tests need an MI355X")
     build.build_library()
     e = Engine(0)
-    e.set_option("group", c["group"])
-    e.set_option("sorted_min_paths", 0)
-    e.set_option("wave_max_paths", 0)
+    e.set_option("group", 0 if c["form"] == "seq" else c["group"])
+    if c["form"] != "auto":
+        e.set_option("sorted_min_paths", 0)
+        e.set_option("wave_max_paths", 0)
     e.set_option("k2h_terrain", c["terrain"])
     e.set_option("k4h_terrain", c["terrain"])
     e.set_option("k2g_chunk", c["chunk"])
@@ -164,9 +172,14 @@ def test_fuzz_parity(oracle_mod, seed):
                 vol.cols.cpu().numpy().view(np.float32))
         pairs = _pairs(c, n3=True)
         gpu = e.eval_generated3d(pairs, ut, vol)
-        assert e.last_kernel() == "K4h+pack"
-        ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host,
-                                   group=e.last_group())
+        g, k = e.last_group(), e.last_kernel()
+        if c["form"] == "sorted":
+            assert k == "K4h+pack"
+        if k.startswith("K4h"):
+            ref = orc.eval_generated_h(pairs, ut, mode="volume", vdesc=vd, vol=host, group=g)
+        else:   # the sequential lane-per-path K4
+            assert g == 0, k
+            ref = orc.eval_paths3d(oracle_mod.gen_paths3d(pairs, ut), vd, host)
         _eq(gpu, ref, KEYS + (("below_terrain", "below"),))
         _selection(gpu, ref, oracle_mod, D)
         return
@@ -177,13 +190,17 @@ def test_fuzz_parity(oracle_mod, seed):
                                        geo.nodata, geo.dem_threshold)
     rec = raster.rec.cpu().numpy().view(np.float32)
     pairs = _pairs(c)
-    gpu = e.eval_generated(pairs, ut, raster=raster)
-    g = e.last_group()
-    if c["opts"]["maxratio_smooth"]:
+    gpu = e.eval_generated(pairs, ut, raster=raster, want_cells=c["cells"])
+    g, k = e.last_group(), e.last_kernel()
+    if c["form"] == "seq":
+        assert g == 0
+    elif c["form"] == "sorted" and not c["opts"]["maxratio_smooth"]:
+        assert k == "K2h+pack"
+    if k.startswith("K2h"):
+        ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=g,
+                                   want_cells=c["cells"])
+    else:   # K2g (maxratio_smooth) in group order, or a sequential-order form (group 0)
         ref = orc.eval_paths(oracle_mod.gen_paths(pairs, ut), mode="raster", rdesc=rd,
-                             rec=rec, group=g)
-    else:
-        assert e.last_kernel() == "K2h+pack"
-        ref = orc.eval_generated_h(pairs, ut, rdesc=rd, rec=rec, group=g)
-    _eq(gpu, ref, KEYS)
+                             rec=rec, group=g, want_cells=c["cells"])
+    _eq(gpu, ref, KEYS + ((("cells", "cells"),) if c["cells"] else ()))
     _selection(gpu, ref, oracle_mod, D)
