@@ -758,6 +758,40 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
         out[w] = (uint32_t)(lane ? (m >> 32) : m);
 }
 
+// the same bits with one wave per block (blocks of >= 8 x 8 cells): the wave reads the block's
+// rows as coalesced runs of min(B, 64) records, stops at the first row step with a non-skippable
+// cell, and lane 0 sets the block's bit (the words zeroed by the caller).  The thread-per-block
+// kernel above reads each lane's block serially, 16 B at a stride of B records across the lanes.
+__global__ __launch_bounds__(256) void k_raster_summary_w(const uint4* __restrict__ rec,
+                                                          int32_t nx, int32_t ny, int32_t shift,
+                                                          int32_t nbx, int32_t n_blocks,
+                                                          uint32_t* __restrict__ out) {
+    const int32_t blk = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (blk >= n_blocks) return;
+    const int lane = threadIdx.x & 63;
+    const int B = 1 << shift, lpr = B < 64 ? B : 64, rpi = 64 / lpr;
+    const int bx = blk % nbx, by = blk / nbx;
+    const int x0 = bx << shift, y0 = by << shift;
+    const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+    const int lc = lane & (lpr - 1), lr = lane / lpr;
+    bool skip = true;
+    for (int r0 = y0; r0 < y1 && skip; r0 += rpi) {
+        bool bad = false;
+        const int iy = r0 + lr;
+        for (int c0 = x0; c0 < x1; c0 += lpr) {
+            const int ix = c0 + lc;
+            if (iy < y1 && ix < x1) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                const uint32_t t = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
+                bad = bad || (r.x & 0x7fffffffu) || (r.y & 0x7fffffffu) ||
+                      (r.w & UAM_FLAG_NFZ) || t;
+            }
+        }
+        skip = __ballot(bad) == 0;
+    }
+    if (skip && lane == 0) atomicOr(out + (blk >> 5), 1u << (blk & 31));
+}
+
 // ---- Packed raster (uam_raster_pack; build-defined, no reference counterpart) --------------
 // The sorted forms are bound by 128-B lines; a 16-B record uses one eighth of its line, and most
 // waypoints need less of it.  The packed copy (layout: PackDims) keeps what each block needs in
@@ -960,6 +994,41 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
         const int sh = lane;  // this lane's 16 blocks are bits [lane, lane + 16) of the ballots
         out[blk >> 4] = spread16((uint32_t)(lo >> sh)) | (spread16((uint32_t)(hi >> sh)) << 1);
     }
+}
+
+// the same codes with one wave per block (blocks of >= 8 x 8 cells): coalesced runs of the
+// block's rows, a stop once a negative psi decides code 3, lane 0 ORs the code into the map
+// (zeroed by uam_raster_pack's memset)
+__global__ __launch_bounds__(256) void k_raster_pack_map_w(const uint4* __restrict__ rec,
+                                                           int32_t nx, int32_t ny, int32_t shift,
+                                                           int32_t nbx, int32_t n_blocks,
+                                                           uint32_t* __restrict__ out) {
+    const int32_t blk = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (blk >= n_blocks) return;
+    const int lane = threadIdx.x & 63;
+    const int B = 1 << shift, lpr = B < 64 ? B : 64, rpi = 64 / lpr;
+    const int bx = blk % nbx, by = blk / nbx;
+    const int x0 = bx << shift, y0 = by << shift;
+    const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+    const int lc = lane & (lpr - 1), lr = lane / lpr;
+    bool need = false, neg = false, nz = false;
+    for (int r0 = y0; r0 < y1 && !neg; r0 += rpi) {
+        const int iy = r0 + lr;
+        for (int c0 = x0; c0 < x1; c0 += lpr) {
+            const int ix = c0 + lc;
+            if (iy < y1 && ix < x1) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                need = need || (r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ);
+                neg = neg || ((r.y >> 31) && r.y != 0x80000000u);  // negative, or a -NaN
+                nz = nz || (r.x & 0x7fffffffu) || ((r.w & UAM_FLAG_NODATA) ? 0u : r.z);
+            }
+        }
+        neg = __ballot(neg) != 0;
+    }
+    need = __ballot(need) != 0;
+    nz = __ballot(nz) != 0;
+    const uint32_t code = need ? (neg ? 3u : 2u) : nz ? 1u : 0u;
+    if (code && lane == 0) atomicOr(out + (blk >> 4), code << ((blk & 15) * 2));
 }
 
 // one wave per bound block: {min, max} of its terrain as read, from the 4-B terrain plane (4 x 8-
@@ -8724,8 +8793,12 @@ int uam_raster_pack(uam_ctx* ctx, const uam_raster_desc* desc, const void* rec, 
     HIP_TRY(hipMemsetAsync(b, 0, (size_t)d.off_scr, s));
     HIP_TRY(hipMemsetAsync(b + d.off_p4, 0, (size_t)(d.bytes - d.off_p4), s));
     const int32_t nb = d.nbx * d.nby;
-    hipLaunchKernelGGL(k_raster_pack_map, dim3(grid_for(nb, 256)), dim3(256), 0, s, r4, kr.nx,
-                       kr.ny, d.sh, d.nbx, nb, (uint32_t*)b);
+    if (d.sh >= 3)  // (the map words were zeroed above)
+        hipLaunchKernelGGL(k_raster_pack_map_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s,
+                           r4, kr.nx, kr.ny, d.sh, d.nbx, nb, (uint32_t*)b);
+    else
+        hipLaunchKernelGGL(k_raster_pack_map, dim3(grid_for(nb, 256)), dim3(256), 0, s, r4,
+                           kr.nx, kr.ny, d.sh, d.nbx, nb, (uint32_t*)b);
     const int64_t cells = (int64_t)kr.nx * kr.ny;
     hipLaunchKernelGGL(k_raster_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, r4,
                        kr, (uint32_t*)(b + d.off_p4), (float*)(b + d.off_t4),
@@ -8764,9 +8837,16 @@ int uam_raster_summary(uam_ctx* ctx, const uam_raster_desc* desc, const void* re
     if (st) return st;
     DeviceGuard dg(ctx->device);
     const int32_t nb = nbx * nby;
-    hipLaunchKernelGGL(k_raster_summary, dim3(grid_for(nb, 256)), dim3(256), 0,
-                       (hipStream_t)stream, (const uint4*)rec, kr.nx, kr.ny, sh, nbx, nb,
-                       summary);
+    if (sh >= 3) {
+        HIP_TRY(hipMemsetAsync(summary, 0, (size_t)((nb + 31) / 32) * 4, (hipStream_t)stream));
+        hipLaunchKernelGGL(k_raster_summary_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0,
+                           (hipStream_t)stream, (const uint4*)rec, kr.nx, kr.ny, sh, nbx, nb,
+                           summary);
+    } else {
+        hipLaunchKernelGGL(k_raster_summary, dim3(grid_for(nb, 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const uint4*)rec, kr.nx, kr.ny, sh, nbx, nb,
+                           summary);
+    }
     HIP_TRY(hipGetLastError());
     return UAM_OK;
 }
