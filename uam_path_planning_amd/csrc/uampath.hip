@@ -758,12 +758,10 @@ __global__ __launch_bounds__(256) void k_raster_summary(const uint4* __restrict_
         out[w] = (uint32_t)(lane ? (m >> 32) : m);
 }
 
-// the same bits with one wave per block (blocks of >= 8 x 8 cells): lane l of step k reads the
-// block's row-major cell 64 k + l (coalesced runs of min(B, 64) records), 8 steps' loads issued
-// before any is tested, the wave stopping at the first batch with a non-skippable cell; lane 0
-// sets the block's bit (the words zeroed by the caller).  The thread-per-block kernel above
-// reads each lane's block serially, 16 B at a stride of B records across the lanes.
-constexpr int SUMW_U = 8;
+// the same bits with one wave per block (blocks of >= 8 x 8 cells): the wave reads the block's
+// rows as coalesced runs of min(B, 64) records, stops at the first row step with a non-skippable
+// cell, and lane 0 sets the block's bit (the words zeroed by the caller).  The thread-per-block
+// kernel above reads each lane's block serially, 16 B at a stride of B records across the lanes.
 __global__ __launch_bounds__(256) void k_raster_summary_w(const uint4* __restrict__ rec,
                                                           int32_t nx, int32_t ny, int32_t shift,
                                                           int32_t nbx, int32_t n_blocks,
@@ -771,27 +769,23 @@ __global__ __launch_bounds__(256) void k_raster_summary_w(const uint4* __restric
     const int32_t blk = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (blk >= n_blocks) return;
     const int lane = threadIdx.x & 63;
+    const int B = 1 << shift, lpr = B < 64 ? B : 64, rpi = 64 / lpr;
     const int bx = blk % nbx, by = blk / nbx;
     const int x0 = bx << shift, y0 = by << shift;
-    const int x1 = min(x0 + (1 << shift), (int)nx), y1 = min(y0 + (1 << shift), (int)ny);
-    const int steps = 1 << (2 * shift - 6);
+    const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+    const int lc = lane & (lpr - 1), lr = lane / lpr;
     bool skip = true;
-    for (int s0 = 0; s0 < steps && skip; s0 += SUMW_U) {
-        uint4 r[SUMW_U];
-        bool in[SUMW_U];
-#pragma unroll
-        for (int u = 0; u < SUMW_U; ++u) {
-            const int k = ((s0 + u) << 6) | lane;
-            const int iy = y0 + (k >> shift), ix = x0 + (k & ((1 << shift) - 1));
-            in[u] = s0 + u < steps && iy < y1 && ix < x1;
-            r[u] = in[u] ? rec[(int64_t)iy * nx + ix] : make_uint4(0u, 0u, 0u, 0u);
-        }
+    for (int r0 = y0; r0 < y1 && skip; r0 += rpi) {
         bool bad = false;
-#pragma unroll
-        for (int u = 0; u < SUMW_U; ++u) {
-            const uint32_t t = (r[u].w & UAM_FLAG_NODATA) ? 0u : r[u].z;  // +0.0f bits
-            bad = bad || (in[u] && ((r[u].x & 0x7fffffffu) || (r[u].y & 0x7fffffffu) ||
-                                    (r[u].w & UAM_FLAG_NFZ) || t));
+        const int iy = r0 + lr;
+        for (int c0 = x0; c0 < x1; c0 += lpr) {
+            const int ix = c0 + lc;
+            if (iy < y1 && ix < x1) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                const uint32_t t = (r.w & UAM_FLAG_NODATA) ? 0u : r.z;  // +0.0f bits
+                bad = bad || (r.x & 0x7fffffffu) || (r.y & 0x7fffffffu) ||
+                      (r.w & UAM_FLAG_NFZ) || t;
+            }
         }
         skip = __ballot(bad) == 0;
     }
@@ -1002,9 +996,9 @@ __global__ __launch_bounds__(256) void k_raster_pack_map(const uint4* __restrict
     }
 }
 
-// the same codes with one wave per block (blocks of >= 8 x 8 cells), k_raster_summary_w's cell
-// order and batches, a stop once a negative psi decides code 3; lane 0 ORs the code into the
-// map (zeroed by uam_raster_pack's memset)
+// the same codes with one wave per block (blocks of >= 8 x 8 cells): coalesced runs of the
+// block's rows, a stop once a negative psi decides code 3, lane 0 ORs the code into the map
+// (zeroed by uam_raster_pack's memset)
 __global__ __launch_bounds__(256) void k_raster_pack_map_w(const uint4* __restrict__ rec,
                                                            int32_t nx, int32_t ny, int32_t shift,
                                                            int32_t nbx, int32_t n_blocks,
@@ -1012,26 +1006,22 @@ __global__ __launch_bounds__(256) void k_raster_pack_map_w(const uint4* __restri
     const int32_t blk = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (blk >= n_blocks) return;
     const int lane = threadIdx.x & 63;
+    const int B = 1 << shift, lpr = B < 64 ? B : 64, rpi = 64 / lpr;
     const int bx = blk % nbx, by = blk / nbx;
     const int x0 = bx << shift, y0 = by << shift;
-    const int x1 = min(x0 + (1 << shift), (int)nx), y1 = min(y0 + (1 << shift), (int)ny);
-    const int steps = 1 << (2 * shift - 6);
+    const int x1 = min(x0 + B, (int)nx), y1 = min(y0 + B, (int)ny);
+    const int lc = lane & (lpr - 1), lr = lane / lpr;
     bool need = false, neg = false, nz = false;
-    for (int s0 = 0; s0 < steps && !neg; s0 += SUMW_U) {
-        uint4 r[SUMW_U];
-        bool in[SUMW_U];
-#pragma unroll
-        for (int u = 0; u < SUMW_U; ++u) {
-            const int k = ((s0 + u) << 6) | lane;
-            const int iy = y0 + (k >> shift), ix = x0 + (k & ((1 << shift) - 1));
-            in[u] = s0 + u < steps && iy < y1 && ix < x1;
-            r[u] = in[u] ? rec[(int64_t)iy * nx + ix] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < SUMW_U; ++u) {  // (a zero record sets nothing)
-            need = need || (r[u].y & 0x7fffffffu) || (r[u].w & UAM_FLAG_NFZ);
-            neg = neg || ((r[u].y >> 31) && r[u].y != 0x80000000u);  // negative, or a -NaN
-            nz = nz || (r[u].x & 0x7fffffffu) || ((r[u].w & UAM_FLAG_NODATA) ? 0u : r[u].z);
+    for (int r0 = y0; r0 < y1 && !neg; r0 += rpi) {
+        const int iy = r0 + lr;
+        for (int c0 = x0; c0 < x1; c0 += lpr) {
+            const int ix = c0 + lc;
+            if (iy < y1 && ix < x1) {
+                const uint4 r = rec[(int64_t)iy * nx + ix];
+                need = need || (r.y & 0x7fffffffu) || (r.w & UAM_FLAG_NFZ);
+                neg = neg || ((r.y >> 31) && r.y != 0x80000000u);  // negative, or a -NaN
+                nz = nz || (r.x & 0x7fffffffu) || ((r.w & UAM_FLAG_NODATA) ? 0u : r.z);
+            }
         }
         neg = __ballot(neg) != 0;
     }
